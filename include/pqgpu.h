@@ -1,0 +1,229 @@
+/*
+ * pqgpu.h — C ABI of the MI355X-native parquet page decoder.
+ *
+ * This is the drop-in boundary for the decode half of parquet-rs 0.4.2 (sunchao/parquet-rs,
+ * /root/reference). It replaces, for a whole column chunk at a time:
+ *
+ *   Decoder<T>::set_data / get           src/encodings/decoding.rs:37-54 (all decoders,
+ *                                        :88-835, via get_decoder :60-79)
+ *   DictDecoder<T>::set_dict             src/encodings/decoding.rs:282-288
+ *   LevelDecoder::{v1,v2,set_data,set_data_range,get}   src/encodings/levels.rs:148-272
+ *   RleDecoder::{get_batch,get_batch_with_dict}         src/encodings/rle.rs:398-487
+ *   BitReader::{get_value,get_batch,...}, unpack32      src/util/bit_util.rs:369-608,
+ *                                                       src/util/bit_packing.rs:29-72
+ *   the decode loop of ColumnReaderImpl::read_batch     src/column/reader.rs:159-265
+ *       (def-level count :212-226, dense values :252-253) and read_new_page /
+ *       set_current_page_encoding / configure_dictionary :269-488
+ *
+ * The reference pulls `batch_size` values at a time through those traits; a GPU cannot be
+ * fed that way, so the ABI decodes whole chunks (all pages of a column chunk in one call)
+ * and a host-side ColumnReader serves read_batch slices from the decoded chunk
+ * (pqg_column_reader_* below). Results are identical to the concatenation of the
+ * reference's read_batch outputs.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. Device buffers are HIP device pointers on the ctx's
+ *    device; the stream argument is a hipStream_t (may be NULL = default stream).
+ *  - The caller owns every buffer; the library never frees caller memory. Page bytes are
+ *    read-only (mirrors ByteBufferPtr, src/util/memory.rs:245-356).
+ *  - One pqg_ctx per GPU; a ctx is single-owner (like the reference's !Send readers).
+ *    Distinct contexts may be used concurrently from different host threads.
+ *  - Status codes: 0 OK; 1 General, 2 NYI, 3 EOF (ParquetError, src/errors.rs:24-51);
+ *    4 = input on which the reference panics; 5 = input on which the reference loops
+ *    forever; 6 = output capacity too small; 7 = invalid argument; 8 = HIP runtime error.
+ *    The library never aborts the process.
+ *  - Encoding / type / page-type ids are the on-disk thrift ids (src/basic.rs:38-47,
+ *    169-218, converted at :387-400, :508-521).
+ */
+#ifndef PQGPU_H
+#define PQGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQG_OK 0
+#define PQG_ERR_GENERAL 1
+#define PQG_ERR_NYI 2
+#define PQG_ERR_EOF 3
+#define PQG_ERR_PANIC 4
+#define PQG_ERR_HANG 5
+#define PQG_ERR_CAPACITY 6
+#define PQG_ERR_INVALID 7
+#define PQG_ERR_HIP 8
+
+/* physical types (basic.rs:38-47) */
+#define PQG_BOOLEAN 0
+#define PQG_INT32 1
+#define PQG_INT64 2
+#define PQG_INT96 3
+#define PQG_FLOAT 4
+#define PQG_DOUBLE 5
+#define PQG_BYTE_ARRAY 6
+#define PQG_FIXED_LEN_BYTE_ARRAY 7
+
+/* encodings (thrift ids) */
+#define PQG_PLAIN 0
+#define PQG_PLAIN_DICTIONARY 2
+#define PQG_RLE 3
+#define PQG_BIT_PACKED 4
+#define PQG_DELTA_BINARY_PACKED 5
+#define PQG_DELTA_LENGTH_BYTE_ARRAY 6
+#define PQG_DELTA_BYTE_ARRAY 7
+#define PQG_RLE_DICTIONARY 8
+
+/* page types (thrift PageType) */
+#define PQG_PAGE_DATA 0
+#define PQG_PAGE_DICTIONARY 2
+#define PQG_PAGE_DATA_V2 3
+
+/* One uncompressed page of a column chunk (Page, src/column/page.rs:28-57). Pages are
+ * given in file order, the dictionary page (if any) first. `offset` locates the payload in
+ * the chunk blob; 16-byte aligned offsets give the fastest dictionary gathers. */
+typedef struct {
+  uint64_t offset;       /* payload offset inside the blob */
+  uint32_t nbytes;       /* uncompressed payload length */
+  uint32_t num_values;   /* DataPage(V2).num_values / DictionaryPage.num_values */
+  int32_t page_type;     /* PQG_PAGE_* */
+  int32_t encoding;      /* value encoding */
+  int32_t def_encoding;  /* data page v1: definition level encoding (RLE / BIT_PACKED) */
+  int32_t rep_encoding;  /* data page v1: repetition level encoding */
+  uint32_t def_len;      /* data page v2: definition_levels_byte_length */
+  uint32_t rep_len;      /* data page v2: repetition_levels_byte_length */
+} pqg_page;
+
+/* Column descriptor subset the decode needs (ColumnDescriptor, schema/types.rs:546-640). */
+typedef struct {
+  int32_t physical_type;
+  int32_t type_length;  /* FIXED_LEN_BYTE_ARRAY only */
+  int16_t max_def;
+  int16_t max_rep;
+} pqg_column;
+
+/* Outputs of one chunk decode, all device memory, 16-byte aligned.
+ *  def_levels / rep_levels: int16, capacity >= sum of data-page num_values; NULL skips the
+ *    stream exactly as read_batch(.., None, ..) does (column/reader.rs:212-250).
+ *  values: dense non-null values (fixed width: 1 B bool, 4 B INT32/FLOAT, 8 B INT64/DOUBLE,
+ *    12 B INT96; BYTE_ARRAY/FLBA: concatenated bytes) with `values_capacity` bytes.
+ *  offsets: BYTE_ARRAY/FLBA only, int64[num_values + 1] byte offsets into `values`.
+ *  The counters are filled by pqg_sync. */
+typedef struct {
+  int16_t *def_levels;
+  int16_t *rep_levels;
+  void *values;
+  uint64_t values_capacity;
+  int64_t *offsets;
+  uint64_t offsets_capacity; /* entries */
+  uint64_t num_levels;       /* out */
+  uint64_t num_values;       /* out */
+  uint64_t num_bytes;        /* out (BYTE_ARRAY/FLBA) */
+} pqg_output;
+
+typedef struct pqg_ctx pqg_ctx;
+
+/* Per-stage device times of the last decode (ms), filled by pqg_sync when timing is on. */
+typedef struct {
+  float prepare_ms, levels_ms, scan_ms, values_ms, total_ms;
+  uint32_t values_kernel; /* encoding whose kernel dominated values_ms */
+} pqg_timings;
+
+int pqg_ctx_create(int device, pqg_ctx **out);
+int pqg_ctx_destroy(pqg_ctx *ctx);
+int pqg_ctx_set_timing(pqg_ctx *ctx, int enabled);
+
+/* Enqueue the decode of one column chunk on `stream` (asynchronous). `blob` is a device
+ * buffer of `blob_len` bytes holding every page payload; `pages` is host memory (copied
+ * during the call). Returns immediately with PQG_OK or an argument error. */
+int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
+                     uint64_t blob_len, const pqg_page *pages, uint32_t npages,
+                     pqg_output *out, void *stream);
+
+/* Wait for the last decode and report its status. On error *first_bad_page names the
+ * lowest page index that failed (the page the reference would fail on first). */
+int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
+int pqg_get_timings(pqg_ctx *ctx, pqg_timings *t);
+const char *pqg_error_message(pqg_ctx *ctx);
+
+/* ---------------------------------------------------------------- host-side reader
+ * The parquet::file::reader surface kept on the host (src/file/reader.rs:51-90, 140-530):
+ * footer + thrift-compact metadata, page headers, decompression (snappy, gzip), then the
+ * GPU decode above. Column readers serve read_batch slices with the reference's contract
+ * (column/reader.rs:159-265). */
+typedef struct pqg_file_reader pqg_file_reader;
+typedef struct pqg_column_reader pqg_column_reader;
+
+int pqg_file_open(const char *path, pqg_file_reader **out);
+int pqg_file_open_memory(const uint8_t *data, uint64_t len, pqg_file_reader **out);
+void pqg_file_close(pqg_file_reader *r);
+const char *pqg_file_error(pqg_file_reader *r);
+int64_t pqg_file_num_rows(pqg_file_reader *r);
+int pqg_file_num_row_groups(pqg_file_reader *r);
+int pqg_file_num_columns(pqg_file_reader *r);
+/* Leaf column descriptor (SchemaDescriptor::column): path is dot-joined. */
+int pqg_file_column(pqg_file_reader *r, int col, pqg_column *out, char *path, size_t path_cap);
+int64_t pqg_row_group_num_rows(pqg_file_reader *r, int rg);
+/* Uncompressed pages of one column chunk (SerializedPageReader::get_next_page). Fills up
+ * to `cap` page descriptors (offsets into an internal host blob that pqg_chunk_blob
+ * returns); returns the page count or a negative status. */
+int pqg_chunk_pages(pqg_file_reader *r, int rg, int col, pqg_page *pages, uint32_t cap);
+int pqg_chunk_blob(pqg_file_reader *r, int rg, int col, const uint8_t **blob, uint64_t *len);
+
+/* ColumnReaderImpl over the GPU decode: the chunk is decoded on `device` in one pass,
+ * read_batch then copies slices to host buffers. def/rep may be NULL (read_batch(None)). */
+int pqg_column_reader_open(pqg_file_reader *r, int rg, int col, pqg_ctx *ctx,
+                           pqg_column_reader **out);
+void pqg_column_reader_close(pqg_column_reader *cr);
+/* Returns status; *values_read / *levels_read as read_batch's tuple. For BYTE_ARRAY/FLBA
+ * `values` receives concatenated bytes (capacity values_bytes_cap) and `lengths` the
+ * per-value byte lengths. */
+int pqg_column_reader_read_batch(pqg_column_reader *cr, size_t batch_size, int16_t *def,
+                                 int16_t *rep, void *values, uint64_t values_bytes_cap,
+                                 uint32_t *lengths, size_t *values_read, size_t *levels_read);
+
+/* ---------------------------------------------------------------- synthetic page writer
+ * Reference-identical writers (RleEncoder rle.rs:55-317, LevelEncoder levels.rs:54-143,
+ * PlainEncoder / DictEncoder / DeltaBitPackEncoder encoding.rs:94-714) used by bench.py to
+ * build the BASELINE.json workloads. Each returns bytes written or 0 on overflow. */
+uint64_t pqg_encode_rle(const uint64_t *values, uint64_t n, int bit_width, uint8_t *out,
+                        uint64_t cap);
+uint64_t pqg_encode_levels_v1(const int16_t *levels, uint64_t n, int16_t max_level,
+                              uint8_t *out, uint64_t cap);
+uint64_t pqg_encode_delta(int physical_type, const void *values, uint64_t n, int block_size,
+                          int mini_blocks, uint8_t *out, uint64_t cap);
+/* Dictionary indices page body: [bit_width byte][RLE hybrid of the indices]. */
+uint64_t pqg_encode_dict_indices(const uint32_t *indices, uint64_t n, int bit_width,
+                                 uint8_t *out, uint64_t cap);
+
+/* Multi-threaded synthetic workload generators (one page per task): see DESIGN.md §4. */
+typedef struct {
+  uint64_t blob_len;
+  uint32_t npages;
+  uint64_t total_levels;
+  uint64_t total_values;
+} pqg_workload_info;
+
+/* Config 2: n levels with Bernoulli(p_null) nulls, max_def 1, PLAIN INT32 values; data
+ * page v1 with `page_levels` levels per page. Pages written into `blob` (host) at 64-byte
+ * aligned offsets; descriptors to `pages`. Call with blob == NULL to size. */
+int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
+                         int threads, uint8_t *blob, uint64_t blob_cap, pqg_page *pages,
+                         uint32_t pages_cap, pqg_workload_info *info);
+/* Config 3: required INT64 column, dictionary of `dict_size` distinct values, n indices
+ * uniform in [0, dict_size): page 0 is the dictionary page. */
+int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                       int threads, uint8_t *blob, uint64_t blob_cap, pqg_page *pages,
+                       uint32_t pages_cap, pqg_workload_info *info);
+/* Config 4: required INT64 column, DELTA_BINARY_PACKED, deltas uniform in
+ * [-2^(delta_bits-1), 2^(delta_bits-1)). */
+int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
+                        int mini_blocks, uint64_t seed, int threads, uint8_t *blob,
+                        uint64_t blob_cap, pqg_page *pages, uint32_t pages_cap,
+                        pqg_workload_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,82 @@
+// pqg_device.hpp — device helpers shared by the CDNA4 decode kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../pqg_internal.hpp"
+
+namespace pqg {
+
+constexpr int WG = 256;       // threads per workgroup (4 waves of 64)
+constexpr int WAVE = 64;
+
+// Record the first error of a page and of the chunk. Results must not depend on which
+// workgroup reports first: the page status keeps the first code, the chunk keeps the
+// lowest bad page index.
+__device__ inline void report(PageWork* pages, ChunkResult* res, int page, int32_t code) {
+  atomicCAS(&pages[page].status, 0, code);
+  atomicMin(&res->first_bad_page, page);
+}
+
+// Little-endian byte load from global memory, guarded by the blob size.
+__device__ inline uint32_t gbyte(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
+  return a < blob_len ? blob[a] : 0u;
+}
+
+// 64-bit little-endian window starting at an arbitrary byte address, guarded.
+__device__ inline uint64_t gload_u64(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
+  uint64_t al = a & ~3ull;
+  uint32_t sh = (uint32_t)(a - al) * 8u;
+  uint32_t w0, w1, w2;
+  if (al + 12 <= blob_len) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + al);
+    w0 = p[0];
+    w1 = p[1];
+    w2 = p[2];
+  } else {
+    uint32_t b[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) b[k] = gbyte(blob, blob_len, al + k);
+    w0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    w1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    w2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
+  }
+  uint64_t lo = ((uint64_t)w1 << 32) | w0;
+  if (sh == 0) return lo;
+  return (lo >> sh) | ((uint64_t)w2 << (64 - sh));
+}
+
+// 64-bit little-endian window from an LDS byte image stored as 32-bit words.
+__device__ inline uint64_t lload_u64(const uint32_t* words, uint32_t byte_idx) {
+  uint32_t wi = byte_idx >> 2;
+  uint32_t sh = (byte_idx & 3u) * 8u;
+  uint64_t lo = ((uint64_t)words[wi + 1] << 32) | words[wi];
+  if (sh == 0) return lo;
+  return (lo >> sh) | ((uint64_t)words[wi + 2] << (64 - sh));
+}
+
+__device__ inline uint32_t lbyte(const uint32_t* words, uint32_t byte_idx) {
+  return (words[byte_idx >> 2] >> ((byte_idx & 3u) * 8u)) & 0xFFu;
+}
+
+__device__ inline uint32_t lane_id() { return __lane_id(); }
+
+__device__ inline int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ inline uint32_t readlane_u(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Block-wide sum of a 64-bit value (256 threads). Uses `scratch` (>= 4 u64) in LDS.
+__device__ inline uint64_t block_sum_u64(uint64_t v, uint64_t* scratch) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  if (threadIdx.x == 0) t = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+  __syncthreads();
+  return t;  // valid in thread 0
+}
+
+}  // namespace pqg

@@ -1,0 +1,764 @@
+// pqg_kernels.hip — CDNA4 (gfx950) kernels for the parquet-rs page-decode hot path.
+//
+//   k_prepare        page layout: level streams + value section per page
+//                    (column/reader.rs:269-380, levels.rs:191-233)
+//   k_rle_levels     RLE/bit-packing hybrid -> i16 def/rep levels + non-null count
+//                    (rle.rs:398-434, levels.rs:249-271, column/reader.rs:212-226)
+//   k_scan_values    dense value offsets per page (column/reader.rs:252-253)
+//   k_dict_gather    RLE_DICTIONARY indices -> dictionary gather (rle.rs:437-487,
+//                    decoding.rs:256-315)
+//   k_plain_copy     PLAIN fixed-width values (decoding.rs:138-186, 228-247)
+//   k_plain_bool     PLAIN booleans (decoding.rs:188-204)
+//   k_finalize       chunk status
+//
+// All work is integer/byte movement bound by HBM: no MFMA. Run discovery for the RLE hybrid
+// is a wave-level walk: every lane of the walking wave parses a speculative run header at
+// its own byte of a 64-byte window (one LDS read each), then the wave hops along the real
+// header chain with v_readlane (registers only) and records runs in an LDS run table.
+// All four waves then expand the table with 8 outputs per lane and coalesced 16-byte stores.
+#include "pqg_device.hpp"
+
+namespace pqg {
+
+// ------------------------------------------------------------------------------ prepare
+
+__device__ inline uint32_t rd_u32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ inline int type_size(int t, int tl) {
+  switch (t) {
+    case T_BOOLEAN: return 1;
+    case T_INT32: return 4;
+    case T_INT64: return 8;
+    case T_INT96: return 12;
+    case T_FLOAT: return 4;
+    case T_DOUBLE: return 8;
+    case T_FLBA: return tl;
+    default: return 0;
+  }
+}
+
+// One v1 level stream (levels.rs:191-211). `start` is the BufferPtr start of the slice
+// within the page; returns bytes consumed or -1 (panic).
+__device__ inline int64_t v1_level_stream(const uint8_t* page, uint32_t nbytes, uint32_t start,
+                                          int enc, int bw, uint32_t nvals, uint32_t& off,
+                                          uint32_t& len, uint8_t& kind) {
+  uint32_t slice_len = nbytes - start;
+  if (enc == E_RLE) {
+    if (slice_len < 4) return -1;
+    int32_t sz = (int32_t)rd_u32(page + start);
+    if (sz < 0 || 4ull + (uint64_t)(uint32_t)sz > slice_len) return -1;
+    off = start + 4;
+    len = (uint32_t)sz;
+    kind = LK_RLE;
+    return 4 + (int64_t)sz;
+  }
+  if (enc == E_BIT_PACKED) {
+    uint64_t num_bytes = ((uint64_t)nvals * (uint64_t)bw + 7) / 8;
+    uint32_t data_size = (uint32_t)(num_bytes < slice_len ? num_bytes : slice_len);
+    // data.range(data.start(), data_size): the start is applied twice
+    if ((uint64_t)start + data_size > slice_len) return -1;
+    off = start + start;
+    len = data_size;
+    kind = LK_BIT_PACKED;
+    return data_size;
+  }
+  return -1;  // LevelDecoder::v1 panics on other encodings (levels.rs:170)
+}
+
+__global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                          PageWork* __restrict__ pages, int npages, ColumnParams cp,
+                          ChunkResult* res) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npages) return;
+  PageWork pw = pages[p];
+  const int32_t host_status = pw.status;  // set by the host for pages the reference rejects
+  pw.rep_kind = pw.def_kind = LK_NONE;
+  pw.rep_off = pw.rep_bytes = pw.def_off = pw.def_bytes = 0;
+  pw.nonnull = 0;
+  pw.nbytes_out = 0;
+  int32_t err = 0;
+  if (host_status) {
+    pages[p].nonnull = 0;
+    return;
+  }
+  if (pw.base + pw.nbytes > blob_len || pw.nbytes > 0x7FFFFFF0u) err = ST_INVALID_ARG;
+  const uint8_t* page = blob + pw.base;
+  if (!err && pw.page_type == P_DATA) {
+    uint32_t start = 0;
+    if (cp.max_rep > 0) {
+      int64_t tb = v1_level_stream(page, pw.nbytes, start, pw.rep_encoding, cp.rep_bit_width,
+                                   pw.num_values, pw.rep_off, pw.rep_bytes, pw.rep_kind);
+      if (tb < 0) err = ST_PANIC;
+      else start += (uint32_t)tb;
+    }
+    if (!err && cp.max_def > 0) {
+      int64_t tb = v1_level_stream(page, pw.nbytes, start, pw.def_encoding, cp.def_bit_width,
+                                   pw.num_values, pw.def_off, pw.def_bytes, pw.def_kind);
+      if (tb < 0) err = ST_PANIC;
+      else start += (uint32_t)tb;
+    }
+    pw.val_off = start;
+    pw.val_bytes = pw.nbytes - start;
+  } else if (!err && pw.page_type == P_DATA_V2) {
+    uint32_t off = 0;
+    if (cp.max_rep > 0) {  // set_data_range(rep_levels_byte_len), column/reader.rs:341-351
+      if ((uint64_t)pw.rep_len > pw.nbytes) err = ST_PANIC;
+      pw.rep_off = 0;
+      pw.rep_bytes = pw.rep_len;
+      pw.rep_kind = LK_RLE;
+      off += pw.rep_len;
+    }
+    if (!err && cp.max_def > 0) {
+      if ((uint64_t)off + pw.def_len > pw.nbytes) err = ST_PANIC;
+      pw.def_off = off;
+      pw.def_bytes = pw.def_len;
+      pw.def_kind = LK_RLE;
+      off += pw.def_len;
+    }
+    if (!err && off > pw.nbytes) err = ST_PANIC;
+    pw.val_off = off;
+    pw.val_bytes = err ? 0 : pw.nbytes - off;
+  } else if (!err && pw.page_type == P_DICTIONARY) {
+    pw.val_off = 0;
+    pw.val_bytes = pw.nbytes;
+  }
+  // Values each page must yield: def == max_def count when levels are read (filled by
+  // k_rle_levels), else the page's level count (column/reader.rs:212-226).
+  bool data = pw.page_type == P_DATA || pw.page_type == P_DATA_V2;
+  if (data && !(cp.max_def > 0 && cp.want_def)) pw.nonnull = pw.num_values;
+  pw.status = err;
+  pages[p] = pw;
+  if (err) atomicMin(&res->first_bad_page, p);
+}
+
+// ------------------------------------------------------------------------------ RLE hybrid
+
+constexpr int BLK = 4096;                 // bytes of stream walked per LDS region
+constexpr int REGION = BLK + 128;         // + look-ahead for headers straddling the edge
+constexpr int REGION_WORDS = REGION / 4 + 4;
+constexpr int RUNCAP = 2048;              // runs per expansion batch
+
+constexpr uint32_t F_BP = 1u, F_EOF = 2u, F_PANIC = 4u;
+constexpr uint32_t RLE_FLAG = 0x80000000u;
+
+struct HybridSmem {
+  uint32_t region[REGION_WORDS];
+  uint32_t start[RUNCAP + 1];
+  uint32_t info[RUNCAP];
+  uint32_t ctl[8];
+  uint64_t red[4];
+};
+
+// Stage [A0, A0 + REGION) of the blob into LDS (all threads).
+__device__ inline void load_region(const uint8_t* blob, uint64_t blob_len, uint64_t A0,
+                                   uint32_t* region) {
+  for (int c = threadIdx.x; c < REGION / 16; c += WG) {
+    uint64_t a = A0 + (uint64_t)c * 16;
+    uint4 v;
+    if (a + 16 <= blob_len) {
+      v = *reinterpret_cast<const uint4*>(blob + a);
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = gbyte(blob, blob_len, a + 4 * k) | (gbyte(blob, blob_len, a + 4 * k + 1) << 8) |
+               (gbyte(blob, blob_len, a + 4 * k + 2) << 16) |
+               (gbyte(blob, blob_len, a + 4 * k + 3) << 24);
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    reinterpret_cast<uint4*>(region)[c] = v;
+  }
+  if (threadIdx.x < 4) region[REGION / 4 + threadIdx.x] = 0;
+}
+
+// Speculative run header at stream position q (rle.rs:490-508): varint indicator, then
+// either a bit-packed run of (ind>>1)*8 values or an RLE run of (ind>>1) copies of a
+// ceil(w/8)-byte little-endian value.
+__device__ inline void parse_header(const uint32_t* region, uint32_t ridx, uint32_t q,
+                                    uint32_t slen, int w, uint32_t& nxt, uint32_t& cnt,
+                                    uint32_t& inf, uint32_t& flg) {
+  uint64_t ind = 0;
+  int vlen = 0;
+  bool complete = false;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    if (!complete && (q + (uint32_t)k) < slen && vlen == k) {
+      uint32_t b = lbyte(region, ridx + k);
+      ind |= (uint64_t)(b & 0x7Fu) << (7 * k);
+      vlen = k + 1;
+      if (!(b & 0x80u)) complete = true;
+    }
+  }
+  nxt = 0xFFFFFFFFu;
+  cnt = 0;
+  inf = 0;
+  if (!complete) {
+    // 10 continuation bytes with an 11th available: get_vlq_int's assert panics
+    flg = (vlen == 10 && q + 10 < slen) ? F_PANIC : F_EOF;
+    return;
+  }
+  uint32_t p = q + (uint32_t)vlen;
+  if (ind & 1) {
+    cnt = (uint32_t)((uint64_t)((int64_t)ind >> 1) * 8ull);  // ((ind >> 1) * 8) as u32
+    inf = p;
+    uint64_t nx = (uint64_t)p + (((uint64_t)cnt * (uint64_t)w) >> 3);
+    nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+    flg = F_BP;
+  } else {
+    cnt = (uint32_t)((int64_t)ind >> 1);
+    uint32_t vb = ((uint32_t)w + 7u) >> 3;
+    if (vb > 8 || (uint64_t)p + vb > slen) {  // assert!(current_value.is_some())
+      flg = F_PANIC;
+      return;
+    }
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < vb; ++k) v |= (uint64_t)lbyte(region, ridx + (uint32_t)vlen + k) << (8 * k);
+    inf = v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v;
+    nxt = p + vb;
+    flg = 0;
+  }
+}
+
+// Decodes `n` values of one RLE/bit-packed hybrid stream [S, S+slen) (absolute blob
+// offsets) with one 256-thread workgroup and calls emit(g, vals, mask) for groups of 8
+// consecutive outputs (g = out_base + index, g % 8 == 0). Returns 0 or a status code.
+// `kind` LK_BIT_PACKED decodes a header-less bit-packed stream (levels.rs:203-209).
+template <class Emit>
+__device__ int32_t hybrid_decode(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                 uint64_t S, uint32_t slen, int w, uint32_t n, int kind,
+                                 uint64_t out_base, HybridSmem& sm, Emit& emit) {
+  const uint32_t lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  uint32_t cur = 0, produced = 0;
+  int32_t err = 0;
+  bool done = (n == 0);
+  uint64_t A0 = S & ~15ull;
+  uint64_t wmask = (w >= 32) ? 0xFFFFFFFFull : ((1ull << w) - 1ull);
+
+  if (kind == LK_BIT_PACKED) {
+    if (n > 0) {
+      if ((uint64_t)n * (uint64_t)w > (uint64_t)slen * 8ull) return ST_EOF;
+      if (w > 32) return ST_PANIC;
+    }
+    if (threadIdx.x == 0) {
+      sm.start[0] = 0;
+      sm.info[0] = 0;
+      sm.start[1] = n;
+    }
+  }
+  if (done) return 0;
+  if (threadIdx.x == 0) sm.ctl[5] = 0;
+  load_region(blob, blob_len, A0, sm.region);
+  __syncthreads();
+
+  while (true) {
+    const uint32_t seg_start = produced;
+    uint32_t nruns = 1;
+    if (kind == LK_BIT_PACKED) {
+      produced = n;
+      done = true;
+    } else {
+      if (wave == 0) {
+        // ---------------- walk: registers + v_readlane only, one wave
+        uint32_t v_nxt = 0, v_cnt = 0, v_inf = 0, v_flg = 0;
+        bool have_win = false;
+        uint32_t wbase = 0;
+        nruns = 0;
+        while (true) {
+          if (produced >= n) {
+            done = true;
+            break;
+          }
+          uint64_t rel = S + cur - A0;
+          if (rel >= BLK) break;
+          if (nruns >= RUNCAP) break;
+          if (cur >= slen) {
+            err = ST_EOF;  // reload() finds no more data: reference stalls (A.4)
+            break;
+          }
+          if (!have_win || cur - wbase >= 64u) {
+            wbase = cur;
+            have_win = true;
+            uint32_t q = wbase + lane;
+            uint32_t ridx = (uint32_t)(S + q - A0);
+            if (ridx + 24 < REGION) {
+              parse_header(sm.region, ridx, q, slen, w, v_nxt, v_cnt, v_inf, v_flg);
+            } else {
+              v_flg = F_EOF;  // never reached by a chain that starts inside the block
+            }
+          }
+          const int l = (int)(cur - wbase);
+          const uint32_t nxt = readlane_u(v_nxt, l);
+          const uint32_t cnt = readlane_u(v_cnt, l);
+          const uint32_t inf = readlane_u(v_inf, l);
+          const uint32_t flg = readlane_u(v_flg, l);
+          if (flg & (F_EOF | F_PANIC)) {
+            err = (flg & F_PANIC) ? ST_PANIC : ST_EOF;
+            break;
+          }
+          if (cnt) {
+            uint32_t left = n - produced;
+            uint32_t need = cnt < left ? cnt : left;
+            if (flg & F_BP) {
+              if (w > 32) {  // BitReader::get_batch asserts num_bits <= 32
+                err = ST_PANIC;
+                break;
+              }
+              if ((uint64_t)inf * 8ull + (uint64_t)need * (uint64_t)w > (uint64_t)slen * 8ull) {
+                err = ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
+                break;
+              }
+            }
+            if (lane == 0) {
+              sm.start[nruns] = produced;
+              sm.info[nruns] = (flg & F_BP) ? inf : (RLE_FLAG | inf);
+            }
+            nruns++;
+            produced += need;
+          }
+          cur = nxt;
+        }
+        if (lane == 0) {
+          sm.start[nruns] = produced;
+          sm.ctl[0] = cur;
+          sm.ctl[1] = produced;
+          sm.ctl[2] = nruns;
+          sm.ctl[3] = (uint32_t)err;
+          sm.ctl[4] = done ? 1u : 0u;
+        }
+      }
+      __syncthreads();
+      cur = sm.ctl[0];
+      produced = sm.ctl[1];
+      nruns = sm.ctl[2];
+      err = (int32_t)sm.ctl[3];
+      done = sm.ctl[4] != 0;
+    }
+    if (err) return err;
+
+    // ---------------- expand [seg_start, produced): 8 outputs per thread per step
+    const uint64_t gb = out_base + seg_start, ge = out_base + produced;
+    for (uint64_t g = (gb & ~7ull) + 8ull * threadIdx.x; g < ge; g += 8ull * WG) {
+      uint32_t o0 = (uint32_t)((g < gb ? gb : g) - out_base);
+      int lo = 0, hi = (int)nruns - 1;
+      while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (sm.start[mid] <= o0) lo = mid;
+        else hi = mid - 1;
+      }
+      int r = lo;
+      uint32_t vals[8];
+      uint32_t mask = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        vals[j] = 0;
+        uint64_t gj = g + (uint64_t)j;
+        if (gj < gb || gj >= ge) continue;
+        uint32_t o = (uint32_t)(gj - out_base);
+        while (o >= sm.start[r + 1]) ++r;
+        uint32_t inf = sm.info[r];
+        if (inf & RLE_FLAG) {
+          vals[j] = inf & 0x7FFFFFFFu;
+        } else {
+          uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - sm.start[r]) * (uint64_t)w;
+          uint64_t abs = S + (bit >> 3);
+          uint64_t x;
+          uint64_t ri = abs - A0;
+          if (abs >= A0 && ri + 12 <= (uint64_t)REGION) x = lload_u64(sm.region, (uint32_t)ri);
+          else x = gload_u64(blob, blob_len, abs);
+          vals[j] = (uint32_t)((x >> (bit & 7)) & wmask);
+        }
+        mask |= 1u << j;
+      }
+      emit(g, vals, mask);
+    }
+    if (emit.err) sm.ctl[5] = (uint32_t)emit.err;
+    __syncthreads();  // run table / region reuse; publishes emit errors
+    if (sm.ctl[5]) return (int32_t)sm.ctl[5];
+    if (done) return 0;
+    if (S + cur - A0 >= BLK) {
+      A0 = (S + cur) & ~15ull;
+      load_region(blob, blob_len, A0, sm.region);
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ levels
+
+struct LevelEmit {
+  int16_t* out;
+  int16_t max_level;
+  bool count;
+  uint64_t nonnull;
+  int32_t err;
+  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
+    if (count) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((mask >> j) & 1) nonnull += ((int16_t)v[j] == max_level) ? 1 : 0;
+    }
+    if (mask == 0xFFu) {
+      uint4 pk;
+      pk.x = (v[0] & 0xFFFFu) | (v[1] << 16);
+      pk.y = (v[2] & 0xFFFFu) | (v[3] << 16);
+      pk.z = (v[4] & 0xFFFFu) | (v[5] << 16);
+      pk.w = (v[6] & 0xFFFFu) | (v[7] << 16);
+      *reinterpret_cast<uint4*>(out + g) = pk;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((mask >> j) & 1) out[g + j] = (int16_t)v[j];
+    }
+  }
+};
+
+// which: 0 = definition levels, 1 = repetition levels. One workgroup per page.
+__global__ void __launch_bounds__(WG) k_rle_levels(const uint8_t* __restrict__ blob,
+                                                   uint64_t blob_len, PageWork* pages,
+                                                   ColumnParams cp, int which,
+                                                   int16_t* __restrict__ out,
+                                                   ChunkResult* res) {
+  __shared__ HybridSmem sm;
+  const int p = blockIdx.x;
+  PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  uint32_t off = which ? pw.rep_off : pw.def_off;
+  uint32_t len = which ? pw.rep_bytes : pw.def_bytes;
+  int kind = which ? pw.rep_kind : pw.def_kind;
+  int w = which ? cp.rep_bit_width : cp.def_bit_width;
+  if (kind == LK_NONE) return;
+  LevelEmit em{out, which ? cp.max_rep : cp.max_def, which == 0, 0, 0};
+  int32_t st = hybrid_decode(blob, blob_len, pw.base + off, len, w, pw.num_values, kind,
+                             pw.level_out, sm, em);
+  if (st) {
+    if (threadIdx.x == 0) report(pages, res, p, st);
+    return;
+  }
+  if (which == 0) {
+    uint64_t t = block_sum_u64(em.nonnull, sm.red);
+    if (threadIdx.x == 0) pages[p].nonnull = t;
+  }
+}
+
+// ------------------------------------------------------------------------------ scan
+
+// Exclusive scan of per-page value counts -> value_out (single workgroup).
+__global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages,
+                                                    ChunkResult* res, int es,
+                                                    uint64_t cap_bytes) {
+  __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint64_t carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < npages; base += WG) {
+    int p = base + threadIdx.x;
+    uint64_t x = 0;
+    if (p < npages) {
+      int t = pages[p].page_type;
+      if (t == P_DATA || t == P_DATA_V2) x = pages[p].nonnull;
+    }
+    // inclusive wave scan
+    uint64_t s = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      uint64_t y = __shfl_up(s, off, 64);
+      if ((threadIdx.x & 63) >= (unsigned)off) s += y;
+    }
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    uint64_t pre = carry_s;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
+    if (p < npages) {
+      pages[p].value_out = pre + s - x;
+      if (es > 0 && x > 0 && (pre + s) * (uint64_t)es > cap_bytes && pages[p].status == 0)
+        report(pages, res, p, ST_CAPACITY);
+    }
+    __syncthreads();
+    if (threadIdx.x == WG - 1) carry_s = pre + s;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) res->total_values = carry_s;
+}
+
+// ------------------------------------------------------------------------------ dictionary
+
+template <int ES>
+struct DictEmit {
+  const uint8_t* dict;  // PLAIN dictionary page payload
+  uint32_t dict_len;
+  bool aligned;
+  uint8_t* out;
+  int32_t err;
+  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!((mask >> j) & 1)) continue;
+      uint32_t idx = v[j];
+      if (idx >= dict_len) {  // dict[idx] out of bounds: the reference panics
+        err = ST_PANIC;
+        continue;
+      }
+      uint8_t* d = out + (g + (uint64_t)j) * ES;
+      const uint8_t* s = dict + (uint64_t)idx * ES;
+      if (ES == 4 && aligned) {
+        *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
+      } else if (ES == 8 && aligned) {
+        *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(s);
+      } else {
+        for (int k = 0; k < ES; ++k) d[k] = s[k];
+      }
+    }
+  }
+};
+
+template <int ES>
+__global__ void __launch_bounds__(WG) k_dict_gather(const uint8_t* __restrict__ blob,
+                                                    uint64_t blob_len, PageWork* pages,
+                                                    int dict_page, uint8_t* __restrict__ out,
+                                                    ChunkResult* res) {
+  __shared__ HybridSmem sm;
+  const int p = blockIdx.x;
+  PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_RLE_DICTIONARY && pw.encoding != E_PLAIN_DICTIONARY) return;
+  if (dict_page < 0) {
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);  // "Decoder for dict should have been set"
+    return;
+  }
+  const PageWork dp = pages[dict_page];
+  if (dp.status != 0) return;
+  uint64_t n = pw.nonnull;
+  if (n == 0) return;
+  if (pw.val_bytes < 1) {  // data.as_ref()[0]
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  const int w = blob[pw.base + pw.val_off];
+  DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
+  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 1, pw.val_bytes - 1, w,
+                             (uint32_t)n, LK_RLE, pw.value_out, sm, em);
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
+}
+
+// Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
+__global__ void k_dict_check(PageWork* pages, int dict_page, int es, ChunkResult* res) {
+  if (threadIdx.x != 0 || dict_page < 0) return;
+  PageWork dp = pages[dict_page];
+  if (dp.status) return;
+  if (dp.encoding != E_PLAIN && dp.encoding != E_PLAIN_DICTIONARY) {
+    report(pages, res, dict_page, ST_NYI);
+    return;
+  }
+  if ((uint64_t)dp.num_values * (uint64_t)es > dp.nbytes) report(pages, res, dict_page, ST_EOF);
+}
+
+// ------------------------------------------------------------------------------ PLAIN
+
+// Copies each page's `nonnull * es` value bytes to out + value_out * es. grid.y = page,
+// grid.x strides 16-byte output chunks. Source alignment is arbitrary (the value section
+// follows the level streams): dword loads + v_alignbyte; the destination is chunked on
+// 16-byte boundaries of the output so stores are dwordx4 except at page edges.
+__global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ blob,
+                                                   uint64_t blob_len, PageWork* pages, int es,
+                                                   int enc_filter, uint8_t* __restrict__ out,
+                                                   ChunkResult* res) {
+  const int p = blockIdx.y;
+  const PageWork& pwr = pages[p];
+  if (pwr.status != 0) return;
+  if (pwr.page_type != P_DATA && pwr.page_type != P_DATA_V2) return;
+  if (pwr.encoding != enc_filter) return;
+  const uint64_t nbytes = pwr.nonnull * (uint64_t)es;
+  if (nbytes > pwr.val_bytes) {  // eof_err!("Not enough bytes to decode")
+    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, res, p, ST_EOF);
+    return;
+  }
+  const uint64_t src = pwr.base + pwr.val_off;
+  const uint64_t dst = pwr.value_out * (uint64_t)es;
+  const uint64_t dend = dst + nbytes;
+  const uint64_t c0 = dst & ~15ull;
+  for (uint64_t c = c0 + ((uint64_t)blockIdx.x * WG + threadIdx.x) * 16ull; c < dend;
+       c += (uint64_t)gridDim.x * WG * 16ull) {
+    const uint64_t lo = c < dst ? dst : c;
+    const uint64_t hi = (c + 16 < dend) ? c + 16 : dend;
+    if (lo == c && hi == c + 16) {
+      const uint64_t s = src + (c - dst);
+      const uint64_t sal = s & ~3ull;
+      const uint32_t sh = (uint32_t)(s - sal);
+      uint32_t w[5];
+      if (sal + 20 <= blob_len) {
+        const uint32_t* sp = reinterpret_cast<const uint32_t*>(blob + sal);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) w[k] = __builtin_nontemporal_load(sp + k);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+          w[k] = gbyte(blob, blob_len, sal + 4 * k) | (gbyte(blob, blob_len, sal + 4 * k + 1) << 8) |
+                 (gbyte(blob, blob_len, sal + 4 * k + 2) << 16) |
+                 (gbyte(blob, blob_len, sal + 4 * k + 3) << 24);
+      }
+      uint4 v;
+      v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+      v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+      v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+      *reinterpret_cast<uint4*>(out + c) = v;
+    } else {
+      for (uint64_t b = lo; b < hi; ++b) out[b] = blob[src + (b - dst)];
+    }
+  }
+}
+
+// PLAIN booleans: LSB-first bits from the value section, one byte (0/1) per value.
+__global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ blob,
+                                                   PageWork* pages, uint8_t* __restrict__ out,
+                                                   ChunkResult* res) {
+  const int p = blockIdx.y;
+  const PageWork& pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_PLAIN) return;
+  const uint64_t n = pw.nonnull;
+  if ((n + 7) / 8 > pw.val_bytes && n > (uint64_t)pw.val_bytes * 8) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, res, p, ST_EOF);
+    return;
+  }
+  const uint8_t* src = blob + pw.base + pw.val_off;
+  for (uint64_t k = (uint64_t)blockIdx.x * WG + threadIdx.x; k * 8 < n;
+       k += (uint64_t)gridDim.x * WG) {
+    uint32_t byte = src[k];
+    for (int j = 0; j < 8; ++j) {
+      uint64_t i = k * 8 + j;
+      if (i < n) out[pw.value_out + i] = (byte >> j) & 1u;
+    }
+  }
+}
+
+// RLE-encoded booleans of data page v2 (RleValueDecoder<Bool>, decoding.rs:323-384):
+// [i32 length][RLE hybrid, bit width 1].
+struct BoolEmit {
+  uint8_t* out;
+  int32_t err;
+  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
+    if (mask == 0xFFu) {
+      uint2 pk;
+      pk.x = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
+      pk.y = (v[4] & 0xFF) | ((v[5] & 0xFF) << 8) | ((v[6] & 0xFF) << 16) | ((v[7] & 0xFF) << 24);
+      *reinterpret_cast<uint2*>(out + g) = pk;
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if ((mask >> j) & 1) out[g + j] = (uint8_t)v[j];
+    }
+  }
+};
+
+__global__ void __launch_bounds__(WG) k_rle_bool(const uint8_t* __restrict__ blob,
+                                                 uint64_t blob_len, PageWork* pages,
+                                                 uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ HybridSmem sm;
+  const int p = blockIdx.x;
+  PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_RLE) return;
+  const uint8_t* vp = blob + pw.base + pw.val_off;
+  if (pw.val_bytes < 4) {
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  int32_t sz = (int32_t)rd_u32(vp);
+  if (sz < 0 || 4ull + (uint64_t)(uint32_t)sz > pw.val_bytes) {  // data.range(4, size) assert
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  BoolEmit em{out, 0};
+  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 4, (uint32_t)sz, 1,
+                             (uint32_t)pw.nonnull, LK_RLE, pw.value_out, sm, em);
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
+}
+
+// ------------------------------------------------------------------------------ finalize
+
+__global__ void k_finalize(PageWork* pages, ChunkResult* res) {
+  if (threadIdx.x != 0) return;
+  int b = res->first_bad_page;
+  res->status = (b != 0x7FFFFFFF) ? pages[b].status : 0;
+}
+
+// ------------------------------------------------------------------------------ launchers
+
+extern "C" {
+
+hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                              int npages, ColumnParams cp, ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_prepare, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, blob_len,
+                     pages, npages, cp, res);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                             int npages, ColumnParams cp, int which, int16_t* out,
+                             ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_rle_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp,
+                     which, out, res);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es,
+                           uint64_t cap_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_values, dim3(1), dim3(WG), 0, s, pages, npages, res, es, cap_bytes);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                           int dict_page, int es, uint8_t* out, ChunkResult* res,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
+  switch (es) {
+    case 1: hipLaunchKernelGGL(k_dict_gather<1>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL(k_dict_gather<4>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
+    case 8: hipLaunchKernelGGL(k_dict_gather<8>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
+    case 12: hipLaunchKernelGGL(k_dict_gather<12>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_plain_copy(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                                 int npages, int es, int enc, uint64_t max_page_bytes,
+                                 uint8_t* out, ChunkResult* res, hipStream_t s) {
+  uint64_t chunks = (max_page_bytes + 16 * WG - 1) / (16 * WG) + 1;
+  if (chunks > 4096) chunks = 4096;
+  hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)chunks, npages), dim3(WG), 0, s, blob,
+                     blob_len, pages, es, enc, out, res);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npages,
+                                 uint64_t max_page_values, uint8_t* out, ChunkResult* res,
+                                 hipStream_t s) {
+  uint64_t chunks = (max_page_values + 8 * WG - 1) / (8 * WG) + 1;
+  if (chunks > 4096) chunks = 4096;
+  hipLaunchKernelGGL(k_plain_bool, dim3((unsigned)chunks, npages), dim3(WG), 0, s, blob, pages,
+                     out, res);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                               int npages, uint8_t* out, ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_rle_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, out, res);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_finalize(PageWork* pages, ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, pages, res);
+  return hipGetLastError();
+}
+
+}  // extern "C"
+
+}  // namespace pqg

@@ -1,0 +1,393 @@
+// chunk_decoder.cpp — pqg_ctx / pqg_decode_chunk / pqg_sync: the host half of the C ABI.
+//
+// Replaces ColumnReaderImpl's decode driving (column/reader.rs:159-488) for a whole chunk:
+// validates the page sequence the way read_new_page / set_current_page_encoding /
+// configure_dictionary would (column/reader.rs:269-488, decoding.rs:60-79), uploads the page
+// table, and enqueues the kernels of device/*.hip on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../../include/pqgpu.h"
+#include "../pqg_internal.hpp"
+
+using namespace pqg;
+
+extern "C" {
+hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams,
+                              ChunkResult*, hipStream_t);
+hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int,
+                             int16_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
+                           hipStream_t);
+hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, int, int, uint8_t*,
+                           ChunkResult*, hipStream_t);
+hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
+                                 uint8_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
+                                 ChunkResult*, hipStream_t);
+hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint8_t*, ChunkResult*,
+                               hipStream_t);
+hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
+                            ChunkResult*, hipStream_t);
+hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
+}
+
+struct pqg_ctx {
+  int device = 0;
+  PageWork* d_pages = nullptr;
+  size_t pages_cap = 0;
+  PageWork* h_pages = nullptr;  // pinned staging
+  ChunkResult* d_res = nullptr;
+  ChunkResult* h_res = nullptr;  // pinned
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  bool timing = false;
+  bool pending = false;
+  int host_status = 0;
+  int host_bad_page = -1;
+  uint32_t values_kernel = 0;
+  pqg_output* out = nullptr;
+  uint64_t total_levels = 0;
+  std::string msg;
+};
+
+static int set_err(pqg_ctx* c, int st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  c->msg = buf;
+  return st;
+}
+
+static int hip_fail(pqg_ctx* c, hipError_t e, const char* what) {
+  return set_err(c, PQG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIPCHK(expr, what)                      \
+  do {                                          \
+    hipError_t _e = (expr);                     \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, what); \
+  } while (0)
+
+static int log2_ceil(uint64_t x) {  // bit_util.rs:91-104
+  if (x == 1) return 0;
+  x -= 1;
+  int r = 0;
+  while (x) {
+    x >>= 1;
+    r++;
+  }
+  return r;
+}
+
+static int value_size(int t, int tl) {
+  switch (t) {
+    case PQG_BOOLEAN: return 1;
+    case PQG_INT32: case PQG_FLOAT: return 4;
+    case PQG_INT64: case PQG_DOUBLE: return 8;
+    case PQG_INT96: return 12;
+    case PQG_FIXED_LEN_BYTE_ARRAY: return tl;
+    default: return 0;
+  }
+}
+
+extern "C" {
+
+int pqg_ctx_create(int device, pqg_ctx** out) {
+  if (!out) return PQG_ERR_INVALID;
+  *out = nullptr;
+  pqg_ctx* ctx = new pqg_ctx();
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete ctx;
+    return PQG_ERR_HIP;
+  }
+  if (hipMalloc(&ctx->d_res, sizeof(ChunkResult)) != hipSuccess ||
+      hipHostMalloc(&ctx->h_res, sizeof(ChunkResult), hipHostMallocDefault) != hipSuccess) {
+    delete ctx;
+    return PQG_ERR_HIP;
+  }
+  for (auto& ev : ctx->ev) hipEventCreate(&ev);
+  *out = ctx;
+  return PQG_OK;
+}
+
+int pqg_ctx_destroy(pqg_ctx* ctx) {
+  if (!ctx) return PQG_OK;
+  hipSetDevice(ctx->device);
+  if (ctx->pending) hipDeviceSynchronize();
+  hipFree(ctx->d_pages);
+  hipHostFree(ctx->h_pages);
+  hipFree(ctx->d_res);
+  hipHostFree(ctx->h_res);
+  for (auto& ev : ctx->ev) hipEventDestroy(ev);
+  delete ctx;
+  return PQG_OK;
+}
+
+int pqg_ctx_set_timing(pqg_ctx* ctx, int enabled) {
+  if (!ctx) return PQG_ERR_INVALID;
+  ctx->timing = enabled != 0;
+  return PQG_OK;
+}
+
+const char* pqg_error_message(pqg_ctx* ctx) { return ctx ? ctx->msg.c_str() : "null ctx"; }
+
+// Host-side checks that read_new_page / set_current_page_encoding / configure_dictionary /
+// get_decoder would make before touching page bytes. Returns the status of the first page
+// they reject (or 0) and writes that page's index.
+static int validate_pages(const pqg_column* col, const pqg_page* pages, uint32_t n, int* bad,
+                          int* dict_page, std::string& why) {
+  *dict_page = -1;
+  const int t = col->physical_type;
+  for (uint32_t i = 0; i < n; ++i) {
+    const pqg_page& p = pages[i];
+    *bad = (int)i;
+    if (p.page_type == PQG_PAGE_DICTIONARY) {
+      if (*dict_page >= 0) {
+        why = "Column cannot have more than one dictionary";
+        return PQG_ERR_GENERAL;  // column/reader.rs:469-471
+      }
+      if (p.encoding != PQG_PLAIN && p.encoding != PQG_PLAIN_DICTIONARY) {
+        why = "Invalid/Unsupported encoding type for dictionary";
+        return PQG_ERR_NYI;  // column/reader.rs:483-486
+      }
+      if (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) {
+        why = "BYTE_ARRAY/FLBA dictionaries are not implemented on the GPU path yet";
+        return PQG_ERR_NYI;
+      }
+      *dict_page = (int)i;
+      continue;
+    }
+    if (p.page_type != PQG_PAGE_DATA && p.page_type != PQG_PAGE_DATA_V2) continue;
+    int enc = p.encoding;
+    if (enc == PQG_PLAIN_DICTIONARY) enc = PQG_RLE_DICTIONARY;
+    switch (enc) {
+      case PQG_RLE_DICTIONARY:
+        if (*dict_page < 0) {
+          why = "Decoder for dict should have been set";
+          return PQG_ERR_PANIC;  // column/reader.rs:396-399
+        }
+        break;
+      case PQG_PLAIN:
+        if (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) {
+          why = "PLAIN BYTE_ARRAY/FLBA is not implemented on the GPU path yet";
+          return PQG_ERR_NYI;
+        }
+        break;
+      case PQG_RLE:
+        if (t != PQG_BOOLEAN) {
+          why = "RleValueDecoder only supports BoolType";
+          return PQG_ERR_PANIC;  // decoding.rs:355-357
+        }
+        break;
+      case PQG_DELTA_BINARY_PACKED:
+        if (t != PQG_INT32 && t != PQG_INT64) {
+          why = "DeltaBitPackDecoder only supports Int32Type and Int64Type";
+          return PQG_ERR_PANIC;
+        }
+        break;
+      case PQG_DELTA_LENGTH_BYTE_ARRAY:
+        if (t != PQG_BYTE_ARRAY) {
+          why = "DeltaLengthByteArrayDecoder only support ByteArrayType";
+          return PQG_ERR_GENERAL;
+        }
+        why = "DELTA_LENGTH_BYTE_ARRAY is not implemented on the GPU path yet";
+        return PQG_ERR_NYI;
+      case PQG_DELTA_BYTE_ARRAY:
+        if (t != PQG_BYTE_ARRAY && t != PQG_FIXED_LEN_BYTE_ARRAY) {
+          why = "DeltaByteArrayDecoder only supports ByteArrayType and FixedLenByteArrayType";
+          return PQG_ERR_GENERAL;
+        }
+        why = "DELTA_BYTE_ARRAY is not implemented on the GPU path yet";
+        return PQG_ERR_NYI;
+      default:
+        why = "Encoding is not supported";
+        return PQG_ERR_NYI;  // get_decoder, decoding.rs:76
+    }
+  }
+  *bad = -1;
+  return PQG_OK;
+}
+
+int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, uint64_t blob_len,
+                     const pqg_page* pages, uint32_t npages, pqg_output* out, void* stream_v) {
+  if (!ctx || !col || !out || (npages && !pages)) return PQG_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream_v;
+  HIPCHK(hipSetDevice(ctx->device), "hipSetDevice");
+  ctx->msg.clear();
+  ctx->host_status = 0;
+  ctx->host_bad_page = -1;
+  ctx->out = out;
+  ctx->stream = s;
+  out->num_levels = out->num_values = out->num_bytes = 0;
+  auto misaligned = [](const void* p) { return p && ((uintptr_t)p & 15u); };
+  if (misaligned(out->def_levels) || misaligned(out->rep_levels) || misaligned(out->values))
+    return set_err(ctx, PQG_ERR_INVALID, "output buffers must be 16-byte aligned");
+  const int t = col->physical_type;
+  if (t < 0 || t > 7) return set_err(ctx, PQG_ERR_INVALID, "bad physical type %d", t);
+  if (t == PQG_FIXED_LEN_BYTE_ARRAY && col->type_length <= 0)
+    return set_err(ctx, PQG_ERR_PANIC, "FLBA requires type_length > 0");
+
+  // ---- page table
+  if (npages > ctx->pages_cap) {
+    size_t cap = npages < 1024 ? 1024 : npages;
+    hipFree(ctx->d_pages);
+    hipHostFree(ctx->h_pages);
+    ctx->d_pages = nullptr;
+    ctx->h_pages = nullptr;
+    HIPCHK(hipMalloc(&ctx->d_pages, cap * sizeof(PageWork)), "hipMalloc pages");
+    HIPCHK(hipHostMalloc(&ctx->h_pages, cap * sizeof(PageWork), hipHostMallocDefault), "hipHostMalloc");
+    ctx->pages_cap = cap;
+  }
+  int bad = -1, dict_page = -1;
+  std::string why;
+  int vst = validate_pages(col, pages, npages, &bad, &dict_page, why);
+  uint64_t level_out = 0, max_page_bytes = 0, max_page_vals = 0;
+  bool enc_present[16] = {};
+  for (uint32_t i = 0; i < npages; ++i) {
+    PageWork& w = ctx->h_pages[i];
+    memset(&w, 0, sizeof(w));
+    w.base = pages[i].offset;
+    w.nbytes = pages[i].nbytes;
+    w.num_values = pages[i].num_values;
+    w.page_type = pages[i].page_type;
+    w.encoding = pages[i].encoding;
+    if (w.page_type != PQG_PAGE_DICTIONARY && w.encoding == PQG_PLAIN_DICTIONARY)
+      w.encoding = PQG_RLE_DICTIONARY;  // column/reader.rs:391-393
+    w.def_encoding = pages[i].def_encoding;
+    w.rep_encoding = pages[i].rep_encoding;
+    w.def_len = pages[i].def_len;
+    w.rep_len = pages[i].rep_len;
+    w.level_out = level_out;
+    if (w.page_type == PQG_PAGE_DATA || w.page_type == PQG_PAGE_DATA_V2) {
+      level_out += w.num_values;
+      if (w.encoding >= 0 && w.encoding < 16) enc_present[w.encoding] = true;
+      if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
+      if (w.num_values > max_page_vals) max_page_vals = w.num_values;
+    }
+    if (vst && (int)i == bad) w.status = vst;
+    if (vst && (int)i > bad) w.status = -1;  // never reached by the reference
+  }
+  if (vst) {
+    ctx->host_status = vst;
+    ctx->host_bad_page = bad;
+    ctx->msg = why;
+  }
+  const bool want_def = col->max_def > 0 && out->def_levels;
+  const bool want_rep = col->max_rep > 0 && out->rep_levels;
+  const uint64_t lev_needed = level_out;
+  // read_batch reports levels only for the streams it reads (column/reader.rs:259)
+  ctx->total_levels = (want_def || want_rep) ? lev_needed : 0;
+
+  ColumnParams cp{};
+  cp.physical_type = t;
+  cp.type_length = col->type_length;
+  cp.max_def = col->max_def;
+  cp.max_rep = col->max_rep;
+  cp.def_bit_width = log2_ceil((uint64_t)(int64_t)col->max_def + 1);
+  cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
+  cp.want_def = want_def;
+  cp.want_rep = want_rep;
+
+  ChunkResult r0{};
+  r0.total_levels = ctx->total_levels;
+  r0.first_bad_page = 0x7FFFFFFF;
+  r0.dict_page = dict_page < 0 ? 0xFFFFFFFFu : (uint32_t)dict_page;
+  *ctx->h_res = r0;
+  if (npages) HIPCHK(hipMemcpyAsync(ctx->d_pages, ctx->h_pages, npages * sizeof(PageWork), hipMemcpyHostToDevice, s), "H2D pages");
+  HIPCHK(hipMemcpyAsync(ctx->d_res, ctx->h_res, sizeof(ChunkResult), hipMemcpyHostToDevice, s), "H2D res");
+
+  const int es = value_size(t, col->type_length);
+  const int np = (int)npages;
+  if (ctx->timing) hipEventRecord(ctx->ev[0], s);
+  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, ctx->d_res, s), "prepare");
+  if (ctx->timing) hipEventRecord(ctx->ev[1], s);
+  if (np && want_def) HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, cp, 0, out->def_levels, ctx->d_res, s), "def levels");
+  if (np && want_rep) HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, cp, 1, out->rep_levels, ctx->d_res, s), "rep levels");
+  if (ctx->timing) hipEventRecord(ctx->ev[2], s);
+  HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
+  if (ctx->timing) hipEventRecord(ctx->ev[3], s);
+  uint8_t* vo = (uint8_t*)out->values;
+  ctx->values_kernel = 0;
+  if (np && vo) {
+    if (enc_present[PQG_PLAIN]) {
+      ctx->values_kernel = PQG_PLAIN;
+      if (t == PQG_BOOLEAN)
+        HIPCHK(pqg_launch_plain_bool(blob, ctx->d_pages, np, max_page_vals, vo, ctx->d_res, s), "plain bool");
+      else if (es > 0)
+        HIPCHK(pqg_launch_plain_copy(blob, blob_len, ctx->d_pages, np, es, PQG_PLAIN, max_page_bytes, vo, ctx->d_res, s), "plain");
+    }
+    if (enc_present[PQG_RLE_DICTIONARY]) {
+      ctx->values_kernel = PQG_RLE_DICTIONARY;
+      HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, dict_page, es, vo, ctx->d_res, s), "dict");
+    }
+    if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
+      ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
+      HIPCHK(pqg_launch_delta(blob, blob_len, ctx->d_pages, np, es, vo, ctx->d_res, s), "delta");
+    }
+    if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
+      ctx->values_kernel = PQG_RLE;
+      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, vo, ctx->d_res, s), "rle bool");
+    }
+  }
+  if (ctx->timing) hipEventRecord(ctx->ev[4], s);
+  HIPCHK(pqg_launch_finalize(ctx->d_pages, ctx->d_res, s), "finalize");
+  HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(ChunkResult), hipMemcpyDeviceToHost, s), "D2H res");
+  HIPCHK(hipEventRecord(ctx->ev[5], s), "event");
+  ctx->pending = true;
+  return PQG_OK;
+}
+
+int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
+  if (!ctx) return PQG_ERR_INVALID;
+  if (first_bad_page) *first_bad_page = -1;
+  if (!ctx->pending) return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
+  hipError_t e = hipEventSynchronize(ctx->ev[5]);
+  ctx->pending = false;
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+  const ChunkResult& r = *ctx->h_res;
+  pqg_output* out = ctx->out;
+  out->num_levels = ctx->total_levels;
+  out->num_values = r.total_values;
+  out->num_bytes = r.total_bytes;
+  int st = 0, page = -1;
+  if (r.first_bad_page != 0x7FFFFFFF) {
+    page = r.first_bad_page;
+    st = r.status;
+  }
+  if (ctx->host_status && (page < 0 || ctx->host_bad_page <= page)) {
+    page = ctx->host_bad_page;
+    st = ctx->host_status;
+  } else if (st) {
+    static const char* names[] = {"OK", "General", "NYI", "EOF", "panic", "hang", "capacity", "invalid", "hip"};
+    set_err(ctx, st, "page %d: %s (reference: %s)", page, st < 9 ? names[st] : "?",
+            st == PQG_ERR_PANIC ? "panics" : st == PQG_ERR_HANG ? "loops forever" : "returns Err");
+  }
+  if (first_bad_page) *first_bad_page = page;
+  return st;
+}
+
+int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
+  if (!ctx || !t) return PQG_ERR_INVALID;
+  memset(t, 0, sizeof(*t));
+  if (!ctx->timing) return PQG_ERR_INVALID;
+  hipEventElapsedTime(&t->prepare_ms, ctx->ev[0], ctx->ev[1]);
+  hipEventElapsedTime(&t->levels_ms, ctx->ev[1], ctx->ev[2]);
+  hipEventElapsedTime(&t->scan_ms, ctx->ev[2], ctx->ev[3]);
+  hipEventElapsedTime(&t->values_ms, ctx->ev[3], ctx->ev[4]);
+  hipEventElapsedTime(&t->total_ms, ctx->ev[0], ctx->ev[5]);
+  t->values_kernel = ctx->values_kernel;
+  return PQG_OK;
+}
+
+}  // extern "C"

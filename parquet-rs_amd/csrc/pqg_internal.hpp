@@ -1,0 +1,85 @@
+// pqg_internal.hpp — structures shared by the host driver (chunk_decoder.cpp) and the
+// CDNA4 kernels (device/*.hip). Not part of the public C ABI (include/pqgpu.h).
+#pragma once
+#include <stdint.h>
+
+namespace pqg {
+
+// Status codes: ParquetError kinds (src/errors.rs:24-51) plus the two outcomes the reference
+// reaches on malformed input (a panic, an endless loop). Mirrors include/pqgpu.h.
+enum Status : int32_t {
+  ST_OK = 0,
+  ST_GENERAL = 1,
+  ST_NYI = 2,
+  ST_EOF = 3,
+  ST_PANIC = 4,  // reference would panic (assert!/bounds)
+  ST_HANG = 5,   // reference would loop forever (rle.rs:414-425, column/reader.rs:182-262)
+  ST_CAPACITY = 6,
+  ST_INVALID_ARG = 7,
+  ST_HIP = 8,
+};
+
+enum PhysType : int32_t {
+  T_BOOLEAN = 0, T_INT32 = 1, T_INT64 = 2, T_INT96 = 3, T_FLOAT = 4, T_DOUBLE = 5,
+  T_BYTE_ARRAY = 6, T_FLBA = 7
+};
+
+enum Enc : int32_t {
+  E_PLAIN = 0, E_PLAIN_DICTIONARY = 2, E_RLE = 3, E_BIT_PACKED = 4, E_DELTA_BINARY_PACKED = 5,
+  E_DELTA_LENGTH_BYTE_ARRAY = 6, E_DELTA_BYTE_ARRAY = 7, E_RLE_DICTIONARY = 8
+};
+
+enum PageType : int32_t { P_DATA = 0, P_INDEX = 1, P_DICTIONARY = 2, P_DATA_V2 = 3 };
+
+enum LevelKind : uint8_t { LK_NONE = 0, LK_RLE = 1, LK_BIT_PACKED = 2 };
+
+// Per-page working record in device memory. The host fills the first block from the page
+// headers; the prepare kernel fills the stream layout; later kernels fill counts.
+struct PageWork {
+  // ---- host-filled
+  uint64_t base;        // byte offset of the uncompressed payload inside the chunk blob
+  uint32_t nbytes;      // payload length
+  uint32_t num_values;  // header num_values (levels for data pages, entries for dict pages)
+  uint64_t level_out;   // index of this page's first level in the level outputs
+  int32_t page_type;
+  int32_t encoding;
+  int32_t def_encoding;
+  int32_t rep_encoding;
+  uint32_t def_len;     // v2
+  uint32_t rep_len;     // v2
+  // ---- prepare kernel
+  uint32_t rep_off, rep_bytes;  // level streams, relative to base
+  uint32_t def_off, def_bytes;
+  uint32_t val_off, val_bytes;  // value section
+  uint8_t rep_kind, def_kind, value_kind, pad0;
+  int32_t status;
+  // ---- levels kernel / scan
+  uint64_t nonnull;     // values this page must yield (def == max_def count, or num_values)
+  uint64_t value_out;   // index of this page's first value in the value output
+  uint64_t byte_out;    // BYTE_ARRAY/FLBA: first byte of this page's values in the byte output
+  uint64_t nbytes_out;  // BYTE_ARRAY/FLBA: bytes this page produces
+};
+
+// Chunk-level result, copied to pinned host memory at the end of a decode.
+struct ChunkResult {
+  uint64_t total_levels;
+  uint64_t total_values;
+  uint64_t total_bytes;
+  int32_t first_bad_page;  // INT32_MAX when clean
+  int32_t status;
+  uint32_t dict_page;      // index of the dictionary page or UINT32_MAX
+  uint32_t pad;
+};
+
+struct ColumnParams {
+  int32_t physical_type;
+  int32_t type_length;
+  int16_t max_def;
+  int16_t max_rep;
+  int32_t def_bit_width;
+  int32_t rep_bit_width;
+  int32_t want_def;  // def_levels output provided (read_batch(Some(def)))
+  int32_t want_rep;
+};
+
+}  // namespace pqg

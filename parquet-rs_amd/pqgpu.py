@@ -1,0 +1,227 @@
+"""Python binding of the MI355X decode library (lib/libpqgpu.so) over its C ABI.
+
+This mirrors the reference's column-reader interface for the decode path (column/reader.rs,
+encodings/decoding.rs): a Column descriptor, a list of uncompressed Pages, and decode results
+of (def levels, rep levels, dense values). PyTorch provides device memory and streams only.
+
+The library must be built (`make -C parquet-rs_amd`); loading fails loudly otherwise. There
+is no CPU fallback on this path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpqgpu.so")
+
+OK, GENERAL, NYI, EOF, PANIC, HANG, CAPACITY, INVALID, HIP = range(9)
+STATUS_NAMES = ["OK", "General", "NYI", "EOF", "Panic", "Hang", "Capacity", "Invalid", "HIP"]
+BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
+PLAIN, PLAIN_DICTIONARY, RLE, BIT_PACKED = 0, 2, 3, 4
+DELTA_BINARY_PACKED, DELTA_LENGTH_BYTE_ARRAY, DELTA_BYTE_ARRAY, RLE_DICTIONARY = 5, 6, 7, 8
+PAGE_DATA, PAGE_DICTIONARY, PAGE_DATA_V2 = 0, 2, 3
+VALUE_SIZE = {BOOLEAN: 1, INT32: 4, INT64: 8, INT96: 12, FLOAT: 4, DOUBLE: 8}
+NP_DTYPE = {BOOLEAN: np.uint8, INT32: np.int32, INT64: np.int64, FLOAT: np.float32,
+            DOUBLE: np.float64}
+
+
+class PqgError(RuntimeError):
+    def __init__(self, status, message, page=-1):
+        super().__init__(f"{STATUS_NAMES[status] if 0 <= status < 9 else status}: {message}"
+                         + (f" (page {page})" if page >= 0 else ""))
+        self.status, self.page = status, page
+
+
+class Page(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("nbytes", C.c_uint32), ("num_values", C.c_uint32),
+                ("page_type", C.c_int32), ("encoding", C.c_int32), ("def_encoding", C.c_int32),
+                ("rep_encoding", C.c_int32), ("def_len", C.c_uint32), ("rep_len", C.c_uint32)]
+
+
+class Column(C.Structure):
+    _fields_ = [("physical_type", C.c_int32), ("type_length", C.c_int32),
+                ("max_def", C.c_int16), ("max_rep", C.c_int16)]
+
+
+class Output(C.Structure):
+    _fields_ = [("def_levels", C.c_void_p), ("rep_levels", C.c_void_p), ("values", C.c_void_p),
+                ("values_capacity", C.c_uint64), ("offsets", C.c_void_p),
+                ("offsets_capacity", C.c_uint64), ("num_levels", C.c_uint64),
+                ("num_values", C.c_uint64), ("num_bytes", C.c_uint64)]
+
+
+class Timings(C.Structure):
+    _fields_ = [("prepare_ms", C.c_float), ("levels_ms", C.c_float), ("scan_ms", C.c_float),
+                ("values_ms", C.c_float), ("total_ms", C.c_float), ("values_kernel", C.c_uint32)]
+
+
+class WorkloadInfo(C.Structure):
+    _fields_ = [("blob_len", C.c_uint64), ("npages", C.c_uint32), ("total_levels", C.c_uint64),
+                ("total_values", C.c_uint64)]
+
+
+EXPORTS = [
+    "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_sync",
+    "pqg_get_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
+    "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
+    "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
+    "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
+    "pqg_column_reader_read_batch", "pqg_encode_rle", "pqg_encode_levels_v1", "pqg_encode_delta",
+    "pqg_encode_dict_indices", "pqg_gen_levels_plain", "pqg_gen_dict_int64",
+    "pqg_gen_delta_int64",
+]
+
+_lib = None
+
+
+def lib():
+    """Load lib/libpqgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {_HERE}`")
+        L = C.CDLL(LIB_PATH)
+        vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
+        L.pqg_ctx_create.argtypes = [i32, C.POINTER(vp)]
+        L.pqg_ctx_destroy.argtypes = [vp]
+        L.pqg_ctx_set_timing.argtypes = [vp, i32]
+        L.pqg_decode_chunk.argtypes = [vp, C.POINTER(Column), vp, u64, C.POINTER(Page), C.c_uint32,
+                                       C.POINTER(Output), vp]
+        L.pqg_sync.argtypes = [vp, C.POINTER(C.c_int)]
+        L.pqg_get_timings.argtypes = [vp, C.POINTER(Timings)]
+        L.pqg_error_message.argtypes = [vp]
+        L.pqg_error_message.restype = C.c_char_p
+        if not hasattr(L, "pqg_gen_levels_plain"):
+            _lib = L
+            return L
+        for name in ("pqg_gen_levels_plain",):
+            getattr(L, name).argtypes = [u64, C.c_double, C.c_uint32, u64, i32, vp, u64,
+                                         C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
+        L.pqg_gen_dict_int64.argtypes = [u64, C.c_uint32, C.c_uint32, u64, i32, vp, u64,
+                                         C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
+        L.pqg_gen_delta_int64.argtypes = [u64, i32, C.c_uint32, i32, i32, u64, i32, vp, u64,
+                                          C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
+        L.pqg_encode_rle.restype = u64
+        L.pqg_encode_rle.argtypes = [vp, u64, i32, vp, u64]
+        L.pqg_encode_levels_v1.restype = u64
+        L.pqg_encode_levels_v1.argtypes = [vp, u64, C.c_int16, vp, u64]
+        L.pqg_encode_delta.restype = u64
+        L.pqg_encode_delta.argtypes = [i32, vp, u64, i32, i32, vp, u64]
+        L.pqg_encode_dict_indices.restype = u64
+        L.pqg_encode_dict_indices.argtypes = [vp, u64, i32, vp, u64]
+        _lib = L
+    return _lib
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Context:
+    """pqg_ctx: one per GPU (pqgpu.h)."""
+
+    def __init__(self, device=0, timing=False):
+        self.device = device
+        h = C.c_void_p()
+        st = lib().pqg_ctx_create(device, C.byref(h))
+        if st:
+            raise PqgError(st, "pqg_ctx_create failed")
+        self.h = h
+        if timing:
+            lib().pqg_ctx_set_timing(self.h, 1)
+
+    def close(self):
+        if self.h:
+            lib().pqg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error_message(self):
+        return lib().pqg_error_message(self.h).decode(errors="replace")
+
+    def decode_async(self, column, blob, blob_len, pages, out, stream=0, npages=None):
+        """Enqueue pqg_decode_chunk. `blob` is a device pointer (int), `pages` a ctypes Page
+        array, `out` an Output struct with device pointers."""
+        n = len(pages) if npages is None else npages
+        st = lib().pqg_decode_chunk(self.h, C.byref(column), C.c_void_p(blob), blob_len, pages,
+                                    n, C.byref(out), C.c_void_p(stream))
+        if st:
+            raise PqgError(st, self.error_message())
+
+    def sync(self):
+        bad = C.c_int(-1)
+        st = lib().pqg_sync(self.h, C.byref(bad))
+        return st, bad.value
+
+    def timings(self):
+        t = Timings()
+        lib().pqg_get_timings(self.h, C.byref(t))
+        return t
+
+
+def make_pages(specs):
+    """Pack page specs (objects with page_type, buf, num_values, encoding, def_encoding,
+    rep_encoding, def_len, rep_len) into a host blob with 64-byte aligned payloads."""
+    arr = (Page * max(len(specs), 1))()
+    parts, off = [], 0
+    for i, s in enumerate(specs):
+        pad = (-off) % 64
+        if pad:
+            parts.append(b"\0" * pad)
+            off += pad
+        arr[i] = Page(off, len(s.buf), s.num_values, s.page_type, s.encoding,
+                      getattr(s, "def_encoding", RLE), getattr(s, "rep_encoding", RLE),
+                      getattr(s, "def_len", 0), getattr(s, "rep_len", 0))
+        parts.append(bytes(s.buf))
+        off += len(s.buf)
+    blob = b"".join(parts) + b"\0" * 64
+    return blob, arr
+
+
+def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_def=True,
+                  want_rep=True, device=None, stream=None, values_capacity=None):
+    """Decode one column chunk on the GPU; returns a dict with numpy def/rep/values.
+
+    Equivalent to reading every batch of ColumnReaderImpl::read_batch (column/reader.rs
+    :159-265) and concatenating: def/rep levels are the full level streams, values the
+    dense non-null values."""
+    torch = _torch()
+    dev = device if device is not None else torch.device("cuda", ctx.device)
+    blob, pages = make_pages(specs)
+    d_blob = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    nlev = sum(s.num_values for s in specs if s.page_type in (PAGE_DATA, PAGE_DATA_V2))
+    es = VALUE_SIZE.get(ptype, max(type_length, 1))
+    cap_vals = values_capacity if values_capacity is not None else max(nlev, 1) * es
+    d_def = torch.empty(max(nlev, 1) + 8, dtype=torch.int16, device=dev) if (want_def and max_def > 0) else None
+    d_rep = torch.empty(max(nlev, 1) + 8, dtype=torch.int16, device=dev) if (want_rep and max_rep > 0) else None
+    d_val = torch.empty(cap_vals + 64, dtype=torch.uint8, device=dev)
+    out = Output(d_def.data_ptr() if d_def is not None else None,
+                 d_rep.data_ptr() if d_rep is not None else None,
+                 d_val.data_ptr(), cap_vals, None, 0, 0, 0, 0)
+    col = Column(ptype, type_length, max_def, max_rep)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    ctx.decode_async(col, d_blob.data_ptr(), len(blob), pages, out, s, npages=len(specs))
+    st, bad = ctx.sync()
+    res = {"status": st, "page": bad, "message": ctx.error_message() if st else "",
+           "num_levels": out.num_levels, "num_values": out.num_values}
+    nl, nv = out.num_levels, out.num_values
+    res["def"] = d_def[:nl].cpu().numpy() if (d_def is not None and not st) else np.zeros(0, np.int16)
+    res["rep"] = d_rep[:nl].cpu().numpy() if (d_rep is not None and not st) else np.zeros(0, np.int16)
+    if not st:
+        raw = d_val[: nv * es].cpu().numpy()
+        if ptype == INT96:
+            res["values"] = raw.reshape(-1, 12)
+        elif ptype in NP_DTYPE:
+            res["values"] = raw.view(NP_DTYPE[ptype])
+        else:
+            res["values"] = raw
+    else:
+        res["values"] = np.zeros(0, np.uint8)
+    return res
