@@ -1,0 +1,318 @@
+#!/usr/bin/env python3
+"""Device-resident Parquet page-decode benchmark (BASELINE.json metric) on MI355X.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config levels|dict|delta] [...]
+
+A step is one decode of the whole synthetic column (BASELINE.json configs[1..3], 1e9
+levels/values per GPU) through the C ABI (pqg_decode_chunk), with the page bytes already
+resident in HBM. For N > 1 the driver launches one rank per GPU via torch.distributed.run;
+every rank decodes its own partition (its own row groups, seed + rank): weak scaling, no
+collective on the data path. Rank 0 prints one JSON line.
+
+The reported roofline is for the dominant kernel, timed with HIP events on the decode stream
+over the timed steps; the CPU baseline is the C restatement of parquet-rs's decode loop
+(oracle/, kind "port") on a bounded sample, one decoder per thread.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="levels", choices=["levels", "dict", "delta"])
+    ap.add_argument("--n", type=float, default=1e9, help="levels/values per GPU")
+    ap.add_argument("--p-null", type=float, default=0.5)
+    ap.add_argument("--page-values", type=int, default=1 << 20)
+    ap.add_argument("--dict-size", type=int, default=65536)
+    ap.add_argument("--delta-bits", type=int, default=16)
+    ap.add_argument("--block-size", type=int, default=512)
+    ap.add_argument("--mini-blocks", type=int, default=4)
+    ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0 / 0.1 variants")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=0x5EED0000)
+    return ap.parse_args()
+
+
+class Workload:
+    """Synthetic pages generated on the host by the reference-identical writers of
+    libpqgpu.so (encoders.cpp) and uploaded once to HBM."""
+
+    def __init__(self, pqgpu, args, rank, kind, p_null=None):
+        import torch
+        L = pqgpu.lib()
+        info = pqgpu.WorkloadInfo()
+        n = int(args.n)
+        seed = args.seed + 2 + 1000003 * rank
+        self.kind = kind
+        self.p_null = p_null
+        if kind == "levels":
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_levels_plain(
+                n, p_null, args.page_values, seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+            self.col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
+            self.es = 4
+        elif kind == "dict":
+            seed = args.seed + 3 + 1000003 * rank
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64(
+                n, args.dict_size, args.page_values, seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+            self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
+            self.es = 8
+        else:
+            seed = args.seed + 4 + 1000003 * rank
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64(
+                n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, seed,
+                args.threads, blob, cap, pages, pcap, C.byref(info))
+            self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
+            self.es = 8
+        st = gen(None, 0, None, 0)
+        assert st == 0, st
+        cap, npg = info.blob_len, info.npages
+        self.host = np.zeros(cap + 64, dtype=np.uint8)
+        self.pages = (pqgpu.Page * npg)()
+        t0 = time.time()
+        st = gen(self.host.ctypes.data_as(C.c_void_p), cap, self.pages, npg)
+        assert st == 0, f"generator failed: {st}"
+        self.gen_s = time.time() - t0
+        self.npages = npg
+        self.levels = info.total_levels
+        self.values = info.total_values
+        self.in_bytes = sum(self.pages[i].nbytes for i in range(npg))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.d_blob = torch.from_numpy(self.host).to(dev)
+        self.blob_len = cap
+        nlev = self.levels
+        self.d_def = torch.empty(nlev + 64, dtype=torch.int16, device=dev) if self.col.max_def > 0 else None
+        self.d_val = torch.empty(self.values * self.es + 64, dtype=torch.uint8, device=dev)
+        self.out = pqgpu.Output(self.d_def.data_ptr() if self.d_def is not None else None, None,
+                                self.d_val.data_ptr(), self.values * self.es, None, 0, 0, 0, 0)
+        # algorithmic bytes per step: encoded page bytes in, decoded bytes out
+        self.level_bytes_in = 0
+        if kind == "levels":
+            for i in range(npg):
+                self.level_bytes_in += int.from_bytes(self.host[self.pages[i].offset:self.pages[i].offset + 4].tobytes(), "little") + 4
+        self.out_bytes = (2 * nlev if self.col.max_def > 0 else 0) + self.values * self.es
+
+    def page_specs(self, count):
+        """First `count` pages as oracle page specs (CPU baseline leg only)."""
+        import pyoracle
+        specs = []
+        for i in range(count):
+            p = self.pages[i]
+            buf = self.host[p.offset:p.offset + p.nbytes].tobytes()
+            specs.append(pyoracle.PageSpec(p.page_type, buf, p.num_values, p.encoding, p.def_encoding,
+                                           p.rep_encoding, p.def_len, p.rep_len))
+        return specs
+
+
+def decode_once(pqgpu, ctx, w, stream):
+    ctx.decode_async(w.col, w.d_blob.data_ptr(), w.blob_len, w.pages, w.out, stream, npages=w.npages)
+
+
+def spot_check(pqgpu, ctx, w, stream):
+    """Sanity check before timing (parity itself is established by tests/ against the
+    oracle): the decode succeeds, yields exactly the generator's value count, and for
+    config 2 the number of def levels equal to max_def matches the value count."""
+    import torch
+    decode_once(pqgpu, ctx, w, stream)
+    st, bad = ctx.sync()
+    assert st == 0, (st, bad, ctx.error_message())
+    assert w.out.num_values == w.values, (w.out.num_values, w.values)
+    if w.d_def is not None:
+        nn = int((w.d_def[: w.levels] == 1).sum().item())
+        assert nn == w.values, (nn, w.values)
+    return True
+
+
+def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
+    import torch
+    for _ in range(warmup):
+        decode_once(pqgpu, ctx, w, stream)
+    ctx.sync()
+    pqgpu.lib().pqg_reset_timings(ctx.h)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        decode_once(pqgpu, ctx, w, stream)
+    st, bad = ctx.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    assert st == 0, (st, bad, ctx.error_message())
+    return (t1 - t0) / steps, ctx.timings()
+
+
+def cpu_baseline(w, seconds, threads):
+    """parquet-rs decode loop restated in C (oracle, kind "port"), one read_batch(1024)
+    column reader per thread over disjoint pages (the reference's Rc types are !Send, so
+    one reader per row group/thread is its only parallelism)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from concurrent.futures import ThreadPoolExecutor
+    first = 1 if w.kind == "dict" else 0
+    dict_spec = w.page_specs(1)[0] if w.kind == "dict" else None
+    # time one page to size the sample
+    sp = w.page_specs(first + 1)[first:]
+    t0 = time.perf_counter()
+    r = pyoracle.read_column(w.col.physical_type, ([dict_spec] if dict_spec else []) + sp,
+                             max_def=w.col.max_def, batch_size=1024)
+    one = time.perf_counter() - t0
+    assert r["status"] == 0
+    npg = max(threads, min(w.npages - first, int(seconds * threads / max(one, 1e-6))))
+    npg = min(npg, w.npages - first)
+    specs = w.page_specs(first + npg)[first:]
+    groups = [specs[i::threads] for i in range(threads)]
+
+    def run(g):
+        pages = ([dict_spec] if dict_spec else []) + g
+        rr = pyoracle.read_column(w.col.physical_type, pages, max_def=w.col.max_def, batch_size=1024)
+        assert rr["status"] == 0, rr["message"]
+        return sum(p.num_values for p in g)
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        n = sum(ex.map(run, groups))
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "values/s", "cores": threads, "kind": "port",
+            "sample": f"{npg} of {w.npages} pages ({n} levels/values), read_batch(1024) per "
+                      f"thread-owned reader, {dt:.1f}s wall"}
+
+
+def copy_ceiling_gbs(nbytes=4 << 30):
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as td
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = td
+    else:
+        torch.cuda.set_device(0)
+    import pqgpu
+    ctx = pqgpu.Context(torch.cuda.current_device(), timing=True)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    kind = args.config
+    w = Workload(pqgpu, args, rank, kind, p_null=args.p_null if kind == "levels" else None)
+    spot_check(pqgpu, ctx, w, stream)
+    per_step, tm = time_steps(pqgpu, ctx, w, stream, args.steps, args.warmup, dist)
+    # max over ranks
+    if dist is not None:
+        t = torch.tensor([per_step], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per_step = float(t.item())
+    units = w.levels if kind == "levels" else w.values
+    value = units * world / per_step
+    step_bytes = w.in_bytes + w.out_bytes
+
+    # dominant kernel roofline (HIP events around each stage on the decode stream)
+    if kind == "levels":
+        lev_b = w.level_bytes_in + 2 * w.levels
+        val_b = 2 * w.values * w.es
+        stages = [("k_rle_levels", tm.levels_ms, lev_b), ("k_plain_copy", tm.values_ms, val_b)]
+    elif kind == "dict":
+        stages = [("k_dict_gather<8>", tm.values_ms, w.in_bytes + w.out_bytes)]
+    else:
+        stages = [("k_delta<8>", tm.values_ms, w.in_bytes + w.out_bytes)]
+    name, ms, nbytes = max(stages, key=lambda s: s[1])
+    achieved = nbytes / (ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "decoded values/s + GB/s, device-resident page decode",
+        "value": value,
+        "unit": "values/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": per_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"levels": "i16 levels + i32 values", "dict": "u16 indices -> i64",
+                  "delta": "i64 (wrapping)"}[kind],
+        "data": "synthetic pages from reference-identical writers (SplitMix64 seeded)",
+        "gbps": step_bytes / per_step / 1e9 * world,
+        "config": {"workload": {"levels": "configs[1]: RLE/bit-packed def levels (max_def 1) + PLAIN INT32",
+                                "dict": "configs[2]: RLE_DICTIONARY INT64, 64K dictionary",
+                                "delta": "configs[3]: DELTA_BINARY_PACKED INT64"}[kind],
+                   "levels_per_gpu": w.levels, "values_per_gpu": w.values,
+                   "pages_per_gpu": w.npages, "page_values": args.page_values,
+                   "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes,
+                   "out_bytes_per_gpu": w.out_bytes,
+                   "block_size": args.block_size if kind == "delta" else None,
+                   "mini_blocks": args.mini_blocks if kind == "delta" else None,
+                   "parallelism": f"row-group partitions x{world}, no collective"},
+        "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": nbytes, "avg_ms": ms},
+        "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
+                      "values": tm.values_ms, "total": tm.total_ms},
+    }
+    if rank == 0:
+        try:
+            result["copy_ceiling_gbs"] = copy_ceiling_gbs()
+        except Exception as e:  # pragma: no cover
+            result["copy_ceiling_gbs"] = str(e)
+    if rank == 0 and args.cpu_baseline and world == 1:
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, min(args.threads, os.cpu_count() or 1))
+    if kind == "levels" and args.variants and world == 1:
+        var = {}
+        for p in (0.0, 0.1):
+            del w
+            torch.cuda.empty_cache()
+            wv = Workload(pqgpu, args, rank, "levels", p_null=p)
+            spot_check(pqgpu, ctx, wv, stream)
+            ps, tv = time_steps(pqgpu, ctx, wv, stream, max(3, args.steps // 2), 2)
+            var[f"p_null={p}"] = {"levels_per_s": wv.levels / ps, "ms_per_step": ps * 1e3,
+                                  "gbps": (wv.in_bytes + wv.out_bytes) / ps / 1e9,
+                                  "levels_ms": tv.levels_ms, "values_ms": tv.values_ms}
+            w = wv
+        result["variants"] = var
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -124,7 +124,7 @@ typedef struct {
 
 typedef struct pqg_ctx pqg_ctx;
 
-/* Per-stage device times of the last decode (ms), filled by pqg_sync when timing is on. */
+/* Per-stage device times (ms) measured with HIP events on the decode stream. */
 typedef struct {
   float prepare_ms, levels_ms, scan_ms, values_ms, total_ms;
   uint32_t values_kernel; /* encoding whose kernel dominated values_ms */
@@ -144,7 +144,9 @@ int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
 /* Wait for the last decode and report its status. On error *first_bad_page names the
  * lowest page index that failed (the page the reference would fail on first). */
 int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
+/* Averages over all decodes since pqg_reset_timings (timing must be enabled). */
 int pqg_get_timings(pqg_ctx *ctx, pqg_timings *t);
+int pqg_reset_timings(pqg_ctx *ctx);
 const char *pqg_error_message(pqg_ctx *ctx);
 
 /* ---------------------------------------------------------------- host-side reader

@@ -38,17 +38,32 @@ hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
 }
 
-struct pqg_ctx {
-  int device = 0;
+// Two staging slots so consecutive async decodes never overwrite pinned memory that an
+// in-flight H2D/D2H copy still reads (slot i is reused only after its last decode ended).
+struct Slot {
   PageWork* d_pages = nullptr;
   size_t pages_cap = 0;
   PageWork* h_pages = nullptr;  // pinned staging
   ChunkResult* d_res = nullptr;
   ChunkResult* h_res = nullptr;  // pinned
+  hipEvent_t ev[6] = {};
+  bool used = false;
+};
+
+struct pqg_ctx {
+  int device = 0;
+  Slot slot[2];
+  int cur = 0;          // slot of the last decode
+  PageWork* d_pages = nullptr;
+  PageWork* h_pages = nullptr;
+  ChunkResult* d_res = nullptr;
+  ChunkResult* h_res = nullptr;
+  hipEvent_t* ev = nullptr;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[8] = {};
   bool timing = false;
   bool pending = false;
+  double acc_ms[5] = {};
+  uint64_t acc_n = 0;
   int host_status = 0;
   int host_bad_page = -1;
   uint32_t values_kernel = 0;
@@ -111,12 +126,15 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     delete ctx;
     return PQG_ERR_HIP;
   }
-  if (hipMalloc(&ctx->d_res, sizeof(ChunkResult)) != hipSuccess ||
-      hipHostMalloc(&ctx->h_res, sizeof(ChunkResult), hipHostMallocDefault) != hipSuccess) {
-    delete ctx;
-    return PQG_ERR_HIP;
+  for (Slot& sl : ctx->slot) {
+    if (hipMalloc(&sl.d_res, sizeof(ChunkResult)) != hipSuccess ||
+        hipHostMalloc(&sl.h_res, sizeof(ChunkResult), hipHostMallocDefault) != hipSuccess) {
+      delete ctx;
+      return PQG_ERR_HIP;
+    }
+    for (auto& ev : sl.ev) hipEventCreate(&ev);
   }
-  for (auto& ev : ctx->ev) hipEventCreate(&ev);
+  ctx->cur = 1;
   *out = ctx;
   return PQG_OK;
 }
@@ -124,12 +142,14 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
 int pqg_ctx_destroy(pqg_ctx* ctx) {
   if (!ctx) return PQG_OK;
   hipSetDevice(ctx->device);
-  if (ctx->pending) hipDeviceSynchronize();
-  hipFree(ctx->d_pages);
-  hipHostFree(ctx->h_pages);
-  hipFree(ctx->d_res);
-  hipHostFree(ctx->h_res);
-  for (auto& ev : ctx->ev) hipEventDestroy(ev);
+  for (Slot& sl : ctx->slot) {
+    if (sl.used) hipEventSynchronize(sl.ev[5]);
+    hipFree(sl.d_pages);
+    hipHostFree(sl.h_pages);
+    hipFree(sl.d_res);
+    hipHostFree(sl.h_res);
+    for (auto& ev : sl.ev) hipEventDestroy(ev);
+  }
   delete ctx;
   return PQG_OK;
 }
@@ -238,17 +258,38 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (t == PQG_FIXED_LEN_BYTE_ARRAY && col->type_length <= 0)
     return set_err(ctx, PQG_ERR_PANIC, "FLBA requires type_length > 0");
 
-  // ---- page table
-  if (npages > ctx->pages_cap) {
-    size_t cap = npages < 1024 ? 1024 : npages;
-    hipFree(ctx->d_pages);
-    hipHostFree(ctx->h_pages);
-    ctx->d_pages = nullptr;
-    ctx->h_pages = nullptr;
-    HIPCHK(hipMalloc(&ctx->d_pages, cap * sizeof(PageWork)), "hipMalloc pages");
-    HIPCHK(hipHostMalloc(&ctx->h_pages, cap * sizeof(PageWork), hipHostMallocDefault), "hipHostMalloc");
-    ctx->pages_cap = cap;
+  // ---- staging slot: wait until its previous decode has finished, harvest its timings
+  ctx->cur ^= 1;
+  Slot& sl = ctx->slot[ctx->cur];
+  if (sl.used) {
+    HIPCHK(hipEventSynchronize(sl.ev[5]), "slot wait");
+    if (ctx->timing) {
+      float ms[5];
+      hipEventElapsedTime(&ms[0], sl.ev[0], sl.ev[1]);
+      hipEventElapsedTime(&ms[1], sl.ev[1], sl.ev[2]);
+      hipEventElapsedTime(&ms[2], sl.ev[2], sl.ev[3]);
+      hipEventElapsedTime(&ms[3], sl.ev[3], sl.ev[4]);
+      hipEventElapsedTime(&ms[4], sl.ev[0], sl.ev[5]);
+      for (int k = 0; k < 5; ++k) ctx->acc_ms[k] += ms[k];
+      ctx->acc_n++;
+    }
+    sl.used = false;
   }
+  if (npages > sl.pages_cap) {
+    size_t cap = npages < 1024 ? 1024 : npages;
+    hipFree(sl.d_pages);
+    hipHostFree(sl.h_pages);
+    sl.d_pages = nullptr;
+    sl.h_pages = nullptr;
+    HIPCHK(hipMalloc(&sl.d_pages, cap * sizeof(PageWork)), "hipMalloc pages");
+    HIPCHK(hipHostMalloc(&sl.h_pages, cap * sizeof(PageWork), hipHostMallocDefault), "hipHostMalloc");
+    sl.pages_cap = cap;
+  }
+  ctx->d_pages = sl.d_pages;
+  ctx->h_pages = sl.h_pages;
+  ctx->d_res = sl.d_res;
+  ctx->h_res = sl.h_res;
+  ctx->ev = sl.ev;
   int bad = -1, dict_page = -1;
   std::string why;
   int vst = validate_pages(col, pages, npages, &bad, &dict_page, why);
@@ -344,6 +385,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   HIPCHK(pqg_launch_finalize(ctx->d_pages, ctx->d_res, s), "finalize");
   HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(ChunkResult), hipMemcpyDeviceToHost, s), "D2H res");
   HIPCHK(hipEventRecord(ctx->ev[5], s), "event");
+  sl.used = true;
   ctx->pending = true;
   return PQG_OK;
 }
@@ -354,6 +396,17 @@ int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
   if (!ctx->pending) return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
   hipError_t e = hipEventSynchronize(ctx->ev[5]);
   ctx->pending = false;
+  if (ctx->timing && e == hipSuccess) {
+    float ms[5];
+    hipEventElapsedTime(&ms[0], ctx->ev[0], ctx->ev[1]);
+    hipEventElapsedTime(&ms[1], ctx->ev[1], ctx->ev[2]);
+    hipEventElapsedTime(&ms[2], ctx->ev[2], ctx->ev[3]);
+    hipEventElapsedTime(&ms[3], ctx->ev[3], ctx->ev[4]);
+    hipEventElapsedTime(&ms[4], ctx->ev[0], ctx->ev[5]);
+    for (int k = 0; k < 5; ++k) ctx->acc_ms[k] += ms[k];
+    ctx->acc_n++;
+    ctx->slot[ctx->cur].used = false;  // harvested
+  }
   if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
   const ChunkResult& r = *ctx->h_res;
   pqg_output* out = ctx->out;
@@ -377,16 +430,26 @@ int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
   return st;
 }
 
+// Average per-stage device time over every decode since the last reset (HIP events recorded
+// on the decode stream between the stages).
 int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
   if (!ctx || !t) return PQG_ERR_INVALID;
   memset(t, 0, sizeof(*t));
-  if (!ctx->timing) return PQG_ERR_INVALID;
-  hipEventElapsedTime(&t->prepare_ms, ctx->ev[0], ctx->ev[1]);
-  hipEventElapsedTime(&t->levels_ms, ctx->ev[1], ctx->ev[2]);
-  hipEventElapsedTime(&t->scan_ms, ctx->ev[2], ctx->ev[3]);
-  hipEventElapsedTime(&t->values_ms, ctx->ev[3], ctx->ev[4]);
-  hipEventElapsedTime(&t->total_ms, ctx->ev[0], ctx->ev[5]);
+  if (!ctx->timing || ctx->acc_n == 0) return PQG_ERR_INVALID;
+  double n = (double)ctx->acc_n;
+  t->prepare_ms = (float)(ctx->acc_ms[0] / n);
+  t->levels_ms = (float)(ctx->acc_ms[1] / n);
+  t->scan_ms = (float)(ctx->acc_ms[2] / n);
+  t->values_ms = (float)(ctx->acc_ms[3] / n);
+  t->total_ms = (float)(ctx->acc_ms[4] / n);
   t->values_kernel = ctx->values_kernel;
+  return PQG_OK;
+}
+
+int pqg_reset_timings(pqg_ctx* ctx) {
+  if (!ctx) return PQG_ERR_INVALID;
+  for (double& x : ctx->acc_ms) x = 0;
+  ctx->acc_n = 0;
   return PQG_OK;
 }
 

@@ -1,0 +1,436 @@
+// encoders.cpp — reference-identical page writers and the synthetic workload generators.
+//
+// The writers restate parquet-rs's encoders so the generated pages are byte-for-byte what
+// the reference would write:
+//   BitWriter            util/bit_util.rs:136-363
+//   RleEncoder           encodings/rle.rs:55-317 (runs <= 504 values, rle.rs:49-50)
+//   LevelEncoder::v1     encodings/levels.rs:54-143 (RLE, 4-byte length prefix)
+//   DictEncoder indices  encodings/encoding.rs:338-355 ([bit width][RLE hybrid])
+//   DeltaBitPackEncoder  encodings/encoding.rs:534-714 (block size / mini-block count are
+//                        parameters; the reference fixes 128 / 4, encoding.rs:508-509)
+// The generators build BASELINE.json configs 2-4 page by page on host threads (pages are
+// independent) for bench.py; see DESIGN.md §4.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "../../../include/pqgpu.h"
+
+namespace {
+
+int64_t ceil_div(int64_t v, int64_t d) { return v / d + (v % d != 0); }
+
+int log2_ceil(uint64_t x) {
+  if (x == 1) return 0;
+  x -= 1;
+  int r = 0;
+  while (x) {
+    x >>= 1;
+    r++;
+  }
+  return r;
+}
+
+size_t num_required_bits(uint64_t x) {
+  for (int i = 63; i >= 0; --i)
+    if (x & (1ULL << i)) return (size_t)i + 1;
+  return 0;
+}
+
+struct BitWriter {
+  uint8_t* buf;
+  size_t max_bytes;
+  uint64_t buffered = 0;
+  size_t byte_offset;
+  size_t bit_offset = 0;
+  bool ok = true;
+  BitWriter(uint8_t* b, size_t cap, size_t start) : buf(b), max_bytes(cap), byte_offset(start) {}
+  void flush() {
+    size_t nb = (size_t)ceil_div((int64_t)bit_offset, 8);
+    if (byte_offset + nb > max_bytes) {
+      ok = false;
+      return;
+    }
+    memcpy(buf + byte_offset, &buffered, nb);
+    buffered = 0;
+    bit_offset = 0;
+    byte_offset += nb;
+  }
+  long skip(size_t n) {
+    flush();
+    if (!ok || byte_offset + n > max_bytes) {
+      ok = false;
+      return -1;
+    }
+    long r = (long)byte_offset;
+    byte_offset += n;
+    return r;
+  }
+  void put_value(uint64_t v, size_t bits) {
+    if (byte_offset * 8 + bit_offset + bits > max_bytes * 8) {
+      ok = false;
+      return;
+    }
+    buffered |= v << bit_offset;
+    bit_offset += bits;
+    if (bit_offset >= 64) {
+      memcpy(buf + byte_offset, &buffered, 8);
+      byte_offset += 8;
+      bit_offset -= 64;
+      size_t sh = bits - bit_offset;
+      buffered = sh < 64 ? (v >> sh) : 0;
+    }
+  }
+  void put_aligned(uint64_t v, size_t nbytes) {
+    long off = skip(nbytes);
+    if (off >= 0) memcpy(buf + off, &v, nbytes);
+  }
+  void put_vlq(uint64_t v) {
+    while (v & 0xFFFFFFFFFFFFFF80ULL) {
+      put_aligned((v & 0x7F) | 0x80, 1);
+      v >>= 7;
+    }
+    put_aligned(v & 0x7F, 1);
+  }
+  void put_zigzag(int64_t v) { put_vlq(((uint64_t)v << 1) ^ (uint64_t)(v >> 63)); }
+};
+
+// RleEncoder, rle.rs:55-317
+struct RleEncoder {
+  int bit_width;
+  BitWriter bw;
+  uint64_t buffered_values[8];
+  size_t num_buffered = 0;
+  uint64_t current_value = 0;
+  size_t repeat_count = 0;
+  size_t bit_packed_count = 0;
+  long indicator_byte_pos = -1;
+  RleEncoder(int w, uint8_t* buf, size_t cap, size_t start) : bit_width(w), bw(buf, cap, start) {}
+
+  void flush_rle_run() {
+    bw.put_vlq((uint64_t)(repeat_count << 1));
+    bw.put_aligned(current_value, (size_t)ceil_div(bit_width, 8));
+    num_buffered = 0;
+    repeat_count = 0;
+  }
+  void flush_bit_packed_run(bool update) {
+    if (indicator_byte_pos < 0) indicator_byte_pos = bw.skip(1);
+    if (indicator_byte_pos < 0) return;
+    for (size_t i = 0; i < num_buffered; ++i) bw.put_value(buffered_values[i], (size_t)bit_width);
+    num_buffered = 0;
+    if (update) {
+      bw.buf[indicator_byte_pos] = (uint8_t)(((bit_packed_count / 8) << 1) | 1);
+      indicator_byte_pos = -1;
+      bit_packed_count = 0;
+    }
+  }
+  void flush_buffered_values() {
+    if (repeat_count >= 8) {
+      num_buffered = 0;
+      if (bit_packed_count > 0) flush_bit_packed_run(true);
+      return;
+    }
+    bit_packed_count += num_buffered;
+    size_t groups = bit_packed_count / 8;
+    flush_bit_packed_run(groups + 1 >= 64);  // MAX_GROUPS_PER_BIT_PACKED_RUN
+    repeat_count = 0;
+  }
+  inline void put(uint64_t v) {
+    if (current_value == v) {
+      repeat_count += 1;
+      if (repeat_count > 8) return;
+    } else {
+      if (repeat_count >= 8) flush_rle_run();
+      repeat_count = 1;
+      current_value = v;
+    }
+    buffered_values[num_buffered++] = v;
+    if (num_buffered == 8) flush_buffered_values();
+  }
+  void flush() {
+    if (bit_packed_count > 0 || repeat_count > 0 || num_buffered > 0) {
+      bool all_repeat = bit_packed_count == 0 && (repeat_count == num_buffered || num_buffered == 0);
+      if (repeat_count > 0 && all_repeat) {
+        flush_rle_run();
+      } else {
+        if (num_buffered > 0)
+          while (num_buffered < 8) buffered_values[num_buffered++] = 0;
+        bit_packed_count += num_buffered;
+        flush_bit_packed_run(true);
+        repeat_count = 0;
+      }
+    }
+  }
+  size_t consume() {
+    flush();
+    bw.flush();
+    return bw.ok ? bw.byte_offset : 0;
+  }
+};
+
+// RleEncoder::max_buffer_size + min_buffer_size (rle.rs:127-150)
+uint64_t rle_bound(int w, uint64_t n) {
+  uint64_t runs = (uint64_t)ceil_div((int64_t)n, 8);
+  uint64_t bp = runs + runs * (uint64_t)w;
+  uint64_t rl = runs * (1 + (uint64_t)ceil_div(w, 8));
+  uint64_t mx = std::max(bp, rl);
+  uint64_t minb = std::max<uint64_t>(1 + (uint64_t)ceil_div(504 * w, 8), 10 + (uint64_t)ceil_div(w, 8));
+  return mx + minb + 16;
+}
+
+// DeltaBitPackEncoder, encoding.rs:534-714, with block_size / mini_blocks parameters.
+template <class T>
+uint64_t delta_encode(const T* v, uint64_t n, int block_size, int nmb, uint8_t* out, uint64_t cap) {
+  const size_t mini = (size_t)block_size / (size_t)nmb;
+  if (mini % 8 != 0 || mini == 0) return 0;
+  uint8_t hdr[64];
+  BitWriter hw(hdr, sizeof(hdr), 0);
+  std::vector<uint8_t> tmp;  // header is written first; body follows it
+  // body writer directly into out at an offset reserved for the header (<= 40 bytes)
+  const size_t HR = 40;
+  if (cap < HR) return 0;
+  BitWriter w(out + HR, cap - HR, 0);
+  std::vector<int64_t> deltas((size_t)block_size);
+  size_t in_block = 0;
+  int64_t first = n ? (int64_t)v[0] : 0, cur = first;
+  auto sub = [](int64_t l, int64_t r) -> int64_t {
+    if (sizeof(T) == 4) return (int64_t)(int32_t)((uint32_t)(int32_t)l - (uint32_t)(int32_t)r);
+    return (int64_t)((uint64_t)l - (uint64_t)r);
+  };
+  auto sub_u64 = [](int64_t l, int64_t r) -> uint64_t {
+    if (sizeof(T) == 4) return (uint64_t)(uint32_t)((uint32_t)(int32_t)l - (uint32_t)(int32_t)r);
+    return (uint64_t)l - (uint64_t)r;
+  };
+  auto flush_block = [&]() {
+    if (in_block == 0) return;
+    int64_t min_delta = INT64_MAX;
+    for (size_t i = 0; i < in_block; ++i) min_delta = std::min(min_delta, deltas[i]);
+    w.put_zigzag(min_delta);
+    long wpos = w.skip((size_t)nmb);
+    if (wpos < 0) return;
+    for (int i = 0; i < nmb; ++i) {
+      size_t m = std::min(mini, in_block);
+      if (m == 0) break;
+      int64_t max_delta = INT64_MIN;
+      for (size_t j = 0; j < m; ++j) max_delta = std::max(max_delta, deltas[i * mini + j]);
+      size_t bwid = num_required_bits(sub_u64(max_delta, min_delta));
+      w.buf[wpos + i] = (uint8_t)bwid;
+      for (size_t j = 0; j < m; ++j) w.put_value(sub_u64(deltas[i * mini + j], min_delta), bwid);
+      for (size_t j = m; j < mini; ++j) w.put_value(0, bwid);
+      in_block -= m;
+    }
+  };
+  for (uint64_t idx = 1; idx < n; ++idx) {
+    int64_t x = (int64_t)v[idx];
+    deltas[in_block++] = sub(x, cur);
+    cur = x;
+    if (in_block == (size_t)block_size) flush_block();
+  }
+  flush_block();
+  hw.put_vlq((uint64_t)block_size);
+  hw.put_vlq((uint64_t)nmb);
+  hw.put_vlq(n);
+  hw.put_zigzag(first);
+  hw.flush();
+  w.flush();
+  if (!w.ok || !hw.ok) return 0;
+  size_t hl = hw.byte_offset;
+  memmove(out + hl, out + HR, w.byte_offset);
+  memcpy(out, hdr, hl);
+  return hl + w.byte_offset;
+}
+
+// SplitMix64: seeded, counter-based, identical in Python (bench.py) and here.
+inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+inline uint64_t page_seed(uint64_t seed, uint64_t page) {
+  uint64_t s = seed ^ (page * 0xD1B54A32D192ED03ULL);
+  return splitmix64(s);
+}
+
+template <class F>
+void parallel_pages(uint32_t npages, int threads, F&& f) {
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  threads = std::min<int>(threads, (int)std::max<uint32_t>(npages, 1));
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t]() {
+      for (uint32_t p = (uint32_t)t; p < npages; p += (uint32_t)threads) f(p);
+    });
+  for (auto& th : ts) th.join();
+}
+
+inline uint64_t align64(uint64_t x) { return (x + 63) & ~63ull; }
+
+}  // namespace
+
+extern "C" {
+
+uint64_t pqg_encode_rle(const uint64_t* values, uint64_t n, int bit_width, uint8_t* out, uint64_t cap) {
+  memset(out, 0, cap);
+  RleEncoder e(bit_width, out, cap, 0);
+  for (uint64_t i = 0; i < n; ++i) e.put(values[i]);
+  return e.consume();
+}
+
+uint64_t pqg_encode_levels_v1(const int16_t* levels, uint64_t n, int16_t max_level, uint8_t* out,
+                              uint64_t cap) {
+  if (cap < 4) return 0;
+  memset(out, 0, cap);
+  RleEncoder e(log2_ceil((uint64_t)(int64_t)max_level + 1), out, cap, 4);
+  for (uint64_t i = 0; i < n; ++i) e.put((uint64_t)(int64_t)levels[i]);
+  size_t end = e.consume();
+  if (!end) return 0;
+  int32_t len = (int32_t)(end - 4);
+  memcpy(out, &len, 4);
+  return end;
+}
+
+uint64_t pqg_encode_delta(int physical_type, const void* values, uint64_t n, int block_size,
+                          int mini_blocks, uint8_t* out, uint64_t cap) {
+  if (physical_type == PQG_INT32)
+    return delta_encode((const int32_t*)values, n, block_size, mini_blocks, out, cap);
+  if (physical_type == PQG_INT64)
+    return delta_encode((const int64_t*)values, n, block_size, mini_blocks, out, cap);
+  return 0;
+}
+
+uint64_t pqg_encode_dict_indices(const uint32_t* idx, uint64_t n, int bit_width, uint8_t* out,
+                                 uint64_t cap) {
+  if (cap < 1) return 0;
+  memset(out, 0, cap);
+  out[0] = (uint8_t)bit_width;
+  RleEncoder e(bit_width, out, cap, 1);
+  for (uint64_t i = 0; i < n; ++i) e.put(idx[i]);
+  return e.consume();
+}
+
+// ------------------------------------------------------------------ config 2
+int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
+                         int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                         uint32_t pages_cap, pqg_workload_info* info) {
+  if (!info || page_levels == 0) return PQG_ERR_INVALID;
+  const uint32_t np = (uint32_t)((n + page_levels - 1) / page_levels);
+  const uint64_t slot = align64(4 + rle_bound(1, page_levels) + 4ull * page_levels);
+  info->npages = np;
+  info->blob_len = slot * np;
+  info->total_levels = n;
+  info->total_values = 0;
+  if (!blob) return PQG_OK;
+  if (blob_cap < slot * np || pages_cap < np) return PQG_ERR_CAPACITY;
+  // a level is null with probability p_null: compare 53-bit uniforms against the threshold
+  const uint64_t thresh = (uint64_t)(p_null * 9007199254740992.0);
+  std::vector<uint64_t> nonnull(np);
+  parallel_pages(np, threads, [&](uint32_t p) {
+    const uint64_t cnt = std::min<uint64_t>(page_levels, n - (uint64_t)p * page_levels);
+    uint8_t* out = blob + (uint64_t)p * slot;
+    uint64_t s = page_seed(seed, p);
+    std::vector<int16_t> lv(cnt);
+    uint64_t nn = 0;
+    for (uint64_t i = 0; i < cnt; ++i) {
+      lv[i] = (splitmix64(s) >> 11) >= thresh ? 1 : 0;
+      nn += (uint64_t)lv[i];
+    }
+    uint64_t ll = pqg_encode_levels_v1(lv.data(), cnt, 1, out, slot - 4 * cnt);
+    int32_t* vals = reinterpret_cast<int32_t*>(out + ll);  // PLAIN INT32 (unaligned ok on x86)
+    for (uint64_t i = 0; i < nn; ++i) {
+      int32_t x = (int32_t)(uint32_t)splitmix64(s);
+      memcpy((uint8_t*)vals + 4 * i, &x, 4);
+    }
+    pqg_page& pg = pages[p];
+    pg.offset = (uint64_t)p * slot;
+    pg.nbytes = (uint32_t)(ll + 4 * nn);
+    pg.num_values = (uint32_t)cnt;
+    pg.page_type = PQG_PAGE_DATA;
+    pg.encoding = PQG_PLAIN;
+    pg.def_encoding = PQG_RLE;
+    pg.rep_encoding = PQG_BIT_PACKED;
+    pg.def_len = pg.rep_len = 0;
+    nonnull[p] = nn;
+  });
+  for (uint64_t x : nonnull) info->total_values += x;
+  return PQG_OK;
+}
+
+// ------------------------------------------------------------------ config 3
+int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                       int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                       uint32_t pages_cap, pqg_workload_info* info) {
+  if (!info || page_values == 0 || dict_size == 0) return PQG_ERR_INVALID;
+  const uint32_t ndata = (uint32_t)((n + page_values - 1) / page_values);
+  const int bw = dict_size == 1 ? 1 : log2_ceil(dict_size);  // encoding.rs:325-334
+  const uint64_t dslot = align64(8ull * dict_size);
+  const uint64_t slot = align64(1 + rle_bound(bw, page_values));
+  info->npages = ndata + 1;
+  info->blob_len = dslot + slot * ndata;
+  info->total_levels = n;
+  info->total_values = n;
+  if (!blob) return PQG_OK;
+  if (blob_cap < info->blob_len || pages_cap < ndata + 1) return PQG_ERR_CAPACITY;
+  // dictionary: distinct values (SplitMix64 of distinct counters is a bijection)
+  uint64_t ds = seed ^ 0xD1C7D1C7ull;
+  for (uint32_t i = 0; i < dict_size; ++i) {
+    uint64_t x = splitmix64(ds);
+    memcpy(blob + 8ull * i, &x, 8);
+  }
+  pages[0] = pqg_page{0, 8u * dict_size, dict_size, PQG_PAGE_DICTIONARY, PQG_PLAIN_DICTIONARY,
+                      PQG_RLE, PQG_RLE, 0, 0};
+  parallel_pages(ndata, threads, [&](uint32_t p) {
+    const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+    uint8_t* out = blob + dslot + (uint64_t)p * slot;
+    uint64_t s = page_seed(seed, p);
+    std::vector<uint32_t> idx(cnt);
+    for (uint64_t i = 0; i < cnt; ++i) idx[i] = (uint32_t)((splitmix64(s) >> 32) * dict_size >> 32);
+    uint64_t l = pqg_encode_dict_indices(idx.data(), cnt, bw, out, slot);
+    pages[p + 1] = pqg_page{dslot + (uint64_t)p * slot, (uint32_t)l, (uint32_t)cnt, PQG_PAGE_DATA,
+                            PQG_PLAIN_DICTIONARY, PQG_RLE, PQG_BIT_PACKED, 0, 0};
+  });
+  return PQG_OK;
+}
+
+// ------------------------------------------------------------------ config 4
+int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
+                        int mini_blocks, uint64_t seed, int threads, uint8_t* blob,
+                        uint64_t blob_cap, pqg_page* pages, uint32_t pages_cap,
+                        pqg_workload_info* info) {
+  if (!info || page_values == 0 || delta_bits < 1 || delta_bits > 63) return PQG_ERR_INVALID;
+  const uint32_t np = (uint32_t)((n + page_values - 1) / page_values);
+  const uint64_t blocks = (page_values + block_size - 1) / block_size + 1;
+  const uint64_t slot = align64(64 + 8ull * page_values + blocks * (10 + mini_blocks) + 8ull * block_size);
+  info->npages = np;
+  info->blob_len = slot * np;
+  info->total_levels = n;
+  info->total_values = n;
+  if (!blob) return PQG_OK;
+  if (blob_cap < info->blob_len || pages_cap < np) return PQG_ERR_CAPACITY;
+  int rc = PQG_OK;
+  parallel_pages(np, threads, [&](uint32_t p) {
+    const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+    uint64_t s = page_seed(seed, p);
+    std::vector<int64_t> v(cnt);
+    uint64_t acc = splitmix64(s);
+    const uint64_t span = 1ull << delta_bits;
+    const int64_t half = (int64_t)(span >> 1);
+    for (uint64_t i = 0; i < cnt; ++i) {
+      v[i] = (int64_t)acc;
+      int64_t d = (int64_t)((splitmix64(s) >> (64 - delta_bits))) - half;
+      acc += (uint64_t)d;  // wrapping prefix sum
+    }
+    uint8_t* out = blob + (uint64_t)p * slot;
+    uint64_t l = delta_encode(v.data(), cnt, block_size, mini_blocks, out, slot);
+    if (!l) rc = PQG_ERR_CAPACITY;
+    pages[p] = pqg_page{(uint64_t)p * slot, (uint32_t)l, (uint32_t)cnt, PQG_PAGE_DATA,
+                        PQG_DELTA_BINARY_PACKED, PQG_RLE, PQG_BIT_PACKED, 0, 0};
+  });
+  return rc;
+}
+
+}  // extern "C"

@@ -63,7 +63,7 @@ class WorkloadInfo(C.Structure):
 
 EXPORTS = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_sync",
-    "pqg_get_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
+    "pqg_get_timings", "pqg_reset_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
     "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
@@ -90,6 +90,7 @@ def lib():
                                        C.POINTER(Output), vp]
         L.pqg_sync.argtypes = [vp, C.POINTER(C.c_int)]
         L.pqg_get_timings.argtypes = [vp, C.POINTER(Timings)]
+        L.pqg_reset_timings.argtypes = [vp]
         L.pqg_error_message.argtypes = [vp]
         L.pqg_error_message.restype = C.c_char_p
         if not hasattr(L, "pqg_gen_levels_plain"):
