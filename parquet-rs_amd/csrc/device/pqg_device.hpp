@@ -23,27 +23,31 @@ __device__ inline uint32_t gbyte(const uint8_t* blob, uint64_t blob_len, uint64_
   return a < blob_len ? blob[a] : 0u;
 }
 
+// Guarded byte-wise tail of gload_u64 (only near the end of the blob). A compact loop, not
+// a call: calls force scratch spills around every call site on AMDGPU.
+__device__ inline uint64_t gload_u64_tail(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
+  uint64_t v = 0;
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) v |= (uint64_t)gbyte(blob, blob_len, a + k) << (8 * k);
+  return v;
+}
+
 // 64-bit little-endian window starting at an arbitrary byte address, guarded.
 __device__ inline uint64_t gload_u64(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
   uint64_t al = a & ~3ull;
+  if (al + 12 > blob_len) return gload_u64_tail(blob, blob_len, a);
   uint32_t sh = (uint32_t)(a - al) * 8u;
-  uint32_t w0, w1, w2;
-  if (al + 12 <= blob_len) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + al);
-    w0 = p[0];
-    w1 = p[1];
-    w2 = p[2];
-  } else {
-    uint32_t b[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) b[k] = gbyte(blob, blob_len, al + k);
-    w0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    w1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-    w2 = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
-  }
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + al);
+  uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
   uint64_t lo = ((uint64_t)w1 << 32) | w0;
   if (sh == 0) return lo;
   return (lo >> sh) | ((uint64_t)w2 << (64 - sh));
+}
+
+// 16 guarded bytes (blob tail) for region staging.
+__device__ inline uint4 gload_u128_tail(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
+  uint64_t lo = gload_u64_tail(blob, blob_len, a), hi = gload_u64_tail(blob, blob_len, a + 8);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 // 64-bit little-endian window from an LDS byte image stored as 32-bit words.

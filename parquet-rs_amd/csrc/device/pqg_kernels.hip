@@ -11,14 +11,14 @@
 //   k_plain_bool     PLAIN booleans (decoding.rs:188-204)
 //   k_finalize       chunk status
 //
-// All work is integer/byte movement bound by HBM: no MFMA. Run discovery for the RLE hybrid
-// is a wave-level walk: every lane of the walking wave parses a speculative run header at
-// its own byte of a 64-byte window (one LDS read each), then the wave hops along the real
-// header chain with v_readlane (registers only) and records runs in an LDS run table.
-// All four waves then expand the table with 8 outputs per lane and coalesced 16-byte stores.
-#include "pqg_device.hpp"
+// All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
+// (walker wave + expander waves, pipelined over LDS-staged regions) is in pqg_hybrid.hpp.
+#include "pqg_hybrid.hpp"
 
 namespace pqg {
+
+__device__ uint32_t g_pqg_debug_mode = 0;
+__device__ unsigned long long g_pqg_stats[16];
 
 // ------------------------------------------------------------------------------ prepare
 
@@ -134,257 +134,7 @@ __global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
 }
 
 // ------------------------------------------------------------------------------ RLE hybrid
-
-constexpr int BLK = 4096;                 // bytes of stream walked per LDS region
-constexpr int REGION = BLK + 128;         // + look-ahead for headers straddling the edge
-constexpr int REGION_WORDS = REGION / 4 + 4;
-constexpr int RUNCAP = 2048;              // runs per expansion batch
-
-constexpr uint32_t F_BP = 1u, F_EOF = 2u, F_PANIC = 4u;
-constexpr uint32_t RLE_FLAG = 0x80000000u;
-
-struct HybridSmem {
-  uint32_t region[REGION_WORDS];
-  uint32_t start[RUNCAP + 1];
-  uint32_t info[RUNCAP];
-  uint32_t ctl[8];
-  uint64_t red[4];
-};
-
-// Stage [A0, A0 + REGION) of the blob into LDS (all threads).
-__device__ inline void load_region(const uint8_t* blob, uint64_t blob_len, uint64_t A0,
-                                   uint32_t* region) {
-  for (int c = threadIdx.x; c < REGION / 16; c += WG) {
-    uint64_t a = A0 + (uint64_t)c * 16;
-    uint4 v;
-    if (a + 16 <= blob_len) {
-      v = *reinterpret_cast<const uint4*>(blob + a);
-    } else {
-      uint32_t w[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        w[k] = gbyte(blob, blob_len, a + 4 * k) | (gbyte(blob, blob_len, a + 4 * k + 1) << 8) |
-               (gbyte(blob, blob_len, a + 4 * k + 2) << 16) |
-               (gbyte(blob, blob_len, a + 4 * k + 3) << 24);
-      v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    reinterpret_cast<uint4*>(region)[c] = v;
-  }
-  if (threadIdx.x < 4) region[REGION / 4 + threadIdx.x] = 0;
-}
-
-// Speculative run header at stream position q (rle.rs:490-508): varint indicator, then
-// either a bit-packed run of (ind>>1)*8 values or an RLE run of (ind>>1) copies of a
-// ceil(w/8)-byte little-endian value.
-__device__ inline void parse_header(const uint32_t* region, uint32_t ridx, uint32_t q,
-                                    uint32_t slen, int w, uint32_t& nxt, uint32_t& cnt,
-                                    uint32_t& inf, uint32_t& flg) {
-  uint64_t ind = 0;
-  int vlen = 0;
-  bool complete = false;
-#pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    if (!complete && (q + (uint32_t)k) < slen && vlen == k) {
-      uint32_t b = lbyte(region, ridx + k);
-      ind |= (uint64_t)(b & 0x7Fu) << (7 * k);
-      vlen = k + 1;
-      if (!(b & 0x80u)) complete = true;
-    }
-  }
-  nxt = 0xFFFFFFFFu;
-  cnt = 0;
-  inf = 0;
-  if (!complete) {
-    // 10 continuation bytes with an 11th available: get_vlq_int's assert panics
-    flg = (vlen == 10 && q + 10 < slen) ? F_PANIC : F_EOF;
-    return;
-  }
-  uint32_t p = q + (uint32_t)vlen;
-  if (ind & 1) {
-    cnt = (uint32_t)((uint64_t)((int64_t)ind >> 1) * 8ull);  // ((ind >> 1) * 8) as u32
-    inf = p;
-    uint64_t nx = (uint64_t)p + (((uint64_t)cnt * (uint64_t)w) >> 3);
-    nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
-    flg = F_BP;
-  } else {
-    cnt = (uint32_t)((int64_t)ind >> 1);
-    uint32_t vb = ((uint32_t)w + 7u) >> 3;
-    if (vb > 8 || (uint64_t)p + vb > slen) {  // assert!(current_value.is_some())
-      flg = F_PANIC;
-      return;
-    }
-    uint64_t v = 0;
-    for (uint32_t k = 0; k < vb; ++k) v |= (uint64_t)lbyte(region, ridx + (uint32_t)vlen + k) << (8 * k);
-    inf = v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v;
-    nxt = p + vb;
-    flg = 0;
-  }
-}
-
-// Decodes `n` values of one RLE/bit-packed hybrid stream [S, S+slen) (absolute blob
-// offsets) with one 256-thread workgroup and calls emit(g, vals, mask) for groups of 8
-// consecutive outputs (g = out_base + index, g % 8 == 0). Returns 0 or a status code.
-// `kind` LK_BIT_PACKED decodes a header-less bit-packed stream (levels.rs:203-209).
-template <class Emit>
-__device__ int32_t hybrid_decode(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                 uint64_t S, uint32_t slen, int w, uint32_t n, int kind,
-                                 uint64_t out_base, HybridSmem& sm, Emit& emit) {
-  const uint32_t lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  uint32_t cur = 0, produced = 0;
-  int32_t err = 0;
-  bool done = (n == 0);
-  uint64_t A0 = S & ~15ull;
-  uint64_t wmask = (w >= 32) ? 0xFFFFFFFFull : ((1ull << w) - 1ull);
-
-  if (kind == LK_BIT_PACKED) {
-    if (n > 0) {
-      if ((uint64_t)n * (uint64_t)w > (uint64_t)slen * 8ull) return ST_EOF;
-      if (w > 32) return ST_PANIC;
-    }
-    if (threadIdx.x == 0) {
-      sm.start[0] = 0;
-      sm.info[0] = 0;
-      sm.start[1] = n;
-    }
-  }
-  if (done) return 0;
-  if (threadIdx.x == 0) sm.ctl[5] = 0;
-  load_region(blob, blob_len, A0, sm.region);
-  __syncthreads();
-
-  while (true) {
-    const uint32_t seg_start = produced;
-    uint32_t nruns = 1;
-    if (kind == LK_BIT_PACKED) {
-      produced = n;
-      done = true;
-    } else {
-      if (wave == 0) {
-        // ---------------- walk: registers + v_readlane only, one wave
-        uint32_t v_nxt = 0, v_cnt = 0, v_inf = 0, v_flg = 0;
-        bool have_win = false;
-        uint32_t wbase = 0;
-        nruns = 0;
-        while (true) {
-          if (produced >= n) {
-            done = true;
-            break;
-          }
-          uint64_t rel = S + cur - A0;
-          if (rel >= BLK) break;
-          if (nruns >= RUNCAP) break;
-          if (cur >= slen) {
-            err = ST_EOF;  // reload() finds no more data: reference stalls (A.4)
-            break;
-          }
-          if (!have_win || cur - wbase >= 64u) {
-            wbase = cur;
-            have_win = true;
-            uint32_t q = wbase + lane;
-            uint32_t ridx = (uint32_t)(S + q - A0);
-            if (ridx + 24 < REGION) {
-              parse_header(sm.region, ridx, q, slen, w, v_nxt, v_cnt, v_inf, v_flg);
-            } else {
-              v_flg = F_EOF;  // never reached by a chain that starts inside the block
-            }
-          }
-          const int l = (int)(cur - wbase);
-          const uint32_t nxt = readlane_u(v_nxt, l);
-          const uint32_t cnt = readlane_u(v_cnt, l);
-          const uint32_t inf = readlane_u(v_inf, l);
-          const uint32_t flg = readlane_u(v_flg, l);
-          if (flg & (F_EOF | F_PANIC)) {
-            err = (flg & F_PANIC) ? ST_PANIC : ST_EOF;
-            break;
-          }
-          if (cnt) {
-            uint32_t left = n - produced;
-            uint32_t need = cnt < left ? cnt : left;
-            if (flg & F_BP) {
-              if (w > 32) {  // BitReader::get_batch asserts num_bits <= 32
-                err = ST_PANIC;
-                break;
-              }
-              if ((uint64_t)inf * 8ull + (uint64_t)need * (uint64_t)w > (uint64_t)slen * 8ull) {
-                err = ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
-                break;
-              }
-            }
-            if (lane == 0) {
-              sm.start[nruns] = produced;
-              sm.info[nruns] = (flg & F_BP) ? inf : (RLE_FLAG | inf);
-            }
-            nruns++;
-            produced += need;
-          }
-          cur = nxt;
-        }
-        if (lane == 0) {
-          sm.start[nruns] = produced;
-          sm.ctl[0] = cur;
-          sm.ctl[1] = produced;
-          sm.ctl[2] = nruns;
-          sm.ctl[3] = (uint32_t)err;
-          sm.ctl[4] = done ? 1u : 0u;
-        }
-      }
-      __syncthreads();
-      cur = sm.ctl[0];
-      produced = sm.ctl[1];
-      nruns = sm.ctl[2];
-      err = (int32_t)sm.ctl[3];
-      done = sm.ctl[4] != 0;
-    }
-    if (err) return err;
-
-    // ---------------- expand [seg_start, produced): 8 outputs per thread per step
-    const uint64_t gb = out_base + seg_start, ge = out_base + produced;
-    for (uint64_t g = (gb & ~7ull) + 8ull * threadIdx.x; g < ge; g += 8ull * WG) {
-      uint32_t o0 = (uint32_t)((g < gb ? gb : g) - out_base);
-      int lo = 0, hi = (int)nruns - 1;
-      while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (sm.start[mid] <= o0) lo = mid;
-        else hi = mid - 1;
-      }
-      int r = lo;
-      uint32_t vals[8];
-      uint32_t mask = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        vals[j] = 0;
-        uint64_t gj = g + (uint64_t)j;
-        if (gj < gb || gj >= ge) continue;
-        uint32_t o = (uint32_t)(gj - out_base);
-        while (o >= sm.start[r + 1]) ++r;
-        uint32_t inf = sm.info[r];
-        if (inf & RLE_FLAG) {
-          vals[j] = inf & 0x7FFFFFFFu;
-        } else {
-          uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - sm.start[r]) * (uint64_t)w;
-          uint64_t abs = S + (bit >> 3);
-          uint64_t x;
-          uint64_t ri = abs - A0;
-          if (abs >= A0 && ri + 12 <= (uint64_t)REGION) x = lload_u64(sm.region, (uint32_t)ri);
-          else x = gload_u64(blob, blob_len, abs);
-          vals[j] = (uint32_t)((x >> (bit & 7)) & wmask);
-        }
-        mask |= 1u << j;
-      }
-      emit(g, vals, mask);
-    }
-    if (emit.err) sm.ctl[5] = (uint32_t)emit.err;
-    __syncthreads();  // run table / region reuse; publishes emit errors
-    if (sm.ctl[5]) return (int32_t)sm.ctl[5];
-    if (done) return 0;
-    if (S + cur - A0 >= BLK) {
-      A0 = (S + cur) & ~15ull;
-      load_region(blob, blob_len, A0, sm.region);
-      __syncthreads();
-    }
-  }
-}
+// see pqg_hybrid.hpp
 
 // ------------------------------------------------------------------------------ levels
 
@@ -416,7 +166,7 @@ struct LevelEmit {
 };
 
 // which: 0 = definition levels, 1 = repetition levels. One workgroup per page.
-__global__ void __launch_bounds__(WG) k_rle_levels(const uint8_t* __restrict__ blob,
+__global__ void __launch_bounds__(WG, 4) k_rle_levels(const uint8_t* __restrict__ blob,
                                                    uint64_t blob_len, PageWork* pages,
                                                    ColumnParams cp, int which,
                                                    int16_t* __restrict__ out,
@@ -516,7 +266,7 @@ struct DictEmit {
 };
 
 template <int ES>
-__global__ void __launch_bounds__(WG) k_dict_gather(const uint8_t* __restrict__ blob,
+__global__ void __launch_bounds__(WG, 4) k_dict_gather(const uint8_t* __restrict__ blob,
                                                     uint64_t blob_len, PageWork* pages,
                                                     int dict_page, uint8_t* __restrict__ out,
                                                     ChunkResult* res) {
@@ -656,7 +406,7 @@ struct BoolEmit {
   }
 };
 
-__global__ void __launch_bounds__(WG) k_rle_bool(const uint8_t* __restrict__ blob,
+__global__ void __launch_bounds__(WG, 4) k_rle_bool(const uint8_t* __restrict__ blob,
                                                  uint64_t blob_len, PageWork* pages,
                                                  uint8_t* __restrict__ out, ChunkResult* res) {
   __shared__ HybridSmem sm;
@@ -752,6 +502,19 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
                                int npages, uint8_t* out, ChunkResult* res, hipStream_t s) {
   hipLaunchKernelGGL(k_rle_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, out, res);
   return hipGetLastError();
+}
+
+// Diagnostics: set the debug mode of the hybrid decoder and read/reset its counters.
+int pqg_debug_set(int mode) {
+  uint32_t m = (uint32_t)mode;
+  unsigned long long z[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_pqg_stats), z, sizeof(z)) != hipSuccess) return 8;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pqg_debug_mode), &m, sizeof(m)) == hipSuccess ? 0 : 8;
+}
+
+int pqg_debug_read(unsigned long long* out16) {
+  hipDeviceSynchronize();
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_pqg_stats), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 8;
 }
 
 hipError_t pqg_launch_finalize(PageWork* pages, ChunkResult* res, hipStream_t s) {
