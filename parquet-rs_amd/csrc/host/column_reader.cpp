@@ -1,0 +1,315 @@
+// column_reader.cpp — pqg_file_* (SerializedFileReader, file/reader.rs:140-330) and
+// pqg_column_reader_* (ColumnReaderImpl::read_batch over a GPU-decoded chunk,
+// column/reader.rs:159-265).
+//
+// read_batch contract served here (derived from the loop at column/reader.rs:175-262):
+//  * def levels requested and max_def > 0: every call returns exactly
+//    min(batch_size, levels left in the chunk) levels and the values whose def == max_def;
+//  * otherwise values = min(batch_size, levels left) (each level slot is one value), and
+//    levels_read = values when rep levels are requested and max_rep > 0, else 0.
+// Chunk errors surface lazily, like the reference: batches that end before the first bad
+// page succeed; the batch that reaches it returns the page's status.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "file_reader.hpp"
+
+using namespace pqg;
+
+struct ChunkPages {
+  std::vector<uint8_t> blob;
+  std::vector<pqg_page> pages;
+  int status = 0;
+  std::string err;
+};
+
+struct pqg_file_reader {
+  std::vector<uint8_t> owned;
+  const uint8_t* data = nullptr;
+  uint64_t len = 0;
+  FileMeta meta;
+  std::string err;
+  std::map<std::pair<int, int>, std::unique_ptr<ChunkPages>> chunks;
+};
+
+struct pqg_column_reader {
+  pqg_column col{};
+  bool is_ba = false;
+  int es = 0;
+  uint64_t total_levels = 0;   // sum of data-page num_values
+  uint64_t total_values = 0;
+  std::vector<int16_t> def, rep;
+  std::vector<uint8_t> values;
+  std::vector<int64_t> offsets;
+  uint64_t L = 0, V = 0;       // level / value cursors
+  int status = 0;              // chunk status
+  uint64_t bad_level = ~0ull;  // first level index of the failing page
+  std::string err;
+};
+
+static int value_size(int t, int tl) {
+  switch (t) {
+    case PQG_BOOLEAN: return 1;
+    case PQG_INT32: case PQG_FLOAT: return 4;
+    case PQG_INT64: case PQG_DOUBLE: return 8;
+    case PQG_INT96: return 12;
+    case PQG_FIXED_LEN_BYTE_ARRAY: return tl;
+    default: return 0;
+  }
+}
+
+static ChunkPages* get_chunk(pqg_file_reader* r, int rg, int col) {
+  auto key = std::make_pair(rg, col);
+  auto it = r->chunks.find(key);
+  if (it != r->chunks.end()) return it->second.get();
+  std::unique_ptr<ChunkPages> c(new ChunkPages());
+  const ColumnChunkMeta& cc = r->meta.row_groups[rg].columns[col];
+  c->status = read_chunk_pages(r->data, r->len, cc, c->blob, c->pages, c->err);
+  ChunkPages* p = c.get();
+  r->chunks[key] = std::move(c);
+  return p;
+}
+
+static bool valid_chunk(pqg_file_reader* r, int rg, int col) {
+  return r && rg >= 0 && rg < (int)r->meta.row_groups.size() && col >= 0 &&
+         col < (int)r->meta.row_groups[rg].columns.size() && col < (int)r->meta.leaves.size();
+}
+
+extern "C" {
+
+int pqg_file_open_memory(const uint8_t* data, uint64_t len, pqg_file_reader** out) {
+  if (!out || (!data && len)) return PQG_ERR_INVALID;
+  pqg_file_reader* r = new pqg_file_reader();
+  r->owned.assign(data, data + len);
+  r->data = r->owned.data();
+  r->len = len;
+  int st = parse_file_metadata(r->data, r->len, r->meta, r->err);
+  *out = r;  // returned even on error so pqg_file_error can explain; caller closes
+  return st;
+}
+
+int pqg_file_open(const char* path, pqg_file_reader** out) {
+  if (!out || !path) return PQG_ERR_INVALID;
+  *out = nullptr;
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    pqg_file_reader* r = new pqg_file_reader();
+    r->err = std::string("cannot open ") + path;
+    *out = r;
+    return PQG_ERR_GENERAL;
+  }
+  std::vector<uint8_t> buf;
+  uint8_t tmp[1 << 16];
+  size_t n;
+  while ((n = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+  fclose(f);
+  pqg_file_reader* r = new pqg_file_reader();
+  r->owned.swap(buf);
+  r->data = r->owned.data();
+  r->len = r->owned.size();
+  int st = parse_file_metadata(r->data, r->len, r->meta, r->err);
+  *out = r;
+  return st;
+}
+
+void pqg_file_close(pqg_file_reader* r) { delete r; }
+const char* pqg_file_error(pqg_file_reader* r) { return r ? r->err.c_str() : "null reader"; }
+int64_t pqg_file_num_rows(pqg_file_reader* r) { return r ? r->meta.num_rows : -1; }
+int pqg_file_num_row_groups(pqg_file_reader* r) { return r ? (int)r->meta.row_groups.size() : -1; }
+int pqg_file_num_columns(pqg_file_reader* r) { return r ? (int)r->meta.leaves.size() : -1; }
+
+int pqg_file_column(pqg_file_reader* r, int col, pqg_column* out, char* path, size_t path_cap) {
+  if (!r || !out || col < 0 || col >= (int)r->meta.leaves.size()) return PQG_ERR_INVALID;
+  const LeafColumn& l = r->meta.leaves[col];
+  out->physical_type = l.physical_type;
+  out->type_length = l.type_length;
+  out->max_def = l.max_def;
+  out->max_rep = l.max_rep;
+  if (path && path_cap) {
+    snprintf(path, path_cap, "%s", l.path.c_str());
+  }
+  return PQG_OK;
+}
+
+int64_t pqg_row_group_num_rows(pqg_file_reader* r, int rg) {
+  if (!r || rg < 0 || rg >= (int)r->meta.row_groups.size()) return -1;
+  return r->meta.row_groups[rg].num_rows;
+}
+
+int pqg_chunk_pages(pqg_file_reader* r, int rg, int col, pqg_page* pages, uint32_t cap) {
+  if (!valid_chunk(r, rg, col)) return -PQG_ERR_INVALID;
+  ChunkPages* c = get_chunk(r, rg, col);
+  if (c->status) {
+    r->err = c->err;
+    return -c->status;
+  }
+  uint32_t n = (uint32_t)c->pages.size();
+  if (pages) memcpy(pages, c->pages.data(), (n < cap ? n : cap) * sizeof(pqg_page));
+  return (int)n;
+}
+
+int pqg_chunk_blob(pqg_file_reader* r, int rg, int col, const uint8_t** blob, uint64_t* len) {
+  if (!valid_chunk(r, rg, col) || !blob || !len) return PQG_ERR_INVALID;
+  ChunkPages* c = get_chunk(r, rg, col);
+  if (c->status) {
+    r->err = c->err;
+    return c->status;
+  }
+  *blob = c->blob.data();
+  *len = c->blob.size();
+  return PQG_OK;
+}
+
+// Decodes the whole chunk on the ctx's device, then keeps the decoded streams on the host.
+int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
+                           pqg_column_reader** out) {
+  if (!valid_chunk(r, rg, col) || !ctx || !out) return PQG_ERR_INVALID;
+  *out = nullptr;
+  ChunkPages* c = get_chunk(r, rg, col);
+  if (c->status) {
+    r->err = c->err;
+    return c->status;
+  }
+  std::unique_ptr<pqg_column_reader> cr(new pqg_column_reader());
+  const LeafColumn& l = r->meta.leaves[col];
+  cr->col.physical_type = l.physical_type;
+  cr->col.type_length = l.type_length;
+  cr->col.max_def = l.max_def;
+  cr->col.max_rep = l.max_rep;
+  cr->is_ba = l.physical_type == PQG_BYTE_ARRAY || l.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
+  cr->es = value_size(l.physical_type, l.type_length);
+  std::vector<uint64_t> page_start;  // level start of each page (data pages)
+  for (const pqg_page& p : c->pages) {
+    page_start.push_back(cr->total_levels);
+    if (p.page_type == PQG_PAGE_DATA || p.page_type == PQG_PAGE_DATA_V2) cr->total_levels += p.num_values;
+  }
+  const uint64_t n = cr->total_levels;
+  // BYTE_ARRAY output bytes are bounded by the page bytes except for DELTA_BYTE_ARRAY prefix
+  // sharing and dictionary repeats; the decode reports the exact size on CAPACITY, so retry once.
+  uint64_t vcap = cr->is_ba && l.physical_type == PQG_BYTE_ARRAY ? c->blob.size() + 64
+                                                                 : (uint64_t)cr->es * n + 64;
+  int st = PQG_OK, bad = -1;
+  std::string msg;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    void *d_blob = nullptr, *d_def = nullptr, *d_rep = nullptr, *d_val = nullptr, *d_off = nullptr;
+    auto cleanup = [&]() {
+      hipFree(d_blob);
+      hipFree(d_def);
+      hipFree(d_rep);
+      hipFree(d_val);
+      hipFree(d_off);
+    };
+    bool ok = hipMalloc(&d_blob, c->blob.size() + 64) == hipSuccess &&
+              hipMemcpy(d_blob, c->blob.data(), c->blob.size(), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMalloc(&d_def, n * 2 + 64) == hipSuccess && hipMalloc(&d_rep, n * 2 + 64) == hipSuccess &&
+              hipMalloc(&d_val, vcap) == hipSuccess &&
+              (!cr->is_ba || hipMalloc(&d_off, (n + 1) * 8 + 64) == hipSuccess);
+    if (!ok) {
+      cleanup();
+      r->err = "HIP allocation/copy failed";
+      return PQG_ERR_HIP;
+    }
+    pqg_output o{};
+    o.def_levels = l.max_def > 0 ? (int16_t*)d_def : nullptr;
+    o.rep_levels = l.max_rep > 0 ? (int16_t*)d_rep : nullptr;
+    o.values = d_val;
+    o.values_capacity = vcap;
+    o.offsets = (int64_t*)d_off;
+    o.offsets_capacity = cr->is_ba ? n + 1 : 0;
+    st = pqg_decode_chunk(ctx, &cr->col, (const uint8_t*)d_blob, c->blob.size(), c->pages.data(),
+                          (uint32_t)c->pages.size(), &o, nullptr);
+    if (st == PQG_OK) st = pqg_sync(ctx, &bad);
+    msg = pqg_error_message(ctx);
+    if (st == PQG_ERR_CAPACITY && attempt == 0 && o.num_bytes > vcap) {
+      vcap = o.num_bytes + 64;
+      cleanup();
+      continue;
+    }
+    if (st == PQG_ERR_HIP || st == PQG_ERR_INVALID) {
+      cleanup();
+      r->err = msg;
+      return st;
+    }
+    cr->total_values = o.num_values;
+    cr->def.resize(n);
+    cr->rep.resize(n);
+    uint64_t vb = cr->is_ba ? o.num_bytes : o.num_values * (uint64_t)cr->es;
+    if (vb > vcap) vb = vcap;
+    cr->values.resize(vb);
+    ok = true;
+    if (l.max_def > 0 && n) ok &= hipMemcpy(cr->def.data(), d_def, n * 2, hipMemcpyDeviceToHost) == hipSuccess;
+    if (l.max_rep > 0 && n) ok &= hipMemcpy(cr->rep.data(), d_rep, n * 2, hipMemcpyDeviceToHost) == hipSuccess;
+    if (vb) ok &= hipMemcpy(cr->values.data(), d_val, vb, hipMemcpyDeviceToHost) == hipSuccess;
+    if (cr->is_ba) {
+      cr->offsets.resize(o.num_values + 1);
+      ok &= hipMemcpy(cr->offsets.data(), d_off, (o.num_values + 1) * 8, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    cleanup();
+    if (!ok) {
+      r->err = "HIP copy failed";
+      return PQG_ERR_HIP;
+    }
+    break;
+  }
+  cr->status = st;
+  cr->err = msg;
+  if (st != PQG_OK) {
+    cr->bad_level = (bad >= 0 && bad < (int)page_start.size()) ? page_start[bad] : 0;
+    // a bad dictionary page (or any failure before the first data page) fails the first batch
+  }
+  *out = cr.release();
+  return PQG_OK;
+}
+
+void pqg_column_reader_close(pqg_column_reader* cr) { delete cr; }
+
+int pqg_column_reader_read_batch(pqg_column_reader* cr, size_t batch_size, int16_t* def,
+                                 int16_t* rep, void* values, uint64_t values_bytes_cap,
+                                 uint32_t* lengths, size_t* values_read, size_t* levels_read) {
+  if (!cr || !values_read || !levels_read) return PQG_ERR_INVALID;
+  *values_read = *levels_read = 0;
+  const bool use_def = def && cr->col.max_def > 0;
+  const bool use_rep = rep && cr->col.max_rep > 0;
+  // The chunk was decoded with its def levels; reading an optional column without them would
+  // make the reference decode one value per level slot, which this reader does not replay.
+  if (cr->col.max_def > 0 && !def) return PQG_ERR_INVALID;
+  uint64_t left = cr->total_levels - cr->L;
+  uint64_t nlev = batch_size < left ? batch_size : left;
+  if (nlev == 0) return PQG_OK;
+  if (cr->status != PQG_OK && cr->L + nlev > cr->bad_level) return cr->status;
+  uint64_t nval = nlev;
+  if (use_def) {
+    nval = 0;
+    const int16_t md = cr->col.max_def;
+    for (uint64_t i = 0; i < nlev; ++i) nval += cr->def[cr->L + i] == md;
+  }
+  if (cr->V + nval > cr->total_values) return PQG_ERR_GENERAL;  // inconsistent chunk
+  if (cr->is_ba) {
+    uint64_t b0 = (uint64_t)cr->offsets[cr->V], b1 = (uint64_t)cr->offsets[cr->V + nval];
+    if (b1 - b0 > values_bytes_cap) return PQG_ERR_CAPACITY;
+    if (values && b1 > b0) memcpy(values, cr->values.data() + b0, b1 - b0);
+    if (lengths)
+      for (uint64_t i = 0; i < nval; ++i)
+        lengths[i] = (uint32_t)(cr->offsets[cr->V + i + 1] - cr->offsets[cr->V + i]);
+  } else {
+    uint64_t nb = nval * (uint64_t)cr->es;
+    if (nb > values_bytes_cap) return PQG_ERR_CAPACITY;
+    if (values && nb) memcpy(values, cr->values.data() + cr->V * cr->es, nb);
+  }
+  if (use_def) memcpy(def, cr->def.data() + cr->L, nlev * 2);
+  if (use_rep) memcpy(rep, cr->rep.data() + cr->L, nlev * 2);
+  cr->L += nlev;
+  cr->V += nval;
+  *values_read = nval;
+  *levels_read = (use_def || use_rep) ? nlev : 0;
+  return PQG_OK;
+}
+
+}  // extern "C"

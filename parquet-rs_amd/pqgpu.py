@@ -93,9 +93,27 @@ def lib():
         L.pqg_reset_timings.argtypes = [vp]
         L.pqg_error_message.argtypes = [vp]
         L.pqg_error_message.restype = C.c_char_p
-        if not hasattr(L, "pqg_gen_levels_plain"):
-            _lib = L
-            return L
+        L.pqg_file_open.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.pqg_file_open_memory.argtypes = [vp, u64, C.POINTER(vp)]
+        L.pqg_file_close.argtypes = [vp]
+        L.pqg_file_close.restype = None
+        L.pqg_file_error.argtypes = [vp]
+        L.pqg_file_error.restype = C.c_char_p
+        for name in ("pqg_file_num_rows",):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = C.c_int64
+        L.pqg_file_num_row_groups.argtypes = [vp]
+        L.pqg_file_num_columns.argtypes = [vp]
+        L.pqg_file_column.argtypes = [vp, i32, C.POINTER(Column), C.c_char_p, C.c_size_t]
+        L.pqg_row_group_num_rows.argtypes = [vp, i32]
+        L.pqg_row_group_num_rows.restype = C.c_int64
+        L.pqg_chunk_pages.argtypes = [vp, i32, i32, C.POINTER(Page), C.c_uint32]
+        L.pqg_chunk_blob.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(u64)]
+        L.pqg_column_reader_open.argtypes = [vp, i32, i32, vp, C.POINTER(vp)]
+        L.pqg_column_reader_close.argtypes = [vp]
+        L.pqg_column_reader_close.restype = None
+        L.pqg_column_reader_read_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, u64, vp,
+                                                   C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
         for name in ("pqg_gen_levels_plain",):
             getattr(L, name).argtypes = [u64, C.c_double, C.c_uint32, u64, i32, vp, u64,
                                          C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
@@ -226,3 +244,135 @@ def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_
     else:
         res["values"] = np.zeros(0, np.uint8)
     return res
+
+
+class FileReader:
+    """SerializedFileReader over the host-side footer/page reader (file/reader.rs:140-330).
+    Host-only: opening a file and listing pages needs no GPU."""
+
+    def __init__(self, path=None, data=None):
+        h = C.c_void_p()
+        if data is not None:
+            buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+            st = lib().pqg_file_open_memory(buf, len(data), C.byref(h))
+        else:
+            st = lib().pqg_file_open(os.fsencode(path), C.byref(h))
+        self.h = h
+        if st:
+            msg = lib().pqg_file_error(h).decode(errors="replace") if h else ""
+            self.close()
+            raise PqgError(st, msg)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pqg_file_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self):
+        return lib().pqg_file_error(self.h).decode(errors="replace")
+
+    @property
+    def num_rows(self):
+        return lib().pqg_file_num_rows(self.h)
+
+    @property
+    def num_row_groups(self):
+        return lib().pqg_file_num_row_groups(self.h)
+
+    @property
+    def num_columns(self):
+        return lib().pqg_file_num_columns(self.h)
+
+    def row_group_num_rows(self, rg):
+        return lib().pqg_row_group_num_rows(self.h, rg)
+
+    def column(self, j):
+        """(dot-joined path, Column descriptor) of leaf j."""
+        col = Column()
+        buf = C.create_string_buffer(1024)
+        st = lib().pqg_file_column(self.h, j, C.byref(col), buf, 1024)
+        if st:
+            raise PqgError(st, "bad column index")
+        return buf.value.decode(), col
+
+    def chunk_pages(self, rg, j):
+        """(host blob bytes, ctypes Page array) of one column chunk, uncompressed."""
+        n = lib().pqg_chunk_pages(self.h, rg, j, None, 0)
+        if n < 0:
+            raise PqgError(-n, self.error())
+        arr = (Page * max(n, 1))()
+        lib().pqg_chunk_pages(self.h, rg, j, arr, n)
+        p, ln = C.c_void_p(), C.c_uint64()
+        st = lib().pqg_chunk_blob(self.h, rg, j, C.byref(p), C.byref(ln))
+        if st:
+            raise PqgError(st, self.error())
+        return C.string_at(p, ln.value), arr, n
+
+    def column_reader(self, rg, j, ctx):
+        return ColumnReader(self, rg, j, ctx)
+
+
+class ColumnReader:
+    """ColumnReaderImpl::read_batch over a chunk decoded on the GPU (column/reader.rs:159-265)."""
+
+    def __init__(self, fr, rg, j, ctx):
+        self.fr = fr
+        self.path, self.col = fr.column(j)
+        h = C.c_void_p()
+        st = lib().pqg_column_reader_open(fr.h, rg, j, ctx.h, C.byref(h))
+        if st:
+            raise PqgError(st, fr.error())
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pqg_column_reader_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def read_batch(self, batch_size, want_def=True, want_rep=True):
+        """Returns (values, def, rep, values_read, levels_read). For BYTE_ARRAY/FLBA values
+        is a list of bytes objects; otherwise a numpy array in the reference layout."""
+        t = self.col.physical_type
+        es = VALUE_SIZE.get(t, 0)
+        ba = t in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY)
+        d = np.zeros(batch_size, np.int16) if want_def and self.col.max_def > 0 else None
+        r = np.zeros(batch_size, np.int16) if want_rep and self.col.max_rep > 0 else None
+        cap = batch_size * es if not ba else 1 << 16
+        while True:
+            vals = np.zeros(max(cap, 1), np.uint8)
+            lens = np.zeros(max(batch_size, 1), np.uint32) if ba else None
+            vr, lr = C.c_size_t(), C.c_size_t()
+            st = lib().pqg_column_reader_read_batch(
+                self.h, batch_size, d.ctypes.data if d is not None else None,
+                r.ctypes.data if r is not None else None, vals.ctypes.data, cap,
+                lens.ctypes.data if lens is not None else None, C.byref(vr), C.byref(lr))
+            if st == CAPACITY and ba:
+                cap *= 4
+                continue
+            break
+        if st:
+            raise PqgError(st, self.fr.error())
+        nv, nl = vr.value, lr.value
+        if ba:
+            out, o = [], 0
+            for k in range(nv):
+                out.append(bytes(vals[o:o + lens[k]]))
+                o += int(lens[k])
+            values = out
+        else:
+            raw = vals[: nv * es]
+            values = raw.reshape(-1, 12) if t == INT96 else raw.view(NP_DTYPE[t])
+        return (values, d[:nl] if d is not None else None, r[:nl] if r is not None else None,
+                nv, nl)
