@@ -1,0 +1,436 @@
+// pqg_bytes.hip — BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY values on CDNA4.
+//
+// Output layout (pqgpu.h): the dense non-null values' bytes concatenated, plus int64 offsets
+// (num_values + 1). The reference hands out ByteArray slices of page memory
+// (data_type.rs:70-98) or, for DELTA_BYTE_ARRAY, freshly built vectors; a device layout of
+// bytes + offsets carries the same values.
+//
+// Two passes over each page, with a chunk-wide scan in between:
+//   index  k_ba_index / k_ba_dict_idx: per value its source address and length
+//          (PLAIN BA :206-226, PLAIN FLBA :228-247, dictionary :256-315 with the dictionary
+//          page decoded by k_ba_dict_prep, DELTA_LENGTH_BYTE_ARRAY :682-712, DELTA_BYTE_ARRAY
+//          :768-835), and the page's output byte count;
+//   scan   k_scan_bytes: page byte offsets, capacity check, final offset;
+//   copy   k_ba_copy (gathers slices) and k_dba_copy (DELTA_BYTE_ARRAY: value i = the first
+//          prefix_i bytes of value i-1 ++ suffix_i, rebuilt in an LDS buffer per page).
+//
+// PLAIN BYTE_ARRAY lengths are inline ([u32 len][bytes]...), so value starts form a serial
+// chain: one lane walks it over LDS-staged 16 KiB regions of the page.
+#include "pqg_delta.hpp"
+#include "pqg_hybrid.hpp"
+
+namespace pqg {
+
+// Walks n PLAIN BYTE_ARRAY values of the stream blob[S, S+slen) (decoding.rs:206-226):
+// PANIC when fewer than 4 bytes remain for a length (read_num_bytes! assert), EOF when the
+// value bytes run past the stream. Writes absolute source addresses and lengths.
+__device__ int32_t plain_ba_walk(DeltaSmem& sm, const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                 uint64_t S, uint32_t slen, uint64_t n, uint64_t* __restrict__ src,
+                                 uint32_t* __restrict__ len) {
+  uint64_t i = 0;
+  uint32_t pos = 0;
+  while (i < n) {
+    const uint64_t A0 = (S + pos) & ~15ull;
+    __syncthreads();
+    delta_load_region(sm, blob, blob_len, A0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int32_t e = 0;
+      while (i < n) {
+        const uint64_t rel = S + pos - A0;
+        if (rel + 4 > (uint64_t)DBLK) break;
+        if ((uint64_t)pos + 4 > slen) {
+          e = ST_PANIC;
+          break;
+        }
+        const uint32_t l = (uint32_t)lload_u64(sm.region, (uint32_t)rel);
+        pos += 4;
+        if ((uint64_t)pos + l > slen) {
+          e = ST_EOF;
+          break;
+        }
+        src[i] = S + pos;
+        len[i] = l;
+        pos += l;
+        ++i;
+      }
+      sm.ctl[0] = (uint32_t)e;
+      sm.ctl[1] = pos;
+      reinterpret_cast<uint64_t*>(&sm.ctl[2])[0] = i;
+    }
+    __syncthreads();
+    const int32_t e = (int32_t)sm.ctl[0];
+    pos = sm.ctl[1];
+    i = reinterpret_cast<uint64_t*>(&sm.ctl[2])[0];
+    if (e) return e;
+  }
+  return 0;
+}
+
+// Block-wide exclusive scan of one u64 per thread; returns the exclusive prefix and the total
+// through `tot`. Uses sm.wsum.
+__device__ inline uint64_t block_exscan(DeltaSmem& sm, uint64_t x, uint64_t& tot) {
+  const int tid = threadIdx.x;
+  uint64_t incl = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint64_t y = __shfl_up(incl, off, 64);
+    if ((tid & 63) >= off) incl += y;
+  }
+  __syncthreads();
+  if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+  __syncthreads();
+  uint64_t pre = 0;
+  for (int w = 0; w < (tid >> 6); ++w) pre += sm.wsum[w];
+  tot = sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+  return pre + incl - x;
+}
+
+// Source addresses of `n` DELTA_LENGTH-style values whose lengths (int32) are in len[0, n)
+// and whose bytes start at D (dlen bytes available). data.range(offset, len) asserts
+// (PANIC) on negative lengths or running past the data.
+__device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen, uint64_t n,
+                                       const uint32_t* len, uint64_t* src) {
+  uint64_t carry = 0;
+  int32_t bad = 0;
+  for (uint64_t b = 0; b < n; b += WG) {
+    const uint64_t i = b + threadIdx.x;
+    const int32_t l = i < n ? (int32_t)len[i] : 0;
+    uint64_t tot;
+    const uint64_t pre = block_exscan(sm, l > 0 ? (uint64_t)l : 0, tot);
+    if (i < n) {
+      if (l < 0 || carry + pre + (uint64_t)l > dlen) bad = 1;
+      else src[i] = D + carry + pre;
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) sm.ctl[5] = 0;
+  __syncthreads();
+  if (bad) sm.ctl[5] = 1;
+  __syncthreads();
+  return sm.ctl[5] ? ST_PANIC : 0;
+}
+
+// Sum of a page's output value lengths -> pages[p].nbytes_out.
+__device__ void page_bytes(DeltaSmem& sm, PageWork* pages, int p, uint64_t n, const uint32_t* len,
+                           const uint32_t* pre) {
+  uint64_t s = 0;
+  for (uint64_t i = threadIdx.x; i < n; i += WG) s += (uint64_t)len[i] + (pre ? (uint64_t)pre[i] : 0);
+  uint64_t t = block_sum_u64(s, sm.wsum);
+  if (threadIdx.x == 0) pages[p].nbytes_out = t;
+}
+
+// Dictionary page of a BYTE_ARRAY / FLBA column: DictDecoder::set_dict decodes every entry
+// with PlainDecoder (decoding.rs:282-288).
+__global__ void __launch_bounds__(WG) k_ba_dict_prep(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, int dict_page, int type_length,
+                                                     uint64_t* dsrc, uint32_t* dlen, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const PageWork dp = pages[dict_page];
+  if (dp.status != 0) return;
+  const uint64_t n = dp.num_values;
+  const uint64_t S = dp.base;
+  int32_t st = 0;
+  if (type_length > 0) {  // FLBA
+    if (n * (uint64_t)type_length > dp.nbytes) st = ST_EOF;
+    else
+      for (uint64_t i = threadIdx.x; i < n; i += WG) {
+        dsrc[i] = S + i * (uint64_t)type_length;
+        dlen[i] = (uint32_t)type_length;
+      }
+  } else {
+    st = plain_ba_walk(sm, blob, blob_len, S, dp.nbytes, n, dsrc, dlen);
+  }
+  if (st && threadIdx.x == 0) report(pages, res, dict_page, st);
+}
+
+struct BaDictEmit {
+  const uint64_t* dsrc;
+  const uint32_t* dlen;
+  uint32_t ndict;
+  uint64_t* src;
+  uint32_t* len;
+  uint64_t bytes;
+  int32_t err;
+  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!((mask >> j) & 1)) continue;
+      const uint32_t idx = v[j];
+      if (idx >= ndict) {  // dict[idx] out of bounds: the reference panics
+        err = ST_PANIC;
+        continue;
+      }
+      const uint32_t l = dlen[idx];
+      src[g + j] = dsrc[idx];
+      len[g + j] = l;
+      bytes += l;
+    }
+  }
+};
+
+__global__ void __launch_bounds__(WG, 4) k_ba_dict_idx(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages, int dict_page,
+                                                    const uint64_t* dsrc, const uint32_t* dlen,
+                                                    uint64_t* vsrc, uint32_t* vlen, ChunkResult* res) {
+  __shared__ HybridSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_RLE_DICTIONARY) return;
+  if (dict_page < 0) {
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  const PageWork dp = pages[dict_page];
+  if (dp.status != 0) return;
+  if (pw.val_bytes < 1) {  // DictDecoder::set_data reads the bit width byte (data[0])
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  const uint64_t n = pw.nonnull;
+  if (n == 0) return;
+  const int w = blob[pw.base + pw.val_off];
+  // hybrid_decode emits global value indices (out_base = value_out)
+  BaDictEmit em{dsrc, dlen, dp.num_values, vsrc, vlen, 0, 0};
+  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 1, pw.val_bytes - 1, w,
+                             (uint32_t)n, LK_RLE, pw.value_out, sm, em);
+  uint64_t t = block_sum_u64(em.bytes, reinterpret_cast<uint64_t*>(sm.red));
+  if (threadIdx.x == 0) {
+    if (st) report(pages, res, p, st);
+    else pages[p].nbytes_out = t;
+  }
+}
+
+__global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                 PageWork* pages, int type_length, uint64_t* vsrc,
+                                                 uint32_t* vlen, uint32_t* vpre, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  const uint64_t n = pw.nonnull, vo = pw.value_out;
+  const uint64_t S = pw.base + pw.val_off;
+  const uint32_t slen = pw.val_bytes;
+  uint64_t* src = vsrc + vo;
+  uint32_t* len = vlen + vo;
+  int32_t st = 0;
+  bool dba = false;
+  switch (pw.encoding) {
+    case E_PLAIN:
+      if (type_length > 0) {
+        if (n * (uint64_t)type_length > slen) st = ST_EOF;
+        else
+          for (uint64_t i = threadIdx.x; i < n; i += WG) {
+            src[i] = S + i * (uint64_t)type_length;
+            len[i] = (uint32_t)type_length;
+          }
+      } else {
+        st = plain_ba_walk(sm, blob, blob_len, S, slen, n, src, len);
+      }
+      break;
+    case E_DELTA_LENGTH_BYTE_ARRAY: {
+      // set_data decodes every length, then data.start_from(get_offset()) (:682-695)
+      DeltaInfo li;
+      st = delta_stream<4>(sm, blob, blob_len, S, slen, ~0ull, n, reinterpret_cast<uint8_t*>(len), li);
+      if (!st && li.total < n) st = ST_EOF;  // the reference returns a short batch
+      if (!st && li.end_off > slen) st = ST_PANIC;
+      if (!st) st = slices_from_lengths(sm, S + li.end_off, slen - li.end_off, n, len, src);
+      break;
+    }
+    case E_DELTA_BYTE_ARRAY: {
+      dba = true;
+      uint32_t* pre = vpre + vo;
+      DeltaInfo pi, si;
+      st = delta_stream<4>(sm, blob, blob_len, S, slen, ~0ull, n, reinterpret_cast<uint8_t*>(pre), pi);
+      if (!st && pi.total < n) st = ST_EOF;
+      if (!st && pi.end_off > slen) st = ST_PANIC;
+      const uint32_t e1 = pi.end_off;
+      if (!st) {
+        __syncthreads();
+        st = delta_stream<4>(sm, blob, blob_len, S + e1, slen - e1, ~0ull, n,
+                             reinterpret_cast<uint8_t*>(len), si);
+      }
+      if (!st && (uint64_t)e1 + si.end_off > slen) st = ST_PANIC;
+      if (!st) {
+        const uint64_t e2 = (uint64_t)e1 + si.end_off;
+        const uint64_t ns = si.total < n ? si.total : n;
+        if (n > 0 && ns == 0) st = ST_PANIC;  // ByteArray::data() before set_data
+        if (!st) st = slices_from_lengths(sm, S + e2, slen - e2, ns, len, src);
+        __syncthreads();
+        if (!st) {
+          // suffix decoder exhausted: `v` keeps the last suffix (decoding.rs:796-801)
+          for (uint64_t i = ns + threadIdx.x; i < n; i += WG) {
+            src[i] = src[ns - 1];
+            len[i] = len[ns - 1];
+          }
+          __syncthreads();
+          // previous_value[0..prefix_len] (:804)
+          int32_t bad = 0;
+          for (uint64_t i = threadIdx.x; i < n; i += WG) {
+            const int32_t pl = (int32_t)pre[i];
+            const uint64_t prev = i ? (uint64_t)pre[i - 1] + len[i - 1] : 0;
+            if (pl < 0 || (uint64_t)pl > prev) bad = 1;
+          }
+          if (threadIdx.x == 0) sm.ctl[6] = 0;
+          __syncthreads();
+          if (bad) sm.ctl[6] = 1;
+          __syncthreads();
+          if (sm.ctl[6]) st = ST_PANIC;
+        }
+      }
+      break;
+    }
+    default:
+      return;  // dictionary pages of data (k_ba_dict_idx)
+  }
+  if (st) {
+    if (threadIdx.x == 0) report(pages, res, p, st);
+    return;
+  }
+  __syncthreads();
+  page_bytes(sm, pages, p, n, len, dba ? vpre + vo : nullptr);
+}
+
+// Page byte offsets (exclusive scan of nbytes_out), the output capacity check and the final
+// offset entry. One workgroup.
+__global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, int npages, ChunkResult* res,
+                                                   uint64_t cap, int64_t* offsets) {
+  __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint64_t carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < npages; base += WG) {
+    const int p = base + threadIdx.x;
+    uint64_t x = 0;
+    if (p < npages) {
+      const int t = pages[p].page_type;
+      if (t == P_DATA || t == P_DATA_V2) x = pages[p].nbytes_out;
+    }
+    uint64_t s = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      uint64_t y = __shfl_up(s, off, 64);
+      if ((threadIdx.x & 63) >= (unsigned)off) s += y;
+    }
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    uint64_t pre = carry_s;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
+    if (p < npages) {
+      pages[p].byte_out = pre + s - x;
+      if (x > 0 && pre + s > cap && pages[p].status == 0) report(pages, res, p, ST_CAPACITY);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    res->total_bytes = carry_s;
+    if (offsets) offsets[res->total_values] = (int64_t)carry_s;
+  }
+}
+
+// Gathers value slices into the output and writes their offsets (all encodings but
+// DELTA_BYTE_ARRAY). One workgroup per page, 256 values per pass.
+__global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
+                                                const uint64_t* __restrict__ vsrc,
+                                                const uint32_t* __restrict__ vlen, uint64_t cap,
+                                                int64_t* __restrict__ offsets,
+                                                uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding == E_DELTA_BYTE_ARRAY) return;
+  if (res->total_bytes > cap) return;
+  const uint64_t n = pw.nonnull, vo = pw.value_out;
+  uint64_t carry = pw.byte_out;
+  for (uint64_t b = 0; b < n; b += WG) {
+    const uint64_t i = b + threadIdx.x;
+    const uint32_t l = i < n ? vlen[vo + i] : 0;
+    uint64_t tot;
+    const uint64_t pre = block_exscan(sm, l, tot);
+    if (i < n) {
+      const uint64_t d = carry + pre;
+      offsets[vo + i] = (int64_t)d;
+      const uint8_t* s = blob + vsrc[vo + i];
+      uint8_t* o = out + d;
+      uint32_t k = 0;
+      for (; k + 8 <= l; k += 8) {
+        uint64_t x;
+        __builtin_memcpy(&x, s + k, 8);
+        __builtin_memcpy(o + k, &x, 8);
+      }
+      for (; k < l; ++k) o[k] = s[k];
+    }
+    carry += tot;
+  }
+}
+
+// DELTA_BYTE_ARRAY values (decoding.rs:788-822), one wave per page: the previous value lives
+// in LDS; value i overwrites bytes [prefix_i, prefix_i + suffix_len) of it and is then
+// streamed to the output.
+constexpr int DBA_PREV = 32768;
+
+__global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
+                                                 const uint64_t* __restrict__ vsrc,
+                                                 const uint32_t* __restrict__ vlen,
+                                                 const uint32_t* __restrict__ vpre, uint64_t cap,
+                                                 int64_t* __restrict__ offsets,
+                                                 uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ uint8_t prev[DBA_PREV];
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_DELTA_BYTE_ARRAY) return;
+  if (res->total_bytes > cap) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t n = pw.nonnull, vo = pw.value_out;
+  uint64_t d = pw.byte_out;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t pl = vpre[vo + i], sl = vlen[vo + i];
+    const uint64_t tot = (uint64_t)pl + sl;
+    if (tot > DBA_PREV) {  // values longer than the LDS buffer: not supported yet
+      if (lane == 0) report(pages, res, p, ST_NYI);
+      return;
+    }
+    const uint8_t* s = blob + vsrc[vo + i];
+    for (uint32_t k = lane; k < sl; k += 64) prev[pl + k] = s[k];
+    __syncthreads();
+    for (uint32_t k = lane; k < tot; k += 64) out[d + k] = prev[k];
+    if (lane == 0) offsets[vo + i] = (int64_t)d;
+    d += tot;
+    __syncthreads();
+  }
+}
+
+extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                                       int npages, int dict_page, int type_length, bool has_dict,
+                                       bool has_dba, uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre,
+                                       uint64_t* dsrc, uint32_t* dlen, uint64_t cap,
+                                       int64_t* offsets, uint8_t* out, ChunkResult* res,
+                                       hipStream_t s) {
+  if (has_dict && dict_page >= 0)
+    hipLaunchKernelGGL(k_ba_dict_prep, dim3(1), dim3(WG), 0, s, blob, blob_len, pages, dict_page,
+                       type_length, dsrc, dlen, res);
+  if (has_dict)
+    hipLaunchKernelGGL(k_ba_dict_idx, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages,
+                       dict_page, dsrc, dlen, vsrc, vlen, res);
+  hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, type_length,
+                     vsrc, vlen, vpre, res);
+  hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);
+  hipLaunchKernelGGL(k_ba_copy, dim3(npages), dim3(WG), 0, s, blob, pages, vsrc, vlen, cap,
+                     offsets, out, res);
+  if (has_dba)
+    hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, vsrc, vlen, vpre,
+                       cap, offsets, out, res);
+  return hipGetLastError();
+}
+
+}  // namespace pqg

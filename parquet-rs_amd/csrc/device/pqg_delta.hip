@@ -1,61 +1,8 @@
-// pqg_delta.hip — DELTA_BINARY_PACKED decode on CDNA4 (decoding.rs:392-619).
-//
-// One 256-thread workgroup per page. The page header (block size, mini-blocks per block,
-// value count, zigzag first value; decoding.rs:501-533) is parsed once. Block headers
-// (zigzag min_delta + one width byte per mini-block, decoding.rs:448-468) sit at
-// data-dependent offsets, so one lane walks them inside an LDS-staged 16 KiB region and
-// records a block table; then all 256 threads unpack 16 consecutive deltas each, run a
-// workgroup-wide 64-bit prefix sum (wrapping, decoding.rs:564-565) and store the values
-// with 16-byte stores. INT32 is the same computation truncated mod 2^32 (decoding.rs:601-609).
-#include "pqg_device.hpp"
+// pqg_delta.hip — DELTA_BINARY_PACKED values (decoding.rs:392-619): one 256-thread workgroup
+// per page running the stream decoder of pqg_delta.hpp over the page's value stream.
+#include "pqg_delta.hpp"
 
 namespace pqg {
-
-constexpr int DBLK = 16384;
-constexpr int DREGION = DBLK + 128;
-constexpr int DREGION_WORDS = DREGION / 4 + 4;
-constexpr int NBCAP = 48;     // blocks per batch
-constexpr int MBCAP = 64;     // mini-blocks per block supported
-constexpr int DPT = 16;       // deltas per thread per pass
-
-struct DeltaSmem {
-  uint32_t region[DREGION_WORDS];
-  uint32_t pay[NBCAP];             // stream-relative payload start of block
-  uint64_t mind[NBCAP];            // min_delta
-  uint32_t first_delta[NBCAP + 1]; // batch-relative delta index of the block's first delta
-  uint8_t width[NBCAP][MBCAP];
-  uint32_t mboff[NBCAP][MBCAP];    // byte offset of mini-block m from pay[b]
-  uint64_t wsum[WG / 64];
-  uint64_t carry;
-  uint32_t ctl[8];
-};
-
-// LEB128 from LDS; returns bytes used, 0 if truncated by the stream end, -1 if > 10 bytes
-// with more data (get_vlq_int assert).
-__device__ inline int lds_vlq(const uint32_t* region, uint32_t ridx, uint32_t q, uint32_t slen,
-                              uint64_t& v) {
-  v = 0;
-  for (int k = 0; k < 10; ++k) {
-    if (q + (uint32_t)k >= slen) return 0;
-    uint32_t b = lbyte(region, ridx + k);
-    v |= (uint64_t)(b & 0x7F) << (7 * k);
-    if (!(b & 0x80)) return k + 1;
-  }
-  return (q + 10 < slen) ? -1 : 0;
-}
-
-__device__ inline int g_vlq(const uint8_t* p, uint32_t q, uint32_t slen, uint64_t& v) {
-  v = 0;
-  for (int k = 0; k < 10; ++k) {
-    if (q + (uint32_t)k >= slen) return 0;
-    uint32_t b = p[q + k];
-    v |= (uint64_t)(b & 0x7F) << (7 * k);
-    if (!(b & 0x80)) return k + 1;
-  }
-  return (q + 10 < slen) ? -1 : 0;
-}
-
-__device__ inline int64_t unzigzag(uint64_t u) { return (int64_t)(u >> 1) ^ -(int64_t)(u & 1); }
 
 template <int ES>  // 4 = INT32, 8 = INT64
 __global__ void __launch_bounds__(WG) k_delta(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -67,250 +14,11 @@ __global__ void __launch_bounds__(WG) k_delta(const uint8_t* __restrict__ blob, 
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED) return;
-  const uint64_t S = pw.base + pw.val_off;
-  const uint32_t slen = pw.val_bytes;
-  const uint8_t* sp = blob + S;
-  const int tid = threadIdx.x;
-
-  // ---- page header, decoding.rs:501-533 (parsed redundantly by every thread: 4 varints)
-  uint64_t block_size, nmb, total, fz;
-  uint32_t q = 0;
-  int32_t err = 0;
-  int l;
-  if ((l = g_vlq(sp, q, slen, block_size)) <= 0) err = l ? ST_PANIC : ST_EOF;
-  q += l > 0 ? l : 0;
-  if (!err && (l = g_vlq(sp, q, slen, nmb)) <= 0) err = l ? ST_PANIC : ST_EOF;
-  q += l > 0 ? l : 0;
-  if (!err && (l = g_vlq(sp, q, slen, total)) <= 0) err = l ? ST_PANIC : ST_EOF;
-  q += l > 0 ? l : 0;
-  if (!err && (l = g_vlq(sp, q, slen, fz)) <= 0) err = l ? ST_PANIC : ST_EOF;
-  q += l > 0 ? l : 0;
-  uint64_t vpmb = 0;
-  if (!err) {
-    if ((int64_t)nmb <= 0) err = ST_PANIC;  // division by zero / widths[0] (decoding.rs:464)
-    else {
-      vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
-      if (vpmb % 8 != 0) err = ST_PANIC;  // assert!(values_per_mini_block % 8 == 0)
-      else if (nmb > MBCAP) err = ST_NYI;
-    }
-  }
-  const uint64_t n_req = pw.nonnull;
-  if (!err && total < n_req) err = ST_EOF;  // the reference returns a short batch here
-  if (err) {
-    if (tid == 0) report(pages, res, p, err);
-    return;
-  }
-  if (n_req == 0) return;
-  uint8_t* o = out + pw.value_out * ES;
-  const int64_t first = unzigzag(fz);
-  if (tid == 0) {
-    if (ES == 4) *reinterpret_cast<int32_t*>(o) = (int32_t)first;
-    else *reinterpret_cast<int64_t*>(o) = first;
-  }
-  if (vpmb == 0) {  // block_size < num_mini_blocks: every mini-block is empty
-    if (n_req > 1 && tid == 0) report(pages, res, p, ST_HANG);
-    return;
-  }
-  const uint64_t vpb = vpmb * nmb;             // deltas per block
-  const uint64_t need = n_req - 1;             // deltas to decode
-  uint64_t done = 0;                           // deltas decoded
-  uint32_t pos = q;                            // next block header
-  uint64_t A0 = (S + pos) & ~15ull;
-  uint64_t carry = (uint64_t)first;            // value before the next delta
-
-  // stage region
-  auto load_region = [&](uint64_t a0) {
-    for (int c = tid; c < DREGION / 16; c += WG) {
-      uint64_t a = a0 + (uint64_t)c * 16;
-      uint4 v;
-      if (a + 16 <= blob_len) v = *reinterpret_cast<const uint4*>(blob + a);
-      else {
-        uint32_t w[4];
-        for (int k = 0; k < 4; ++k)
-          w[k] = gbyte(blob, blob_len, a + 4 * k) | (gbyte(blob, blob_len, a + 4 * k + 1) << 8) |
-                 (gbyte(blob, blob_len, a + 4 * k + 2) << 16) | (gbyte(blob, blob_len, a + 4 * k + 3) << 24);
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      reinterpret_cast<uint4*>(sm.region)[c] = v;
-    }
-    if (tid < 4) sm.region[DREGION / 4 + tid] = 0;
-  };
-  load_region(A0);
-  __syncthreads();
-
-  while (done < need) {
-    // ---------------- walk block headers (one lane)
-    if (tid == 0) {
-      uint32_t nb = 0;
-      uint64_t dcount = 0;
-      int32_t e = 0;
-      uint32_t cur = pos;
-      while (nb < NBCAP && done + dcount < need) {
-        uint64_t rel = S + cur - A0;
-        if (rel >= DBLK) break;
-        uint32_t ridx = (uint32_t)rel;
-        uint64_t zz;
-        int vl = lds_vlq(sm.region, ridx, cur, slen, zz);
-        if (vl <= 0) {
-          e = vl ? ST_PANIC : ST_EOF;  // "Not enough data to decode 'min_delta'"
-          break;
-        }
-        if ((uint64_t)cur + vl + nmb > slen) {
-          e = ST_EOF;  // "Not enough data to decode 'width'"
-          break;
-        }
-        uint64_t left = need - done - dcount;
-        uint64_t inblk = left < vpb ? left : vpb;
-        uint32_t mneed = (uint32_t)((inblk + vpmb - 1) / vpmb);
-        uint32_t payload = cur + (uint32_t)vl + (uint32_t)nmb;
-        uint64_t boff = 0;
-        for (uint32_t m = 0; m < (uint32_t)nmb; ++m) {
-          uint32_t wdt = lbyte(sm.region, ridx + (uint32_t)vl + m);
-          sm.width[nb][m] = (uint8_t)wdt;
-          sm.mboff[nb][m] = (uint32_t)boff;
-          if (m < mneed) {
-            if (wdt > (ES == 4 ? 32u : 64u)) {
-              e = ST_PANIC;  // get_batch / get_value assert on num_bits
-              break;
-            }
-            // the reference loads the whole mini-block, padding included (decoding.rs:472-495)
-            if ((uint64_t)payload + boff + (vpmb * wdt) / 8 > slen) {
-              e = (ES == 4) ? ST_PANIC : ST_EOF;
-              break;
-            }
-          }
-          boff += (vpmb * wdt) / 8;
-        }
-        if (e) break;
-        sm.pay[nb] = payload;
-        sm.mind[nb] = (uint64_t)unzigzag(zz);
-        sm.first_delta[nb] = (uint32_t)dcount;
-        dcount += inblk;
-        nb++;
-        uint64_t nx = (uint64_t)payload + boff;
-        cur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
-      }
-      sm.first_delta[nb] = (uint32_t)dcount;
-      sm.ctl[0] = nb;
-      sm.ctl[1] = (uint32_t)dcount;
-      sm.ctl[2] = (uint32_t)e;
-      sm.ctl[3] = cur;
-    }
-    __syncthreads();
-    const uint32_t nb = sm.ctl[0];
-    const uint32_t dcount = sm.ctl[1];
-    const int32_t e = (int32_t)sm.ctl[2];
-    const uint32_t ncur = sm.ctl[3];
-    if (e) {
-      if (tid == 0) report(pages, res, p, e);
-      return;
-    }
-    if (nb == 0) {  // next header lies beyond this region: move the region
-      __syncthreads();
-      A0 = (S + ncur) & ~15ull;
-      pos = ncur;
-      load_region(A0);
-      __syncthreads();
-      continue;
-    }
-
-    // ---------------- expand: 16 deltas per thread per pass
-    for (uint32_t pass = 0; pass < dcount; pass += DPT * WG) {
-      const uint32_t d0 = pass + (uint32_t)tid * DPT;
-      uint64_t v[DPT];
-      uint64_t s = 0;
-      if (d0 < dcount) {
-        // locate block of d0
-        int b = 0;
-        while (b + 1 < (int)nb && sm.first_delta[b + 1] <= d0) ++b;
-        uint64_t inb = d0 - sm.first_delta[b];
-        uint32_t m = (uint32_t)(inb / vpmb);
-        uint32_t k = (uint32_t)(inb - (uint64_t)m * vpmb);
-#pragma unroll
-        for (int j = 0; j < DPT; ++j) {
-          v[j] = 0;
-          if (d0 + j < dcount) {
-            const uint32_t wdt = sm.width[b][m];
-            const uint64_t bit = ((uint64_t)sm.pay[b] + sm.mboff[b][m]) * 8ull + (uint64_t)k * wdt;
-            const uint64_t abs = S + (bit >> 3);
-            const uint32_t sh = (uint32_t)(bit & 7);
-            uint64_t x;
-            const uint64_t ri = abs - A0;
-            if (abs >= A0 && ri + 12 <= (uint64_t)DREGION) x = lload_u64(sm.region, (uint32_t)ri);
-            else x = gload_u64(blob, blob_len, abs);
-            uint64_t raw;
-            if (wdt == 0) raw = 0;
-            else if (wdt + sh <= 64) {
-              raw = x >> sh;
-              if (wdt < 64) raw &= (1ull << wdt) - 1ull;
-            } else {  // 58..64-bit deltas straddle a 64-bit window
-              uint64_t hi = (abs >= A0 && ri + 20 <= (uint64_t)DREGION)
-                                ? lload_u64(sm.region, (uint32_t)ri + 8)
-                                : gload_u64(blob, blob_len, abs + 8);
-              raw = (x >> sh) | (hi << (64 - sh));
-              if (wdt < 64) raw &= (1ull << wdt) - 1ull;
-            }
-            v[j] = sm.mind[b] + raw;  // min_delta + delta (wrapping)
-            s += v[j];
-            if (++k == vpmb) {
-              k = 0;
-              if (++m == (uint32_t)nmb) {
-                m = 0;
-                ++b;
-              }
-            }
-          }
-        }
-      }
-      // workgroup exclusive scan of s
-      uint64_t incl = s;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        uint64_t y = __shfl_up(incl, off, 64);
-        if ((tid & 63) >= off) incl += y;
-      }
-      if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
-      __syncthreads();
-      uint64_t pre = carry;
-      for (int w = 0; w < (tid >> 6); ++w) pre += sm.wsum[w];
-      pre += incl - s;
-      uint64_t tot = carry + sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
-      if (d0 < dcount) {
-        // output index of delta d is (done + d + 1)
-        uint64_t oi = done + d0 + 1;
-        uint64_t acc = pre;
-        if (ES == 8) {
-          int64_t* op = reinterpret_cast<int64_t*>(o);
-#pragma unroll
-          for (int j = 0; j < DPT; ++j) {
-            if (d0 + j < dcount) {
-              acc += v[j];
-              op[oi + j] = (int64_t)acc;
-            }
-          }
-        } else {
-          int32_t* op = reinterpret_cast<int32_t*>(o);
-#pragma unroll
-          for (int j = 0; j < DPT; ++j) {
-            if (d0 + j < dcount) {
-              acc += v[j];
-              op[oi + j] = (int32_t)(uint32_t)acc;
-            }
-          }
-        }
-      }
-      __syncthreads();
-      carry = tot;
-    }
-    done += dcount;
-    pos = ncur;
-    __syncthreads();
-    if (done < need && S + pos - A0 >= DBLK) {
-      A0 = (S + pos) & ~15ull;
-      load_region(A0);
-      __syncthreads();
-    }
-  }
+  DeltaInfo info;
+  // the decoder's set_data ignores num_values; read_batch asks for the non-null count
+  int32_t st = delta_stream<ES>(sm, blob, blob_len, pw.base + pw.val_off, pw.val_bytes, pw.nonnull,
+                                pw.nonnull, out + pw.value_out * ES, info);
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 
 extern "C" hipError_t pqg_launch_delta(const uint8_t* blob, uint64_t blob_len, PageWork* pages,

@@ -26,9 +26,10 @@ namespace pqg {
 
 // Diagnostic counters (pqg_debug_set / pqg_debug_read): mode bit 0 skips expansion, bit 1
 // skips the walk after the first batch, bit 2 accumulates s_memtime stamps. Mode 0 is the
-// production path (one scalar load per workgroup).
-extern __device__ uint32_t g_pqg_debug_mode;
-extern __device__ unsigned long long g_pqg_stats[16];
+// production path (one scalar load per workgroup). Each translation unit has its own copy
+// (no relocatable device code); the switches act on the kernels of pqg_kernels.hip.
+static __device__ uint32_t g_pqg_debug_mode = 0;
+static __device__ unsigned long long g_pqg_stats[16];
 
 __device__ inline uint64_t hb_clock() { return __builtin_amdgcn_s_memtime(); }
 

@@ -17,8 +17,6 @@
 
 namespace pqg {
 
-__device__ uint32_t g_pqg_debug_mode = 0;
-__device__ unsigned long long g_pqg_stats[16];
 
 // ------------------------------------------------------------------------------ prepare
 

@@ -36,6 +36,9 @@ hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint8_t
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, int, bool, bool,
+                            uint64_t*, uint32_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t,
+                            int64_t*, uint8_t*, ChunkResult*, hipStream_t);
 }
 
 // Two staging slots so consecutive async decodes never overwrite pinned memory that an
@@ -48,6 +51,15 @@ struct Slot {
   ChunkResult* h_res = nullptr;  // pinned
   hipEvent_t ev[6] = {};
   bool used = false;
+  // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix;
+  // per dictionary entry source address and length
+  uint64_t* vsrc = nullptr;
+  uint32_t* vlen = nullptr;
+  uint32_t* vpre = nullptr;
+  size_t vcap = 0;
+  uint64_t* dsrc = nullptr;
+  uint32_t* dlen = nullptr;
+  size_t dcap = 0;
 };
 
 struct pqg_ctx {
@@ -148,6 +160,11 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipHostFree(sl.h_pages);
     hipFree(sl.d_res);
     hipHostFree(sl.h_res);
+    hipFree(sl.vsrc);
+    hipFree(sl.vlen);
+    hipFree(sl.vpre);
+    hipFree(sl.dsrc);
+    hipFree(sl.dlen);
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   delete ctx;
@@ -181,10 +198,6 @@ static int validate_pages(const pqg_column* col, const pqg_page* pages, uint32_t
         why = "Invalid/Unsupported encoding type for dictionary";
         return PQG_ERR_NYI;  // column/reader.rs:483-486
       }
-      if (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) {
-        why = "BYTE_ARRAY/FLBA dictionaries are not implemented on the GPU path yet";
-        return PQG_ERR_NYI;
-      }
       *dict_page = (int)i;
       continue;
     }
@@ -199,10 +212,6 @@ static int validate_pages(const pqg_column* col, const pqg_page* pages, uint32_t
         }
         break;
       case PQG_PLAIN:
-        if (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) {
-          why = "PLAIN BYTE_ARRAY/FLBA is not implemented on the GPU path yet";
-          return PQG_ERR_NYI;
-        }
         break;
       case PQG_RLE:
         if (t != PQG_BOOLEAN) {
@@ -221,15 +230,13 @@ static int validate_pages(const pqg_column* col, const pqg_page* pages, uint32_t
           why = "DeltaLengthByteArrayDecoder only support ByteArrayType";
           return PQG_ERR_GENERAL;
         }
-        why = "DELTA_LENGTH_BYTE_ARRAY is not implemented on the GPU path yet";
-        return PQG_ERR_NYI;
+        break;
       case PQG_DELTA_BYTE_ARRAY:
         if (t != PQG_BYTE_ARRAY && t != PQG_FIXED_LEN_BYTE_ARRAY) {
           why = "DeltaByteArrayDecoder only supports ByteArrayType and FixedLenByteArrayType";
           return PQG_ERR_GENERAL;
         }
-        why = "DELTA_BYTE_ARRAY is not implemented on the GPU path yet";
-        return PQG_ERR_NYI;
+        break;
       default:
         why = "Encoding is not supported";
         return PQG_ERR_NYI;  // get_decoder, decoding.rs:76
@@ -348,8 +355,35 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (npages) HIPCHK(hipMemcpyAsync(ctx->d_pages, ctx->h_pages, npages * sizeof(PageWork), hipMemcpyHostToDevice, s), "H2D pages");
   HIPCHK(hipMemcpyAsync(ctx->d_res, ctx->h_res, sizeof(ChunkResult), hipMemcpyHostToDevice, s), "H2D res");
 
-  const int es = value_size(t, col->type_length);
+  const bool is_ba = t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY;
+  const int es = is_ba ? 0 : value_size(t, col->type_length);
   const int np = (int)npages;
+  if (is_ba && out->values) {
+    if (!out->offsets || out->offsets_capacity < lev_needed + 1)
+      return set_err(ctx, PQG_ERR_INVALID, "BYTE_ARRAY/FLBA output needs offsets[num_levels + 1]");
+    size_t need = lev_needed ? lev_needed : 1;
+    if (need > sl.vcap) {
+      hipFree(sl.vsrc);
+      hipFree(sl.vlen);
+      hipFree(sl.vpre);
+      sl.vsrc = nullptr;
+      sl.vlen = sl.vpre = nullptr;
+      HIPCHK(hipMalloc(&sl.vsrc, need * 8), "hipMalloc vsrc");
+      HIPCHK(hipMalloc(&sl.vlen, need * 4), "hipMalloc vlen");
+      HIPCHK(hipMalloc(&sl.vpre, need * 4), "hipMalloc vpre");
+      sl.vcap = need;
+    }
+    size_t dn = dict_page >= 0 && pages[dict_page].num_values ? pages[dict_page].num_values : 1;
+    if (dn > sl.dcap) {
+      hipFree(sl.dsrc);
+      hipFree(sl.dlen);
+      sl.dsrc = nullptr;
+      sl.dlen = nullptr;
+      HIPCHK(hipMalloc(&sl.dsrc, dn * 8), "hipMalloc dsrc");
+      HIPCHK(hipMalloc(&sl.dlen, dn * 4), "hipMalloc dlen");
+      sl.dcap = dn;
+    }
+  }
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, ctx->d_res, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
@@ -360,7 +394,18 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
   uint8_t* vo = (uint8_t*)out->values;
   ctx->values_kernel = 0;
-  if (np && vo) {
+  if (np && vo && is_ba) {
+    ctx->values_kernel = enc_present[PQG_RLE_DICTIONARY] ? PQG_RLE_DICTIONARY
+                         : enc_present[PQG_DELTA_BYTE_ARRAY] ? PQG_DELTA_BYTE_ARRAY
+                         : enc_present[PQG_DELTA_LENGTH_BYTE_ARRAY] ? PQG_DELTA_LENGTH_BYTE_ARRAY
+                                                                     : PQG_PLAIN;
+    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, dict_page,
+                            t == PQG_FIXED_LEN_BYTE_ARRAY ? col->type_length : 0,
+                            enc_present[PQG_RLE_DICTIONARY], enc_present[PQG_DELTA_BYTE_ARRAY],
+                            sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, out->values_capacity,
+                            out->offsets, vo, ctx->d_res, s),
+           "byte arrays");
+  } else if (np && vo) {
     if (enc_present[PQG_PLAIN]) {
       ctx->values_kernel = PQG_PLAIN;
       if (t == PQG_BOOLEAN)

@@ -210,30 +210,50 @@ def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_
 
     Equivalent to reading every batch of ColumnReaderImpl::read_batch (column/reader.rs
     :159-265) and concatenating: def/rep levels are the full level streams, values the
-    dense non-null values."""
+    dense non-null values (BYTE_ARRAY/FLBA: list of bytes, plus "offsets" and "bytes")."""
     torch = _torch()
     dev = device if device is not None else torch.device("cuda", ctx.device)
     blob, pages = make_pages(specs)
     d_blob = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
     nlev = sum(s.num_values for s in specs if s.page_type in (PAGE_DATA, PAGE_DATA_V2))
+    ba = ptype in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY)
     es = VALUE_SIZE.get(ptype, max(type_length, 1))
-    cap_vals = values_capacity if values_capacity is not None else max(nlev, 1) * es
+    if values_capacity is not None:
+        cap_vals = values_capacity
+    elif ba:
+        cap_vals = max(len(blob), 64)
+    else:
+        cap_vals = max(nlev, 1) * es
     d_def = torch.empty(max(nlev, 1) + 8, dtype=torch.int16, device=dev) if (want_def and max_def > 0) else None
     d_rep = torch.empty(max(nlev, 1) + 8, dtype=torch.int16, device=dev) if (want_rep and max_rep > 0) else None
-    d_val = torch.empty(cap_vals + 64, dtype=torch.uint8, device=dev)
-    out = Output(d_def.data_ptr() if d_def is not None else None,
-                 d_rep.data_ptr() if d_rep is not None else None,
-                 d_val.data_ptr(), cap_vals, None, 0, 0, 0, 0)
+    d_off = torch.empty(nlev + 2, dtype=torch.int64, device=dev) if ba else None
     col = Column(ptype, type_length, max_def, max_rep)
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    ctx.decode_async(col, d_blob.data_ptr(), len(blob), pages, out, s, npages=len(specs))
-    st, bad = ctx.sync()
+    for attempt in range(2):
+        d_val = torch.empty(cap_vals + 64, dtype=torch.uint8, device=dev)
+        out = Output(d_def.data_ptr() if d_def is not None else None,
+                     d_rep.data_ptr() if d_rep is not None else None,
+                     d_val.data_ptr(), cap_vals, d_off.data_ptr() if ba else None,
+                     nlev + 1 if ba else 0, 0, 0, 0)
+        ctx.decode_async(col, d_blob.data_ptr(), len(blob), pages, out, s, npages=len(specs))
+        st, bad = ctx.sync()
+        if st == CAPACITY and ba and attempt == 0 and values_capacity is None and out.num_bytes > cap_vals:
+            cap_vals = int(out.num_bytes)
+            continue
+        break
     res = {"status": st, "page": bad, "message": ctx.error_message() if st else "",
-           "num_levels": out.num_levels, "num_values": out.num_values}
+           "num_levels": out.num_levels, "num_values": out.num_values, "num_bytes": out.num_bytes}
     nl, nv = out.num_levels, out.num_values
     res["def"] = d_def[:nl].cpu().numpy() if (d_def is not None and not st) else np.zeros(0, np.int16)
     res["rep"] = d_rep[:nl].cpu().numpy() if (d_rep is not None and not st) else np.zeros(0, np.int16)
-    if not st:
+    if st:
+        res["values"] = np.zeros(0, np.uint8)
+    elif ba:
+        offs = d_off[: nv + 1].cpu().numpy()
+        raw = d_val[: out.num_bytes].cpu().numpy().tobytes()
+        res["offsets"], res["bytes"] = offs, raw
+        res["values"] = [raw[offs[i]:offs[i + 1]] for i in range(nv)]
+    else:
         raw = d_val[: nv * es].cpu().numpy()
         if ptype == INT96:
             res["values"] = raw.reshape(-1, 12)
@@ -241,8 +261,6 @@ def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_
             res["values"] = raw.view(NP_DTYPE[ptype])
         else:
             res["values"] = raw
-    else:
-        res["values"] = np.zeros(0, np.uint8)
     return res
 
 

@@ -1,0 +1,203 @@
+"""GPU parity for BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY columns against the C oracle: PLAIN
+(decoding.rs:206-247), dictionary (:256-315), DELTA_LENGTH_BYTE_ARRAY (:629-712) and
+DELTA_BYTE_ARRAY (:722-835), including the error classes the reference raises."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import pqgpu
+    c = pqgpu.Context(0)
+    yield c
+    c.close()
+
+
+def rand_strings(rng, n, lo=0, hi=40, alphabet=b"abcdefghij"):
+    lens = rng.integers(lo, hi + 1, n)
+    a = np.frombuffer(alphabet, np.uint8)
+    return [bytes(a[rng.integers(0, len(a), l)]) for l in lens]
+
+
+def sorted_strings(rng, n):
+    """Shared prefixes, the case DELTA_BYTE_ARRAY exists for."""
+    base = [b"http://www.example.com/" + b"/".join(rand_strings(rng, 3, 1, 6)) for _ in range(n)]
+    return sorted(base)
+
+
+def check(oracle, ctx, ptype, pages, max_def=0, type_length=-1, expect=0):
+    import pqgpu
+    ref = oracle.read_column(ptype, pages, max_def=max_def, type_length=type_length)
+    got = pqgpu.decode_column(ctx, ptype, pages, max_def=max_def, type_length=type_length)
+    assert ref["status"] == expect, ref["message"]
+    assert got["status"] == expect, got["message"]
+    if expect:
+        return got, ref
+    if max_def:
+        np.testing.assert_array_equal(got["def"], ref["def"])
+    assert got["num_values"] == len(ref["values"])
+    assert got["bytes"] == ref["bytes"]
+    np.testing.assert_array_equal(got["offsets"], ref["offsets"])
+    return got, ref
+
+
+def optional_pages(oracle, rng, sizes, p_null, make_values, encode, encoding, v2=False):
+    pages = []
+    for n in sizes:
+        lv = (rng.random(n) >= p_null).astype(np.int16)
+        vals = make_values(int(lv.sum()))
+        body = encode(vals)
+        if v2:
+            lev = oracle.level_encode(lv, 1, oracle.RLE, v2=True)
+            pages.append(oracle.PageSpec(oracle.PAGE_DATA_V2, lev + body, n, encoding, def_len=len(lev)))
+        else:
+            lev = oracle.level_encode(lv, 1)
+            pages.append(oracle.PageSpec(oracle.PAGE_DATA, lev + body, n, encoding))
+    return pages
+
+
+@pytest.mark.parametrize("p_null", [0.0, 0.3, 1.0])
+def test_plain_byte_array(oracle, ctx, p_null):
+    rng = np.random.default_rng(1)
+    pages = optional_pages(oracle, rng, [1, 100, 5000, 20000], p_null,
+                           lambda n: rand_strings(rng, n), oracle.plain_encode_ba, oracle.PLAIN)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+def test_plain_byte_array_long_values(oracle, ctx):
+    rng = np.random.default_rng(2)
+    vals = rand_strings(rng, 300, 0, 70000)
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.plain_encode_ba(vals), len(vals), oracle.PLAIN)]
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+
+
+@pytest.mark.parametrize("tl", [1, 12, 16, 37])
+def test_plain_flba(oracle, ctx, tl):
+    rng = np.random.default_rng(tl)
+    pages = optional_pages(oracle, rng, [10, 3000], 0.2, lambda n: rand_strings(rng, n, tl, tl),
+                           lambda v: oracle.plain_encode_ba(v, fixed=True), oracle.PLAIN)
+    check(oracle, ctx, oracle.FIXED_LEN_BYTE_ARRAY, pages, max_def=1, type_length=tl)
+
+
+def _dict_pages(oracle, rng, ptype, distinct, sizes, p_null, fixed=False, v2=False):
+    dict_vals = list(dict.fromkeys(distinct))
+    dpage = oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode_ba(dict_vals, fixed=fixed),
+                            len(dict_vals), oracle.PLAIN)
+    bw = max(1, int(np.ceil(np.log2(len(dict_vals)))))
+
+    def enc(vals):
+        return bytes([bw]) + oracle.rle_encode(np.array(vals, np.uint64), bw)
+
+    pages = optional_pages(oracle, rng, sizes, p_null,
+                           lambda n: rng.integers(0, len(dict_vals), n).tolist(), enc,
+                           oracle.RLE_DICTIONARY, v2=v2)
+    return [dpage] + pages
+
+
+def test_dictionary_byte_array(oracle, ctx):
+    rng = np.random.default_rng(3)
+    pages = _dict_pages(oracle, rng, oracle.BYTE_ARRAY, rand_strings(rng, 500, 0, 30), [100, 7000, 1], 0.25)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+def test_dictionary_flba_v2(oracle, ctx):
+    rng = np.random.default_rng(4)
+    pages = _dict_pages(oracle, rng, oracle.FIXED_LEN_BYTE_ARRAY, rand_strings(rng, 300, 16, 16),
+                        [4000, 900], 0.1, fixed=True, v2=True)
+    check(oracle, ctx, oracle.FIXED_LEN_BYTE_ARRAY, pages, max_def=1, type_length=16)
+
+
+@pytest.mark.parametrize("p_null", [0.0, 0.4])
+def test_delta_length_byte_array(oracle, ctx, p_null):
+    rng = np.random.default_rng(5)
+    pages = optional_pages(oracle, rng, [1, 129, 6000, 30000], p_null,
+                           lambda n: rand_strings(rng, n, 0, 50), oracle.delta_length_encode,
+                           oracle.DELTA_LENGTH_BYTE_ARRAY)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+@pytest.mark.parametrize("p_null", [0.0, 0.4])
+def test_delta_byte_array(oracle, ctx, p_null):
+    rng = np.random.default_rng(6)
+    pages = optional_pages(oracle, rng, [1, 200, 5000], p_null, lambda n: sorted_strings(rng, n),
+                           oracle.delta_byte_array_encode, oracle.DELTA_BYTE_ARRAY, v2=True)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+def test_delta_byte_array_flba(oracle, ctx):
+    rng = np.random.default_rng(7)
+    vals = sorted(rand_strings(rng, 3000, 10, 10, b"ab"))
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_byte_array_encode(vals), len(vals),
+                             oracle.DELTA_BYTE_ARRAY)]
+    check(oracle, ctx, oracle.FIXED_LEN_BYTE_ARRAY, pages, type_length=10)
+
+
+def test_mixed_encodings_in_one_chunk(oracle, ctx):
+    """Dictionary pages, then fallback pages in other encodings (writer fallback)."""
+    rng = np.random.default_rng(8)
+    pages = _dict_pages(oracle, rng, oracle.BYTE_ARRAY, rand_strings(rng, 100), [3000], 0.2)
+    pages += optional_pages(oracle, rng, [2000], 0.2, lambda n: rand_strings(rng, n), oracle.plain_encode_ba, oracle.PLAIN)
+    pages += optional_pages(oracle, rng, [2000], 0.2, lambda n: rand_strings(rng, n), oracle.delta_length_encode,
+                            oracle.DELTA_LENGTH_BYTE_ARRAY)
+    pages += optional_pages(oracle, rng, [2000], 0.2, lambda n: sorted_strings(rng, n), oracle.delta_byte_array_encode,
+                            oracle.DELTA_BYTE_ARRAY)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+# ---- errors: same status class and page as the oracle
+
+def _err(oracle, ctx, ptype, pages, **kw):
+    import pqgpu
+    ref = oracle.read_column(ptype, pages, **kw)
+    got = pqgpu.decode_column(ctx, ptype, pages, **kw)
+    assert ref["status"] != 0
+    assert got["status"] == ref["status"], (got["message"], ref["message"])
+    return got
+
+
+def test_plain_ba_truncated_length_prefix(oracle, ctx):
+    body = oracle.plain_encode_ba([b"abc", b"de"])[:-4]  # second value's length cut
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, body, 2, oracle.PLAIN)])
+
+
+def test_plain_ba_truncated_value(oracle, ctx):
+    body = oracle.plain_encode_ba([b"abc", b"defgh"])[:-2]
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, body, 2, oracle.PLAIN)])
+
+
+def test_dlba_lengths_past_data(oracle, ctx):
+    body = oracle.delta_length_encode([b"abcdef", b"ghijkl"])[:-3]
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, body, 2, oracle.DELTA_LENGTH_BYTE_ARRAY)])
+
+
+def test_dba_prefix_longer_than_previous(oracle, ctx):
+    # prefix lengths [0, 9] with a 3-byte first value: previous_value[0..9] panics
+    prefixes = oracle.delta_encode(oracle.INT32, np.array([0, 9], np.int32))
+    suffixes = oracle.delta_length_encode([b"abc", b"x"])
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, prefixes + suffixes, 2, oracle.DELTA_BYTE_ARRAY)])
+
+
+def test_dba_suffix_reuse(oracle, ctx):
+    """More prefixes than suffixes: the reference reuses the last suffix (decoding.rs:796-801)."""
+    prefixes = oracle.delta_encode(oracle.INT32, np.array([0, 1, 2], np.int32))
+    suffixes = oracle.delta_length_encode([b"ab"])
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, prefixes + suffixes, 3, oracle.DELTA_BYTE_ARRAY)]
+    got, ref = check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+    assert ref["values"] == [b"ab", b"aab", b"aaab"]
+
+
+def test_bad_dictionary_index_ba(oracle, ctx):
+    dpage = oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode_ba([b"a", b"b"]), 2, oracle.PLAIN)
+    body = bytes([2]) + oracle.rle_encode(np.array([0, 3, 1], np.uint64), 2)
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [dpage, oracle.PageSpec(oracle.PAGE_DATA, body, 3, oracle.RLE_DICTIONARY)])
+
+
+def test_truncated_dictionary_page_ba(oracle, ctx):
+    dbytes = oracle.plain_encode_ba([b"abc", b"defg"])[:-1]
+    dpage = oracle.PageSpec(oracle.PAGE_DICTIONARY, dbytes, 2, oracle.PLAIN)
+    body = bytes([1]) + oracle.rle_encode(np.array([0, 1], np.uint64), 1)
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [dpage, oracle.PageSpec(oracle.PAGE_DATA, body, 2, oracle.RLE_DICTIONARY)])
