@@ -43,10 +43,14 @@ def parse():
     ap.add_argument("--mini-blocks", type=int, default=4)
     ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0 / 0.1 variants")
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--pcie", type=int, default=1, help="also time the host-to-host (PCIe) rate")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0x5EED0000)
     return ap.parse_args()
+
+
+from sharding import shard_seed  # noqa: E402  (row-group partition per rank)
 
 
 class Workload:
@@ -58,7 +62,7 @@ class Workload:
         L = pqgpu.lib()
         info = pqgpu.WorkloadInfo()
         n = int(args.n)
-        seed = args.seed + 2 + 1000003 * rank
+        seed = shard_seed(args.seed + 2, rank)
         self.kind = kind
         self.p_null = p_null
         if kind == "levels":
@@ -67,13 +71,13 @@ class Workload:
             self.col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
             self.es = 4
         elif kind == "dict":
-            seed = args.seed + 3 + 1000003 * rank
+            seed = shard_seed(args.seed + 3, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64(
                 n, args.dict_size, args.page_values, seed, args.threads, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
         else:
-            seed = args.seed + 4 + 1000003 * rank
+            seed = shard_seed(args.seed + 4, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64(
                 n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, seed,
                 args.threads, blob, cap, pages, pcap, C.byref(info))
@@ -195,6 +199,35 @@ def cpu_baseline(w, seconds, threads):
                       f"thread-owned reader, {dt:.1f}s wall"}
 
 
+def pcie_inclusive(pqgpu, ctx, w, stream, iters=3):
+    """Host-to-host rate of the same decode (north_star): pinned page bytes -> HBM, decode,
+    decoded levels/values -> pinned host memory, all on the decode stream."""
+    import torch
+    h_blob = torch.from_numpy(w.host).pin_memory()
+    h_def = torch.empty(w.levels, dtype=torch.int16).pin_memory() if w.d_def is not None else None
+    h_val = torch.empty(w.values * w.es, dtype=torch.uint8).pin_memory()
+    s = torch.cuda.ExternalStream(stream)
+    best = None
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            w.d_blob.copy_(h_blob, non_blocking=True)
+            decode_once(pqgpu, ctx, w, stream)
+            if h_def is not None:
+                h_def.copy_(w.d_def[: w.levels], non_blocking=True)
+            h_val.copy_(w.d_val[: w.values * w.es], non_blocking=True)
+        st, bad = ctx.sync()
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        assert st == 0, (st, bad)
+        best = dt if best is None else min(best, dt)
+    units = w.levels if w.kind == "levels" else w.values
+    moved = w.blob_len + (2 * w.levels if h_def is not None else 0) + w.values * w.es
+    return {"values_per_s": units / best, "ms": best * 1e3, "pcie_bytes": moved,
+            "note": "pinned H2D of page bytes + decode + D2H of decoded levels/values, best of %d" % iters}
+
+
 def copy_ceiling_gbs(nbytes=4 << 30):
     import torch
     a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
@@ -228,6 +261,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     import pqgpu
+    import sharding
     ctx = pqgpu.Context(torch.cuda.current_device(), timing=True)
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -235,11 +269,7 @@ def main():
     w = Workload(pqgpu, args, rank, kind, p_null=args.p_null if kind == "levels" else None)
     spot_check(pqgpu, ctx, w, stream)
     per_step, tm = time_steps(pqgpu, ctx, w, stream, args.steps, args.warmup, dist)
-    # max over ranks
-    if dist is not None:
-        t = torch.tensor([per_step], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        per_step = float(t.item())
+    per_step = sharding.max_over_ranks(per_step, dist, device="cuda")
     units = w.levels if kind == "levels" else w.values
     value = units * world / per_step
     step_bytes = w.in_bytes + w.out_bytes
@@ -257,7 +287,7 @@ def main():
     achieved = nbytes / (ms * 1e-3) / 1e9
 
     result = {
-        "metric": "decoded values/s + GB/s, device-resident page decode",
+        "metric": "decoded values/s + GB/s, device-resident page decode, 1/2/4/8 MI355X",
         "value": value,
         "unit": "values/s",
         "n_gpus": world,
@@ -267,8 +297,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"levels": "i16 levels + i32 values", "dict": "u16 indices -> i64",
-                  "delta": "i64 (wrapping)"}[kind],
+        "dtype": {"levels": "int16 levels + int32 values", "dict": "uint16 indices -> int64",
+                  "delta": "int64 (wrapping)"}[kind],
         "data": "synthetic pages from reference-identical writers (SplitMix64 seeded)",
         "gbps": step_bytes / per_step / 1e9 * world,
         "config": {"workload": {"levels": "configs[1]: RLE/bit-packed def levels (max_def 1) + PLAIN INT32",
@@ -292,6 +322,8 @@ def main():
             result["copy_ceiling_gbs"] = copy_ceiling_gbs()
         except Exception as e:  # pragma: no cover
             result["copy_ceiling_gbs"] = str(e)
+    if rank == 0 and args.pcie and world == 1:
+        result["pcie_inclusive"] = pcie_inclusive(pqgpu, ctx, w, stream)
     if rank == 0 and args.cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, min(args.threads, os.cpu_count() or 1))
     if kind == "levels" and args.variants and world == 1:
