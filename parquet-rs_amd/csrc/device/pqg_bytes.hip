@@ -17,7 +17,7 @@
 // PLAIN BYTE_ARRAY lengths are inline ([u32 len][bytes]...), so value starts form a serial
 // chain: one lane walks it over LDS-staged 16 KiB regions of the page.
 #include "pqg_delta.hpp"
-#include "pqg_hybrid.hpp"
+#include "pqg_runs.hpp"
 
 namespace pqg {
 
@@ -170,38 +170,29 @@ struct BaDictEmit {
   }
 };
 
-__global__ void __launch_bounds__(WG, 4) k_ba_dict_idx(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages, int dict_page,
-                                                    const uint64_t* dsrc, const uint32_t* dlen,
-                                                    uint64_t* vsrc, uint32_t* vlen, ChunkResult* res) {
-  __shared__ HybridSmem sm;
-  const int p = blockIdx.x;
-  const PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_RLE_DICTIONARY) return;
-  if (dict_page < 0) {
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
-    return;
-  }
-  const PageWork dp = pages[dict_page];
-  if (dp.status != 0) return;
-  if (pw.val_bytes < 1) {  // DictDecoder::set_data reads the bit width byte (data[0])
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
-    return;
-  }
-  const uint64_t n = pw.nonnull;
-  if (n == 0) return;
-  const int w = blob[pw.base + pw.val_off];
-  // hybrid_decode emits global value indices (out_base = value_out)
-  BaDictEmit em{dsrc, dlen, dp.num_values, vsrc, vlen, 0, 0};
-  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 1, pw.val_bytes - 1, w,
-                             (uint32_t)n, LK_RLE, pw.value_out, sm, em);
-  uint64_t t = block_sum_u64(em.bytes, reinterpret_cast<uint64_t*>(sm.red));
-  if (threadIdx.x == 0) {
-    if (st) report(pages, res, p, st);
-    else pages[p].nbytes_out = t;
-  }
+// Dictionary indices -> (source, length) of the entry, expand pass over all tiles (the index
+// pass is k_run_index with SS_DICT); page byte counts accumulate per tile.
+__global__ void __launch_bounds__(WG) k_expand_badict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                      PageWork* pages,
+                                                      const uint32_t* __restrict__ tile_page,
+                                                      const RunCkpt* __restrict__ ck, ColumnParams cp,
+                                                      int dict_page, const uint64_t* dsrc,
+                                                      const uint32_t* dlen, uint64_t* vsrc,
+                                                      uint32_t* vlen, ChunkResult* res) {
+  __shared__ ExpandSmem sm;
+  int p;
+  Stream s;
+  uint32_t lo, hi, next_pos;
+  RunCkpt c;
+  if (dict_page < 0 || pages[dict_page].status != 0) return;
+  if (!expand_setup(blob, pages, tile_page, ck, cp, SS_DICT, p, s, lo, hi, c, next_pos)) return;
+  // emitted indices are global value indices (out = value_out)
+  BaDictEmit em{dsrc, dlen, pages[dict_page].num_values, vsrc, vlen, 0, 0};
+  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
+  const uint64_t t = block_sum_u64(em.bytes, sm.red);
+  if (em.err) report(pages, res, p, em.err);
+  if (threadIdx.x == 0 && t)
+    atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nbytes_out), (unsigned long long)t);
 }
 
 __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -410,18 +401,29 @@ __global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blo
   }
 }
 
+// Dictionary pages: k_ba_dict_prep, then the caller's index pass (pqg_launch_run_index with
+// SS_DICT) between this and pqg_launch_bytes.
+extern "C" hipError_t pqg_launch_ba_dict_prep(const uint8_t* blob, uint64_t blob_len,
+                                              PageWork* pages, int dict_page, int type_length,
+                                              uint64_t* dsrc, uint32_t* dlen, ChunkResult* res,
+                                              hipStream_t s) {
+  if (dict_page >= 0)
+    hipLaunchKernelGGL(k_ba_dict_prep, dim3(1), dim3(WG), 0, s, blob, blob_len, pages, dict_page,
+                       type_length, dsrc, dlen, res);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                       int npages, int dict_page, int type_length, bool has_dict,
-                                       bool has_dba, uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre,
+                                       int npages, uint32_t ntiles, ColumnParams cp,
+                                       const uint32_t* tile_page, const RunCkpt* ck, int dict_page,
+                                       int type_length, bool has_dict, bool has_dba,
+                                       uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre,
                                        uint64_t* dsrc, uint32_t* dlen, uint64_t cap,
                                        int64_t* offsets, uint8_t* out, ChunkResult* res,
                                        hipStream_t s) {
-  if (has_dict && dict_page >= 0)
-    hipLaunchKernelGGL(k_ba_dict_prep, dim3(1), dim3(WG), 0, s, blob, blob_len, pages, dict_page,
-                       type_length, dsrc, dlen, res);
-  if (has_dict)
-    hipLaunchKernelGGL(k_ba_dict_idx, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages,
-                       dict_page, dsrc, dlen, vsrc, vlen, res);
+  if (has_dict && ntiles)
+    hipLaunchKernelGGL(k_expand_badict, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages,
+                       tile_page, ck, cp, dict_page, dsrc, dlen, vsrc, vlen, res);
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, type_length,
                      vsrc, vlen, vpre, res);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);

@@ -12,8 +12,8 @@
 //   k_finalize       chunk status
 //
 // All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
-// (walker wave + expander waves, pipelined over LDS-staged regions) is in pqg_hybrid.hpp.
-#include "pqg_hybrid.hpp"
+// (index pass + grid-wide expand pass) is in pqg_runs.hpp.
+#include "pqg_runs.hpp"
 
 namespace pqg {
 
@@ -67,10 +67,11 @@ __device__ inline int64_t v1_level_stream(const uint8_t* page, uint32_t nbytes, 
 
 __global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
                           PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                          ChunkResult* res) {
+                          uint32_t* __restrict__ tile_page, ChunkResult* res) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npages) return;
   PageWork pw = pages[p];
+  for (uint32_t k = 0; k < pw.ntiles; ++k) tile_page[pw.ltile0 + k] = (uint32_t)p;
   const int32_t host_status = pw.status;  // set by the host for pages the reference rejects
   pw.rep_kind = pw.def_kind = LK_NONE;
   pw.rep_off = pw.rep_bytes = pw.def_off = pw.def_bytes = 0;
@@ -131,10 +132,29 @@ __global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
   if (err) atomicMin(&res->first_bad_page, p);
 }
 
-// ------------------------------------------------------------------------------ RLE hybrid
-// see pqg_hybrid.hpp
+// ------------------------------------------------------------------------------ hybrid streams
 
-// ------------------------------------------------------------------------------ levels
+// Index pass over stream `sel` of every page (one wave per page), pqg_runs.hpp.
+__global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                  PageWork* pages, ColumnParams cp, int sel,
+                                                  int dict_page, RunCkpt* __restrict__ ck,
+                                                  ChunkResult* res) {
+  __shared__ IndexSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  Stream s;
+  if (!get_stream(blob, pw, sel, cp, s)) return;
+  if (sel == SS_DICT) {
+    if (dict_page < 0) {  // "Decoder for dict should have been set"
+      if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+      return;
+    }
+    if (pages[dict_page].status != 0) return;
+  }
+  const int32_t st = run_index(blob, blob_len, s, ck + pw.ltile0, sm);
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
+}
 
 struct LevelEmit {
   int16_t* out;
@@ -163,32 +183,26 @@ struct LevelEmit {
   }
 };
 
-// which: 0 = definition levels, 1 = repetition levels. One workgroup per page.
-__global__ void __launch_bounds__(WG, 4) k_rle_levels(const uint8_t* __restrict__ blob,
-                                                   uint64_t blob_len, PageWork* pages,
-                                                   ColumnParams cp, int which,
-                                                   int16_t* __restrict__ out,
-                                                   ChunkResult* res) {
-  __shared__ HybridSmem sm;
-  const int p = blockIdx.x;
-  PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  uint32_t off = which ? pw.rep_off : pw.def_off;
-  uint32_t len = which ? pw.rep_bytes : pw.def_bytes;
-  int kind = which ? pw.rep_kind : pw.def_kind;
-  int w = which ? cp.rep_bit_width : cp.def_bit_width;
-  if (kind == LK_NONE) return;
-  LevelEmit em{out, which ? cp.max_rep : cp.max_def, which == 0, 0, 0};
-  int32_t st = hybrid_decode(blob, blob_len, pw.base + off, len, w, pw.num_values, kind,
-                             pw.level_out, sm, em);
-  if (st) {
-    if (threadIdx.x == 0) report(pages, res, p, st);
-    return;
-  }
-  if (which == 0) {
-    uint64_t t = block_sum_u64(em.nonnull, sm.red);
-    if (threadIdx.x == 0) pages[p].nonnull = t;
+// Expand pass of a level stream (which: SS_DEF / SS_REP); def levels also count the values
+// read_batch will ask for (def == max_def, column/reader.rs:212-226).
+__global__ void __launch_bounds__(WG) k_expand_levels(const uint8_t* __restrict__ blob,
+                                                      uint64_t blob_len, PageWork* pages,
+                                                      const uint32_t* __restrict__ tile_page,
+                                                      const RunCkpt* __restrict__ ck,
+                                                      ColumnParams cp, int which,
+                                                      int16_t* __restrict__ out) {
+  __shared__ ExpandSmem sm;
+  int p;
+  Stream s;
+  uint32_t lo, hi, next_pos;
+  RunCkpt c;
+  if (!expand_setup(blob, pages, tile_page, ck, cp, which, p, s, lo, hi, c, next_pos)) return;
+  LevelEmit em{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
+  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
+  if (which == SS_DEF) {
+    const uint64_t t = block_sum_u64(em.nonnull, sm.red);
+    if (threadIdx.x == 0 && t) atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nonnull),
+                                         (unsigned long long)t);
   }
 }
 
@@ -264,33 +278,23 @@ struct DictEmit {
 };
 
 template <int ES>
-__global__ void __launch_bounds__(WG, 4) k_dict_gather(const uint8_t* __restrict__ blob,
-                                                    uint64_t blob_len, PageWork* pages,
+__global__ void __launch_bounds__(WG) k_expand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages,
+                                                    const uint32_t* __restrict__ tile_page,
+                                                    const RunCkpt* __restrict__ ck, ColumnParams cp,
                                                     int dict_page, uint8_t* __restrict__ out,
                                                     ChunkResult* res) {
-  __shared__ HybridSmem sm;
-  const int p = blockIdx.x;
-  PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_RLE_DICTIONARY && pw.encoding != E_PLAIN_DICTIONARY) return;
-  if (dict_page < 0) {
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);  // "Decoder for dict should have been set"
-    return;
-  }
-  const PageWork dp = pages[dict_page];
-  if (dp.status != 0) return;
-  uint64_t n = pw.nonnull;
-  if (n == 0) return;
-  if (pw.val_bytes < 1) {  // data.as_ref()[0]
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
-    return;
-  }
-  const int w = blob[pw.base + pw.val_off];
+  __shared__ ExpandSmem sm;
+  int p;
+  Stream s;
+  uint32_t lo, hi, next_pos;
+  RunCkpt c;
+  if (dict_page < 0 || pages[dict_page].status != 0) return;
+  if (!expand_setup(blob, pages, tile_page, ck, cp, SS_DICT, p, s, lo, hi, c, next_pos)) return;
+  const PageWork& dp = pages[dict_page];
   DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
-  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 1, pw.val_bytes - 1, w,
-                             (uint32_t)n, LK_RLE, pw.value_out, sm, em);
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
+  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
+  if (em.err) report(pages, res, p, em.err);
 }
 
 // Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
@@ -404,29 +408,19 @@ struct BoolEmit {
   }
 };
 
-__global__ void __launch_bounds__(WG, 4) k_rle_bool(const uint8_t* __restrict__ blob,
-                                                 uint64_t blob_len, PageWork* pages,
-                                                 uint8_t* __restrict__ out, ChunkResult* res) {
-  __shared__ HybridSmem sm;
-  const int p = blockIdx.x;
-  PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_RLE) return;
-  const uint8_t* vp = blob + pw.base + pw.val_off;
-  if (pw.val_bytes < 4) {
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
-    return;
-  }
-  int32_t sz = (int32_t)rd_u32(vp);
-  if (sz < 0 || 4ull + (uint64_t)(uint32_t)sz > pw.val_bytes) {  // data.range(4, size) assert
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
-    return;
-  }
+__global__ void __launch_bounds__(WG) k_expand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages,
+                                                    const uint32_t* __restrict__ tile_page,
+                                                    const RunCkpt* __restrict__ ck, ColumnParams cp,
+                                                    uint8_t* __restrict__ out) {
+  __shared__ ExpandSmem sm;
+  int p;
+  Stream s;
+  uint32_t lo, hi, next_pos;
+  RunCkpt c;
+  if (!expand_setup(blob, pages, tile_page, ck, cp, SS_BOOL, p, s, lo, hi, c, next_pos)) return;
   BoolEmit em{out, 0};
-  int32_t st = hybrid_decode(blob, blob_len, pw.base + pw.val_off + 4, (uint32_t)sz, 1,
-                             (uint32_t)pw.nonnull, LK_RLE, pw.value_out, sm, em);
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
+  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
 }
 
 // ------------------------------------------------------------------------------ finalize
@@ -442,17 +436,32 @@ __global__ void k_finalize(PageWork* pages, ChunkResult* res) {
 extern "C" {
 
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                              int npages, ColumnParams cp, ChunkResult* res, hipStream_t s) {
+                              int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
+                              hipStream_t s) {
   hipLaunchKernelGGL(k_prepare, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, blob_len,
-                     pages, npages, cp, res);
+                     pages, npages, cp, tile_page, res);
   return hipGetLastError();
 }
 
+hipError_t pqg_launch_run_index(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                                int npages, ColumnParams cp, int sel, int dict_page, RunCkpt* ck,
+                                ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
+                     dict_page, ck, res);
+  return hipGetLastError();
+}
+
+// Level stream `which` (0 def, 1 rep): index pass, then the grid-wide expand pass.
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                             int npages, ColumnParams cp, int which, int16_t* out,
+                             int npages, uint32_t ntiles, ColumnParams cp, int which,
+                             const uint32_t* tile_page, RunCkpt* ck, int16_t* out,
                              ChunkResult* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_rle_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp,
-                     which, out, res);
+  const int sel = which ? SS_REP : SS_DEF;
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
+                     -1, ck, res);
+  if (ntiles)
+    hipLaunchKernelGGL(k_expand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages,
+                       tile_page, ck, cp, sel, out);
   return hipGetLastError();
 }
 
@@ -463,14 +472,18 @@ hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es
 }
 
 hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                           int dict_page, int es, uint8_t* out, ChunkResult* res,
+                           uint32_t ntiles, ColumnParams cp, int dict_page, int es,
+                           const uint32_t* tile_page, RunCkpt* ck, uint8_t* out, ChunkResult* res,
                            hipStream_t s) {
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
+                     dict_page, ck, res);
+  if (!ntiles) return hipGetLastError();
   switch (es) {
-    case 1: hipLaunchKernelGGL(k_dict_gather<1>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL(k_dict_gather<4>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL(k_dict_gather<8>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL(k_dict_gather<12>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dict_page, out, res); break;
+    case 1: hipLaunchKernelGGL(k_expand_dict<1>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL(k_expand_dict<4>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
+    case 8: hipLaunchKernelGGL(k_expand_dict<8>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
+    case 12: hipLaunchKernelGGL(k_expand_dict<12>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -497,22 +510,15 @@ hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npage
 }
 
 hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                               int npages, uint8_t* out, ChunkResult* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_rle_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, out, res);
+                               int npages, uint32_t ntiles, ColumnParams cp,
+                               const uint32_t* tile_page, RunCkpt* ck, uint8_t* out,
+                               ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
+                     -1, ck, res);
+  if (ntiles)
+    hipLaunchKernelGGL(k_expand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages,
+                       tile_page, ck, cp, out);
   return hipGetLastError();
-}
-
-// Diagnostics: set the debug mode of the hybrid decoder and read/reset its counters.
-int pqg_debug_set(int mode) {
-  uint32_t m = (uint32_t)mode;
-  unsigned long long z[16] = {};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_pqg_stats), z, sizeof(z)) != hipSuccess) return 8;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_pqg_debug_mode), &m, sizeof(m)) == hipSuccess ? 0 : 8;
-}
-
-int pqg_debug_read(unsigned long long* out16) {
-  hipDeviceSynchronize();
-  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_pqg_stats), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 8;
 }
 
 hipError_t pqg_launch_finalize(PageWork* pages, ChunkResult* res, hipStream_t s) {

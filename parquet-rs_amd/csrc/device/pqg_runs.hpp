@@ -1,0 +1,474 @@
+// pqg_runs.hpp — RLE/bit-packing hybrid decode (rle.rs:320-509) as two grid-wide passes.
+//
+// Run headers sit at data-dependent byte offsets, so finding them is a serial walk, while
+// expanding runs into outputs is embarrassingly parallel. The decode is split accordingly:
+//
+//   index  (run_index, one wave per stream): walks the header chain of a page's stream inside
+//          LDS-staged 8 KiB regions, checks everything the reference checks while reading
+//          (Err / panic / endless loop), and writes one checkpoint per
+//          expand tile: the header position of the run holding the tile's first output.
+//   expand (run_expand, one 256-thread workgroup per tile of RUN_TILE outputs, all pages of
+//          the chunk in one grid): stages the tile's stream bytes in LDS, re-walks the few
+//          runs of the tile from its checkpoint into an LDS run list, then every lane expands
+//          8 consecutive outputs twice (two coalesced 2048-output halves) through an Emit
+//          functor (levels, dictionary gather, booleans, byte-array dictionary slices).
+//
+// The walk is the only serial part and it touches header bytes only; the expansion runs over
+// the whole chunk at once, so its cost is the output bandwidth.
+#pragma once
+#include "pqg_device.hpp"
+
+namespace pqg {
+
+constexpr int IX_REG = 8192;                  // index walker region (bytes)
+constexpr int IX_WORDS = (IX_REG + 64) / 4;
+constexpr int EX_STAGE = 10240;               // expand staging window (bytes)
+constexpr int EX_WORDS = (EX_STAGE + 64) / 4;
+constexpr int EX_RCAP = 512;                  // runs per expand batch
+constexpr uint32_t RF_BP = 1u, RF_EOF = 2u, RF_PANIC = 4u;
+constexpr uint32_t R_RLE = 0x80000000u;
+
+enum StreamSel : int { SS_DEF = 0, SS_REP = 1, SS_DICT = 2, SS_BOOL = 3 };
+
+// One hybrid stream of one page.
+struct Stream {
+  uint64_t S;      // absolute blob offset of the stream
+  uint32_t slen;   // stream bytes
+  uint32_t n;      // outputs the reader asks for
+  int w;           // bit width
+  int kind;        // LK_RLE (hybrid) / LK_BIT_PACKED (header-less, levels.rs:203-209)
+  uint64_t out;    // global index of the page's first output
+  int32_t err;     // error found before any run is read
+};
+
+__device__ inline uint32_t rd_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Stream `sel` of page pw; false if the page has none.
+//  SS_DEF / SS_REP: level streams located by k_prepare (levels.rs:191-233);
+//  SS_DICT: RLE_DICTIONARY indices, [bit width byte][hybrid] (decoding.rs:292-300);
+//  SS_BOOL: RleValueDecoder<Bool>, [i32 length][hybrid, w = 1] (decoding.rs:339-349).
+__device__ inline bool get_stream(const uint8_t* blob, const PageWork& pw, int sel,
+                                  const ColumnParams& cp, Stream& s) {
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return false;
+  s.err = 0;
+  s.kind = LK_RLE;
+  if (sel == SS_DEF || sel == SS_REP) {
+    const int kind = sel == SS_DEF ? pw.def_kind : pw.rep_kind;
+    if (kind == LK_NONE) return false;
+    s.kind = kind;
+    s.S = pw.base + (sel == SS_DEF ? pw.def_off : pw.rep_off);
+    s.slen = sel == SS_DEF ? pw.def_bytes : pw.rep_bytes;
+    s.w = sel == SS_DEF ? cp.def_bit_width : cp.rep_bit_width;
+    s.n = pw.num_values;
+    s.out = pw.level_out;
+    return true;
+  }
+  s.n = (uint32_t)pw.nonnull;
+  s.out = pw.value_out;
+  if (sel == SS_DICT) {
+    if (pw.encoding != E_RLE_DICTIONARY) return false;
+    if (pw.val_bytes < 1) {  // data.as_ref()[0]
+      s.err = ST_PANIC;
+      s.S = pw.base + pw.val_off;
+      s.slen = 0;
+      s.w = 0;
+      return true;
+    }
+    s.w = blob[pw.base + pw.val_off];
+    s.S = pw.base + pw.val_off + 1;
+    s.slen = pw.val_bytes - 1;
+    return true;
+  }
+  // SS_BOOL
+  if (pw.encoding != E_RLE) return false;
+  s.w = 1;
+  s.S = pw.base + pw.val_off + 4;
+  s.slen = 0;
+  if (pw.val_bytes < 4) {
+    s.err = ST_PANIC;
+    return true;
+  }
+  const int32_t sz = (int32_t)rd_le32(blob + pw.base + pw.val_off);
+  if (sz < 0 || 4ull + (uint64_t)(uint32_t)sz > pw.val_bytes) {  // data.range(4, size) assert
+    s.err = ST_PANIC;
+    return true;
+  }
+  s.slen = (uint32_t)sz;
+  return true;
+}
+
+// ------------------------------------------------------------------------------ header parse
+
+// Slow, general header parse (varints up to 10 bytes, values up to 8 bytes) from an LDS
+// image; the reference encoder never needs it (1-2 byte headers, <= 4-byte values).
+__device__ inline void run_parse_slow(const uint32_t* region, uint32_t ridx, uint32_t q,
+                                      uint32_t slen, int w, uint32_t& nxt, uint32_t& cnt,
+                                      uint32_t& inf, uint32_t& flg) {
+  uint64_t ind = 0;
+  int vlen = 0;
+  bool complete = false;
+#pragma unroll 1
+  for (int k = 0; k < 10; ++k) {
+    if (q + (uint32_t)k >= slen) break;
+    const uint32_t b = lbyte(region, ridx + k);
+    ind |= (uint64_t)(b & 0x7Fu) << (7 * k);
+    vlen = k + 1;
+    if (!(b & 0x80u)) {
+      complete = true;
+      break;
+    }
+  }
+  nxt = 0xFFFFFFFFu;
+  cnt = 0;
+  inf = 0;
+  if (!complete) {  // bit_util.rs:564-580: 11th byte -> assert; end of data -> None
+    flg = (vlen == 10 && q + 10 < slen) ? RF_PANIC : RF_EOF;
+    return;
+  }
+  const uint32_t p = q + (uint32_t)vlen;
+  if (ind & 1) {
+    cnt = (uint32_t)((uint64_t)((int64_t)ind >> 1) * 8ull);
+    inf = p;
+    const uint64_t nx = (uint64_t)p + (((uint64_t)cnt * (uint64_t)w) >> 3);
+    nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+    flg = RF_BP;
+  } else {
+    cnt = (uint32_t)((int64_t)ind >> 1);
+    const uint32_t vb = ((uint32_t)w + 7u) >> 3;
+    if (vb > 8 || (uint64_t)p + vb > slen) {
+      flg = RF_PANIC;
+      return;
+    }
+    uint64_t v = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < vb; ++k) v |= (uint64_t)lbyte(region, ridx + (uint32_t)vlen + k) << (8 * k);
+    inf = v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v;
+    nxt = p + vb;
+    flg = 0;
+  }
+}
+
+// Header at stream position q (LDS index ridx): one-byte headers (every header the reference
+// writes for runs < 64 values or <= 63 groups) take a short path; longer varints a branchless
+// LEB128 decode of a 16-byte window; anything unusual the slow path. (rle.rs:490-508,
+// bit_util.rs:538-580)
+__device__ inline void run_parse(const uint32_t* region, uint32_t ridx, uint32_t q, uint32_t slen,
+                                 int w, uint32_t& nxt, uint32_t& cnt, uint32_t& inf,
+                                 uint32_t& flg) {
+  const uint32_t avail = q < slen ? slen - q : 0u;
+  const uint32_t vb = ((uint32_t)w + 7u) >> 3;
+  const uint64_t lo8 = lload_u64(region, ridx);
+  const uint32_t b0 = (uint32_t)lo8 & 0xFFu;
+  if (!(b0 & 0x80u) && avail >= 1u + ((b0 & 1u) ? 0u : vb) && vb <= 4u) {
+    const uint32_t p = q + 1u;
+    if (b0 & 1u) {
+      cnt = (b0 >> 1) * 8u;
+      inf = p;
+      nxt = p + ((cnt * (uint32_t)w) >> 3);
+      flg = RF_BP;
+    } else {
+      cnt = b0 >> 1;
+      uint32_t v = (uint32_t)(lo8 >> 8);
+      if (vb < 4) v &= (1u << (8 * vb)) - 1u;
+      inf = v > 0x7FFFFFFFu ? 0x7FFFFFFFu : v;
+      nxt = p + vb;
+      flg = 0;
+    }
+    return;
+  }
+  const uint64_t hi8 = lload_u64(region, ridx + 8);
+  const uint64_t lo = lo8;
+  const uint64_t t = ~lo & 0x8080808080808080ull;
+  const uint32_t vlen = t ? ((uint32_t)__builtin_ctzll(t) >> 3) + 1u : 9u;
+  uint64_t y = lo & 0x7F7F7F7F7F7F7F7Full;
+  if (vlen < 8) y &= (1ull << (8 * vlen)) - 1ull;
+  y = (y & 0x007F007F007F007Full) | ((y & 0x7F007F007F007F00ull) >> 1);
+  y = (y & 0x00003FFF00003FFFull) | ((y & 0x3FFF00003FFF0000ull) >> 2);
+  const uint64_t ind = (y & 0x000000000FFFFFFFull) | ((y & 0x0FFFFFFF00000000ull) >> 4);
+  const uint32_t p = q + vlen;
+  const bool bp = (ind & 1) != 0;
+  const uint32_t vs = vlen * 8u;
+  uint64_t v = (vs < 64) ? ((lo >> vs) | (vs ? (hi8 << (64 - vs)) : 0ull)) : hi8;
+  if (vb < 8) v &= (1ull << (8 * vb)) - 1ull;
+  const bool fast = t != 0 && vlen + (bp ? 0u : vb) <= avail && (bp || (vb <= 8 && vlen + vb <= 9));
+  if (fast) {
+    if (bp) {
+      cnt = (uint32_t)((ind >> 1) * 8ull);
+      inf = p;
+      const uint64_t nx = (uint64_t)p + (((uint64_t)cnt * (uint64_t)w) >> 3);
+      nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+      flg = RF_BP;
+    } else {
+      cnt = (uint32_t)(ind >> 1);
+      inf = v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v;
+      nxt = p + vb;
+      flg = 0;
+    }
+  } else {
+    run_parse_slow(region, ridx, q, slen, w, nxt, cnt, inf, flg);
+  }
+}
+
+// Header parse straight from global memory (walks that leave their staged window).
+__device__ inline void run_parse_global(const uint8_t* blob, uint64_t blob_len, uint64_t S,
+                                        uint32_t q, uint32_t slen, int w, uint32_t& nxt,
+                                        uint32_t& cnt, uint32_t& inf, uint32_t& flg) {
+  uint32_t tmp[8];
+  const uint64_t a = S + q;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint64_t x = a + 4u * k;
+    tmp[k] = gbyte(blob, blob_len, x) | (gbyte(blob, blob_len, x + 1) << 8) |
+             (gbyte(blob, blob_len, x + 2) << 16) | (gbyte(blob, blob_len, x + 3) << 24);
+  }
+  tmp[6] = tmp[7] = 0;
+  run_parse(tmp, 0, q, slen, w, nxt, cnt, inf, flg);
+}
+
+// ------------------------------------------------------------------------------ index pass
+
+struct IndexSmem {
+  uint32_t region[IX_WORDS];
+};
+
+// Walks stream s of page p (one wave, all lanes uniform) and writes the checkpoints of its
+// expand tiles to ck[0 .. ceil(n / RUN_TILE)). Returns a status.
+__device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                    const Stream& s, RunCkpt* __restrict__ ck, IndexSmem& sm) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (s.err) return s.err;
+  const uint32_t n = s.n;
+  if (n == 0) return 0;
+  const int w = s.w;
+  if (s.kind == LK_BIT_PACKED) {  // one header-less run (levels.rs:203-209)
+    if ((uint64_t)n * (uint64_t)w > (uint64_t)s.slen * 8ull) return ST_EOF;
+    if (w > 32) return ST_PANIC;
+    return 0;
+  }
+  const uint64_t S = s.S;
+  const uint32_t slen = s.slen;
+  uint32_t cur = 0, produced = 0, next_tile = 0;
+  uint64_t A0 = ~0ull;
+  while (true) {
+    if (produced >= n) return 0;
+    if (cur >= slen) return ST_EOF;  // reload() finds no more data: the reference stalls (A.4)
+    if (A0 == ~0ull || S + cur < A0 || S + cur - A0 >= (uint64_t)IX_REG) {
+      A0 = (S + cur) & ~15ull;
+      for (uint32_t c = lane; c < (IX_REG + 64) / 16; c += 64) {
+        const uint64_t a = A0 + (uint64_t)c * 16;
+        const uint4 v = (a + 16 <= blob_len) ? *reinterpret_cast<const uint4*>(blob + a)
+                                             : gload_u128_tail(blob, blob_len, a);
+        reinterpret_cast<uint4*>(sm.region)[c] = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+    }
+    uint32_t nxt, cnt, inf, flg;
+    run_parse(sm.region, (uint32_t)(S + cur - A0), cur, slen, w, nxt, cnt, inf, flg);
+    if (flg & (RF_EOF | RF_PANIC)) return (flg & RF_PANIC) ? ST_PANIC : ST_EOF;
+    if (cnt) {
+      const uint32_t left = n - produced;
+      const uint32_t need = cnt < left ? cnt : left;
+      if (flg & RF_BP) {
+        if (w > 32) return ST_PANIC;  // BitReader::get_batch asserts num_bits <= 32
+        if ((uint64_t)inf * 8ull + (uint64_t)need * (uint64_t)w > (uint64_t)slen * 8ull)
+          return ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
+      }
+      while (next_tile * RUN_TILE < produced + need) {
+        if (lane == 0) ck[next_tile] = RunCkpt{cur, produced};
+        ++next_tile;
+      }
+      produced += need;
+    }
+    cur = nxt;
+  }
+}
+
+// ------------------------------------------------------------------------------ expand pass
+
+struct ExpandSmem {
+  uint32_t stage[EX_WORDS];
+  uint32_t start[EX_RCAP + 1];
+  uint32_t info[EX_RCAP];
+  uint32_t ctl[4];
+  uint64_t red[4];
+};
+
+// Expand outputs [lo, hi) of stream s (page-relative indices) from checkpoint c, with the
+// 256 threads of the workgroup. Uniform control flow; stream already validated by run_index.
+template <class Emit>
+__device__ inline void run_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                  const Stream& s, RunCkpt c, uint32_t next_pos, uint32_t lo,
+                                  uint32_t hi, ExpandSmem& sm, Emit& emit) {
+  const int tid = threadIdx.x;
+  const int w = s.w;
+  const uint64_t S = s.S;
+  const uint32_t slen = s.slen;
+  const uint64_t wmask = (w >= 32) ? 0xFFFFFFFFull : ((1ull << w) - 1ull);
+  // ---- stage the tile's stream bytes
+  uint32_t q0;
+  if (s.kind == LK_BIT_PACKED) {
+    q0 = (uint32_t)(((uint64_t)lo * (uint64_t)w) >> 3);
+    c.pos = 0;
+    c.first = 0;
+  } else {
+    q0 = c.pos;
+  }
+  const uint64_t A0 = (S + q0) & ~15ull;
+  const uint32_t first_eff = s.kind == LK_BIT_PACKED ? lo : (c.first < lo ? c.first : lo);
+  const uint64_t need_end = S + (uint64_t)q0 + 64 + ((uint64_t)(hi - first_eff) * (uint64_t)w + 7) / 8 +
+                            (s.kind == LK_BIT_PACKED ? 0 : 2 * (uint64_t)(hi - lo));
+  const uint64_t S_end = S + slen + 16;
+  // the tile's runs end in the run whose header is the next tile's checkpoint
+  const uint64_t next_end = S + (uint64_t)next_pos + 32 + ((uint64_t)RUN_TILE * (uint64_t)w + 7) / 8;
+  uint64_t A1 = need_end < S_end ? need_end : S_end;
+  if (A1 > next_end) A1 = next_end;
+  if (A1 > A0 + EX_STAGE) A1 = A0 + EX_STAGE;
+  const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+  for (uint32_t k = tid; k < nchunks; k += WG) {
+    const uint64_t a = A0 + (uint64_t)k * 16;
+    const uint4 v = (a + 16 <= blob_len) ? *reinterpret_cast<const uint4*>(blob + a)
+                                         : gload_u128_tail(blob, blob_len, a);
+    reinterpret_cast<uint4*>(sm.stage)[k] = v;
+  }
+  if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
+  const uint64_t staged = (uint64_t)nchunks * 16;  // bytes [A0, A0 + staged) valid
+  __syncthreads();
+
+  uint32_t cur = c.pos, produced = c.first, seg_lo = lo;
+  while (seg_lo < hi) {
+    // ---- walk: runs covering [seg_lo, seg_hi) into the LDS run list (wave 0, uniform)
+    if (tid < 64) {
+      uint32_t nr = 0;
+      if (s.kind == LK_BIT_PACKED) {
+        if (tid == 0) {
+          sm.start[0] = 0;
+          sm.info[0] = 0;
+          sm.start[1] = hi;
+        }
+        nr = 1;
+        produced = hi;
+      } else {
+        while (produced < hi && nr < (uint32_t)EX_RCAP) {
+          if (cur >= slen) break;  // cannot happen on a stream run_index accepted
+          uint32_t nxt, cnt, inf, flg;
+          const uint64_t ri = S + cur - A0;
+          if (S + cur >= A0 && ri + 24 <= staged)
+            run_parse(sm.stage, (uint32_t)ri, cur, slen, w, nxt, cnt, inf, flg);
+          else
+            run_parse_global(blob, blob_len, S, cur, slen, w, nxt, cnt, inf, flg);
+          if (cnt) {
+            const uint32_t left = s.n - produced;
+            const uint32_t need = cnt < left ? cnt : left;
+            if (produced + need > seg_lo) {
+              if (tid == 0) {
+                sm.start[nr] = produced;
+                sm.info[nr] = (flg & RF_BP) ? inf : (R_RLE | inf);
+              }
+              ++nr;
+            }
+            produced += need;
+          }
+          cur = nxt;
+        }
+        if (tid == 0) sm.start[nr] = produced;
+      }
+      if (tid == 0) sm.ctl[0] = nr;
+    }
+    __syncthreads();
+    const uint32_t nr = sm.ctl[0];
+    if (nr == 0) break;  // defensive: nothing left to expand
+    const uint32_t seg_hi = sm.start[nr] < hi ? sm.start[nr] : hi;
+    if (seg_hi <= seg_lo) break;
+    // ---- expand: lane chunks of 8 outputs, two coalesced halves per tile
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t g = lo + (uint32_t)half * (RUN_TILE / 2) + (uint32_t)tid * 8u;
+      if (g + 8 <= seg_lo || g >= seg_hi) continue;
+      uint32_t v[8];
+      uint32_t mask = 0;
+      const uint32_t o0 = g < seg_lo ? seg_lo : g;
+      int a = 0, b = (int)nr - 1;
+      while (a < b) {
+        const int mid = (a + b + 1) >> 1;
+        if (sm.start[mid] <= o0) a = mid;
+        else b = mid - 1;
+      }
+      int r = a;
+      const uint32_t inf0 = sm.info[r];
+      const bool one_run = g >= seg_lo && g + 8 <= seg_hi && g + 8 <= sm.start[r + 1];
+      const uint64_t bit0 = (uint64_t)inf0 * 8ull + (uint64_t)(g - sm.start[r]) * (uint64_t)w;
+      const uint64_t ri0 = S + (bit0 >> 3) - A0;
+      if (one_run && ((inf0 & R_RLE) || (S + (bit0 >> 3) >= A0 && ri0 + (uint64_t)w + 12 <= staged))) {
+        if (inf0 & R_RLE) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = inf0 & 0x7FFFFFFFu;
+        } else if (w <= 7) {
+          const uint64_t x = lload_u64(sm.stage, (uint32_t)ri0);
+          const uint32_t s0 = (uint32_t)(bit0 & 7);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (uint32_t)((x >> (s0 + j * w)) & wmask);
+        } else {
+          const uint32_t rb = (uint32_t)(ri0 * 8ull + (bit0 & 7));
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t bb = rb + (uint32_t)(j * w);
+            v[j] = (uint32_t)((lload_u64(sm.stage, bb >> 3) >> (bb & 7)) & wmask);
+          }
+        }
+        mask = 0xFFu;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = 0;
+          const uint32_t oj = g + (uint32_t)j;
+          if (oj < seg_lo || oj >= seg_hi) continue;
+          while (oj >= sm.start[r + 1]) ++r;
+          const uint32_t inf = sm.info[r];
+          if (inf & R_RLE) {
+            v[j] = inf & 0x7FFFFFFFu;
+          } else {
+            const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(oj - sm.start[r]) * (uint64_t)w;
+            const uint64_t abs = S + (bit >> 3);
+            const uint64_t ri = abs - A0;
+            const uint64_t x = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
+                                                                : gload_u64(blob, blob_len, abs);
+            v[j] = (uint32_t)((x >> (bit & 7)) & wmask);
+          }
+          mask |= 1u << j;
+        }
+      }
+      if (mask) emit(s.out + g, v, mask);
+    }
+    seg_lo = seg_hi;
+    __syncthreads();
+  }
+}
+
+// Common front of the expand kernels: tile -> page, stream and output range.
+__device__ inline bool expand_setup(const uint8_t* blob, PageWork* pages, const uint32_t* tile_page,
+                                    const RunCkpt* ck, ColumnParams cp, int sel, int& p,
+                                    Stream& s, uint32_t& lo, uint32_t& hi, RunCkpt& c,
+                                    uint32_t& next_pos) {
+  const uint32_t t = blockIdx.x;
+  p = (int)tile_page[t];
+  const PageWork& pw = pages[p];
+  if (pw.status != 0) return false;
+  if (!get_stream(blob, pw, sel, cp, s) || s.err) return false;
+  const uint32_t k = t - pw.ltile0;
+  lo = k * RUN_TILE;
+  if (lo >= s.n) return false;
+  hi = lo + RUN_TILE < s.n ? lo + RUN_TILE : s.n;
+  if (s.kind == LK_BIT_PACKED) {
+    c = RunCkpt{0, 0};
+    next_pos = s.slen;
+  } else {
+    c = ck[t];
+    next_pos = hi < s.n ? ck[t + 1].pos : s.slen;
+  }
+  return true;
+}
+
+}  // namespace pqg

@@ -19,26 +19,31 @@
 using namespace pqg;
 
 extern "C" {
-hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams,
+hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, uint32_t*,
                               ChunkResult*, hipStream_t);
-hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int,
-                             int16_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
+                                RunCkpt*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
+                             const uint32_t*, RunCkpt*, int16_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
-hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, int, int, uint8_t*,
-                           ChunkResult*, hipStream_t);
+hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
+                           int, const uint32_t*, RunCkpt*, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
                                  uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
                                  ChunkResult*, hipStream_t);
-hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint8_t*, ChunkResult*,
-                               hipStream_t);
+hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
+                               const uint32_t*, RunCkpt*, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, int, bool, bool,
-                            uint64_t*, uint32_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t,
-                            int64_t*, uint8_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
+                                   uint32_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
+                            const uint32_t*, const RunCkpt*, int, int, bool, bool, uint64_t*,
+                            uint32_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int64_t*,
+                            uint8_t*, ChunkResult*, hipStream_t);
 }
 
 // Two staging slots so consecutive async decodes never overwrite pinned memory that an
@@ -60,6 +65,10 @@ struct Slot {
   uint64_t* dsrc = nullptr;
   uint32_t* dlen = nullptr;
   size_t dcap = 0;
+  // hybrid-stream expand tiles: tile -> page map and one checkpoint array per stream kind
+  uint32_t* tile_page = nullptr;
+  RunCkpt* ck[3] = {};  // def, rep, values
+  size_t tcap = 0;
 };
 
 struct pqg_ctx {
@@ -165,6 +174,8 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.vpre);
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
+    hipFree(sl.tile_page);
+    for (RunCkpt* c : sl.ck) hipFree(c);
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   delete ctx;
@@ -301,6 +312,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   std::string why;
   int vst = validate_pages(col, pages, npages, &bad, &dict_page, why);
   uint64_t level_out = 0, max_page_bytes = 0, max_page_vals = 0;
+  uint32_t total_tiles = 0;
   bool enc_present[16] = {};
   for (uint32_t i = 0; i < npages; ++i) {
     PageWork& w = ctx->h_pages[i];
@@ -317,7 +329,11 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     w.def_len = pages[i].def_len;
     w.rep_len = pages[i].rep_len;
     w.level_out = level_out;
+    w.ltile0 = total_tiles;
+    w.ntiles = 0;
     if (w.page_type == PQG_PAGE_DATA || w.page_type == PQG_PAGE_DATA_V2) {
+      w.ntiles = (uint32_t)(((uint64_t)w.num_values + RUN_TILE - 1) / RUN_TILE);
+      total_tiles += w.ntiles;
       level_out += w.num_values;
       if (w.encoding >= 0 && w.encoding < 16) enc_present[w.encoding] = true;
       if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
@@ -384,11 +400,29 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       sl.dcap = dn;
     }
   }
+  // expand-tile bookkeeping of the hybrid streams (tile -> page, checkpoints per stream kind)
+  if (total_tiles + 1 > sl.tcap) {
+    hipFree(sl.tile_page);
+    sl.tile_page = nullptr;
+    for (RunCkpt*& c : sl.ck) {
+      hipFree(c);
+      c = nullptr;
+    }
+    size_t cap = (size_t)total_tiles + 1024;
+    HIPCHK(hipMalloc(&sl.tile_page, cap * sizeof(uint32_t)), "hipMalloc tile_page");
+    for (RunCkpt*& c : sl.ck) HIPCHK(hipMalloc(&c, (cap + 1) * sizeof(RunCkpt)), "hipMalloc ckpt");
+    sl.tcap = cap;
+  }
+  const uint32_t nt = total_tiles;
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
-  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, ctx->d_res, s), "prepare");
+  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
-  if (np && want_def) HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, cp, 0, out->def_levels, ctx->d_res, s), "def levels");
-  if (np && want_rep) HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, cp, 1, out->rep_levels, ctx->d_res, s), "rep levels");
+  if (np && want_def)
+    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.ck[0],
+                             out->def_levels, ctx->d_res, s), "def levels");
+  if (np && want_rep)
+    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.ck[1],
+                             out->rep_levels, ctx->d_res, s), "rep levels");
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
   HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
@@ -399,8 +433,15 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
                          : enc_present[PQG_DELTA_BYTE_ARRAY] ? PQG_DELTA_BYTE_ARRAY
                          : enc_present[PQG_DELTA_LENGTH_BYTE_ARRAY] ? PQG_DELTA_LENGTH_BYTE_ARRAY
                                                                      : PQG_PLAIN;
-    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, dict_page,
-                            t == PQG_FIXED_LEN_BYTE_ARRAY ? col->type_length : 0,
+    const int tl = t == PQG_FIXED_LEN_BYTE_ARRAY ? col->type_length : 0;
+    if (enc_present[PQG_RLE_DICTIONARY]) {
+      HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
+                                     ctx->d_res, s), "byte-array dictionary");
+      HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
+                                  sl.ck[2], ctx->d_res, s), "dictionary index pass");
+    }
+    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.ck[2], dict_page,
+                            tl,
                             enc_present[PQG_RLE_DICTIONARY], enc_present[PQG_DELTA_BYTE_ARRAY],
                             sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, out->values_capacity,
                             out->offsets, vo, ctx->d_res, s),
@@ -415,7 +456,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
     if (enc_present[PQG_RLE_DICTIONARY]) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
-      HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, dict_page, es, vo, ctx->d_res, s), "dict");
+      HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
+                             sl.ck[2], vo, ctx->d_res, s), "dict");
     }
     if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
@@ -423,7 +465,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
     if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
       ctx->values_kernel = PQG_RLE;
-      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, vo, ctx->d_res, s), "rle bool");
+      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.ck[2], vo,
+                                 ctx->d_res, s), "rle bool");
     }
   }
   if (ctx->timing) hipEventRecord(ctx->ev[4], s);

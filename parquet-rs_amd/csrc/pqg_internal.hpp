@@ -47,6 +47,8 @@ struct PageWork {
   int32_t rep_encoding;
   uint32_t def_len;     // v2
   uint32_t rep_len;     // v2
+  uint32_t ltile0;      // first expand tile of this page (tiles of RUN_TILE levels)
+  uint32_t ntiles;      // expand tiles of this page (0 for dictionary pages)
   // ---- prepare kernel
   uint32_t rep_off, rep_bytes;  // level streams, relative to base
   uint32_t def_off, def_bytes;
@@ -69,6 +71,15 @@ struct ChunkResult {
   int32_t status;
   uint32_t dict_page;      // index of the dictionary page or UINT32_MAX
   uint32_t pad;
+};
+
+// Outputs per expand tile of the RLE/bit-packed hybrid decoder (device/pqg_runs.hpp).
+constexpr uint32_t RUN_TILE = 4096;
+
+// Walk checkpoint of one expand tile: the header of the run holding the tile's first output.
+struct RunCkpt {
+  uint32_t pos;    // stream-relative byte offset of the run header
+  uint32_t first;  // page-relative index of the run's first output
 };
 
 struct ColumnParams {
