@@ -34,3 +34,497 @@ extern "C" hipError_t pqg_launch_delta(const uint8_t* blob, uint64_t blob_len, P
 }
 
 }  // namespace pqg
+
+// =============================================================================== tiled path
+//
+// DELTA_BINARY_PACKED over the whole chunk at once (BASELINE config 4):
+//   k_delta_index  one wave per page walks the block headers (zigzag min_delta + mini-block
+//                  widths, decoding.rs:448-468) over 8 KiB regions prefetched one ahead,
+//                  checks everything the reference checks, and gives every tile of
+//                  DELTA_TILE values the records of the blocks its values need;
+//   k_delta_expand one 256-thread workgroup per tile: 16 deltas per thread, unpacked from an
+//                  LDS-staged window, a workgroup scan, and a decoupled look-back across the
+//                  page's tiles for the running value (value_i = first + sum of
+//                  min_delta + delta over d < i, wrapping, decoding.rs:560-566).
+// Pages with more than DELTA_MBMAX mini-blocks per block, or a tile needing more than
+// DELTA_BCAP blocks, fall back to k_delta above.
+#include "pqg_runs.hpp"
+
+namespace pqg {
+
+__device__ inline uint32_t rfl32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// zigzag/ULEB128 from a wave-uniform 16-byte window (lo, hi): returns bytes used, 0 when the
+// stream ends first, -1 for > 10 bytes (get_vlq_int assert).
+__device__ inline int vlq16(uint64_t lo, uint64_t hi, uint32_t avail, uint64_t& v) {
+  v = 0;
+#pragma unroll 1
+  for (int k = 0; k < 10; ++k) {
+    if ((uint32_t)k >= avail) return 0;
+    const uint32_t b = (uint32_t)((k < 8 ? (lo >> (8 * k)) : (hi >> (8 * (k - 8)))) & 0xFF);
+    v |= (uint64_t)(b & 0x7F) << (7 * k);
+    if (!(b & 0x80)) return k + 1;
+  }
+  return avail > 10 ? -1 : 0;
+}
+
+template <int ES>
+__global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages, DeltaTables dt, ChunkResult* res) {
+  __shared__ IndexSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  const uint32_t lane = threadIdx.x & 63;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  DeltaPage info{0, 0, 0, 0, 0};
+  if (pw.status != 0) {
+    if (lane == 0) dt.page[p] = info;
+    return;
+  }
+  const uint64_t S = pw.base + pw.val_off;
+  const uint32_t slen = pw.val_bytes;
+  const uint8_t* sp = blob + S;
+  // ---- stream header (decoding.rs:501-533), parsed by every lane
+  uint64_t block_size, nmb, total, fz;
+  uint32_t q = 0;
+  int32_t err = 0;
+  int l;
+  if ((l = g_vlq(sp, q, slen, block_size)) <= 0) err = l ? ST_PANIC : ST_EOF;
+  q += l > 0 ? l : 0;
+  if (!err && (l = g_vlq(sp, q, slen, nmb)) <= 0) err = l ? ST_PANIC : ST_EOF;
+  q += l > 0 ? l : 0;
+  if (!err && (l = g_vlq(sp, q, slen, total)) <= 0) err = l ? ST_PANIC : ST_EOF;
+  q += l > 0 ? l : 0;
+  if (!err && (l = g_vlq(sp, q, slen, fz)) <= 0) err = l ? ST_PANIC : ST_EOF;
+  q += l > 0 ? l : 0;
+  uint64_t vpmb = 0;
+  if (!err) {
+    if ((int64_t)nmb <= 0) err = ST_PANIC;
+    else {
+      vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
+      if (vpmb % 8 != 0) err = ST_PANIC;
+    }
+  }
+  const uint64_t n = pw.nonnull;
+  if (!err && total < n) err = ST_EOF;  // the reference returns a short batch here
+  if (!err && n > 1 && vpmb == 0) err = ST_HANG;
+  if (err) {
+    if (lane == 0) {
+      dt.page[p] = info;
+      report(pages, res, p, err);
+    }
+    return;
+  }
+  info.first = (uint64_t)unzigzag(fz);
+  info.vpmb = (uint32_t)vpmb;
+  info.nmb = (uint32_t)nmb;
+  if (nmb > DELTA_MBMAX || vpmb > 0xFFFFFFu) {  // per-page kernel
+    if (lane == 0) dt.page[p] = info;
+    return;
+  }
+  const uint32_t need = n > 0 ? (uint32_t)(n - 1) : 0u;  // deltas to decode
+  const uint32_t vpb = (uint32_t)(vpmb * nmb);
+  const uint32_t wmax = ES == 4 ? 32u : 64u;
+  const uint32_t nblocks = vpb ? (need + vpb - 1) / vpb : 0u;
+  const uint32_t nmb32 = (uint32_t)nmb, vpmb32 = (uint32_t)vpmb;
+  DeltaBlock* const tb = dt.blocks + (uint64_t)pw.ltile0 * DELTA_BCAP;
+  // ---- block walk: a scalar hop loop follows up to 64 block headers (varint length and the
+  // sum of the mini-block widths give the next header), then the 64 lanes decode, check and
+  // record those blocks in parallel
+  const uint64_t G = S & ~15ull;
+  const uint32_t off0 = (uint32_t)(S - G);
+  const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint4 pf[9];
+  uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
+  uint32_t cur = q, b = 0;
+  bool overflow = false;
+  while (b < nblocks) {
+    if (cur >= slen) {  // "Not enough data to decode 'min_delta'"
+      err = ST_EOF;
+      break;
+    }
+    const uint32_t r = (off0 + cur) / IX_REG;
+    if (r != cur_r) {
+      if (r != pf_r) ix_fetch(blob, blob_len, G + (uint64_t)r * IX_REG, lane, pf);
+      ix_install(sm.region, lane, pf);
+      cur_r = r;
+      pf_r = 0xFFFFFFFFu;
+      if (r + 1 < nregions) {
+        ix_fetch(blob, blob_len, G + (uint64_t)(r + 1) * IX_REG, lane, pf);
+        pf_r = r + 1;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t rbase = r * IX_REG - off0;  // stream offset of region byte 0
+    uint32_t posv = 0, k = 0;
+    while (k < 64 && b + k < nblocks) {
+      if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;  // 64-byte overlap holds the header
+      const uint32_t rel = cur - rbase;
+      const uint64_t w0 = lload_u64(sm.region, rel);
+      const uint32_t x0 = rfl32((uint32_t)w0), x1 = rfl32((uint32_t)(w0 >> 32));
+      const uint64_t lo = ((uint64_t)x1 << 32) | x0;
+      const uint64_t t8 = ~lo & 0x8080808080808080ull;
+      posv = lane == k ? cur : posv;
+      ++k;
+      if (!t8 || nmb32 > 8) break;  // long varint / many widths: the batch finishes this block
+      const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
+      const uint64_t w1 = lload_u64(sm.region, rel + vl);
+      const uint64_t wy = ((uint64_t)rfl32((uint32_t)(w1 >> 32)) << 32) | rfl32((uint32_t)w1);
+      const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
+      uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+      const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+      cur = cur + vl + nmb32 + (vpmb32 >> 3) * sumw;
+    }
+    // ---- batch: lane j = block b + j
+    const bool in = lane < k;
+    const uint32_t bb = b + lane;
+    int32_t e = 0;
+    uint64_t zz = 0;
+    uint32_t vl = 0, wpos = 0, payload = 0, nxt = 0;
+    if (in) {
+      const uint32_t pos = posv;
+      if (pos >= slen) e = ST_EOF;  // "Not enough data to decode 'min_delta'"
+      else {
+        const uint32_t rel = pos - rbase;
+        const uint64_t lo = lload_u64(sm.region, rel), hi = lload_u64(sm.region, rel + 8);
+        const int l = vlq16(lo, hi, slen - pos, zz);
+        if (l <= 0) e = l ? ST_PANIC : ST_EOF;
+        else if ((uint64_t)pos + l + nmb32 > slen) e = ST_EOF;  // "... 'width'"
+        else {
+          vl = (uint32_t)l;
+          wpos = pos + vl;
+          payload = wpos + nmb32;
+          const uint32_t left = need - bb * vpb;
+          const uint32_t inblk = left < vpb ? left : vpb;
+          const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
+          uint64_t boff = 0;
+          for (uint32_t m = 0; m < nmb32; ++m) {
+            const uint32_t wdt = lbyte(sm.region, rel + vl + m);
+            if (m < mneed && !e) {
+              if (wdt > wmax) e = ST_PANIC;  // get_batch / get_value assert on num_bits
+              else if ((uint64_t)payload + boff + (vpmb * wdt) / 8 > slen)
+                e = (ES == 4) ? ST_PANIC : ST_EOF;  // the whole mini-block is loaded
+            }
+            boff += (vpmb * wdt) / 8;
+          }
+          const uint64_t nx = (uint64_t)payload + boff;
+          nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+        }
+      }
+    }
+    const uint64_t emask = __ballot(e != 0);
+    if (emask) {
+      err = __shfl(e, __builtin_ctzll(emask), 64);
+      break;
+    }
+    if (in) {  // records for the tiles of values whose deltas fall in this block
+      const uint32_t d0 = bb * vpb;
+      const uint32_t left = need - d0;
+      const uint32_t d1 = d0 + (left < vpb ? left : vpb);
+      const DeltaBlock rec{wpos, payload, (uint64_t)unzigzag(zz)};
+      for (uint32_t t = (d0 + 1) / DELTA_TILE; t <= d1 / DELTA_TILE; ++t) {
+        const uint32_t vlo = t * DELTA_TILE;
+        const uint32_t slot = bb - (vlo > 0 ? vlo - 1 : 0) / vpb;
+        if (slot >= DELTA_BCAP) overflow = true;
+        else tb[(uint64_t)t * DELTA_BCAP + slot] = rec;
+      }
+    }
+    overflow = __ballot(overflow) != 0;
+    // the last block of the batch decides where the next batch starts
+    cur = __shfl(nxt, (int)k - 1, 64);
+    b += k;
+  }
+  if (err) {
+    if (lane == 0) {
+      dt.page[p] = info;
+      report(pages, res, p, err);
+    }
+    return;
+  }
+  info.tiled = overflow ? 0u : 1u;
+  if (lane == 0) dt.page[p] = info;
+}
+
+struct DeltaExpandSmem {
+  uint32_t stage[EX_WORDS];
+  DeltaBlock blk[DELTA_BCAP];
+  uint32_t mboff[DELTA_BCAP][DELTA_MBMAX];  // byte offset of mini-block m from blk.pos
+  uint8_t mbw[DELTA_BCAP][DELTA_MBMAX];
+  uint64_t wsum[WG / 64];
+  uint64_t prefix;
+};
+
+__device__ inline uint32_t atomic_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint64_t atomic_ld64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                     uint32_t ntiles, DeltaTables dt, uint32_t epoch,
+                                                     uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ DeltaExpandSmem sm;
+  const int tid = threadIdx.x;
+  // One tile per workgroup: the look-back needs tile t-1 to be owned by an earlier (already
+  // dispatched) workgroup that does not itself wait on a later tile.
+  for (uint32_t it = 0; it < 1; ++it) {
+    const uint32_t t = blockIdx.x + it;
+    if (t >= ntiles) break;
+    const int p = (int)tile_page[t];
+    const PageWork& pw = pages[p];
+    if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) continue;
+    if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) continue;
+    const DeltaPage info = dt.page[p];
+    if (!info.tiled) continue;
+    const uint32_t n = (uint32_t)pw.nonnull;
+    const uint32_t k = t - pw.ltile0;
+    const uint32_t lo = k * DELTA_TILE;
+    if (lo >= n) continue;
+    const uint32_t hi = lo + DELTA_TILE < n ? lo + DELTA_TILE : n;
+    const uint64_t S = pw.base + pw.val_off;
+    const uint32_t vpmb = info.vpmb, nmb = info.nmb, vpb = vpmb * nmb;
+    // deltas of the tile: d in [lo - 1, hi - 1), d >= 0
+    const uint32_t dlo = lo > 0 ? lo - 1 : 0;
+    const bool anyd = hi >= 2;
+    const uint32_t blo = dlo / vpb;
+    const uint32_t bhi = anyd ? (hi - 2) / vpb : blo;
+    const uint32_t nb = bhi - blo + 1;
+    const DeltaBlock* recs = dt.blocks + (uint64_t)t * DELTA_BCAP;
+    // ---- block records, widths and mini-block offsets
+    if ((uint32_t)tid < nb) {
+      const DeltaBlock rb = recs[tid];
+      sm.blk[tid] = rb;
+      uint32_t off = 0;
+      for (uint32_t m = 0; m < nmb; ++m) {
+        const uint32_t wdt = blob[S + rb.wpos + m];
+        sm.mbw[tid][m] = (uint8_t)wdt;
+        sm.mboff[tid][m] = off;
+        off += (vpmb * wdt) >> 3;
+      }
+    }
+    __syncthreads();
+    // ---- stage the payload from the tile's first delta on
+    uint64_t A0;
+    {
+      const uint32_t r0 = dlo - blo * vpb;
+      const uint32_t m0 = r0 / vpmb;
+      const uint64_t bit0 = ((uint64_t)sm.blk[0].pos + sm.mboff[0][m0]) * 8ull +
+                            (uint64_t)(r0 - m0 * vpmb) * sm.mbw[0][m0];
+      A0 = (S + (bit0 >> 3)) & ~15ull;
+    }
+    const uint64_t S_end = S + pw.val_bytes + 16;
+    const uint64_t A1 = A0 + EX_STAGE < S_end ? A0 + EX_STAGE : S_end;
+    const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+    {
+      constexpr int PER = (EX_STAGE / 16 + WG - 1) / WG;
+      uint4 v[PER];
+      const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
+        if (ci < nchunks) {
+          const uint64_t a = A0 + (uint64_t)ci * 16;
+          v[c] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
+        if (ci < nchunks) reinterpret_cast<uint4*>(sm.stage)[ci] = v[c];
+      }
+      if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
+    }
+    const uint64_t staged = (uint64_t)nchunks * 16;
+    __syncthreads();
+    // ---- 16 deltas per thread: values lo + 16*tid + j
+    uint64_t x[DPT];
+    uint64_t s = 0;
+    {
+      const uint32_t i0 = lo + (uint32_t)tid * DPT;
+      const uint32_t d0 = i0 > 0 ? i0 - 1 : 0;
+      uint32_t bi = d0 / vpb - blo;
+      uint32_t rr = d0 - (bi + blo) * vpb;
+      uint32_t m = rr / vpmb;
+      uint32_t kk = rr - m * vpmb;
+#pragma unroll
+      for (int j = 0; j < DPT; ++j) {
+        const uint32_t i = i0 + (uint32_t)j;
+        x[j] = 0;
+        if (i >= 1 && i < hi && bi < nb) {
+          const uint32_t wdt = sm.mbw[bi][m];
+          const uint64_t bit = ((uint64_t)sm.blk[bi].pos + sm.mboff[bi][m]) * 8ull + (uint64_t)kk * wdt;
+          const uint64_t abs = S + (bit >> 3);
+          const uint32_t sh = (uint32_t)(bit & 7);
+          const uint64_t ri = abs - A0;
+          uint64_t raw = 0;
+          if (wdt) {
+            uint64_t lo64 = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
+                                                             : gload_u64(blob, blob_len, abs);
+            raw = lo64 >> sh;
+            if (wdt + sh > 64) {
+              const uint64_t hi64 = (abs >= A0 && ri + 20 <= staged) ? lload_u64(sm.stage, (uint32_t)ri + 8)
+                                                                     : gload_u64(blob, blob_len, abs + 8);
+              raw |= hi64 << (64 - sh);
+            }
+            if (wdt < 64) raw &= (1ull << wdt) - 1ull;
+          }
+          x[j] = sm.blk[bi].min_delta + raw;  // min_delta + delta (wrapping)
+        }
+        if (i >= 1) {  // advance to the next delta
+          if (++kk == vpmb) {
+            kk = 0;
+            if (++m == nmb) {
+              m = 0;
+              ++bi;
+            }
+          }
+        }
+        s += x[j];
+      }
+    }
+    // ---- workgroup scan of the thread sums
+    uint64_t incl = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, 64);
+      if ((tid & 63) >= off) incl += y;
+    }
+    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint64_t pre = incl - s;
+    for (int wv = 0; wv < (tid >> 6); ++wv) pre += sm.wsum[wv];
+    // ---- decoupled look-back over the page's tiles (wave 0: 64 predecessors per probe)
+    if (tid < 64) {
+      const uint32_t lane = tid;
+      const uint64_t T = sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+      uint64_t P = 0;
+      if (k == 0) {
+        if (lane == 0) {
+          __hip_atomic_store(&dt.inc[t], T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_s_waitcnt(0);
+          __hip_atomic_store(&dt.flag[t], epoch * 4u + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        if (lane == 0) {
+          __hip_atomic_store(&dt.agg[t], T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_s_waitcnt(0);
+          __hip_atomic_store(&dt.flag[t], epoch * 4u + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t first = pw.ltile0;  // the page's tile 0 always ends a look-back
+        uint32_t base = t - 1;
+        uint32_t spins = 0;
+        while (true) {
+          const bool valid = base >= first + lane;  // lane probes tile base - lane
+          const uint32_t qt = base - lane;
+          const uint32_t f = valid ? atomic_ld(&dt.flag[qt]) : 0u;
+          const bool ready = valid && (f >> 2) == epoch && (f & 3u) != 0;
+          const uint64_t incl = __ballot(ready && (f & 3u) == 2u);
+          const uint32_t L = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+          const uint64_t need = (L >= 64 ? ~0ull : ((1ull << L) - 1ull)) & __ballot(valid);
+          if (need & ~__ballot(ready)) {  // a predecessor has not published yet
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) {  // never expected: stop instead of hanging the GPU
+              if (lane == 0) report(pages, res, p, ST_HANG);
+              break;
+            }
+            continue;
+          }
+          uint64_t v = 0;
+          if (lane < L && valid) v = atomic_ld64(&dt.agg[qt]);
+          else if (lane == L) v = atomic_ld64(&dt.inc[qt]);
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+          P += v;
+          if (L < 64) break;
+          base -= 64;
+        }
+        if (lane == 0) {
+          __hip_atomic_store(&dt.inc[t], P + T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_s_waitcnt(0);
+          __hip_atomic_store(&dt.flag[t], epoch * 4u + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (lane == 0) sm.prefix = P;
+    }
+    __syncthreads();
+    // ---- values
+    {
+      uint64_t acc = info.first + sm.prefix + pre;
+      const uint32_t i0 = lo + (uint32_t)tid * DPT;
+      if (i0 < hi) {
+        if (ES == 8) {
+          int64_t* op = reinterpret_cast<int64_t*>(out) + pw.value_out + i0;
+          if (i0 + DPT <= hi && !(pw.value_out & 1)) {  // 16-byte aligned stores
+#pragma unroll
+            for (int j = 0; j < DPT; j += 2) {
+              const uint64_t v0 = acc + x[j];
+              const uint64_t v1 = v0 + x[j + 1];
+              acc = v1;
+              *reinterpret_cast<uint4*>(op + j) =
+                  make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+              acc += x[j];
+              if (i0 + j < hi) op[j] = (int64_t)acc;
+            }
+          }
+        } else {
+          int32_t* op = reinterpret_cast<int32_t*>(out) + pw.value_out + i0;
+#pragma unroll
+          for (int j = 0; j < DPT; ++j) {
+            acc += x[j];
+            if (i0 + j < hi) op[j] = (int32_t)(uint32_t)acc;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Per-page fallback for pages the tiled path does not take (k_delta with a page filter).
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, DeltaTables dt,
+                                                   uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const int p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (dt.page[p].tiled) return;
+  DeltaInfo info;
+  int32_t st = delta_stream<ES>(sm, blob, blob_len, pw.base + pw.val_off, pw.val_bytes, pw.nonnull,
+                                pw.nonnull, out + pw.value_out * ES, info);
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
+}
+
+extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                                             int npages, uint32_t ntiles, const uint32_t* tile_page,
+                                             DeltaTables dt, uint32_t epoch, int es, uint8_t* out,
+                                             ChunkResult* res, hipStream_t s) {
+  const dim3 eg(ntiles);
+  if (es == 8) {
+    hipLaunchKernelGGL(k_delta_index<8>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
+    if (ntiles) hipLaunchKernelGGL(k_delta_expand<8>, eg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, epoch, out, res);
+    hipLaunchKernelGGL(k_delta_rest<8>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
+  } else if (es == 4) {
+    hipLaunchKernelGGL(k_delta_index<4>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
+    if (ntiles) hipLaunchKernelGGL(k_delta_expand<4>, eg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, epoch, out, res);
+    hipLaunchKernelGGL(k_delta_rest<4>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pqg

@@ -59,6 +59,12 @@ __device__ inline uint64_t lload_u64(const uint32_t* words, uint32_t byte_idx) {
   return (lo >> sh) | ((uint64_t)words[wi + 2] << (64 - sh));
 }
 
+// 32-bit little-endian window from an LDS byte image (two dword reads + v_alignbyte).
+__device__ inline uint32_t lload_u32(const uint32_t* words, uint32_t byte_idx) {
+  const uint32_t wi = byte_idx >> 2;
+  return __builtin_amdgcn_alignbyte(words[wi + 1], words[wi], byte_idx & 3u);
+}
+
 __device__ inline uint32_t lbyte(const uint32_t* words, uint32_t byte_idx) {
   return (words[byte_idx >> 2] >> ((byte_idx & 3u) * 8u)) & 0xFFu;
 }

@@ -137,8 +137,7 @@ __global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
 // Index pass over stream `sel` of every page (one wave per page), pqg_runs.hpp.
 __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                   PageWork* pages, ColumnParams cp, int sel,
-                                                  int dict_page, RunCkpt* __restrict__ ck,
-                                                  ChunkResult* res) {
+                                                  int dict_page, RunTables rt, ChunkResult* res) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
   const PageWork pw = pages[p];
@@ -152,7 +151,8 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
     }
     if (pages[dict_page].status != 0) return;
   }
-  const int32_t st = run_index(blob, blob_len, s, ck + pw.ltile0, sm);
+  const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0,
+                              rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT, rt.nruns + pw.ltile0, sm);
   if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 
@@ -168,6 +168,7 @@ struct LevelEmit {
       for (int j = 0; j < 8; ++j)
         if ((mask >> j) & 1) nonnull += ((int16_t)v[j] == max_level) ? 1 : 0;
     }
+    if (!out) return;  // diagnostics: no stores
     if (mask == 0xFFu) {
       uint4 pk;
       pk.x = (v[0] & 0xFFFFu) | (v[1] << 16);
@@ -187,22 +188,30 @@ struct LevelEmit {
 // read_batch will ask for (def == max_def, column/reader.rs:212-226).
 __global__ void __launch_bounds__(WG) k_expand_levels(const uint8_t* __restrict__ blob,
                                                       uint64_t blob_len, PageWork* pages,
-                                                      const uint32_t* __restrict__ tile_page,
-                                                      const RunCkpt* __restrict__ ck,
+                                                      const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                      RunTables rt,
                                                       ColumnParams cp, int which,
                                                       int16_t* __restrict__ out) {
   __shared__ ExpandSmem sm;
+  const int dbg = cp.debug;
   int p;
   Stream s;
-  uint32_t lo, hi, next_pos;
+  uint32_t lo, hi, next_pos, nrec;
   RunCkpt c;
-  if (!expand_setup(blob, pages, tile_page, ck, cp, which, p, s, lo, hi, c, next_pos)) return;
-  LevelEmit em{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
-  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
-  if (which == SS_DEF) {
-    const uint64_t t = block_sum_u64(em.nonnull, sm.red);
-    if (threadIdx.x == 0 && t) atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nonnull),
-                                         (unsigned long long)t);
+  const uint2* recs;
+  for (uint32_t i = 0; i < EX_TPW; ++i) {
+    const uint32_t t = blockIdx.x * EX_TPW + i;
+    if (t >= ntiles) break;
+    if (!expand_setup(blob, pages, tile_page, rt, cp, which, t, p, s, lo, hi, c, next_pos, recs, nrec))
+      continue;
+    if (dbg & 1) continue;
+    LevelEmit em{(dbg & 4) ? nullptr : out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
+    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
+    if (which == SS_DEF && !(dbg & 2)) {
+      const uint64_t nn = block_sum_u64(em.nonnull, sm.red);
+      if (threadIdx.x == 0 && nn) atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nonnull),
+                                            (unsigned long long)nn);
+    }
   }
 }
 
@@ -280,21 +289,27 @@ struct DictEmit {
 template <int ES>
 __global__ void __launch_bounds__(WG) k_expand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                     PageWork* pages,
-                                                    const uint32_t* __restrict__ tile_page,
-                                                    const RunCkpt* __restrict__ ck, ColumnParams cp,
+                                                    const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                    RunTables rt, ColumnParams cp,
                                                     int dict_page, uint8_t* __restrict__ out,
                                                     ChunkResult* res) {
   __shared__ ExpandSmem sm;
   int p;
   Stream s;
-  uint32_t lo, hi, next_pos;
+  uint32_t lo, hi, next_pos, nrec;
   RunCkpt c;
+  const uint2* recs;
   if (dict_page < 0 || pages[dict_page].status != 0) return;
-  if (!expand_setup(blob, pages, tile_page, ck, cp, SS_DICT, p, s, lo, hi, c, next_pos)) return;
-  const PageWork& dp = pages[dict_page];
-  DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
-  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
-  if (em.err) report(pages, res, p, em.err);
+  for (uint32_t i = 0; i < EX_TPW; ++i) {
+    const uint32_t t = blockIdx.x * EX_TPW + i;
+    if (t >= ntiles) break;
+    if (!expand_setup(blob, pages, tile_page, rt, cp, SS_DICT, t, p, s, lo, hi, c, next_pos, recs, nrec))
+      continue;
+    const PageWork& dp = pages[dict_page];
+    DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
+    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
+    if (em.err) report(pages, res, p, em.err);
+  }
 }
 
 // Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
@@ -410,17 +425,23 @@ struct BoolEmit {
 
 __global__ void __launch_bounds__(WG) k_expand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                     PageWork* pages,
-                                                    const uint32_t* __restrict__ tile_page,
-                                                    const RunCkpt* __restrict__ ck, ColumnParams cp,
+                                                    const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                    RunTables rt, ColumnParams cp,
                                                     uint8_t* __restrict__ out) {
   __shared__ ExpandSmem sm;
   int p;
   Stream s;
-  uint32_t lo, hi, next_pos;
+  uint32_t lo, hi, next_pos, nrec;
   RunCkpt c;
-  if (!expand_setup(blob, pages, tile_page, ck, cp, SS_BOOL, p, s, lo, hi, c, next_pos)) return;
-  BoolEmit em{out, 0};
-  run_expand(blob, blob_len, s, c, next_pos, lo, hi, sm, em);
+  const uint2* recs;
+  for (uint32_t i = 0; i < EX_TPW; ++i) {
+    const uint32_t t = blockIdx.x * EX_TPW + i;
+    if (t >= ntiles) break;
+    if (!expand_setup(blob, pages, tile_page, rt, cp, SS_BOOL, t, p, s, lo, hi, c, next_pos, recs, nrec))
+      continue;
+    BoolEmit em{out, 0};
+    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
+  }
 }
 
 // ------------------------------------------------------------------------------ finalize
@@ -444,24 +465,24 @@ hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* 
 }
 
 hipError_t pqg_launch_run_index(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                int npages, ColumnParams cp, int sel, int dict_page, RunCkpt* ck,
+                                int npages, ColumnParams cp, int sel, int dict_page, RunTables rt,
                                 ChunkResult* res, hipStream_t s) {
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
-                     dict_page, ck, res);
+                     dict_page, rt, res);
   return hipGetLastError();
 }
 
 // Level stream `which` (0 def, 1 rep): index pass, then the grid-wide expand pass.
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                              int npages, uint32_t ntiles, ColumnParams cp, int which,
-                             const uint32_t* tile_page, RunCkpt* ck, int16_t* out,
+                             const uint32_t* tile_page, RunTables rt, int16_t* out,
                              ChunkResult* res, hipStream_t s) {
   const int sel = which ? SS_REP : SS_DEF;
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
-                     -1, ck, res);
+                     -1, rt, res);
   if (ntiles)
-    hipLaunchKernelGGL(k_expand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages,
-                       tile_page, ck, cp, sel, out);
+    hipLaunchKernelGGL(k_expand_levels, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages,
+                       tile_page, ntiles, rt, cp, sel, out);
   return hipGetLastError();
 }
 
@@ -473,17 +494,17 @@ hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es
 
 hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                            uint32_t ntiles, ColumnParams cp, int dict_page, int es,
-                           const uint32_t* tile_page, RunCkpt* ck, uint8_t* out, ChunkResult* res,
+                           const uint32_t* tile_page, RunTables rt, uint8_t* out, ChunkResult* res,
                            hipStream_t s) {
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
-                     dict_page, ck, res);
+                     dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
   switch (es) {
-    case 1: hipLaunchKernelGGL(k_expand_dict<1>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL(k_expand_dict<4>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL(k_expand_dict<8>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL(k_expand_dict<12>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ck, cp, dict_page, out, res); break;
+    case 1: hipLaunchKernelGGL(k_expand_dict<1>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL(k_expand_dict<4>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
+    case 8: hipLaunchKernelGGL(k_expand_dict<8>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
+    case 12: hipLaunchKernelGGL(k_expand_dict<12>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -511,13 +532,13 @@ hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npage
 
 hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                                int npages, uint32_t ntiles, ColumnParams cp,
-                               const uint32_t* tile_page, RunCkpt* ck, uint8_t* out,
+                               const uint32_t* tile_page, RunTables rt, uint8_t* out,
                                ChunkResult* res, hipStream_t s) {
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
-                     -1, ck, res);
+                     -1, rt, res);
   if (ntiles)
-    hipLaunchKernelGGL(k_expand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages,
-                       tile_page, ck, cp, out);
+    hipLaunchKernelGGL(k_expand_bool, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages,
+                       tile_page, ntiles, rt, cp, out);
   return hipGetLastError();
 }
 

@@ -233,15 +233,56 @@ struct IndexSmem {
   uint32_t region[IX_WORDS];
 };
 
-// Walks stream s of page p (one wave, all lanes uniform) and writes the checkpoints of its
-// expand tiles to ck[0 .. ceil(n / RUN_TILE)). Returns a status.
+constexpr int IX_CHUNKS = (IX_REG + 64) / 16;  // 16-byte chunks per region (64-byte overlap)
+
+// Region r of the walker's grid: bytes [G + r*IX_REG, G + (r+1)*IX_REG + 64), loaded by the
+// whole wave into registers (one wave-instruction per KiB, all in flight together).
+__device__ inline void ix_fetch(const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t A0,
+                                uint32_t lane, uint4 (&v)[9]) {
+  if (A0 + IX_REG + 64 <= blob_len) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const uint32_t c = lane + 64u * (uint32_t)k;
+      if (k < 8 || c < (uint32_t)IX_CHUNKS) v[k] = *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16);
+    }
+  } else {  // blob tail: guarded byte loads (unrolled: v must stay in registers)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const uint32_t c = lane + 64u * (uint32_t)k;
+      if (k < 8 || c < (uint32_t)IX_CHUNKS) v[k] = gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
+    }
+  }
+}
+
+__device__ inline void ix_install(uint32_t* region, uint32_t lane, const uint4 (&v)[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const uint32_t c = lane + 64u * (uint32_t)k;
+    if (k < 8 || c < (uint32_t)IX_CHUNKS) reinterpret_cast<uint4*>(region)[c] = v[k];
+  }
+}
+
+__device__ inline uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// Walks stream s of one page with one wave and writes, per expand tile k of the stream:
+// ck[k] = header of the run holding the tile's first output; runs[k*RUN_CAPT + j] = the tile's
+// runs (page-relative first output, RLE value | payload offset); nruns[k] = their count
+// (> RUN_CAPT: records incomplete, the expand pass re-walks the tile). Every check the
+// reference makes while reading the stream is made here. Returns a status.
+//
+// The serial part is reduced to the header chain itself: a scalar loop follows up to 64
+// headers (one LDS read, a few SALU ops and a v_writelane per hop), then the 64 lanes parse
+// those headers in parallel, prefix-sum their output counts, check them and write records,
+// checkpoints and counts together.
 __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                    const Stream& s, RunCkpt* __restrict__ ck, IndexSmem& sm) {
+                                    const Stream& s, RunCkpt* __restrict__ ck,
+                                    uint2* __restrict__ runs, uint32_t* __restrict__ nruns,
+                                    IndexSmem& sm) {
   const uint32_t lane = threadIdx.x & 63;
   if (s.err) return s.err;
   const uint32_t n = s.n;
   if (n == 0) return 0;
-  const int w = s.w;
+  const uint32_t w = (uint32_t)s.w;
   if (s.kind == LK_BIT_PACKED) {  // one header-less run (levels.rs:203-209)
     if ((uint64_t)n * (uint64_t)w > (uint64_t)s.slen * 8ull) return ST_EOF;
     if (w > 32) return ST_PANIC;
@@ -249,40 +290,132 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
   }
   const uint64_t S = s.S;
   const uint32_t slen = s.slen;
-  uint32_t cur = 0, produced = 0, next_tile = 0;
-  uint64_t A0 = ~0ull;
+  const uint64_t G = S & ~15ull;            // region grid origin
+  const uint32_t off0 = (uint32_t)(S - G);  // stream byte 0 in grid coordinates
+  const uint32_t vb = (w + 7u) >> 3;
+  const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
+  const uint64_t lanes_below = (1ull << lane) - 1ull;
+  uint4 pf[9];
+  uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
+  uint32_t cur = 0;            // next header
+  uint32_t produced = 0;       // outputs before `cur`'s run
+  uint32_t carry_tile = 0;     // tile of output `produced`
+  uint32_t carry_j = 0;        // records already written for carry_tile
   while (true) {
-    if (produced >= n) return 0;
     if (cur >= slen) return ST_EOF;  // reload() finds no more data: the reference stalls (A.4)
-    if (A0 == ~0ull || S + cur < A0 || S + cur - A0 >= (uint64_t)IX_REG) {
-      A0 = (S + cur) & ~15ull;
-      for (uint32_t c = lane; c < (IX_REG + 64) / 16; c += 64) {
-        const uint64_t a = A0 + (uint64_t)c * 16;
-        const uint4 v = (a + 16 <= blob_len) ? *reinterpret_cast<const uint4*>(blob + a)
-                                             : gload_u128_tail(blob, blob_len, a);
-        reinterpret_cast<uint4*>(sm.region)[c] = v;
+    const uint32_t r = (off0 + cur) / IX_REG;
+    if (r != cur_r) {
+      if (r != pf_r) ix_fetch(blob, blob_len, G + (uint64_t)r * IX_REG, lane, pf);
+      ix_install(sm.region, lane, pf);
+      cur_r = r;
+      pf_r = 0xFFFFFFFFu;
+      if (r + 1 < nregions) {  // prefetch the next region while this one is walked
+        ix_fetch(blob, blob_len, G + (uint64_t)(r + 1) * IX_REG, lane, pf);
+        pf_r = r + 1;
       }
-      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region writes done (vmcnt untouched)
       __builtin_amdgcn_wave_barrier();
     }
-    uint32_t nxt, cnt, inf, flg;
-    run_parse(sm.region, (uint32_t)(S + cur - A0), cur, slen, w, nxt, cnt, inf, flg);
-    if (flg & (RF_EOF | RF_PANIC)) return (flg & RF_PANIC) ? ST_PANIC : ST_EOF;
-    if (cnt) {
-      const uint32_t left = n - produced;
-      const uint32_t need = cnt < left ? cnt : left;
-      if (flg & RF_BP) {
-        if (w > 32) return ST_PANIC;  // BitReader::get_batch asserts num_bits <= 32
-        if ((uint64_t)inf * 8ull + (uint64_t)need * (uint64_t)w > (uint64_t)slen * 8ull)
-          return ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
+    const uint32_t rbase = r * IX_REG - off0;  // stream offset of region byte 0
+    // ---- hop loop: follow up to 64 headers inside this region (uniform, scalar)
+    uint32_t posv = 0, k = 0;
+    uint32_t acc = produced;  // < n before each add, so acc + min(cnt, n) < 2^32
+    while (k < 64) {
+      if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
+      const uint32_t rel = cur - rbase;
+      const uint32_t wi = rel >> 2;
+      const uint32_t x = rfl(__builtin_amdgcn_alignbyte(sm.region[wi + 1], sm.region[wi], rel & 3u));
+      const uint32_t b0 = x & 0xFFu;
+      uint32_t cnt, nxt;
+      bool stop = false;
+      if (!(b0 & 0x80u) && vb <= 3u) {
+        const uint32_t half = b0 >> 1;
+        if (b0 & 1u) {
+          cnt = half << 3;
+          nxt = cur + 1u + half * w;
+        } else {
+          cnt = half;
+          nxt = cur + 1u + vb;
+        }
+      } else {
+        uint32_t inf, flg;
+        run_parse(sm.region, rel, cur, slen, (int)w, nxt, cnt, inf, flg);
+        nxt = rfl(nxt);
+        cnt = rfl(cnt);
+        stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
       }
-      while (next_tile * RUN_TILE < produced + need) {
-        if (lane == 0) ck[next_tile] = RunCkpt{cur, produced};
-        ++next_tile;
-      }
-      produced += need;
+      posv = lane == k ? cur : posv;  // v_cmp + v_cndmask
+      ++k;
+      acc += cnt < n ? cnt : n;
+      cur = nxt;
+      if (stop || acc >= n) break;
     }
-    cur = nxt;
+    if (k == 0) continue;  // region boundary: reload
+    // ---- batch: lane l re-parses header l
+    const bool in = lane < k;
+    uint32_t nx, cnt = 0, inf = 0, flg = 0;
+    if (in) run_parse(sm.region, posv - rbase, posv, slen, (int)w, nx, cnt, inf, flg);
+    // exclusive scan of counts
+    uint64_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint64_t before = (uint64_t)produced + incl - cnt;
+    const uint32_t need = before >= n ? 0u : (uint32_t)((uint64_t)cnt < n - before ? cnt : n - before);
+    const bool bp = (flg & RF_BP) != 0;
+    int32_t e = 0;
+    if (in) {
+      if (flg & (RF_EOF | RF_PANIC)) e = (flg & RF_PANIC) ? ST_PANIC : ST_EOF;
+      else if (need && bp && w > 32) e = ST_PANIC;  // BitReader::get_batch asserts num_bits <= 32
+      else if (need && bp && (uint64_t)inf * 8ull + (uint64_t)need * w > (uint64_t)slen * 8ull)
+        e = ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
+    }
+    const uint64_t emask = __ballot(e != 0);
+    if (emask) return __shfl(e, __builtin_ctzll(emask), 64);
+    // records: lanes whose run yields outputs
+    const bool valid = in && need > 0;
+    const uint64_t V = __ballot(valid);
+    const uint32_t tile = (uint32_t)(before / RUN_TILE);
+    const uint32_t end_level = (uint32_t)before + need;          // one past the run's last output
+    const uint32_t end_tile = (end_level - 1u) / RUN_TILE;        // tile of its last output
+    // previous valid lane (its tile decides whether this lane starts a tile group)
+    const uint64_t vb_below = V & lanes_below;
+    const int prev = vb_below ? 63 - __builtin_clzll(vb_below) : -1;
+    const uint32_t prev_tile = __shfl(tile, prev < 0 ? 0 : prev, 64);
+    const bool head = valid && (prev < 0 || prev_tile != tile);
+    const uint64_t H = __ballot(head);
+    const uint64_t hb = H & (lanes_below | (1ull << lane));
+    const int hl = hb ? 63 - __builtin_clzll(hb) : 0;             // head lane of this lane's group
+    const uint32_t rank = (uint32_t)__builtin_popcountll(V & lanes_below & ~((1ull << hl) - 1ull));
+    const uint32_t head_before = __shfl((uint32_t)before, hl, 64);
+    const uint32_t base = tile == carry_tile ? carry_j : (head_before > tile * RUN_TILE ? 1u : 0u);
+    const uint32_t j = base + rank;
+    const uint32_t info = bp ? inf : (R_RLE | (inf > 0x7FFFFFFFu ? 0x7FFFFFFFu : inf));
+    if (valid) {
+      if (j == 0) ck[tile] = RunCkpt{posv, (uint32_t)before};
+      if (j < RUN_CAPT) runs[(uint64_t)tile * RUN_CAPT + j] = make_uint2((uint32_t)before, info);
+      const bool done_tile = end_tile > tile || end_level == (tile + 1) * RUN_TILE || end_level >= n;
+      if (done_tile) nruns[tile] = j + 1;
+      for (uint32_t t = tile + 1; t <= end_tile; ++t) {  // the run continues into later tiles
+        ck[t] = RunCkpt{posv, (uint32_t)before};
+        runs[(uint64_t)t * RUN_CAPT] = make_uint2((uint32_t)before, info);
+        if (t < end_tile || end_level == (t + 1) * RUN_TILE || end_level >= n) nruns[t] = 1;
+      }
+    }
+    // carry to the next batch (from the last valid lane)
+    if (V) {
+      const int L = 63 - __builtin_clzll(V);
+      const uint32_t lt = rfl(__shfl(tile, L, 64));
+      const uint32_t lj = rfl(__shfl(j, L, 64));
+      const uint32_t le = rfl(__shfl(end_level, L, 64));
+      const uint32_t let = rfl(__shfl(end_tile, L, 64));
+      produced = le;
+      carry_tile = le / RUN_TILE;
+      carry_j = (let == carry_tile) ? (lt == carry_tile ? lj + 1 : 1u) : 0u;
+    }
+    if (produced >= n) return 0;
   }
 }
 
@@ -290,8 +423,9 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
 
 struct ExpandSmem {
   uint32_t stage[EX_WORDS];
-  uint32_t start[EX_RCAP + 1];
-  uint32_t info[EX_RCAP];
+  uint32_t start[EX_RCAP + 2];
+  uint32_t info[EX_RCAP + 1];
+  uint32_t fix[RUN_TILE / 8];  // output chunks left to the general path
   uint32_t ctl[4];
   uint64_t red[4];
 };
@@ -300,7 +434,8 @@ struct ExpandSmem {
 // 256 threads of the workgroup. Uniform control flow; stream already validated by run_index.
 template <class Emit>
 __device__ inline void run_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                  const Stream& s, RunCkpt c, uint32_t next_pos, uint32_t lo,
+                                  const Stream& s, RunCkpt c, uint32_t next_pos,
+                                  const uint2* __restrict__ recs, uint32_t nrec, uint32_t lo,
                                   uint32_t hi, ExpandSmem& sm, Emit& emit) {
   const int tid = threadIdx.x;
   const int w = s.w;
@@ -327,20 +462,55 @@ __device__ inline void run_expand(const uint8_t* __restrict__ blob, uint64_t blo
   if (A1 > next_end) A1 = next_end;
   if (A1 > A0 + EX_STAGE) A1 = A0 + EX_STAGE;
   const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
-  for (uint32_t k = tid; k < nchunks; k += WG) {
-    const uint64_t a = A0 + (uint64_t)k * 16;
-    const uint4 v = (a + 16 <= blob_len) ? *reinterpret_cast<const uint4*>(blob + a)
-                                         : gload_u128_tail(blob, blob_len, a);
-    reinterpret_cast<uint4*>(sm.stage)[k] = v;
+  const bool have_recs = s.kind != LK_BIT_PACKED && nrec <= RUN_CAPT;
+  {
+    // all loads in flight together: the tile's bytes and its run records
+    constexpr int PER = (EX_STAGE / 16 + WG - 1) / WG;
+    uint4 v[PER];
+    const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t cidx = (uint32_t)tid + (uint32_t)(k * WG);
+      if (cidx < nchunks) {
+        const uint64_t a = A0 + (uint64_t)cidx * 16;
+        v[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+      }
+    }
+    uint2 rr = make_uint2(0, 0);
+    if (have_recs && (uint32_t)tid < nrec) rr = recs[tid];
+    uint2 rr2 = make_uint2(0, 0);
+    if (have_recs && (uint32_t)tid + WG < nrec) rr2 = recs[tid + WG];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t cidx = (uint32_t)tid + (uint32_t)(k * WG);
+      if (cidx < nchunks) reinterpret_cast<uint4*>(sm.stage)[cidx] = v[k];
+    }
+    if (have_recs) {
+      if ((uint32_t)tid < nrec) {
+        sm.start[tid] = rr.x;
+        sm.info[tid] = rr.y;
+      }
+      if ((uint32_t)tid + WG < nrec) {
+        sm.start[tid + WG] = rr2.x;
+        sm.info[tid + WG] = rr2.y;
+      }
+      if (tid == 0) {
+        sm.start[nrec] = hi;
+        sm.start[nrec + 1] = hi;
+        sm.ctl[0] = nrec;
+      }
+    }
   }
   if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
   const uint64_t staged = (uint64_t)nchunks * 16;  // bytes [A0, A0 + staged) valid
   __syncthreads();
 
   uint32_t cur = c.pos, produced = c.first, seg_lo = lo;
+  bool first_batch = true;
   while (seg_lo < hi) {
-    // ---- walk: runs covering [seg_lo, seg_hi) into the LDS run list (wave 0, uniform)
-    if (tid < 64) {
+    // ---- runs covering [seg_lo, seg_hi) into the LDS run list: the index pass's records, or
+    // a re-walk from the checkpoint when the tile has more runs than it keeps (wave 0, uniform)
+    if (!(have_recs && first_batch) && tid < 64) {
       uint32_t nr = 0;
       if (s.kind == LK_BIT_PACKED) {
         if (tid == 0) {
@@ -375,84 +545,126 @@ __device__ inline void run_expand(const uint8_t* __restrict__ blob, uint64_t blo
         }
         if (tid == 0) sm.start[nr] = produced;
       }
-      if (tid == 0) sm.ctl[0] = nr;
+      if (tid == 0) {
+        sm.ctl[0] = nr;
+        sm.start[nr + 1] = sm.start[nr];
+      }
     }
+    if (tid == 0) sm.ctl[1] = 0;
     __syncthreads();
     const uint32_t nr = sm.ctl[0];
     if (nr == 0) break;  // defensive: nothing left to expand
     const uint32_t seg_hi = sm.start[nr] < hi ? sm.start[nr] : hi;
     if (seg_hi <= seg_lo) break;
-    // ---- expand: lane chunks of 8 outputs, two coalesced halves per tile
+    // ---- expand: lane chunks of 8 outputs, two coalesced halves per tile. Chunks inside one
+    // or two runs (nearly all) take a branch-free path: per output, pick run a or a+1, one LDS
+    // window read, shift and mask. Chunks over three or more runs, or whose payload is not
+    // staged, go to a list handled after the barrier by the general path.
+    const uint32_t sb32 = (uint32_t)(A0 - S);  // stream offset of staged byte 0 (mod 2^32)
+    const uint32_t wm = (uint32_t)wmask;
+    const uint32_t stg = (uint32_t)staged;
 #pragma unroll 1
     for (int half = 0; half < 2; ++half) {
       const uint32_t g = lo + (uint32_t)half * (RUN_TILE / 2) + (uint32_t)tid * 8u;
       if (g + 8 <= seg_lo || g >= seg_hi) continue;
+      const uint32_t o0 = g < seg_lo ? seg_lo : g;
+      uint32_t a = 0;
+#pragma unroll
+      for (uint32_t step = EX_RCAP / 2; step; step >>= 1)
+        if (a + step < nr && sm.start[a + step] <= o0) a += step;
+      const uint32_t stA = sm.start[a], infA = sm.info[a];
+      const uint32_t stB = sm.start[a + 1];
+      const uint32_t infB = sm.info[a + 1 < nr ? a + 1 : a];
+      const uint32_t stC = sm.start[a + 2 <= nr ? a + 2 : nr];
+      const uint32_t end = g + 8 < seg_hi ? g + 8 : seg_hi;
+      bool fixup = end > stC;  // three or more runs
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t oj = g + (uint32_t)j;
+        const bool inB = oj >= stB;
+        const uint32_t inf = inB ? infB : infA;
+        const uint32_t d = oj - (inB ? stB : stA);
+        const uint32_t rel = inf - sb32;
+        const uint32_t bit = rel * 8u + d * (uint32_t)w;
+        const bool rle = (inf & R_RLE) != 0;
+        const bool ok = rle || (d < (1u << 20) && rel < stg && (bit >> 3) + 12u <= stg);
+        const uint32_t byte = ok && !rle ? bit >> 3 : 0u;
+        uint32_t val;
+        if (w <= 24) val = (lload_u32(sm.stage, byte) >> (bit & 7)) & wm;
+        else val = (uint32_t)(lload_u64(sm.stage, byte) >> (bit & 7)) & wm;
+        val = rle ? (inf & 0x7FFFFFFFu) : val;
+        const bool in = oj >= seg_lo && oj < seg_hi;
+        fixup |= in && !ok;
+        v[j] = in ? val : 0u;
+      }
+      if (fixup) {
+        const uint32_t slot = atomicAdd(&sm.ctl[1], 1u);
+        sm.fix[slot] = g;
+        continue;
+      }
+      uint32_t mask = 0xFFu;
+      if (g < seg_lo || g + 8 > seg_hi) {
+        mask = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (g + j >= seg_lo && g + j < seg_hi) mask |= 1u << j;
+      }
+      emit(s.out + g, v, mask);
+    }
+    __syncthreads();
+    // ---- general path for the listed chunks (one lane each)
+    const uint32_t nfix = sm.ctl[1];
+    for (uint32_t f = tid; f < nfix; f += WG) {
+      const uint32_t g = sm.fix[f];
+      const uint32_t o0 = g < seg_lo ? seg_lo : g;
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t step = EX_RCAP / 2; step; step >>= 1)
+        if (r + step < nr && sm.start[r + step] <= o0) r += step;
+      uint32_t st = sm.start[r], nst = sm.start[r + 1], inf = sm.info[r];
       uint32_t v[8];
       uint32_t mask = 0;
-      const uint32_t o0 = g < seg_lo ? seg_lo : g;
-      int a = 0, b = (int)nr - 1;
-      while (a < b) {
-        const int mid = (a + b + 1) >> 1;
-        if (sm.start[mid] <= o0) a = mid;
-        else b = mid - 1;
-      }
-      int r = a;
-      const uint32_t inf0 = sm.info[r];
-      const bool one_run = g >= seg_lo && g + 8 <= seg_hi && g + 8 <= sm.start[r + 1];
-      const uint64_t bit0 = (uint64_t)inf0 * 8ull + (uint64_t)(g - sm.start[r]) * (uint64_t)w;
-      const uint64_t ri0 = S + (bit0 >> 3) - A0;
-      if (one_run && ((inf0 & R_RLE) || (S + (bit0 >> 3) >= A0 && ri0 + (uint64_t)w + 12 <= staged))) {
-        if (inf0 & R_RLE) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = inf0 & 0x7FFFFFFFu;
-        } else if (w <= 7) {
-          const uint64_t x = lload_u64(sm.stage, (uint32_t)ri0);
-          const uint32_t s0 = (uint32_t)(bit0 & 7);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (uint32_t)((x >> (s0 + j * w)) & wmask);
-        } else {
-          const uint32_t rb = (uint32_t)(ri0 * 8ull + (bit0 & 7));
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t bb = rb + (uint32_t)(j * w);
-            v[j] = (uint32_t)((lload_u64(sm.stage, bb >> 3) >> (bb & 7)) & wmask);
-          }
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t oj = g + (uint32_t)j;
+        v[j] = 0;
+        if (oj < seg_lo || oj >= seg_hi) continue;
+        while (oj >= nst && r + 1 < nr) {
+          ++r;
+          st = nst;
+          nst = sm.start[r + 1];
+          inf = sm.info[r];
         }
-        mask = 0xFFu;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          v[j] = 0;
-          const uint32_t oj = g + (uint32_t)j;
-          if (oj < seg_lo || oj >= seg_hi) continue;
-          while (oj >= sm.start[r + 1]) ++r;
-          const uint32_t inf = sm.info[r];
-          if (inf & R_RLE) {
-            v[j] = inf & 0x7FFFFFFFu;
-          } else {
-            const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(oj - sm.start[r]) * (uint64_t)w;
-            const uint64_t abs = S + (bit >> 3);
-            const uint64_t ri = abs - A0;
-            const uint64_t x = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
-                                                                : gload_u64(blob, blob_len, abs);
-            v[j] = (uint32_t)((x >> (bit & 7)) & wmask);
-          }
-          mask |= 1u << j;
+        uint32_t val = inf & 0x7FFFFFFFu;
+        if (!(inf & R_RLE)) {
+          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(oj - st) * (uint64_t)w;
+          const uint64_t abs = S + (bit >> 3);
+          const uint64_t ri = abs - A0;
+          const uint64_t x = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
+                                                              : gload_u64(blob, blob_len, abs);
+          val = (uint32_t)((x >> (bit & 7)) & wmask);
         }
+        v[j] = val;
+        mask |= 1u << j;
       }
-      if (mask) emit(s.out + g, v, mask);
+      emit(s.out + g, v, mask);
     }
     seg_lo = seg_hi;
+    first_batch = false;
     __syncthreads();
   }
 }
 
 // Common front of the expand kernels: tile -> page, stream and output range.
+// Expand tiles per workgroup: the per-tile setup (page lookup, stream, checkpoint) is scalar
+// work that a larger grain amortises.
+constexpr uint32_t EX_TPW = 4;
+
 __device__ inline bool expand_setup(const uint8_t* blob, PageWork* pages, const uint32_t* tile_page,
-                                    const RunCkpt* ck, ColumnParams cp, int sel, int& p,
-                                    Stream& s, uint32_t& lo, uint32_t& hi, RunCkpt& c,
-                                    uint32_t& next_pos) {
-  const uint32_t t = blockIdx.x;
+                                    const RunTables& rt, ColumnParams cp, int sel, uint32_t t,
+                                    int& p, Stream& s, uint32_t& lo, uint32_t& hi, RunCkpt& c,
+                                    uint32_t& next_pos, const uint2*& recs, uint32_t& nrec) {
   p = (int)tile_page[t];
   const PageWork& pw = pages[p];
   if (pw.status != 0) return false;
@@ -464,9 +676,13 @@ __device__ inline bool expand_setup(const uint8_t* blob, PageWork* pages, const 
   if (s.kind == LK_BIT_PACKED) {
     c = RunCkpt{0, 0};
     next_pos = s.slen;
+    nrec = 1;
+    recs = nullptr;
   } else {
-    c = ck[t];
-    next_pos = hi < s.n ? ck[t + 1].pos : s.slen;
+    recs = rt.runs + (uint64_t)t * RUN_CAPT;
+    c = rt.ck[t];
+    next_pos = hi < s.n ? rt.ck[t + 1].pos : s.slen;
+    nrec = rt.nruns[t];
   }
   return true;
 }

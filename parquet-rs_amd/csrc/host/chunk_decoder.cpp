@@ -8,6 +8,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -22,26 +23,28 @@ extern "C" {
 hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, uint32_t*,
                               ChunkResult*, hipStream_t);
 hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
-                                RunCkpt*, ChunkResult*, hipStream_t);
+                                RunTables, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                             const uint32_t*, RunCkpt*, int16_t*, ChunkResult*, hipStream_t);
+                             const uint32_t*, RunTables, int16_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                           int, const uint32_t*, RunCkpt*, uint8_t*, ChunkResult*, hipStream_t);
+                           int, const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
                                  uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
                                  ChunkResult*, hipStream_t);
 hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
-                               const uint32_t*, RunCkpt*, uint8_t*, ChunkResult*, hipStream_t);
+                               const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
+                                  DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
                                    uint32_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
-                            const uint32_t*, const RunCkpt*, int, int, bool, bool, uint64_t*,
+                            const uint32_t*, RunTables, int, int, bool, bool, uint64_t*,
                             uint32_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int64_t*,
                             uint8_t*, ChunkResult*, hipStream_t);
 }
@@ -67,8 +70,10 @@ struct Slot {
   size_t dcap = 0;
   // hybrid-stream expand tiles: tile -> page map and one checkpoint array per stream kind
   uint32_t* tile_page = nullptr;
-  RunCkpt* ck[3] = {};  // def, rep, values
+  RunTables rt[3] = {};  // def, rep, values (index-pass outputs)
   size_t tcap = 0;
+  DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
+  size_t dt_tcap = 0, dt_pcap = 0;
 };
 
 struct pqg_ctx {
@@ -84,6 +89,7 @@ struct pqg_ctx {
   bool timing = false;
   bool pending = false;
   double acc_ms[5] = {};
+  uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
   uint64_t acc_n = 0;
   int host_status = 0;
   int host_bad_page = -1;
@@ -175,7 +181,16 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
     hipFree(sl.tile_page);
-    for (RunCkpt* c : sl.ck) hipFree(c);
+    for (RunTables& t : sl.rt) {
+      hipFree(t.ck);
+      hipFree(t.runs);
+      hipFree(t.nruns);
+    }
+    hipFree(sl.dt.page);
+    hipFree(sl.dt.blocks);
+    hipFree(sl.dt.agg);
+    hipFree(sl.dt.inc);
+    hipFree(sl.dt.flag);
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   delete ctx;
@@ -362,6 +377,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
   cp.want_def = want_def;
   cp.want_rep = want_rep;
+  static const int dbg_env = getenv("PQG_DEBUG") ? atoi(getenv("PQG_DEBUG")) : 0;
+  cp.debug = dbg_env;
 
   ChunkResult r0{};
   r0.total_levels = ctx->total_levels;
@@ -404,24 +421,39 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (total_tiles + 1 > sl.tcap) {
     hipFree(sl.tile_page);
     sl.tile_page = nullptr;
-    for (RunCkpt*& c : sl.ck) {
-      hipFree(c);
-      c = nullptr;
+    for (RunTables& r : sl.rt) {
+      hipFree(r.ck);
+      hipFree(r.runs);
+      hipFree(r.nruns);
+      r = RunTables{};
     }
+    sl.tcap = 0;
     size_t cap = (size_t)total_tiles + 1024;
     HIPCHK(hipMalloc(&sl.tile_page, cap * sizeof(uint32_t)), "hipMalloc tile_page");
-    for (RunCkpt*& c : sl.ck) HIPCHK(hipMalloc(&c, (cap + 1) * sizeof(RunCkpt)), "hipMalloc ckpt");
     sl.tcap = cap;
   }
+  // run tables are allocated per stream kind on first use
+  auto tables = [&](int k) -> hipError_t {
+    RunTables& r = sl.rt[k];
+    if (r.ck) return hipSuccess;
+    hipError_t e = hipMalloc(&r.ck, (sl.tcap + 1) * sizeof(RunCkpt));
+    if (e == hipSuccess) e = hipMalloc(&r.runs, sl.tcap * RUN_CAPT * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&r.nruns, sl.tcap * sizeof(uint32_t));
+    return e;
+  };
+  const bool hybrid_values = enc_present[PQG_RLE_DICTIONARY] || (enc_present[PQG_RLE] && t == PQG_BOOLEAN);
+  if (want_def) HIPCHK(tables(0), "hipMalloc run tables");
+  if (want_rep) HIPCHK(tables(1), "hipMalloc run tables");
+  if (hybrid_values && out->values) HIPCHK(tables(2), "hipMalloc run tables");
   const uint32_t nt = total_tiles;
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
   if (np && want_def)
-    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.ck[0],
+    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              out->def_levels, ctx->d_res, s), "def levels");
   if (np && want_rep)
-    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.ck[1],
+    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
                              out->rep_levels, ctx->d_res, s), "rep levels");
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
   HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
@@ -438,9 +470,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
                                      ctx->d_res, s), "byte-array dictionary");
       HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
-                                  sl.ck[2], ctx->d_res, s), "dictionary index pass");
+                                  sl.rt[2], ctx->d_res, s), "dictionary index pass");
     }
-    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.ck[2], dict_page,
+    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2], dict_page,
                             tl,
                             enc_present[PQG_RLE_DICTIONARY], enc_present[PQG_DELTA_BYTE_ARRAY],
                             sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, out->values_capacity,
@@ -457,15 +489,39 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (enc_present[PQG_RLE_DICTIONARY]) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
       HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
-                             sl.ck[2], vo, ctx->d_res, s), "dict");
+                             sl.rt[2], vo, ctx->d_res, s), "dict");
     }
     if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
-      HIPCHK(pqg_launch_delta(blob, blob_len, ctx->d_pages, np, es, vo, ctx->d_res, s), "delta");
+      if (nt > sl.dt_tcap || (size_t)np > sl.dt_pcap) {
+        hipFree(sl.dt.page);
+        hipFree(sl.dt.blocks);
+        hipFree(sl.dt.agg);
+        hipFree(sl.dt.inc);
+        hipFree(sl.dt.flag);
+        sl.dt = DeltaTables{};
+        sl.dt_tcap = sl.dt_pcap = 0;
+        const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
+        HIPCHK(hipMalloc(&sl.dt.page, pc * sizeof(DeltaPage)), "hipMalloc delta pages");
+        HIPCHK(hipMalloc(&sl.dt.blocks, tc * DELTA_BCAP * sizeof(DeltaBlock)), "hipMalloc delta blocks");
+        HIPCHK(hipMalloc(&sl.dt.agg, tc * sizeof(uint64_t)), "hipMalloc delta agg");
+        HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
+        HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
+        HIPCHK(hipMemsetAsync(sl.dt.flag, 0, tc * sizeof(uint32_t), s), "memset delta flags");
+        sl.dt_tcap = tc;
+        sl.dt_pcap = pc;
+      }
+      ctx->epoch = (ctx->epoch + 1) & 0x3FFFFFFFu;
+      if (ctx->epoch == 0) {  // wrapped: flags from 2^30 decodes ago could match
+        HIPCHK(hipMemsetAsync(sl.dt.flag, 0, sl.dt_tcap * sizeof(uint32_t), s), "memset delta flags");
+        ctx->epoch = 1;
+      }
+      HIPCHK(pqg_launch_delta_tiled(blob, blob_len, ctx->d_pages, np, nt, sl.tile_page, sl.dt, ctx->epoch,
+                                    es, vo, ctx->d_res, s), "delta");
     }
     if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
       ctx->values_kernel = PQG_RLE;
-      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.ck[2], vo,
+      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2], vo,
                                  ctx->d_res, s), "rle bool");
     }
   }

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>  // uint2
+
 namespace pqg {
 
 // Status codes: ParquetError kinds (src/errors.rs:24-51) plus the two outcomes the reference
@@ -76,10 +78,49 @@ struct ChunkResult {
 // Outputs per expand tile of the RLE/bit-packed hybrid decoder (device/pqg_runs.hpp).
 constexpr uint32_t RUN_TILE = 4096;
 
+// Run records kept per expand tile by the index pass (more runs: the expand pass re-walks the
+// tile from its checkpoint).
+constexpr uint32_t RUN_CAPT = 256;
+
 // Walk checkpoint of one expand tile: the header of the run holding the tile's first output.
 struct RunCkpt {
   uint32_t pos;    // stream-relative byte offset of the run header
   uint32_t first;  // page-relative index of the run's first output
+};
+
+// Index-pass outputs of one stream kind, indexed by expand tile.
+struct RunTables {
+  RunCkpt* ck;      // [tiles + 1]
+  uint2* runs;      // [tiles * RUN_CAPT]
+  uint32_t* nruns;  // [tiles]
+};
+
+// DELTA_BINARY_PACKED index-pass outputs (device/pqg_delta.hip). Tiles of DELTA_TILE values
+// per page; each tile keeps the records of the blocks its values need.
+constexpr uint32_t DELTA_TILE = 4096;
+constexpr uint32_t DELTA_BCAP = 64;   // block records per tile (more: per-page fallback kernel)
+constexpr uint32_t DELTA_MBMAX = 16;  // mini-blocks per block on the tiled path
+
+struct DeltaBlock {
+  uint32_t wpos;      // stream offset of the block's mini-block width bytes
+  uint32_t pos;       // stream offset of its first mini-block
+  uint64_t min_delta;
+};
+
+struct DeltaPage {
+  uint64_t first;     // first value (zigzag-decoded)
+  uint32_t vpmb;      // values per mini-block
+  uint32_t nmb;       // mini-blocks per block
+  uint32_t tiled;     // 1: tiles/records valid; 0: decode with the per-page kernel
+  uint32_t pad;
+};
+
+struct DeltaTables {
+  DeltaPage* page;    // [npages]
+  DeltaBlock* blocks; // [tiles * DELTA_BCAP]
+  uint64_t* agg;      // [tiles] tile sums (decoupled look-back)
+  uint64_t* inc;      // [tiles] inclusive prefixes
+  uint32_t* flag;     // [tiles] epoch * 4 + {1 aggregate, 2 inclusive}
 };
 
 struct ColumnParams {
@@ -91,6 +132,7 @@ struct ColumnParams {
   int32_t rep_bit_width;
   int32_t want_def;  // def_levels output provided (read_batch(Some(def)))
   int32_t want_rep;
+  int32_t debug;     // diagnostics switches (PQG_DEBUG), 0 in production
 };
 
 }  // namespace pqg
