@@ -341,6 +341,11 @@ def main():
                                   "levels_ms": tv.levels_ms, "values_ms": tv.values_ms}
             w = wv
         result["variants"] = var
+    if os.environ.get("PQG_DEBUG") and int(os.environ["PQG_DEBUG"]) & 16:
+        st4 = (C.c_double * 4)()
+        pqgpu.lib().pqg_debug_stamps(ctx.h, st4)
+        result["debug_stamps"] = {"waves": st4[3], "desc_cyc": st4[0], "expand_cyc": st4[1],
+                                  "tail_cyc": st4[2]}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

@@ -170,35 +170,22 @@ struct BaDictEmit {
   }
 };
 
-// Dictionary indices -> (source, length) of the entry, expand pass over all tiles (the index
-// pass is k_run_index with SS_DICT); page byte counts accumulate per tile.
-__global__ void __launch_bounds__(WG) k_expand_badict(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                      PageWork* pages,
-                                                      const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                                      RunTables rt, ColumnParams cp,
-                                                      int dict_page, const uint64_t* dsrc,
-                                                      const uint32_t* dlen, uint64_t* vsrc,
-                                                      uint32_t* vlen, ChunkResult* res) {
-  __shared__ ExpandSmem sm;
-  int p;
-  Stream s;
-  uint32_t lo, hi, next_pos, nrec;
-  RunCkpt c;
-  const uint2* recs;
-  if (dict_page < 0 || pages[dict_page].status != 0) return;
-  for (uint32_t i = 0; i < EX_TPW; ++i) {
-    const uint32_t t = blockIdx.x * EX_TPW + i;
-    if (t >= ntiles) break;
-    if (!expand_setup(blob, pages, tile_page, rt, cp, SS_DICT, t, p, s, lo, hi, c, next_pos, recs, nrec))
-      continue;
-    // emitted indices are global value indices (out = value_out)
-    BaDictEmit em{dsrc, dlen, pages[dict_page].num_values, vsrc, vlen, 0, 0};
-    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
-    const uint64_t tb = block_sum_u64(em.bytes, sm.red);
-    if (em.err) report(pages, res, p, em.err);
-    if (threadIdx.x == 0 && tb)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nbytes_out), (unsigned long long)tb);
-  }
+// Dictionary indices -> (source, length) of the entry: wave expand pass over the tiles of the
+// index pass (k_run_index with SS_DICT); per quarter-tile byte totals go to rt.qcount.
+__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_badict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                       PageWork* pages, RunTables rt, int dict_page,
+                                                       const uint64_t* dsrc, const uint32_t* dlen,
+                                                       uint64_t* vsrc, uint32_t* vlen, ChunkResult* res) {
+  __shared__ WaveSmem sm;
+  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
+  BaDictEmit em{dsrc, dlen, dict_page >= 0 ? pages[dict_page].num_values : 0u, vsrc, vlen, 0, 0};
+  if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, sm, em);
+  const uint64_t bad = __ballot(em.err != 0);
+  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
+  uint64_t b = em.bytes;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) b += __shfl_xor(b, off, 64);
+  if ((threadIdx.x & 63) == 0) rt.qcount[blockIdx.x] = (uint32_t)min(b, (uint64_t)0xFFFFFFFFu);
 }
 
 __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -419,17 +406,21 @@ extern "C" hipError_t pqg_launch_ba_dict_prep(const uint8_t* blob, uint64_t blob
   return hipGetLastError();
 }
 
+extern "C" hipError_t pqg_launch_badict_expand(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
+                                               uint32_t ntiles, RunTables rt, int dict_page,
+                                               uint64_t* vsrc, uint32_t* vlen, uint64_t* dsrc,
+                                               uint32_t* dlen, ChunkResult* res, hipStream_t s) {
+  if (ntiles)
+    hipLaunchKernelGGL(k_wexpand_badict, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, pages, rt,
+                       dict_page, dsrc, dlen, vsrc, vlen, res);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                       int npages, uint32_t ntiles, ColumnParams cp,
-                                       const uint32_t* tile_page, RunTables rt, int dict_page,
-                                       int type_length, bool has_dict, bool has_dba,
-                                       uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre,
-                                       uint64_t* dsrc, uint32_t* dlen, uint64_t cap,
+                                       int npages, int type_length, bool has_dba, uint64_t* vsrc,
+                                       uint32_t* vlen, uint32_t* vpre, uint64_t cap,
                                        int64_t* offsets, uint8_t* out, ChunkResult* res,
                                        hipStream_t s) {
-  if (has_dict && ntiles)
-    hipLaunchKernelGGL(k_expand_badict, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages,
-                       tile_page, ntiles, rt, cp, dict_page, dsrc, dlen, vsrc, vlen, res);
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, type_length,
                      vsrc, vlen, vpre, res);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);

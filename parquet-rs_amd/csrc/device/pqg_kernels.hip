@@ -18,6 +18,7 @@
 namespace pqg {
 
 
+
 // ------------------------------------------------------------------------------ prepare
 
 __device__ inline uint32_t rd_u32(const uint8_t* p) {
@@ -184,34 +185,57 @@ struct LevelEmit {
   }
 };
 
-// Expand pass of a level stream (which: SS_DEF / SS_REP); def levels also count the values
-// read_batch will ask for (def == max_def, column/reader.rs:212-226).
-__global__ void __launch_bounds__(WG) k_expand_levels(const uint8_t* __restrict__ blob,
-                                                      uint64_t blob_len, PageWork* pages,
-                                                      const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                                      RunTables rt,
-                                                      ColumnParams cp, int which,
-                                                      int16_t* __restrict__ out) {
-  __shared__ ExpandSmem sm;
-  const int dbg = cp.debug;
-  int p;
-  Stream s;
-  uint32_t lo, hi, next_pos, nrec;
-  RunCkpt c;
-  const uint2* recs;
-  for (uint32_t i = 0; i < EX_TPW; ++i) {
-    const uint32_t t = blockIdx.x * EX_TPW + i;
-    if (t >= ntiles) break;
-    if (!expand_setup(blob, pages, tile_page, rt, cp, which, t, p, s, lo, hi, c, next_pos, recs, nrec))
-      continue;
-    if (dbg & 1) continue;
-    LevelEmit em{(dbg & 4) ? nullptr : out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
-    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
-    if (which == SS_DEF && !(dbg & 2)) {
-      const uint64_t nn = block_sum_u64(em.nonnull, sm.red);
-      if (threadIdx.x == 0 && nn) atomicAdd(reinterpret_cast<unsigned long long*>(&pages[p].nonnull),
-                                            (unsigned long long)nn);
-    }
+// Quarter-tile descriptors of stream `sel` (one thread per quarter), read by the wave expand
+// kernels.
+__global__ void __launch_bounds__(WG) k_quarter_desc(const uint8_t* __restrict__ blob, const PageWork* pages,
+                                                     const uint32_t* __restrict__ tile_page,
+                                                     uint32_t ntiles, RunTables rt, ColumnParams cp,
+                                                     int sel, int dict_page) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= ntiles * 4) return;
+  rt.desc[i] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, i >> 2, i & 3);
+}
+
+// Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
+__global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint32_t* __restrict__ qcount,
+                                                    int field) {
+  __shared__ uint64_t red[WG / 64];
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  const uint32_t q0 = pw.ltile0 * 4u, nq = pw.ntiles * 4u;
+  uint64_t s = 0;
+  for (uint32_t i = threadIdx.x; i < nq; i += WG) s += qcount[q0 + i];
+  const uint64_t t = block_sum_u64(s, red);
+  if (threadIdx.x == 0) {
+    if (field == 0) pages[p].nonnull = t;
+    else pages[p].nbytes_out = t;
+  }
+}
+
+// Expand pass of a level stream (which: SS_DEF / SS_REP), one wave per quarter tile; def
+// levels also count the values read_batch will ask for (def == max_def, column/reader.rs:212-226).
+__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                       RunTables rt, ColumnParams cp, int which,
+                                                       int16_t* __restrict__ out) {
+  __shared__ WaveSmem sm;
+  const bool stamps = (cp.debug & 16) != 0;
+  const uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
+  const uint64_t c1 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  LevelEmit em{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
+  if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, sm, em);
+  const uint64_t c2 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  if (which == SS_DEF) {
+    const uint32_t nn = wave_sum_u32((uint32_t)em.nonnull);
+    if ((threadIdx.x & 63) == 0) rt.qcount[blockIdx.x] = nn;
+  }
+  if (stamps && cp.dbgbuf) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t c3 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0)
+      reinterpret_cast<uint4*>(cp.dbgbuf)[blockIdx.x] =
+          make_uint4((uint32_t)(c1 - c0), (uint32_t)(c2 - c1), (uint32_t)(c3 - c2), (uint32_t)(c0 >> 8));
   }
 }
 
@@ -287,29 +311,17 @@ struct DictEmit {
 };
 
 template <int ES>
-__global__ void __launch_bounds__(WG) k_expand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages,
-                                                    const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                                    RunTables rt, ColumnParams cp,
-                                                    int dict_page, uint8_t* __restrict__ out,
-                                                    ChunkResult* res) {
-  __shared__ ExpandSmem sm;
-  int p;
-  Stream s;
-  uint32_t lo, hi, next_pos, nrec;
-  RunCkpt c;
-  const uint2* recs;
-  if (dict_page < 0 || pages[dict_page].status != 0) return;
-  for (uint32_t i = 0; i < EX_TPW; ++i) {
-    const uint32_t t = blockIdx.x * EX_TPW + i;
-    if (t >= ntiles) break;
-    if (!expand_setup(blob, pages, tile_page, rt, cp, SS_DICT, t, p, s, lo, hi, c, next_pos, recs, nrec))
-      continue;
-    const PageWork& dp = pages[dict_page];
-    DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
-    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
-    if (em.err) report(pages, res, p, em.err);
-  }
+__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, RunTables rt, int dict_page,
+                                                     uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ WaveSmem sm;
+  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
+  if (!d.qhi) return;
+  const PageWork& dp = pages[dict_page];
+  DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
+  wave_expand(blob, blob_len, d, rt.runs, sm, em);
+  const uint64_t bad = __ballot(em.err != 0);
+  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
 }
 
 // Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
@@ -423,25 +435,13 @@ struct BoolEmit {
   }
 };
 
-__global__ void __launch_bounds__(WG) k_expand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages,
-                                                    const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                                    RunTables rt, ColumnParams cp,
-                                                    uint8_t* __restrict__ out) {
-  __shared__ ExpandSmem sm;
-  int p;
-  Stream s;
-  uint32_t lo, hi, next_pos, nrec;
-  RunCkpt c;
-  const uint2* recs;
-  for (uint32_t i = 0; i < EX_TPW; ++i) {
-    const uint32_t t = blockIdx.x * EX_TPW + i;
-    if (t >= ntiles) break;
-    if (!expand_setup(blob, pages, tile_page, rt, cp, SS_BOOL, t, p, s, lo, hi, c, next_pos, recs, nrec))
-      continue;
-    BoolEmit em{out, 0};
-    run_expand(blob, blob_len, s, c, next_pos, recs, nrec, lo, hi, sm, em);
-  }
+__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     RunTables rt, uint8_t* __restrict__ out) {
+  __shared__ WaveSmem sm;
+  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
+  if (!d.qhi) return;
+  BoolEmit em{out, 0};
+  wave_expand(blob, blob_len, d, rt.runs, sm, em);
 }
 
 // ------------------------------------------------------------------------------ finalize
@@ -472,7 +472,22 @@ hipError_t pqg_launch_run_index(const uint8_t* blob, uint64_t blob_len, PageWork
   return hipGetLastError();
 }
 
-// Level stream `which` (0 def, 1 rep): index pass, then the grid-wide expand pass.
+hipError_t pqg_launch_tile_desc(const uint8_t* blob, PageWork* pages, uint32_t ntiles,
+                                const uint32_t* tile_page, RunTables rt, ColumnParams cp, int sel,
+                                int dict_page, hipStream_t s) {
+  if (ntiles)
+    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+                       ntiles, rt, cp, sel, dict_page);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_page_counts(PageWork* pages, int npages, RunTables rt, int field, hipStream_t s) {
+  hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, field);
+  return hipGetLastError();
+}
+
+// Level stream `which` (0 def, 1 rep): index pass, tile descriptors, wave expand pass, and for
+// def levels the per-page non-null counts.
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                              int npages, uint32_t ntiles, ColumnParams cp, int which,
                              const uint32_t* tile_page, RunTables rt, int16_t* out,
@@ -480,9 +495,12 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   const int sel = which ? SS_REP : SS_DEF;
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
                      -1, rt, res);
-  if (ntiles)
-    hipLaunchKernelGGL(k_expand_levels, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages,
-                       tile_page, ntiles, rt, cp, sel, out);
+  if (ntiles) {
+    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+                       ntiles, rt, cp, sel, -1);
+    hipLaunchKernelGGL(k_wexpand_levels, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, rt, cp, sel, out);
+    if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
+  }
   return hipGetLastError();
 }
 
@@ -500,11 +518,14 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
+  hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+                     ntiles, rt, cp, (int)SS_DICT, dict_page);
+  const dim3 g(ntiles * 4);
   switch (es) {
-    case 1: hipLaunchKernelGGL(k_expand_dict<1>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL(k_expand_dict<4>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL(k_expand_dict<8>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL(k_expand_dict<12>, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, rt, cp, dict_page, out, res); break;
+    case 1: hipLaunchKernelGGL(k_wexpand_dict<1>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL(k_wexpand_dict<4>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 8: hipLaunchKernelGGL(k_wexpand_dict<8>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 12: hipLaunchKernelGGL(k_wexpand_dict<12>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -536,9 +557,11 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
                                ChunkResult* res, hipStream_t s) {
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
                      -1, rt, res);
-  if (ntiles)
-    hipLaunchKernelGGL(k_expand_bool, dim3((ntiles + EX_TPW - 1) / EX_TPW), dim3(WG), 0, s, blob, blob_len, pages,
-                       tile_page, ntiles, rt, cp, out);
+  if (ntiles) {
+    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+                       ntiles, rt, cp, (int)SS_BOOL, -1);
+    hipLaunchKernelGGL(k_wexpand_bool, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, rt, out);
+  }
   return hipGetLastError();
 }
 

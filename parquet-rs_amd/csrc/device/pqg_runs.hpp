@@ -688,3 +688,384 @@ __device__ inline bool expand_setup(const uint8_t* blob, PageWork* pages, const 
 }
 
 }  // namespace pqg
+
+// ============================================================================ wave expand
+//
+// One independent wave per quarter tile (1024 outputs): no workgroup barriers, small LDS,
+// so many waves per CU hide the two memory round trips each quarter costs (its tile
+// descriptor, then its run records and payload bytes together).
+namespace pqg {
+
+constexpr uint32_t WX_OUT = RUN_TILE / 4;  // outputs per wave
+constexpr int WX_STAGE = 4096;             // staged payload bytes per batch
+constexpr int WX_RCAP = 256;               // runs per batch
+
+struct WaveSmem {
+  uint32_t stage[(WX_STAGE + 64) / 4];
+  uint32_t start[WX_RCAP + 2];
+  uint32_t info[WX_RCAP + 1];
+  uint32_t fix[WX_OUT / 8];
+  uint32_t ctl[4];
+};
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+__device__ inline uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+  return v;
+}
+
+// Expand the runs in sm.start/info[0, nr) (sm.start[nr] = end) over outputs
+// [seg_lo, seg_hi) of the quarter [qlo, qlo + WX_OUT), payload staged from stream offset
+// sbase (sb32 = low 32 bits) for `staged` bytes.
+template <class Emit>
+__device__ inline void wave_expand_batch(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                         uint64_t S, uint64_t out, uint32_t w, uint32_t qlo,
+                                         uint32_t seg_lo, uint32_t seg_hi, uint32_t nr,
+                                         uint64_t A0, uint32_t staged, WaveSmem& sm, Emit& emit) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t sb32 = (uint32_t)(A0 - S);
+  const uint32_t wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
+  const uint64_t wm64 = w >= 64 ? ~0ull : ((1ull << w) - 1ull);
+  if (lane == 0) sm.ctl[1] = 0;
+  wave_sync();
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    const uint32_t g = qlo + (uint32_t)half * (WX_OUT / 2) + lane * 8u;
+    if (g + 8 <= seg_lo || g >= seg_hi) continue;
+    const uint32_t o0 = g < seg_lo ? seg_lo : g;
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t step = WX_RCAP / 2; step; step >>= 1)
+      if (a + step < nr && sm.start[a + step] <= o0) a += step;
+    const uint32_t stA = sm.start[a], infA = sm.info[a];
+    const uint32_t stB = sm.start[a + 1];
+    const uint32_t infB = sm.info[a + 1 < nr ? a + 1 : a];
+    const uint32_t stC = sm.start[a + 2 <= nr ? a + 2 : nr];
+    const uint32_t end = g + 8 < seg_hi ? g + 8 : seg_hi;
+    bool fixup = end > stC;  // three or more runs
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t oj = g + (uint32_t)j;
+      const bool inB = oj >= stB;
+      const uint32_t inf = inB ? infB : infA;
+      const uint32_t d = oj - (inB ? stB : stA);
+      const uint32_t rel = inf - sb32;
+      const uint32_t bit = rel * 8u + d * w;
+      const bool rle = (inf & R_RLE) != 0;
+      const bool ok = rle || (d < (1u << 20) && rel < staged && (bit >> 3) + 12u <= staged);
+      const uint32_t byte = ok && !rle ? bit >> 3 : 0u;
+      uint32_t val;
+      if (w <= 24) val = (lload_u32(sm.stage, byte) >> (bit & 7)) & wm;
+      else val = (uint32_t)(lload_u64(sm.stage, byte) >> (bit & 7)) & wm;
+      val = rle ? (inf & 0x7FFFFFFFu) : val;
+      const bool in = oj >= seg_lo && oj < seg_hi;
+      fixup |= in && !ok;
+      v[j] = in ? val : 0u;
+    }
+    if (fixup) {
+      const uint32_t slot = atomicAdd(&sm.ctl[1], 1u);
+      sm.fix[slot] = g;
+      continue;
+    }
+    uint32_t mask = 0xFFu;
+    if (g < seg_lo || g + 8 > seg_hi) {
+      mask = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (g + j >= seg_lo && g + j < seg_hi) mask |= 1u << j;
+    }
+    emit(out + g, v, mask);
+  }
+  wave_sync();
+  const uint32_t nfix = sm.ctl[1];
+  for (uint32_t f = lane; f < nfix; f += 64) {  // general path, one lane per chunk
+    const uint32_t g = sm.fix[f];
+    const uint32_t o0 = g < seg_lo ? seg_lo : g;
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t step = WX_RCAP / 2; step; step >>= 1)
+      if (r + step < nr && sm.start[r + step] <= o0) r += step;
+    uint32_t st = sm.start[r], nst = sm.start[r + 1], inf = sm.info[r];
+    uint32_t v[8];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t oj = g + (uint32_t)j;
+      v[j] = 0;
+      if (oj < seg_lo || oj >= seg_hi) continue;
+      while (oj >= nst && r + 1 < nr) {
+        ++r;
+        st = nst;
+        nst = sm.start[r + 1];
+        inf = sm.info[r];
+      }
+      uint32_t val = inf & 0x7FFFFFFFu;
+      if (!(inf & R_RLE)) {
+        const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(oj - st) * (uint64_t)w;
+        const uint64_t abs = S + (bit >> 3);
+        const uint64_t ri = abs - A0;
+        const uint64_t x = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
+                                                            : gload_u64(blob, blob_len, abs);
+        val = (uint32_t)((x >> (bit & 7)) & wm64);
+      }
+      v[j] = val;
+      mask |= 1u << j;
+    }
+    emit(out + g, v, mask);
+  }
+  wave_sync();
+}
+
+// Stage the payload bytes the runs sm.start/info[0, nr) need for outputs [seg_lo, seg_hi).
+__device__ inline uint32_t wave_stage(const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t S,
+                                      uint32_t slen, uint32_t w, uint32_t seg_lo, uint32_t seg_hi,
+                                      uint32_t nr, WaveSmem& sm, uint64_t& A0) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (uint32_t r = lane; r < nr; r += 64) {
+    const uint32_t inf = sm.info[r];
+    if (inf & R_RLE) continue;
+    const uint32_t st = sm.start[r], en = sm.start[r + 1];
+    const uint32_t a = seg_lo > st ? seg_lo : st;
+    const uint32_t b = seg_hi < en ? seg_hi : en;
+    if (a >= b) continue;
+    const uint64_t b0 = (uint64_t)inf + (((uint64_t)(a - st) * w) >> 3);
+    const uint64_t b1 = (uint64_t)inf + (((uint64_t)(b - st) * w + 7) >> 3) + 8;
+    lo = min(lo, (uint32_t)min(b0, (uint64_t)0xFFFFFFFFu));
+    hi = max(hi, (uint32_t)min(b1, (uint64_t)0xFFFFFFFFu));
+  }
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
+  if (lo >= hi) {  // RLE only: nothing to stage
+    A0 = S;
+    return 0;
+  }
+  A0 = (S + lo) & ~15ull;
+  uint64_t A1 = S + (uint64_t)hi;
+  if (A1 > S + slen + 16) A1 = S + slen + 16;
+  if (A1 > A0 + WX_STAGE) A1 = A0 + WX_STAGE;
+  const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+  constexpr int PER = WX_STAGE / 16 / 64;
+  uint4 v[PER];
+  const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t c = lane + 64u * (uint32_t)k;
+    if (c < nchunks) {
+      const uint64_t a = A0 + (uint64_t)c * 16;
+      v[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t c = lane + 64u * (uint32_t)k;
+    if (c < nchunks) reinterpret_cast<uint4*>(sm.stage)[c] = v[k];
+  }
+  if (lane < 16) sm.stage[nchunks * 4 + lane] = 0;
+  wave_sync();
+  return nchunks * 16;
+}
+
+// Descriptor of quarter q of tile t for stream `sel` (k_quarter_desc: one thread per quarter).
+__device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
+                                     const uint32_t* tile_page, const RunTables& rt,
+                                     const ColumnParams& cp, int sel, int dict_page, uint32_t t,
+                                     uint32_t q) {
+  QDesc d{};
+  const uint32_t p = tile_page[t];
+  const PageWork& pw = pages[p];
+  d.page = p;
+  if (pw.status != 0) return d;
+  if (sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0)) return d;
+  Stream s;
+  if (!get_stream(blob, pw, sel, cp, s) || s.err) return d;
+  const uint32_t k = t - pw.ltile0;
+  const uint32_t lo = k * RUN_TILE + q * WX_OUT;
+  if (lo >= s.n) return d;
+  const uint32_t hi = lo + WX_OUT < s.n ? lo + WX_OUT : s.n;
+  d.S = s.S;
+  d.out = s.out;
+  d.slen = s.slen;
+  d.qlo = lo;
+  d.qhi = hi;
+  d.w = (uint32_t)s.w;
+  d.kind = (uint32_t)s.kind;
+  const uint32_t w = d.w;
+  if (s.kind == LK_BIT_PACKED) {  // one header-less run from output 0
+    d.rec = 0;
+    d.nrec = 1;
+    d.blo = (uint32_t)(((uint64_t)lo * w) >> 3);
+    d.bhi = (uint32_t)min((((uint64_t)hi * w + 7) >> 3) + 8, (uint64_t)s.slen + 8);
+    return d;
+  }
+  const RunCkpt c = rt.ck[t];
+  d.ckpos = c.pos;
+  d.ckfirst = c.first;
+  const uint32_t nrec = rt.nruns[t];
+  if (nrec > RUN_CAPT) {
+    d.rec = RUN_REWALK;
+    return d;
+  }
+  const uint2* recs = rt.runs + (uint64_t)t * RUN_CAPT;
+  // a0: last record starting at or before lo; a1: last record starting before hi
+  uint32_t a0 = 0, a1 = 0;
+  for (uint32_t step = RUN_CAPT / 2; step; step >>= 1) {
+    if (a0 + step < nrec && recs[a0 + step].x <= lo) a0 += step;
+    if (a1 + step < nrec && recs[a1 + step].x < hi) a1 += step;
+  }
+  d.rec = t * RUN_CAPT + a0;
+  d.nrec = a1 - a0 + 1;
+  // payload bytes of the bit-packed runs among them (stream offsets increase with the index)
+  uint32_t blo = 0xFFFFFFFFu, bhi = 0;
+  for (uint32_t r = a0; r <= a1; ++r) {
+    const uint2 x = recs[r];
+    if (x.y & R_RLE) continue;
+    const uint32_t st = x.x, en = r + 1 < nrec ? recs[r + 1].x : hi;
+    const uint32_t u = lo > st ? lo : st, v = hi < en ? hi : en;
+    blo = (uint32_t)min((uint64_t)blo, (uint64_t)x.y + (((uint64_t)(u - st) * w) >> 3));
+    break;
+  }
+  for (uint32_t r = a1 + 1; r-- > a0;) {
+    const uint2 x = recs[r];
+    if (x.y & R_RLE) continue;
+    const uint32_t st = x.x, en = r + 1 < nrec ? recs[r + 1].x : hi;
+    const uint32_t v = hi < en ? hi : en;
+    bhi = (uint32_t)min((uint64_t)x.y + ((((uint64_t)(v - st)) * w + 7) >> 3) + 8, (uint64_t)0xFFFFFFF0u);
+    break;
+  }
+  if (bhi) {
+    d.blo = blo;
+    d.bhi = bhi;
+  }
+  return d;
+}
+
+// Loads a quarter descriptor with one wave (16 lanes x 4 bytes), uniform result.
+__device__ inline QDesc load_qdesc(const QDesc* dp) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(dp);
+  const uint32_t x = lane < 16 ? w[lane] : 0u;
+  QDesc d;
+  uint32_t* o = reinterpret_cast<uint32_t*>(&d);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) o[k] = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
+  return d;
+}
+
+// Expand the quarter described by d: its run records and payload bytes are fetched together
+// (one memory round trip), then every lane expands 2 x 8 outputs.
+template <class Emit>
+__device__ inline void wave_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                   const QDesc& d, const uint2* __restrict__ runs, WaveSmem& sm,
+                                   Emit& emit) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t qlo = d.qlo, qhi = d.qhi, w = d.w;
+  uint64_t A0 = d.S;
+  if (d.rec != RUN_REWALK) {
+    for (uint32_t b = 0; b < d.nrec; b += WX_RCAP) {
+      const uint32_t nr = d.nrec - b < (uint32_t)WX_RCAP ? d.nrec - b : (uint32_t)WX_RCAP;
+      // ---- run records and payload window, all loads in flight together
+      uint2 rr[WX_RCAP / 64];
+#pragma unroll
+      for (int k = 0; k < WX_RCAP / 64; ++k) {
+        const uint32_t r = lane + 64u * (uint32_t)k;
+        rr[k] = (d.kind == LK_BIT_PACKED) ? make_uint2(0u, 0u)
+                                          : (r < nr ? runs[d.rec + b + r] : make_uint2(0u, 0u));
+      }
+      const uint32_t seg_lo = b == 0 ? qlo : sm.start[WX_RCAP];  // carried from the previous batch
+      const uint32_t seg_hi = (d.kind != LK_BIT_PACKED && b + nr < d.nrec) ? runs[d.rec + b + nr].x : qhi;
+      uint32_t staged = 0;
+      constexpr int PER = WX_STAGE / 16 / 64;
+      uint4 v[PER];
+      uint32_t nchunks = 0;
+      if (d.bhi) {
+        A0 = (d.S + d.blo) & ~15ull;
+        uint64_t A1 = d.S + (uint64_t)d.bhi;
+        if (A1 > A0 + WX_STAGE) A1 = A0 + WX_STAGE;
+        nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+        const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const uint32_t c = lane + 64u * (uint32_t)k;
+          if (c < nchunks) {
+            const uint64_t a = A0 + (uint64_t)c * 16;
+            v[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+          }
+        }
+        staged = nchunks * 16;
+      }
+#pragma unroll
+      for (int k = 0; k < WX_RCAP / 64; ++k) {
+        const uint32_t r = lane + 64u * (uint32_t)k;
+        if (r < nr) {
+          sm.start[r] = rr[k].x;
+          sm.info[r] = rr[k].y;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t c = lane + 64u * (uint32_t)k;
+        if (c < nchunks) reinterpret_cast<uint4*>(sm.stage)[c] = v[k];
+      }
+      if (lane < 16) sm.stage[nchunks * 4 + lane] = 0;
+      if (lane == 0) {
+        sm.start[nr] = seg_hi;
+        sm.start[nr + 1] = seg_hi;
+      }
+      wave_sync();
+      wave_expand_batch(blob, blob_len, d.S, d.out, w, qlo, seg_lo, seg_hi, nr, A0, staged, sm, emit);
+      if (lane == 0) sm.start[WX_RCAP] = seg_hi;
+      wave_sync();
+    }
+    return;
+  }
+  // more runs than the index kept: re-walk from the checkpoint (uniform, global reads)
+  uint32_t cur = d.ckpos, produced = d.ckfirst, seg_lo = qlo;
+  while (seg_lo < qhi) {
+    uint32_t nr = 0;
+    while (produced < qhi && nr < (uint32_t)WX_RCAP && cur < d.slen) {
+      uint32_t nxt, cnt, inf, flg;
+      run_parse_global(blob, blob_len, d.S, cur, d.slen, (int)w, nxt, cnt, inf, flg);
+      if (cnt) {
+        const uint32_t need = cnt;
+        if (produced + need > seg_lo) {
+          if (lane == 0) {
+            sm.start[nr] = produced;
+            sm.info[nr] = (flg & RF_BP) ? inf : (R_RLE | inf);
+          }
+          ++nr;
+        }
+        produced += need;
+      }
+      cur = nxt;
+    }
+    if (nr == 0) break;
+    const uint32_t seg_hi = produced < qhi ? produced : qhi;
+    if (lane == 0) {
+      sm.start[nr] = seg_hi;
+      sm.start[nr + 1] = seg_hi;
+    }
+    wave_sync();
+    const uint32_t staged = wave_stage(blob, blob_len, d.S, d.slen, w, seg_lo, seg_hi, nr, sm, A0);
+    wave_expand_batch(blob, blob_len, d.S, d.out, w, qlo, seg_lo, seg_hi, nr, A0, staged, sm, emit);
+    seg_lo = seg_hi;
+  }
+}
+
+}  // namespace pqg

@@ -43,10 +43,13 @@ hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint
                                   DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
                                    uint32_t*, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
-                            const uint32_t*, RunTables, int, int, bool, bool, uint64_t*,
-                            uint32_t*, uint32_t*, uint64_t*, uint32_t*, uint64_t, int64_t*,
-                            uint8_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, bool, uint64_t*, uint32_t*,
+                            uint32_t*, uint64_t, int64_t*, uint8_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_badict_expand(const uint8_t*, uint64_t, PageWork*, uint32_t, RunTables, int,
+                                    uint64_t*, uint32_t*, uint64_t*, uint32_t*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_tile_desc(const uint8_t*, PageWork*, uint32_t, const uint32_t*, RunTables,
+                                ColumnParams, int, int, hipStream_t);
+hipError_t pqg_launch_page_counts(PageWork*, int, RunTables, int, hipStream_t);
 }
 
 // Two staging slots so consecutive async decodes never overwrite pinned memory that an
@@ -90,6 +93,9 @@ struct pqg_ctx {
   bool pending = false;
   double acc_ms[5] = {};
   uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
+  uint64_t* dbgbuf = nullptr;  // diagnostics (PQG_DEBUG bit 4)
+  size_t dbg_cap = 0;
+  uint32_t dbg_n = 0;
   uint64_t acc_n = 0;
   int host_status = 0;
   int host_bad_page = -1;
@@ -185,6 +191,8 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
       hipFree(t.ck);
       hipFree(t.runs);
       hipFree(t.nruns);
+      hipFree(t.desc);
+      hipFree(t.qcount);
     }
     hipFree(sl.dt.page);
     hipFree(sl.dt.blocks);
@@ -379,6 +387,18 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   cp.want_rep = want_rep;
   static const int dbg_env = getenv("PQG_DEBUG") ? atoi(getenv("PQG_DEBUG")) : 0;
   cp.debug = dbg_env;
+  cp.dbgbuf = nullptr;
+  if (dbg_env & 16) {
+    const size_t need = (size_t)total_tiles * 4 * 16;
+    if (need > ctx->dbg_cap) {
+      hipFree(ctx->dbgbuf);
+      ctx->dbgbuf = nullptr;
+      HIPCHK(hipMalloc(&ctx->dbgbuf, need), "hipMalloc dbg");
+      ctx->dbg_cap = need;
+    }
+    ctx->dbg_n = total_tiles * 4;
+    cp.dbgbuf = ctx->dbgbuf;
+  }
 
   ChunkResult r0{};
   r0.total_levels = ctx->total_levels;
@@ -425,6 +445,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       hipFree(r.ck);
       hipFree(r.runs);
       hipFree(r.nruns);
+      hipFree(r.desc);
+      hipFree(r.qcount);
       r = RunTables{};
     }
     sl.tcap = 0;
@@ -439,6 +461,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     hipError_t e = hipMalloc(&r.ck, (sl.tcap + 1) * sizeof(RunCkpt));
     if (e == hipSuccess) e = hipMalloc(&r.runs, sl.tcap * RUN_CAPT * sizeof(uint2));
     if (e == hipSuccess) e = hipMalloc(&r.nruns, sl.tcap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&r.desc, sl.tcap * 4 * sizeof(QDesc));
+    if (e == hipSuccess) e = hipMalloc(&r.qcount, sl.tcap * 4 * sizeof(uint32_t));
     return e;
   };
   const bool hybrid_values = enc_present[PQG_RLE_DICTIONARY] || (enc_present[PQG_RLE] && t == PQG_BOOLEAN);
@@ -471,12 +495,15 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
                                      ctx->d_res, s), "byte-array dictionary");
       HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
                                   sl.rt[2], ctx->d_res, s), "dictionary index pass");
+      HIPCHK(pqg_launch_tile_desc(blob, ctx->d_pages, nt, sl.tile_page, sl.rt[2], cp, 2, dict_page, s),
+             "dictionary tiles");
+      HIPCHK(pqg_launch_badict_expand(blob, blob_len, ctx->d_pages, nt, sl.rt[2], dict_page, sl.vsrc,
+                                      sl.vlen, sl.dsrc, sl.dlen, ctx->d_res, s), "dictionary expand");
+      HIPCHK(pqg_launch_page_counts(ctx->d_pages, np, sl.rt[2], 1, s), "dictionary byte counts");
     }
-    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2], dict_page,
-                            tl,
-                            enc_present[PQG_RLE_DICTIONARY], enc_present[PQG_DELTA_BYTE_ARRAY],
-                            sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, out->values_capacity,
-                            out->offsets, vo, ctx->d_res, s),
+    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, tl, enc_present[PQG_DELTA_BYTE_ARRAY],
+                            sl.vsrc, sl.vlen, sl.vpre, out->values_capacity, out->offsets, vo,
+                            ctx->d_res, s),
            "byte arrays");
   } else if (np && vo) {
     if (enc_present[PQG_PLAIN]) {
@@ -587,6 +614,27 @@ int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
   t->values_ms = (float)(ctx->acc_ms[3] / n);
   t->total_ms = (float)(ctx->acc_ms[4] / n);
   t->values_kernel = ctx->values_kernel;
+  return PQG_OK;
+}
+
+// Diagnostics: average per-wave phase cycles of the last decode's wave expand kernel
+// (PQG_DEBUG bit 4). out[0..2] = desc, expand, tail cycles; out[3] = waves.
+int pqg_debug_stamps(pqg_ctx* ctx, double* out4) {
+  if (!ctx || !ctx->dbgbuf || !out4) return PQG_ERR_INVALID;
+  std::vector<uint32_t> h((size_t)ctx->dbg_n * 4);
+  if (hipMemcpy(h.data(), ctx->dbgbuf, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
+  double a = 0, b = 0, c = 0;
+  uint64_t n = 0;
+  for (uint32_t i = 0; i < ctx->dbg_n; ++i) {
+    a += h[4 * i];
+    b += h[4 * i + 1];
+    c += h[4 * i + 2];
+    ++n;
+  }
+  out4[0] = a / (double)(n ? n : 1);
+  out4[1] = b / (double)(n ? n : 1);
+  out4[2] = c / (double)(n ? n : 1);
+  out4[3] = (double)n;
   return PQG_OK;
 }
 

@@ -80,7 +80,7 @@ constexpr uint32_t RUN_TILE = 4096;
 
 // Run records kept per expand tile by the index pass (more runs: the expand pass re-walks the
 // tile from its checkpoint).
-constexpr uint32_t RUN_CAPT = 256;
+constexpr uint32_t RUN_CAPT = 512;
 
 // Walk checkpoint of one expand tile: the header of the run holding the tile's first output.
 struct RunCkpt {
@@ -88,11 +88,31 @@ struct RunCkpt {
   uint32_t first;  // page-relative index of the run's first output
 };
 
+// Everything the expand pass needs about one quarter tile (RUN_TILE / 4 outputs), gathered by
+// k_quarter_desc (64 bytes).
+struct QDesc {
+  uint64_t S;        // absolute blob offset of the stream
+  uint64_t out;      // global index of the stream's output 0 (page output base)
+  uint32_t qlo, qhi; // page-relative outputs [qlo, qhi); qhi == 0: nothing to do
+  uint32_t rec;      // first run record (index into RunTables::runs), RUN_REWALK: re-walk
+  uint32_t nrec;     // run records overlapping the quarter
+  uint32_t blo, bhi; // stream bytes holding the quarter's bit-packed payload (bhi == 0: none)
+  uint32_t slen;     // stream bytes
+  uint32_t w;        // bit width
+  uint32_t kind;     // LK_RLE / LK_BIT_PACKED
+  uint32_t page;
+  uint32_t ckpos;    // re-walk: checkpoint header and its run's first output
+  uint32_t ckfirst;
+};
+constexpr uint32_t RUN_REWALK = 0xFFFFFFFFu;
+
 // Index-pass outputs of one stream kind, indexed by expand tile.
 struct RunTables {
   RunCkpt* ck;      // [tiles + 1]
   uint2* runs;      // [tiles * RUN_CAPT]
   uint32_t* nruns;  // [tiles]
+  QDesc* desc;      // [tiles * 4]
+  uint32_t* qcount; // [tiles * 4] per quarter-tile counts (def levels == max_def; byte totals)
 };
 
 // DELTA_BINARY_PACKED index-pass outputs (device/pqg_delta.hip). Tiles of DELTA_TILE values
@@ -133,6 +153,8 @@ struct ColumnParams {
   int32_t want_def;  // def_levels output provided (read_batch(Some(def)))
   int32_t want_rep;
   int32_t debug;     // diagnostics switches (PQG_DEBUG), 0 in production
+  uint32_t pad;
+  uint64_t* dbgbuf;  // diagnostics: per-wave s_memtime phases (PQG_DEBUG bit 4)
 };
 
 }  // namespace pqg
