@@ -13,7 +13,7 @@
 //
 // All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
 // (index pass + grid-wide expand pass) is in pqg_runs.hpp.
-#include "pqg_runs.hpp"
+#include "pqg_texpand.hpp"
 
 namespace pqg {
 
@@ -194,6 +194,62 @@ __global__ void __launch_bounds__(WG) k_quarter_desc(const uint8_t* __restrict__
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= ntiles * 4) return;
   rt.desc[i] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, i >> 2, i & 3);
+}
+
+// Tile descriptors of stream `sel` (one thread per tile), read by the tile expand kernels.
+__global__ void __launch_bounds__(WG) k_tile_desc(const uint8_t* __restrict__ blob, const PageWork* pages,
+                                                  const uint32_t* __restrict__ tile_page,
+                                                  uint32_t ntiles, RunTables rt, ColumnParams cp,
+                                                  int sel, int dict_page) {
+  const uint32_t t = blockIdx.x * WG + threadIdx.x;
+  if (t >= ntiles) return;
+  rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, t, 0, RUN_TILE);
+}
+
+// Tile expand of a level stream (which: SS_DEF / SS_REP), pqg_texpand.hpp. Def levels also
+// count the values read_batch will ask for; the tile's count goes to qcount[4t] (the other
+// three quarter slots are zeroed for k_page_counts).
+__global__ void __launch_bounds__(WG) k_texpand_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                       RunTables rt, ColumnParams cp, int which,
+                                                       int16_t* __restrict__ out) {
+  __shared__ TileSmem sm;
+  __shared__ uint32_t red[WG / 64];
+  const QDesc d = rt.desc[blockIdx.x];
+  TxLevels em{out + d.out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0u};
+  if (d.qhi) tile_expand(blob, blob_len, d, rt.runs, sm, em);
+  if (which == SS_DEF) {
+    const uint32_t nn = wave_sum_u32(em.nonnull);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nn;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      reinterpret_cast<uint4*>(rt.qcount)[blockIdx.x] = make_uint4(red[0] + red[1] + red[2] + red[3], 0u, 0u, 0u);
+  }
+}
+
+// Tile expand of RLE_DICTIONARY indices with the dictionary gather.
+template <int ES>
+__global__ void __launch_bounds__(WG) k_texpand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, RunTables rt, int dict_page,
+                                                     uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ TileSmem sm;
+  const QDesc d = rt.desc[blockIdx.x];
+  if (!d.qhi) return;
+  const PageWork& dp = pages[dict_page];
+  TxDict<ES> em{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
+                out + d.out * (uint64_t)ES, 0};
+  tile_expand(blob, blob_len, d, rt.runs, sm, em);
+  const uint64_t bad = __ballot(em.err != 0);
+  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
+}
+
+// Tile expand of RLE booleans (data page v2 values).
+__global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     RunTables rt, uint8_t* __restrict__ out) {
+  __shared__ TileSmem sm;
+  const QDesc d = rt.desc[blockIdx.x];
+  if (!d.qhi) return;
+  TxBool em{out + d.out};
+  tile_expand(blob, blob_len, d, rt.runs, sm, em);
 }
 
 // Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
@@ -496,9 +552,9 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
                      -1, rt, res);
   if (ntiles) {
-    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+    hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    hipLaunchKernelGGL(k_wexpand_levels, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, rt, cp, sel, out);
+    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, rt, cp, sel, out);
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();
@@ -518,14 +574,14 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
-  hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+  hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
-  const dim3 g(ntiles * 4);
+  const dim3 g(ntiles);
   switch (es) {
-    case 1: hipLaunchKernelGGL(k_wexpand_dict<1>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL(k_wexpand_dict<4>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL(k_wexpand_dict<8>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL(k_wexpand_dict<12>, g, dim3(64), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 1: hipLaunchKernelGGL(k_texpand_dict<1>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL(k_texpand_dict<4>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 8: hipLaunchKernelGGL(k_texpand_dict<8>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 12: hipLaunchKernelGGL(k_texpand_dict<12>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -558,9 +614,9 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
                      -1, rt, res);
   if (ntiles) {
-    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
+    hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);
-    hipLaunchKernelGGL(k_wexpand_bool, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, rt, out);
+    hipLaunchKernelGGL(k_texpand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, rt, out);
   }
   return hipGetLastError();
 }

@@ -882,11 +882,12 @@ __device__ inline uint32_t wave_stage(const uint8_t* __restrict__ blob, uint64_t
   return nchunks * 16;
 }
 
-// Descriptor of quarter q of tile t for stream `sel` (k_quarter_desc: one thread per quarter).
+// Descriptor of outputs [q * span, (q + 1) * span) of tile t for stream `sel` (k_quarter_desc:
+// one thread per quarter; k_tile_desc: one thread per tile with span = RUN_TILE).
 __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
                                      const uint32_t* tile_page, const RunTables& rt,
                                      const ColumnParams& cp, int sel, int dict_page, uint32_t t,
-                                     uint32_t q) {
+                                     uint32_t q, uint32_t span = WX_OUT) {
   QDesc d{};
   const uint32_t p = tile_page[t];
   const PageWork& pw = pages[p];
@@ -896,9 +897,9 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   Stream s;
   if (!get_stream(blob, pw, sel, cp, s) || s.err) return d;
   const uint32_t k = t - pw.ltile0;
-  const uint32_t lo = k * RUN_TILE + q * WX_OUT;
+  const uint32_t lo = k * RUN_TILE + q * span;
   if (lo >= s.n) return d;
-  const uint32_t hi = lo + WX_OUT < s.n ? lo + WX_OUT : s.n;
+  const uint32_t hi = lo + span < s.n ? lo + span : s.n;
   d.S = s.S;
   d.out = s.out;
   d.slen = s.slen;
