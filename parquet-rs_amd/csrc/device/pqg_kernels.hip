@@ -206,50 +206,93 @@ __global__ void __launch_bounds__(WG) k_tile_desc(const uint8_t* __restrict__ bl
   rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, t, 0, RUN_TILE);
 }
 
-// Tile expand of a level stream (which: SS_DEF / SS_REP), pqg_texpand.hpp. Def levels also
-// count the values read_batch will ask for; the tile's count goes to qcount[4t] (the other
-// three quarter slots are zeroed for k_page_counts).
-__global__ void __launch_bounds__(WG) k_texpand_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                       RunTables rt, ColumnParams cp, int which,
-                                                       int16_t* __restrict__ out) {
-  __shared__ TileSmem sm;
-  __shared__ uint32_t red[WG / 64];
-  const QDesc d = rt.desc[blockIdx.x];
-  TxLevels em{out + d.out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0u};
-  if (d.qhi) tile_expand(blob, blob_len, d, rt.runs, sm, em);
-  if (which == SS_DEF) {
+// Tile expand of a level stream (which: SS_DEF / SS_REP), pqg_texpand.hpp, persistent grid.
+// Def levels also count the values read_batch will ask for: each wave writes its count of the
+// tile to qcount[4t + wave] (k_page_counts sums them per page).
+struct LevelsMaker {
+  int16_t* out;
+  int16_t maxl;
+  bool count;
+  uint32_t* qcount;
+  __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
+  __device__ void done(const QDesc&, uint32_t t, TxLevels& em) {
+    if (!count) return;
     const uint32_t nn = wave_sum_u32(em.nonnull);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nn;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      reinterpret_cast<uint4*>(rt.qcount)[blockIdx.x] = make_uint4(red[0] + red[1] + red[2] + red[3], 0u, 0u, 0u);
+    if ((threadIdx.x & 63) == 0) qcount[4 * t + (threadIdx.x >> 6)] = nn;
   }
-}
+};
 
-// Tile expand of RLE_DICTIONARY indices with the dictionary gather.
-template <int ES>
-__global__ void __launch_bounds__(WG) k_texpand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, RunTables rt, int dict_page,
-                                                     uint8_t* __restrict__ out, ChunkResult* res) {
-  __shared__ TileSmem sm;
-  const QDesc d = rt.desc[blockIdx.x];
-  if (!d.qhi) return;
-  const PageWork& dp = pages[dict_page];
-  TxDict<ES> em{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
-                out + d.out * (uint64_t)ES, 0};
-  tile_expand(blob, blob_len, d, rt.runs, sm, em);
-  const uint64_t bad = __ballot(em.err != 0);
-  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
-}
+#define PQG_TEXPAND_LEVELS(NAME, ATTR)                                                              \
+  __global__ void ATTR __launch_bounds__(WG) NAME(const uint8_t* __restrict__ blob, uint64_t blob_len, \
+                                                  uint32_t ntiles, RunTables rt, ColumnParams cp,     \
+                                                  int which, int16_t* __restrict__ out) {             \
+    __shared__ TileSmem sm;                                                                       \
+    LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount};  \
+    tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                  \
+  }
+PQG_TEXPAND_LEVELS(k_texpand_levels, )
+PQG_TEXPAND_LEVELS(k_texpand_levels_e6, __attribute__((amdgpu_waves_per_eu(6, 8))))
+PQG_TEXPAND_LEVELS(k_texpand_levels_e8, __attribute__((amdgpu_waves_per_eu(8, 8))))
+
+// Tile expand of RLE_DICTIONARY indices with the dictionary gather. MODE 1 (diagnostics,
+// PQG_DEBUG bits 8-11 = 1) writes the index instead of gathering.
+template <int ES, int MODE>
+struct DictMaker {
+  const uint8_t* dict;
+  uint32_t ndict;
+  bool aligned;
+  uint8_t* out;
+  PageWork* pages;
+  ChunkResult* res;
+  __device__ TxDict<ES, MODE> make(const QDesc& d) {
+    return TxDict<ES, MODE>{dict, ndict, aligned, out + d.out * (uint64_t)ES, 0};
+  }
+  __device__ void done(const QDesc& d, uint32_t, TxDict<ES, MODE>& em) {
+    const uint64_t bad = __ballot(em.err != 0);
+    if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
+  }
+};
+
+#define PQG_TEXPAND_DICT(NAME, ATTR)                                                                  \
+  template <int ES, int MODE = 0>                                                                     \
+  __global__ void ATTR __launch_bounds__(WG) NAME(const uint8_t* __restrict__ blob, uint64_t blob_len, \
+                                                  uint32_t ntiles, PageWork* pages, RunTables rt,     \
+                                                  int dict_page, uint8_t* __restrict__ out,           \
+                                                  ChunkResult* res) {                                 \
+    __shared__ TileSmem sm;                                                                         \
+    if (dict_page < 0) return;                                                                      \
+    const PageWork& dp = pages[dict_page];                                                          \
+    DictMaker<ES, MODE> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
+                           out, pages, res};                                                        \
+    tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                    \
+  }
+PQG_TEXPAND_DICT(k_texpand_dict, )
+PQG_TEXPAND_DICT(k_texpand_dict_e5, __attribute__((amdgpu_waves_per_eu(5, 8))))
+PQG_TEXPAND_DICT(k_texpand_dict_e6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
 // Tile expand of RLE booleans (data page v2 values).
+struct BoolMaker {
+  uint8_t* out;
+  __device__ TxBool make(const QDesc& d) { return TxBool{out + d.out}; }
+  __device__ void done(const QDesc&, uint32_t, TxBool&) {}
+};
+
 __global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     RunTables rt, uint8_t* __restrict__ out) {
+                                                     uint32_t ntiles, RunTables rt, uint8_t* __restrict__ out) {
   __shared__ TileSmem sm;
-  const QDesc d = rt.desc[blockIdx.x];
-  if (!d.qhi) return;
-  TxBool em{out + d.out};
-  tile_expand(blob, blob_len, d, rt.runs, sm, em);
+  BoolMaker mk{out};
+  tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);
+}
+
+// Persistent grid of a tile expand kernel: as many workgroups as fit on the chip at once.
+template <class K>
+static inline uint32_t tx_grid(K kernel, uint32_t ntiles) {
+  int cus = 0, dev = 0, per = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WG, 0) != hipSuccess || per <= 0) per = 2;
+  const uint32_t g = (uint32_t)cus * (uint32_t)per;
+  return ntiles < g ? ntiles : g;
 }
 
 // Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
@@ -554,7 +597,11 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, rt, cp, sel, out);
+    switch ((cp.debug >> 8) & 15) {  // diagnostics variants (PQG_DEBUG bits 8-11)
+      case 2: hipLaunchKernelGGL(k_texpand_levels_e6, dim3(tx_grid(k_texpand_levels_e6, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
+      case 3: hipLaunchKernelGGL(k_texpand_levels_e8, dim3(tx_grid(k_texpand_levels_e8, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
+      default: hipLaunchKernelGGL(k_texpand_levels, dim3(tx_grid(k_texpand_levels, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
+    }
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();
@@ -576,12 +623,21 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   if (!ntiles) return hipGetLastError();
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
-  const dim3 g(ntiles);
+  const dim3 g(tx_grid(k_texpand_dict<8>, ntiles));
   switch (es) {
-    case 1: hipLaunchKernelGGL(k_texpand_dict<1>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL(k_texpand_dict<4>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL(k_texpand_dict<8>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL(k_texpand_dict<12>, g, dim3(WG), 0, s, blob, blob_len, pages, rt, dict_page, out, res); break;
+    case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
+    case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
+    case 8:
+      if (((cp.debug >> 8) & 15) == 1)  // diagnostics: no gather
+        hipLaunchKernelGGL((k_texpand_dict<8, 1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
+      else if (((cp.debug >> 8) & 15) == 2)
+        hipLaunchKernelGGL((k_texpand_dict_e5<8>), dim3(tx_grid(k_texpand_dict_e5<8>, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
+      else if (((cp.debug >> 8) & 15) == 3)
+        hipLaunchKernelGGL((k_texpand_dict_e6<8>), dim3(tx_grid(k_texpand_dict_e6<8>, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
+      else
+        hipLaunchKernelGGL((k_texpand_dict<8>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
+      break;
+    case 12: hipLaunchKernelGGL((k_texpand_dict<12>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -616,7 +672,7 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);
-    hipLaunchKernelGGL(k_texpand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, rt, out);
+    hipLaunchKernelGGL(k_texpand_bool, dim3(tx_grid(k_texpand_bool, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
   }
   return hipGetLastError();
 }

@@ -33,56 +33,63 @@ struct TileSmem {
   uint32_t ctl[4];
 };
 
-// Values of outputs [g, g + V) (page-relative) clipped to [seg_lo, seg_hi), from the runs
-// sm.start/info[0, nr) (sm.start[nr] = segment end). The bit-packed payload is read from the
-// LDS window of `staged` bytes at stream offset sb32, or from global memory outside it.
-// Returns the mask of outputs inside the segment.
-template <int V>
-__device__ inline uint32_t tx_values(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t g,
-                                     uint32_t seg_lo, uint32_t seg_hi, uint32_t w, uint32_t wm,
-                                     uint32_t sb32, uint32_t staged, bool wide,
-                                     const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                     uint64_t S, uint32_t (&v)[V]) {
-  if (g >= seg_hi || g + V <= seg_lo) {
-#pragma unroll
-    for (int j = 0; j < V; ++j) v[j] = 0;
-    return 0;
-  }
-  const uint32_t o0 = g < seg_lo ? seg_lo : g;
+// Run holding page-relative output o: binary search over sm.start[0, nr).
+__device__ inline uint32_t tx_find(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t o) {
   uint32_t a = 0;
   for (uint32_t step = lgn; step; step >>= 1)
-    if (a + step < nr && sm.start[a + step] <= o0) a += step;
-  uint32_t stA = sm.start[a], infA = sm.info[a], stB = sm.start[a + 1];
-  const uint32_t lim = staged * 8u;
-  uint32_t mask = 0;
+    if (a + step < nr && sm.start[a + step] <= o) a += step;
+  return a;
+}
+
+// Fast path for the V outputs [g, g + V): all inside the segment (caller checks), in at most
+// two runs, bit-packed payload inside the LDS window (lim = staged bits). Values go to v;
+// returns false when any of that does not hold (the slow path then produces the group).
+template <int V>
+__device__ inline bool tx_fast(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t g,
+                               uint32_t seg_hi, uint32_t w, uint32_t wm, uint32_t sb32,
+                               uint32_t lim, uint32_t (&v)[V]) {
+  const uint32_t a = tx_find(sm, nr, lgn, g);
+  const uint32_t stA = sm.start[a], infA = sm.info[a];
+  const uint32_t stB = sm.start[a + 1];
+  const uint32_t infB = sm.info[a + 1 < nr ? a + 1 : a];
+  const uint32_t stC = sm.start[a + 2 <= nr ? a + 2 : nr];
+  bool ok = g + V <= stC && g + V <= seg_hi;
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const uint32_t o = g + (uint32_t)j;
-    if (o >= stB && a + 1 < nr) {  // every run holds >= 1 output: at most one step per output
-      ++a;
-      stA = stB;
-      infA = sm.info[a];
-      stB = sm.start[a + 1];
-    }
-    uint32_t val = infA & 0x7FFFFFFFu;
-    if (!(infA & R_RLE)) {
-      const uint32_t bit = (infA - sb32) * 8u + (o - stA) * w;  // exact unless `wide`
-      if (!wide && bit + w <= lim) {
-        const uint32_t wi = bit >> 5;
-        val = __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
-      } else {
-        const uint64_t b64 = (uint64_t)infA * 8ull + (uint64_t)(o - stA) * (uint64_t)w;
-        val = (uint32_t)(gload_u64(blob, blob_len, S + (b64 >> 3)) >> (b64 & 7)) & wm;
-      }
-    }
-    const bool in = o >= seg_lo && o < seg_hi;
-    v[j] = in ? val : 0u;
-    mask |= (in ? 1u : 0u) << j;
+    const bool inB = o >= stB;
+    const uint32_t inf = inB ? infB : infA;
+    const uint32_t st = inB ? stB : stA;
+    const bool rle = (inf & R_RLE) != 0;
+    const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
+    const bool in = rle || bit + w <= lim;
+    ok = ok && in;
+    const uint32_t wi = (in && !rle) ? bit >> 5 : 0u;
+    const uint32_t x = __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
+    v[j] = rle ? (inf & 0x7FFFFFFFu) : x;
   }
-  return mask;
+  return ok;
 }
 
-// Expand outputs [seg_lo, seg_hi) of the tile starting at page-relative output lo.
+// One output, any case: LDS window or global memory (64-bit offsets).
+__device__ inline uint32_t tx_one(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t o,
+                                  uint32_t w, uint32_t wm, uint32_t sb32, uint32_t lim,
+                                  const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t S) {
+  const uint32_t a = tx_find(sm, nr, lgn, o);
+  const uint32_t st = sm.start[a], inf = sm.info[a];
+  if (inf & R_RLE) return inf & 0x7FFFFFFFu;
+  const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
+  if (bit + w <= lim) {
+    const uint32_t wi = bit >> 5;
+    return __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
+  }
+  const uint64_t b64 = (uint64_t)inf * 8ull + (uint64_t)(o - st) * (uint64_t)w;
+  return (uint32_t)(gload_u64(blob, blob_len, S + (b64 >> 3)) >> (b64 & 7)) & wm;
+}
+
+// Expand outputs [seg_lo, seg_hi) of the tile starting at page-relative output lo. Groups
+// that take the fast path are handed to the emitter E::PG at a time (put: all-or-nothing
+// masks); the others are produced one output at a time (put1) in a rolled loop.
 template <class E>
 __device__ inline void tx_range(const TileSmem& sm, uint32_t nr, uint32_t lo, uint32_t seg_lo,
                                 uint32_t seg_hi, uint32_t w, uint32_t sb32, uint32_t staged,
@@ -90,84 +97,120 @@ __device__ inline void tx_range(const TileSmem& sm, uint32_t nr, uint32_t lo, ui
                                 uint64_t S, E& em) {
   constexpr int V = E::V;
   constexpr int NG = (int)TX_PER / V;
+  constexpr int PG = E::PG < NG ? E::PG : NG;
+  constexpr uint32_t stride = WG * V;
   const uint32_t wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
   const uint32_t lgn = nr > 1 ? 1u << (31 - __builtin_clz(nr - 1)) : 0u;
+  const uint32_t lim = wide ? 0u : staged * 8u;
   const uint32_t g0 = lo + threadIdx.x * (uint32_t)V;
-  uint32_t v[NG][V];
-  uint32_t m[NG];
+  uint32_t slow = 0;  // groups left to the slow path
 #pragma unroll
-  for (int s = 0; s < NG; ++s)
-    m[s] = tx_values<V>(sm, nr, lgn, g0 + (uint32_t)s * (WG * V), seg_lo, seg_hi, w, wm, sb32,
-                        staged, wide, blob, blob_len, S, v[s]);
-  em.template put<NG>(g0, (uint32_t)(WG * V), v, m);
+  for (int c = 0; c < NG; c += PG) {
+    uint32_t v[PG][V];
+    uint32_t m[PG];
+#pragma unroll
+    for (int s = 0; s < PG; ++s) {
+      const uint32_t g = g0 + (uint32_t)(c + s) * stride;
+      const bool inside = g >= seg_lo && g < seg_hi;
+      const bool f = inside && tx_fast<V>(sm, nr, lgn, g, seg_hi, w, wm, sb32, lim, v[s]);
+      m[s] = f ? (V == 32 ? 0xFFFFFFFFu : (1u << V) - 1u) : 0u;
+      if (!f && g + V > seg_lo && g < seg_hi) slow |= 1u << (c + s);
+    }
+    em.template put<PG>(g0 + (uint32_t)c * stride, stride, v, m);
+  }
+#pragma unroll 1
+  while (slow) {
+    const int s = __builtin_ctz(slow);
+    slow &= slow - 1;
+    const uint32_t g = g0 + (uint32_t)s * stride;
+#pragma unroll 1
+    for (uint32_t j = 0; j < (uint32_t)V; ++j) {
+      const uint32_t o = g + j;
+      if (o < seg_lo || o >= seg_hi) continue;
+      em.put1(o, tx_one(sm, nr, lgn, o, w, wm, sb32, lim, blob, blob_len, S));
+    }
+  }
 }
 
-// Expand the tile described by d (k_tile_desc) through emitter em.
-template <class E>
-__device__ inline void tile_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                   const QDesc& d, const uint2* __restrict__ runs, TileSmem& sm,
-                                   E& em) {
+// Loads of one tile in flight: run records and the payload window (single-batch tiles).
+struct TileLoad {
+  uint2 r0, r1;
+  uint4 pv[TX_CHUNKS];
+  uint32_t nchunks;
+  uint64_t A0;
+};
+
+__device__ inline bool tx_wide(const QDesc& d) { return d.slen >= (1u << 28); }  // bit offsets could wrap
+
+__device__ inline void tx_issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const QDesc& d,
+                                const uint2* __restrict__ runs, TileLoad& f) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t lo = d.qlo, hi = d.qhi, w = d.w;
-  const bool wide = d.slen >= (1u << 28);  // 32-bit bit offsets could wrap
-  if (d.rec != RUN_REWALK) {
-    // ---- one batch: run records and payload window, every load in flight together
-    const bool hl = d.kind == LK_BIT_PACKED;  // one header-less run from output 0
-    const uint32_t nr = hl ? 1u : d.nrec;
-    uint2 r0 = make_uint2(0u, 0u), r1 = make_uint2(0u, 0u);
-    if (!hl) {
-      if (tid < nr) r0 = runs[d.rec + tid];
-      if (tid + WG < nr) r1 = runs[d.rec + tid + WG];
-    }
-    uint64_t A0 = d.S;
-    uint32_t nchunks = 0;
-    uint4 pv[TX_CHUNKS];
-    if (d.bhi && !wide) {
-      A0 = (d.S + d.blo) & ~15ull;
-      uint64_t A1 = d.S + (uint64_t)d.bhi;
-      if (A1 > A0 + TX_STAGE) A1 = A0 + TX_STAGE;
-      nchunks = (uint32_t)((A1 - A0 + 15) / 16);
-      const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
-#pragma unroll
-      for (int k = 0; k < TX_CHUNKS; ++k) {
-        const uint32_t c = tid + (uint32_t)(k * WG);
-        if (c < nchunks) {
-          const uint64_t a = A0 + (uint64_t)c * 16;
-          pv[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
-        }
-      }
-    }
-    if (hl) {
-      if (tid == 0) {
-        sm.start[0] = 0;
-        sm.info[0] = 0;
-      }
-    } else {
-      if (tid < nr) {
-        sm.start[tid] = r0.x;
-        sm.info[tid] = r0.y;
-      }
-      if (tid + WG < nr) {
-        sm.start[tid + WG] = r1.x;
-        sm.info[tid + WG] = r1.y;
-      }
-    }
-    if (tid == 0) {
-      sm.start[nr] = hi;
-      sm.start[nr + 1] = hi;
-    }
+  f.r0 = f.r1 = make_uint2(0u, 0u);
+  f.nchunks = 0;
+  f.A0 = d.S;
+  if (!d.qhi || d.rec == RUN_REWALK) return;
+  if (d.kind != LK_BIT_PACKED) {
+    if (tid < d.nrec) f.r0 = runs[d.rec + tid];
+    if (tid + WG < d.nrec) f.r1 = runs[d.rec + tid + WG];
+  }
+  if (d.bhi && !tx_wide(d)) {
+    const uint64_t A0 = (d.S + d.blo) & ~15ull;
+    uint64_t A1 = d.S + (uint64_t)d.bhi;
+    if (A1 > A0 + TX_STAGE) A1 = A0 + TX_STAGE;
+    const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+    const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
 #pragma unroll
     for (int k = 0; k < TX_CHUNKS; ++k) {
       const uint32_t c = tid + (uint32_t)(k * WG);
-      if (c < nchunks) reinterpret_cast<uint4*>(sm.stage)[c] = pv[k];
+      if (c < nchunks) {
+        const uint64_t a = A0 + (uint64_t)c * 16;
+        f.pv[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+      }
     }
-    if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
-    __syncthreads();
-    tx_range(sm, nr, lo, lo, hi, w, (uint32_t)(A0 - d.S), nchunks * 16, wide, blob, blob_len,
-             d.S, em);
-    return;
+    f.A0 = A0;
+    f.nchunks = nchunks;
   }
-  // ---- more runs than the index kept: wave 0 re-walks from the checkpoint in batches
+}
+
+__device__ inline uint32_t tx_nrec(const QDesc& d) { return d.kind == LK_BIT_PACKED ? 1u : d.nrec; }
+
+__device__ inline void tx_install(const QDesc& d, const TileLoad& f, TileSmem& sm) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nr = tx_nrec(d);
+  if (d.kind == LK_BIT_PACKED) {  // one header-less run from output 0
+    if (tid == 0) {
+      sm.start[0] = 0;
+      sm.info[0] = 0;
+    }
+  } else {
+    if (tid < nr) {
+      sm.start[tid] = f.r0.x;
+      sm.info[tid] = f.r0.y;
+    }
+    if (tid + WG < nr) {
+      sm.start[tid + WG] = f.r1.x;
+      sm.info[tid + WG] = f.r1.y;
+    }
+  }
+  if (tid == 0) {
+    sm.start[nr] = d.qhi;
+    sm.start[nr + 1] = d.qhi;
+  }
+#pragma unroll
+  for (int k = 0; k < TX_CHUNKS; ++k) {
+    const uint32_t c = tid + (uint32_t)(k * WG);
+    if (c < f.nchunks) reinterpret_cast<uint4*>(sm.stage)[c] = f.pv[k];
+  }
+  if (tid < 16) sm.stage[f.nchunks * 4 + tid] = 0;
+}
+
+// Tile with more runs than the index kept: wave 0 re-walks from the checkpoint in batches,
+// payload read from global memory. Barriers inside; LDS free on entry and on exit.
+template <class E>
+__device__ inline void tx_rewalk(const uint8_t* __restrict__ blob, uint64_t blob_len, const QDesc& d,
+                                 TileSmem& sm, E& em) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lo = d.qlo, hi = d.qhi, w = d.w;
   uint32_t cur = d.ckpos, produced = d.ckfirst, seg_lo = lo;
   while (seg_lo < hi) {
     if (tid < 64) {
@@ -204,6 +247,61 @@ __device__ inline void tile_expand(const uint8_t* __restrict__ blob, uint64_t bl
     __syncthreads();
     seg_lo = seg_hi;
   }
+  __syncthreads();
+}
+
+// Persistent tile loop: workgroup b expands tiles b, b + grid, b + 2 grid, ... The loads of
+// the next tile (descriptor, then its records and payload into registers) are issued before
+// the current tile is expanded, so their latency hides behind its gathers and stores.
+// M::make(d) builds the tile's emitter, M::done(d, t, em) runs after it (per-wave counts).
+template <class M>
+__device__ inline void tile_loop(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                 const QDesc* __restrict__ desc, uint32_t ntiles,
+                                 const uint2* __restrict__ runs, TileSmem& sm, M& mk) {
+  uint32_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  const uint32_t G = gridDim.x;
+  const uint32_t lane = threadIdx.x & 63;
+  // Descriptors travel as one dword per lane (lanes 0-15, one VGPR) two tiles ahead and are
+  // made uniform (v_readlane) when their tile's loads are issued, one tile ahead.
+  auto fetch = [&](uint32_t tt) -> uint32_t {
+    return (tt < ntiles && lane < 16) ? reinterpret_cast<const uint32_t*>(desc + tt)[lane] : 0u;
+  };
+  auto uniform = [&](uint32_t x) {
+    QDesc q;
+    uint32_t* o = reinterpret_cast<uint32_t*>(&q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
+    return q;
+  };
+  QDesc d = uniform(fetch(t));
+  uint32_t xn = fetch(t + G);
+  TileLoad f;
+  tx_issue(blob, blob_len, d, runs, f);
+  while (true) {
+    const bool single = d.qhi && d.rec != RUN_REWALK;
+    const uint32_t sb32 = (uint32_t)(f.A0 - d.S), staged = f.nchunks * 16u;
+    if (single) tx_install(d, f, sm);
+    __syncthreads();
+    const uint32_t tn = t + G;
+    QDesc dn;
+    if (tn < ntiles) {
+      dn = uniform(xn);
+      xn = fetch(tn + G);
+      tx_issue(blob, blob_len, dn, runs, f);
+    }
+    auto em = mk.make(d);
+    if (single)
+      tx_range(sm, tx_nrec(d), d.qlo, d.qlo, d.qhi, d.w, sb32, staged, tx_wide(d), blob, blob_len,
+               d.S, em);
+    else if (d.qhi)
+      tx_rewalk(blob, blob_len, d, sm, em);
+    mk.done(d, t, em);
+    if (tn >= ntiles) break;
+    __syncthreads();
+    d = dn;
+    t = tn;
+  }
 }
 
 // ------------------------------------------------------------------------------ emitters
@@ -215,6 +313,7 @@ __device__ inline void tile_expand(const uint8_t* __restrict__ blob, uint64_t bl
 // read_batch will ask for (def == max_def, column/reader.rs:212-226).
 struct TxLevels {
   static constexpr int V = 8;
+  static constexpr int PG = 2;
   int16_t* out;  // page output base
   int16_t maxl;
   bool count;
@@ -229,45 +328,43 @@ struct TxLevels {
           nonnull += (((m[s] >> j) & 1u) && (int16_t)v[s][j] == maxl) ? 1u : 0u;
       }
       int16_t* o = out + g0 + (uint32_t)s * stride;
-      if (m[s] == 0xFFu) {
+      if (m[s]) {
         uint4 pk;
         pk.x = (v[s][0] & 0xFFFFu) | (v[s][1] << 16);
         pk.y = (v[s][2] & 0xFFFFu) | (v[s][3] << 16);
         pk.z = (v[s][4] & 0xFFFFu) | (v[s][5] << 16);
         pk.w = (v[s][6] & 0xFFFFu) | (v[s][7] << 16);
         *reinterpret_cast<uint4*>(o) = pk;
-      } else if (m[s]) {
-#pragma unroll
-        for (int j = 0; j < V; ++j)
-          if ((m[s] >> j) & 1u) o[j] = (int16_t)v[s][j];
       }
     }
+  }
+  __device__ void put1(uint32_t o, uint32_t v) {
+    if (count) nonnull += (int16_t)v == maxl ? 1u : 0u;
+    out[o] = (int16_t)v;
   }
 };
 
 // RLE booleans (RleValueDecoder<bool>, decoding.rs:323-384), one byte per value.
 struct TxBool {
   static constexpr int V = 16;
+  static constexpr int PG = 1;
   uint8_t* out;
   template <int NG>
   __device__ void put(uint32_t g0, uint32_t stride, const uint32_t (&v)[NG][V], const uint32_t (&m)[NG]) {
 #pragma unroll
     for (int s = 0; s < NG; ++s) {
       uint8_t* o = out + g0 + (uint32_t)s * stride;
-      if (m[s] == 0xFFFFu) {
+      if (m[s]) {
         uint32_t q[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           q[k] = (v[s][4 * k] & 0xFFu) | ((v[s][4 * k + 1] & 0xFFu) << 8) |
                  ((v[s][4 * k + 2] & 0xFFu) << 16) | ((v[s][4 * k + 3] & 0xFFu) << 24);
         *reinterpret_cast<uint4*>(o) = make_uint4(q[0], q[1], q[2], q[3]);
-      } else if (m[s]) {
-#pragma unroll
-        for (int j = 0; j < V; ++j)
-          if ((m[s] >> j) & 1u) o[j] = (uint8_t)v[s][j];
       }
     }
   }
+  __device__ void put1(uint32_t o, uint32_t v) { out[o] = (uint8_t)v; }
 };
 
 // Dictionary gather (DictDecoder::get -> RleDecoder::get_batch_with_dict, decoding.rs:303-315,
@@ -278,9 +375,10 @@ struct TxDictTraits {
   static constexpr int V = ES == 8 ? 2 : ES == 4 ? 4 : ES == 12 ? 4 : 16;
 };
 
-template <int ES>
+template <int ES, int MODE = 0>
 struct TxDict {
   static constexpr int V = TxDictTraits<ES>::V;
+  static constexpr int PG = ES == 8 ? 4 : 2;
   const uint8_t* dict;  // PLAIN dictionary page payload
   uint32_t ndict;
   bool aligned;         // dict payload aligned to its value size
@@ -301,7 +399,9 @@ struct TxDict {
           const bool ok = want && idx < ndict;
           err |= (want && !ok) ? ST_PANIC : 0;
           T t = 0;
-          if (ok) {
+          if (MODE == 1) {
+            t = idx;
+          } else if (ok) {
             if (aligned) {
               t = reinterpret_cast<const T*>(dict)[idx];
             } else {
@@ -315,16 +415,12 @@ struct TxDict {
 #pragma unroll
       for (int s = 0; s < NG; ++s) {
         T* o = reinterpret_cast<T*>(out) + g0 + (uint64_t)s * stride;
-        if (m[s] == (1u << V) - 1u) {
+        if (m[s]) {
           if constexpr (ES == 8)
             *reinterpret_cast<uint4*>(o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32),
                                                       (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
           else
             *reinterpret_cast<uint4*>(o) = make_uint4(x[s][0], x[s][1], x[s][2], x[s][3]);
-        } else if (m[s]) {
-#pragma unroll
-          for (int j = 0; j < V; ++j)
-            if ((m[s] >> j) & 1u) o[j] = x[s][j];
         }
       }
     } else {  // 1-byte (BOOLEAN) and 12-byte (INT96) values: byte copies
@@ -352,6 +448,23 @@ struct TxDict {
             for (int k = 0; k < ES; ++k) o[k] = p[k];
           }
         }
+    }
+  }
+  __device__ void put1(uint32_t o, uint32_t idx) {
+    if (idx >= ndict) {
+      err = ST_PANIC;
+      return;
+    }
+    uint8_t* d = out + (uint64_t)o * ES;
+    const uint8_t* p = dict + (uint64_t)idx * ES;
+    if (MODE == 1) {
+      *reinterpret_cast<uint32_t*>(d) = idx;
+    } else if ((ES == 4 || ES == 8) && aligned) {
+      if constexpr (ES == 8) *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(p);
+      else *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(p);
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < ES; ++k) d[k] = p[k];
     }
   }
 };
