@@ -41,11 +41,15 @@ extern "C" hipError_t pqg_launch_delta(const uint8_t* blob, uint64_t blob_len, P
 //   k_delta_index  one wave per page walks the block headers (zigzag min_delta + mini-block
 //                  widths, decoding.rs:448-468) over 8 KiB regions prefetched one ahead,
 //                  checks everything the reference checks, and gives every tile of
-//                  DELTA_TILE values the records of the blocks its values need;
-//   k_delta_expand one 256-thread workgroup per tile: 16 deltas per thread, unpacked from an
-//                  LDS-staged window, a workgroup scan, and a decoupled look-back across the
-//                  page's tiles for the running value (value_i = first + sum of
-//                  min_delta + delta over d < i, wrapping, decoding.rs:560-566).
+//                  DELTA_TILE values the records of the blocks its values need (with their
+//                  mini-block widths);
+//   k_delta_sums   one 256-thread workgroup per tile: 16 deltas per thread unpacked from an
+//                  LDS-staged window, summed (min_delta + delta, wrapping);
+//   k_delta_tscan  per page, the running value at each tile start (value_i = first + sum of
+//                  min_delta + delta over d < i, wrapping, decoding.rs:560-566);
+//   k_delta_expand the same unpack, a workgroup scan from the tile's start value, and stores
+//                  through an LDS transpose (1 KiB of contiguous output per store instruction).
+// No workgroup waits on another (no look-back), so no dispatch-order assumption is needed.
 // Pages with more than DELTA_MBMAX mini-blocks per block, or a tile needing more than
 // DELTA_BCAP blocks, fall back to k_delta above.
 #include "pqg_runs.hpp"
@@ -224,7 +228,12 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
       const uint32_t d0 = bb * vpb;
       const uint32_t left = need - d0;
       const uint32_t d1 = d0 + (left < vpb ? left : vpb);
-      const DeltaBlock rec{wpos, payload, (uint64_t)unzigzag(zz)};
+      DeltaBlock rec{wpos, payload, (uint64_t)unzigzag(zz), {}};
+      {
+        const uint32_t rel = posv - rbase + vl;
+#pragma unroll
+        for (uint32_t m = 0; m < DELTA_MBMAX; ++m) rec.w[m] = m < nmb32 ? (uint8_t)lbyte(sm.region, rel + m) : 0;
+      }
       for (uint32_t t = (d0 + 1) / DELTA_TILE; t <= d1 / DELTA_TILE; ++t) {
         const uint32_t vlo = t * DELTA_TILE;
         const uint32_t slot = bb - (vlo > 0 ? vlo - 1 : 0) / vpb;
@@ -248,241 +257,298 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   if (lane == 0) dt.page[p] = info;
 }
 
+
+constexpr int DX_STAGE = 10240;                        // staged payload bytes per tile
+constexpr int DX_OUTB = DELTA_TILE / 2 * 8;            // half a tile of 8-byte values (16 KiB)
+constexpr int DX_UNION = DX_OUTB > DX_STAGE + 64 ? DX_OUTB : DX_STAGE + 64;
+
 struct DeltaExpandSmem {
-  uint32_t stage[EX_WORDS];
-  DeltaBlock blk[DELTA_BCAP];
-  uint32_t mboff[DELTA_BCAP][DELTA_MBMAX];  // byte offset of mini-block m from blk.pos
+  union {
+    uint32_t stage[DX_UNION / 4];   // payload window, then the transposed output halves
+    uint4 outq[DX_UNION / 16];
+  };
+  uint64_t mind[DELTA_BCAP];
+  uint32_t pos[DELTA_BCAP];         // block payload offsets (stream-relative)
+  uint32_t mboff[DELTA_BCAP][DELTA_MBMAX];  // byte offset of mini-block m from pos
   uint8_t mbw[DELTA_BCAP][DELTA_MBMAX];
   uint64_t wsum[WG / 64];
   uint64_t prefix;
 };
 
-__device__ inline uint32_t atomic_ld(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline uint64_t atomic_ld64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Front of the DELTA_BINARY_PACKED tile passes (decoding.rs:535-566): tile t's block records
+// (with their mini-block widths, round trip 1) and payload window (round trip 2), then 16
+// consecutive deltas per thread into x (mini-block parameters hoisted, one 32-bit funnel shift
+// per delta for widths <= 32) and their wrapping sum into s. False: nothing to do for tile t.
+template <int ES>
+__device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
+                                        uint64_t blob_len, PageWork* pages,
+                                        const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                        const DeltaTables& dt, uint32_t t, int& p, DeltaPage& info,
+                                        uint32_t& lo, uint32_t& hi, uint64_t (&x)[DPT], uint64_t& s) {
+  const int tid = threadIdx.x;
+  if (t >= ntiles) return false;
+  p = (int)tile_page[t];
+  const PageWork& pw = pages[p];
+  if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) return false;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return false;
+  info = dt.page[p];
+  if (!info.tiled) return false;
+  const uint32_t n = (uint32_t)pw.nonnull;
+  const uint32_t k = t - pw.ltile0;
+  lo = k * DELTA_TILE;
+  if (lo >= n) return false;
+  hi = lo + DELTA_TILE < n ? lo + DELTA_TILE : n;
+  const uint64_t S = pw.base + pw.val_off;
+  const uint32_t vpmb = info.vpmb, nmb = info.nmb, vpb = vpmb * nmb;
+  // deltas of the tile: d in [lo - 1, hi - 1), d >= 0
+  const uint32_t dlo = lo > 0 ? lo - 1 : 0;
+  const bool anyd = hi >= 2;
+  const uint32_t blo = dlo / vpb;
+  const uint32_t bhi = anyd ? (hi - 2) / vpb : blo;
+  const uint32_t nb = bhi - blo + 1;
+  const DeltaBlock* recs = dt.blocks + (uint64_t)t * DELTA_BCAP;
+  // ---- block records: payload offset, min_delta, widths and mini-block offsets
+  if ((uint32_t)tid < nb) {
+    const uint4* rq = reinterpret_cast<const uint4*>(recs + tid);
+    const uint4 r0 = rq[0], r1 = rq[1];
+    sm.pos[tid] = r0.y;
+    sm.mind[tid] = (uint64_t)r0.z | ((uint64_t)r0.w << 32);
+    const uint32_t wv[4] = {r1.x, r1.y, r1.z, r1.w};
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < DELTA_MBMAX; ++m) {
+      const uint32_t wdt = (wv[m >> 2] >> (8 * (m & 3))) & 0xFFu;
+      sm.mbw[tid][m] = (uint8_t)wdt;
+      sm.mboff[tid][m] = off;
+      off += m < nmb ? (vpmb * wdt) >> 3 : 0u;
+    }
+  }
+  __syncthreads();
+  // ---- payload window from the tile's first delta on
+  uint64_t A0;
+  {
+    const uint32_t r0 = dlo - blo * vpb;
+    const uint32_t m0 = r0 / vpmb;
+    const uint64_t bit0 = ((uint64_t)sm.pos[0] + sm.mboff[0][m0]) * 8ull +
+                          (uint64_t)(r0 - m0 * vpmb) * sm.mbw[0][m0];
+    A0 = (S + (bit0 >> 3)) & ~15ull;
+  }
+  const uint64_t S_end = S + pw.val_bytes + 16;
+  const uint64_t A1 = A0 + DX_STAGE < S_end ? A0 + DX_STAGE : S_end;
+  const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
+  {
+    constexpr int PER = (DX_STAGE / 16 + WG - 1) / WG;
+    uint4 v[PER];
+    const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
+      if (ci < nchunks) {
+        const uint64_t a = A0 + (uint64_t)ci * 16;
+        v[c] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
+      if (ci < nchunks) sm.outq[ci] = v[c];
+    }
+    if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
+  }
+  const uint32_t lim = nchunks * 128u;  // staged bits
+  const uint64_t sbase = A0 - S;        // stream offset of staged byte 0
+  __syncthreads();
+  // ---- 16 deltas per thread: values lo + 16*tid + j
+  s = 0;
+  const uint32_t i0 = lo + (uint32_t)tid * DPT;
+  const uint32_t d0 = i0 > 0 ? i0 - 1 : 0;
+  uint32_t bi = d0 / vpb - blo;
+  const uint32_t rr = d0 - (bi + blo) * vpb;
+  uint32_t m = rr / vpmb;
+  uint32_t kk = rr - m * vpmb;
+  uint32_t wdt = 0;
+  int64_t base = 0;  // bit offset of the mini-block's delta 0 relative to the staged window
+  uint64_t mn = 0;
+  auto mb = [&]() {
+    const uint32_t bs = bi < nb ? bi : 0u;
+    wdt = sm.mbw[bs][m];
+    base = ((int64_t)sm.pos[bs] + (int64_t)sm.mboff[bs][m] - (int64_t)sbase) * 8;
+    mn = sm.mind[bs];
+  };
+  mb();
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const uint32_t i = i0 + (uint32_t)j;
+    x[j] = 0;
+    if (i >= 1 && i < hi && bi < nb) {
+      const int64_t bit = base + (int64_t)kk * wdt;
+      uint64_t raw = 0;
+      if (wdt) {
+        if (bit >= 0 && bit + wdt <= (int64_t)lim) {
+          const uint32_t b32 = (uint32_t)bit, wi = b32 >> 5;
+          const uint32_t w0 = sm.stage[wi], w1 = sm.stage[wi + 1];
+          if (wdt <= 32) {  // window bits [sh, sh + 32)
+            const uint32_t r = __builtin_amdgcn_alignbit(w1, w0, b32 & 31u);
+            raw = wdt == 32 ? r : (r & ((1u << wdt) - 1u));
+          } else {          // window bits [sh, sh + 64)
+            const uint32_t w2 = sm.stage[wi + 2];
+            const uint64_t lo64 = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, b32 & 31u) << 32) |
+                                  __builtin_amdgcn_alignbit(w1, w0, b32 & 31u);
+            raw = wdt >= 64 ? lo64 : (lo64 & ((1ull << wdt) - 1ull));
+          }
+        } else {  // outside the staged window: global memory
+          const uint64_t gb = (uint64_t)(bit + (int64_t)sbase * 8);
+          const uint64_t abs = S + (gb >> 3);
+          const uint32_t sh = (uint32_t)(gb & 7);
+          uint64_t r = gload_u64(blob, blob_len, abs) >> sh;
+          if (wdt + sh > 64) r |= gload_u64(blob, blob_len, abs + 8) << (64 - sh);
+          raw = wdt >= 64 ? r : (r & ((1ull << wdt) - 1ull));
+        }
+      }
+      x[j] = mn + raw;  // min_delta + delta (wrapping)
+    }
+    if (i >= 1) {  // advance to the next delta
+      if (++kk == vpmb) {
+        kk = 0;
+        if (++m == nmb) {
+          m = 0;
+          ++bi;
+        }
+        mb();
+      }
+    }
+    s += x[j];
+  }
+  return true;
 }
 
+// Tile sums: wrapping sum of min_delta + delta over each tile's deltas -> dt.agg[t].
 template <int ES>
-__global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                     uint32_t ntiles, DeltaTables dt, uint32_t epoch,
-                                                     uint8_t* __restrict__ out, ChunkResult* res) {
+__global__ void __launch_bounds__(WG) k_delta_sums(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                   uint32_t ntiles, DeltaTables dt) {
   __shared__ DeltaExpandSmem sm;
-  const int tid = threadIdx.x;
-  // One tile per workgroup: the look-back needs tile t-1 to be owned by an earlier (already
-  // dispatched) workgroup that does not itself wait on a later tile.
-  for (uint32_t it = 0; it < 1; ++it) {
-    const uint32_t t = blockIdx.x + it;
-    if (t >= ntiles) break;
-    const int p = (int)tile_page[t];
-    const PageWork& pw = pages[p];
-    if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) continue;
-    if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) continue;
-    const DeltaPage info = dt.page[p];
-    if (!info.tiled) continue;
-    const uint32_t n = (uint32_t)pw.nonnull;
-    const uint32_t k = t - pw.ltile0;
-    const uint32_t lo = k * DELTA_TILE;
-    if (lo >= n) continue;
-    const uint32_t hi = lo + DELTA_TILE < n ? lo + DELTA_TILE : n;
-    const uint64_t S = pw.base + pw.val_off;
-    const uint32_t vpmb = info.vpmb, nmb = info.nmb, vpb = vpmb * nmb;
-    // deltas of the tile: d in [lo - 1, hi - 1), d >= 0
-    const uint32_t dlo = lo > 0 ? lo - 1 : 0;
-    const bool anyd = hi >= 2;
-    const uint32_t blo = dlo / vpb;
-    const uint32_t bhi = anyd ? (hi - 2) / vpb : blo;
-    const uint32_t nb = bhi - blo + 1;
-    const DeltaBlock* recs = dt.blocks + (uint64_t)t * DELTA_BCAP;
-    // ---- block records, widths and mini-block offsets
-    if ((uint32_t)tid < nb) {
-      const DeltaBlock rb = recs[tid];
-      sm.blk[tid] = rb;
-      uint32_t off = 0;
-      for (uint32_t m = 0; m < nmb; ++m) {
-        const uint32_t wdt = blob[S + rb.wpos + m];
-        sm.mbw[tid][m] = (uint8_t)wdt;
-        sm.mboff[tid][m] = off;
-        off += (vpmb * wdt) >> 3;
-      }
-    }
-    __syncthreads();
-    // ---- stage the payload from the tile's first delta on
-    uint64_t A0;
-    {
-      const uint32_t r0 = dlo - blo * vpb;
-      const uint32_t m0 = r0 / vpmb;
-      const uint64_t bit0 = ((uint64_t)sm.blk[0].pos + sm.mboff[0][m0]) * 8ull +
-                            (uint64_t)(r0 - m0 * vpmb) * sm.mbw[0][m0];
-      A0 = (S + (bit0 >> 3)) & ~15ull;
-    }
-    const uint64_t S_end = S + pw.val_bytes + 16;
-    const uint64_t A1 = A0 + EX_STAGE < S_end ? A0 + EX_STAGE : S_end;
-    const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
-    {
-      constexpr int PER = (EX_STAGE / 16 + WG - 1) / WG;
-      uint4 v[PER];
-      const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
-        if (ci < nchunks) {
-          const uint64_t a = A0 + (uint64_t)ci * 16;
-          v[c] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const uint32_t ci = (uint32_t)tid + (uint32_t)(c * WG);
-        if (ci < nchunks) reinterpret_cast<uint4*>(sm.stage)[ci] = v[c];
-      }
-      if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
-    }
-    const uint64_t staged = (uint64_t)nchunks * 16;
-    __syncthreads();
-    // ---- 16 deltas per thread: values lo + 16*tid + j
-    uint64_t x[DPT];
-    uint64_t s = 0;
-    {
-      const uint32_t i0 = lo + (uint32_t)tid * DPT;
-      const uint32_t d0 = i0 > 0 ? i0 - 1 : 0;
-      uint32_t bi = d0 / vpb - blo;
-      uint32_t rr = d0 - (bi + blo) * vpb;
-      uint32_t m = rr / vpmb;
-      uint32_t kk = rr - m * vpmb;
-#pragma unroll
-      for (int j = 0; j < DPT; ++j) {
-        const uint32_t i = i0 + (uint32_t)j;
-        x[j] = 0;
-        if (i >= 1 && i < hi && bi < nb) {
-          const uint32_t wdt = sm.mbw[bi][m];
-          const uint64_t bit = ((uint64_t)sm.blk[bi].pos + sm.mboff[bi][m]) * 8ull + (uint64_t)kk * wdt;
-          const uint64_t abs = S + (bit >> 3);
-          const uint32_t sh = (uint32_t)(bit & 7);
-          const uint64_t ri = abs - A0;
-          uint64_t raw = 0;
-          if (wdt) {
-            uint64_t lo64 = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
-                                                             : gload_u64(blob, blob_len, abs);
-            raw = lo64 >> sh;
-            if (wdt + sh > 64) {
-              const uint64_t hi64 = (abs >= A0 && ri + 20 <= staged) ? lload_u64(sm.stage, (uint32_t)ri + 8)
-                                                                     : gload_u64(blob, blob_len, abs + 8);
-              raw |= hi64 << (64 - sh);
-            }
-            if (wdt < 64) raw &= (1ull << wdt) - 1ull;
-          }
-          x[j] = sm.blk[bi].min_delta + raw;  // min_delta + delta (wrapping)
-        }
-        if (i >= 1) {  // advance to the next delta
-          if (++kk == vpmb) {
-            kk = 0;
-            if (++m == nmb) {
-              m = 0;
-              ++bi;
-            }
-          }
-        }
-        s += x[j];
-      }
-    }
-    // ---- workgroup scan of the thread sums
-    uint64_t incl = s;
+  const uint32_t t = blockIdx.x;
+  int p;
+  DeltaPage info;
+  uint32_t lo, hi;
+  uint64_t x[DPT], s;
+  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
+    return;
+  const uint64_t T = block_sum_u64(s, sm.wsum);
+  if (threadIdx.x == 0) dt.agg[t] = T;
+}
+
+// Running value at each tile start: dt.inc[t] = first + the page's earlier tile sums (one
+// workgroup per page; wrapping, as the reference's i64 adds).
+__global__ void __launch_bounds__(WG) k_delta_tscan(const PageWork* pages, DeltaTables dt) {
+  __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint64_t carry;
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  const DeltaPage info = dt.page[p];
+  if (!info.tiled) return;
+  const uint32_t n = (uint32_t)pw.nonnull;
+  const uint32_t nt = (n + DELTA_TILE - 1) / DELTA_TILE;
+  if (threadIdx.x == 0) carry = info.first;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nt; b0 += WG) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nt ? dt.agg[pw.ltile0 + i] : 0ull;
+    uint64_t incl = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const uint64_t y = __shfl_up(incl, off, 64);
-      if ((tid & 63) >= off) incl += y;
+      if ((threadIdx.x & 63) >= (unsigned)off) incl += y;
     }
-    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
     __syncthreads();
-    uint64_t pre = incl - s;
-    for (int wv = 0; wv < (tid >> 6); ++wv) pre += sm.wsum[wv];
-    // ---- decoupled look-back over the page's tiles (wave 0: 64 predecessors per probe)
-    if (tid < 64) {
-      const uint32_t lane = tid;
-      const uint64_t T = sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
-      uint64_t P = 0;
-      if (k == 0) {
-        if (lane == 0) {
-          __hip_atomic_store(&dt.inc[t], T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_s_waitcnt(0);
-          __hip_atomic_store(&dt.flag[t], epoch * 4u + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        if (lane == 0) {
-          __hip_atomic_store(&dt.agg[t], T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_s_waitcnt(0);
-          __hip_atomic_store(&dt.flag[t], epoch * 4u + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const uint32_t first = pw.ltile0;  // the page's tile 0 always ends a look-back
-        uint32_t base = t - 1;
-        uint32_t spins = 0;
-        while (true) {
-          const bool valid = base >= first + lane;  // lane probes tile base - lane
-          const uint32_t qt = base - lane;
-          const uint32_t f = valid ? atomic_ld(&dt.flag[qt]) : 0u;
-          const bool ready = valid && (f >> 2) == epoch && (f & 3u) != 0;
-          const uint64_t incl = __ballot(ready && (f & 3u) == 2u);
-          const uint32_t L = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
-          const uint64_t need = (L >= 64 ? ~0ull : ((1ull << L) - 1ull)) & __ballot(valid);
-          if (need & ~__ballot(ready)) {  // a predecessor has not published yet
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {  // never expected: stop instead of hanging the GPU
-              if (lane == 0) report(pages, res, p, ST_HANG);
-              break;
-            }
-            continue;
-          }
-          uint64_t v = 0;
-          if (lane < L && valid) v = atomic_ld64(&dt.agg[qt]);
-          else if (lane == L) v = atomic_ld64(&dt.inc[qt]);
+    uint64_t pre = carry;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += wsum[w];
+    if (i < nt) dt.inc[pw.ltile0 + i] = pre + incl - v;
+    __syncthreads();
+    if (threadIdx.x == WG - 1) carry = pre + incl;
+    __syncthreads();
+  }
+}
+
+// Tile expand: running values from dt.inc[t] plus the in-tile scan, stored through an LDS
+// transpose so that every store instruction writes 1 KiB of contiguous output: half h =
+// threads [128h, 128h + 128) hold tile values [2048h, 2048h + 2048) and the half leaves as
+// 16-byte chunks, chunk c by thread c % 256.
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                     uint32_t ntiles, DeltaTables dt,
+                                                     uint8_t* __restrict__ out) {
+  __shared__ DeltaExpandSmem sm;
+  const int tid = threadIdx.x;
+  const uint32_t t = blockIdx.x;
+  int p;
+  DeltaPage info;
+  uint32_t lo, hi;
+  uint64_t x[DPT], s;
+  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
+    return;
+  const PageWork& pw = pages[p];
+  // ---- workgroup scan of the thread sums
+  uint64_t incl = s;
 #pragma unroll
-          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-          P += v;
-          if (L < 64) break;
-          base -= 64;
-        }
-        if (lane == 0) {
-          __hip_atomic_store(&dt.inc[t], P + T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_s_waitcnt(0);
-          __hip_atomic_store(&dt.flag[t], epoch * 4u + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if ((tid & 63) >= off) incl += y;
+  }
+  if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+  if (tid == 0) sm.prefix = dt.inc[t];
+  __syncthreads();
+  uint64_t acc = sm.prefix + incl - s;
+  for (int wv = 0; wv < (tid >> 6); ++wv) acc += sm.wsum[wv];
+  uint64_t val[DPT];
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    acc += x[j];
+    val[j] = acc;
+  }
+  const uint32_t cnt = hi - lo;
+  uint8_t* const ob = out + (pw.value_out + lo) * (uint64_t)ES;
+  constexpr uint32_t HALF = DELTA_TILE / 2;  // values per half
+  constexpr uint32_t CPT = DPT * ES / 16;    // 16-byte chunks per thread
+  constexpr uint32_t NCH = HALF * ES / 16;   // chunks per half
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if ((tid >> 7) == h) {
+      const uint32_t tl = (uint32_t)tid & 127u;
+#pragma unroll
+      for (uint32_t c = 0; c < CPT; ++c) {
+        uint4 q;
+        if (ES == 8)
+          q = make_uint4((uint32_t)val[2 * c], (uint32_t)(val[2 * c] >> 32), (uint32_t)val[2 * c + 1],
+                         (uint32_t)(val[2 * c + 1] >> 32));
+        else
+          q = make_uint4((uint32_t)val[4 * c], (uint32_t)val[4 * c + 1], (uint32_t)val[4 * c + 2],
+                         (uint32_t)val[4 * c + 3]);
+        const uint32_t ci = tl * CPT + c;   // chunk within the half
+        sm.outq[ci ^ (tl & 7u)] = q;        // xor swizzle against bank conflicts
       }
-      if (lane == 0) sm.prefix = P;
     }
     __syncthreads();
-    // ---- values
-    {
-      uint64_t acc = info.first + sm.prefix + pre;
-      const uint32_t i0 = lo + (uint32_t)tid * DPT;
-      if (i0 < hi) {
-        if (ES == 8) {
-          int64_t* op = reinterpret_cast<int64_t*>(out) + pw.value_out + i0;
-          if (i0 + DPT <= hi && !(pw.value_out & 1)) {  // 16-byte aligned stores
 #pragma unroll
-            for (int j = 0; j < DPT; j += 2) {
-              const uint64_t v0 = acc + x[j];
-              const uint64_t v1 = v0 + x[j + 1];
-              acc = v1;
-              *reinterpret_cast<uint4*>(op + j) =
-                  make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
-            }
-          } else {
+    for (uint32_t r = 0; r < NCH / WG; ++r) {
+      const uint32_t ci = (uint32_t)tid + r * WG;
+      const uint4 q = sm.outq[ci ^ ((ci / CPT) & 7u)];
+      const uint32_t v0 = h * HALF + ci * (16 / ES);  // first tile value of the chunk
+      uint8_t* dst = ob + (uint64_t)v0 * ES;
+      if (v0 + 16 / ES <= cnt) {
+        *reinterpret_cast<uint4*>(dst) = q;
+      } else if (v0 < cnt) {
+        const uint32_t qa[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-            for (int j = 0; j < DPT; ++j) {
-              acc += x[j];
-              if (i0 + j < hi) op[j] = (int64_t)acc;
-            }
-          }
-        } else {
-          int32_t* op = reinterpret_cast<int32_t*>(out) + pw.value_out + i0;
-#pragma unroll
-          for (int j = 0; j < DPT; ++j) {
-            acc += x[j];
-            if (i0 + j < hi) op[j] = (int32_t)(uint32_t)acc;
-          }
+        for (uint32_t e = 0; e < 16 / ES; ++e) {
+          if (v0 + e >= cnt) break;
+          if (ES == 8) reinterpret_cast<uint64_t*>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
+          else reinterpret_cast<uint32_t*>(dst)[e] = qa[e];
         }
       }
     }
@@ -508,22 +574,27 @@ __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ b
   if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 
+template <int ES>
+static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, uint8_t* out,
+                        ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
+  if (ntiles) {
+    hipLaunchKernelGGL(k_delta_sums<ES>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt);
+    hipLaunchKernelGGL(k_delta_tscan, dim3(npages), dim3(WG), 0, s, pages, dt);
+    hipLaunchKernelGGL(k_delta_expand<ES>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, out);
+  }
+  hipLaunchKernelGGL(k_delta_rest<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
+}
+
 extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                                              int npages, uint32_t ntiles, const uint32_t* tile_page,
                                              DeltaTables dt, uint32_t epoch, int es, uint8_t* out,
                                              ChunkResult* res, hipStream_t s) {
-  const dim3 eg(ntiles);
-  if (es == 8) {
-    hipLaunchKernelGGL(k_delta_index<8>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
-    if (ntiles) hipLaunchKernelGGL(k_delta_expand<8>, eg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, epoch, out, res);
-    hipLaunchKernelGGL(k_delta_rest<8>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
-  } else if (es == 4) {
-    hipLaunchKernelGGL(k_delta_index<4>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
-    if (ntiles) hipLaunchKernelGGL(k_delta_expand<4>, eg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, epoch, out, res);
-    hipLaunchKernelGGL(k_delta_rest<4>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
-  } else {
-    return hipErrorInvalidValue;
-  }
+  (void)epoch;  // tile prefixes come from k_delta_tscan: no cross-workgroup flags
+  if (es == 8) delta_tiled<8>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s);
+  else if (es == 4) delta_tiled<4>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -125,6 +125,7 @@ struct DeltaBlock {
   uint32_t wpos;      // stream offset of the block's mini-block width bytes
   uint32_t pos;       // stream offset of its first mini-block
   uint64_t min_delta;
+  uint8_t w[DELTA_MBMAX];  // mini-block bit widths (the expand pass needs no second round trip)
 };
 
 struct DeltaPage {
