@@ -341,7 +341,7 @@ def main():
                                   "levels_ms": tv.levels_ms, "values_ms": tv.values_ms}
             w = wv
         result["variants"] = var
-    if os.environ.get("PQG_DEBUG") and int(os.environ["PQG_DEBUG"]) & 16:
+    if os.environ.get("PQG_DEBUG") and int(os.environ["PQG_DEBUG"]) & 48:
         st4 = (C.c_double * 4)()
         pqgpu.lib().pqg_debug_stamps(ctx.h, st4)
         result["debug_stamps"] = {"waves": st4[3], "desc_cyc": st4[0], "expand_cyc": st4[1],

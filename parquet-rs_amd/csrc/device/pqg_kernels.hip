@@ -153,7 +153,8 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
     if (pages[dict_page].status != 0) return;
   }
   const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0,
-                              rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT, rt.nruns + pw.ltile0, sm);
+                              rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT, rt.nruns + pw.ltile0, sm,
+                              (cp.debug & 32) && cp.dbgbuf ? cp.dbgbuf + 2 * p : nullptr);
   if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 

@@ -277,8 +277,22 @@ __device__ inline uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_r
 __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                     const Stream& s, RunCkpt* __restrict__ ck,
                                     uint2* __restrict__ runs, uint32_t* __restrict__ nruns,
-                                    IndexSmem& sm) {
+                                    IndexSmem& sm, uint64_t* stamps = nullptr) {
   const uint32_t lane = threadIdx.x & 63;
+  // diagnostics (PQG_DEBUG bit 5): s_memtime cycles in region fetches, hop loops, batches
+  uint64_t t_fetch = 0, t_hop = 0, t_batch = 0, t0 = 0;
+  auto stamp = [&](uint64_t& acc) {
+    if (stamps) {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      acc += t1 - t0;
+      t0 = t1;
+    }
+  };
+  auto flush = [&]() {
+    if (stamps && lane == 0)
+      *reinterpret_cast<uint4*>(stamps) = make_uint4((uint32_t)t_fetch, (uint32_t)t_hop, (uint32_t)t_batch, 0u);
+  };
+  if (stamps) t0 = __builtin_amdgcn_s_memtime();
   if (s.err) return s.err;
   const uint32_t n = s.n;
   if (n == 0) return 0;
@@ -315,41 +329,59 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region writes done (vmcnt untouched)
       __builtin_amdgcn_wave_barrier();
+      stamp(t_fetch);
     }
     const uint32_t rbase = r * IX_REG - off0;  // stream offset of region byte 0
-    // ---- hop loop: follow up to 64 headers inside this region (uniform, scalar)
+    // ---- hop loop: follow up to 64 headers inside this region (uniform, scalar). The 64 lanes
+    // first decode a header at each of the 64 stream positions from the current one (one-byte
+    // form: next header and output count); the chain then takes two v_readlane and a few SALU
+    // ops per hop until it leaves those 64 bytes. Other header forms take run_parse.
     uint32_t posv = 0, k = 0;
     uint32_t acc = produced;  // < n before each add, so acc + min(cnt, n) < 2^32
-    while (k < 64) {
+    bool stop = false;
+    while (k < 64 && !stop && acc < n) {
       if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
-      const uint32_t rel = cur - rbase;
-      const uint32_t wi = rel >> 2;
-      const uint32_t x = rfl(__builtin_amdgcn_alignbyte(sm.region[wi + 1], sm.region[wi], rel & 3u));
-      const uint32_t b0 = x & 0xFFu;
-      uint32_t cnt, nxt;
-      bool stop = false;
-      if (!(b0 & 0x80u) && vb <= 3u) {
+      // candidate headers at cur + lane (one-byte form); ~0u marks any other form
+      const uint32_t wbase = cur;
+      uint32_t nxv, cnv;
+      {
+        const uint32_t q = cur + lane;
+        const uint32_t rel = q - rbase;
+        const uint32_t b0 = (q < slen && rel < (uint32_t)(IX_REG + 60)) ? lbyte(sm.region, rel) : 0x80u;
         const uint32_t half = b0 >> 1;
-        if (b0 & 1u) {
-          cnt = half << 3;
-          nxt = cur + 1u + half * w;
-        } else {
-          cnt = half;
-          nxt = cur + 1u + vb;
-        }
-      } else {
-        uint32_t inf, flg;
-        run_parse(sm.region, rel, cur, slen, (int)w, nxt, cnt, inf, flg);
-        nxt = rfl(nxt);
-        cnt = rfl(cnt);
-        stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
+        const bool fast = !(b0 & 0x80u) && vb <= 3u;
+        nxv = !fast ? 0xFFFFFFFFu : ((b0 & 1u) ? q + 1u + half * w : q + 1u + vb);
+        cnv = (b0 & 1u) ? half << 3 : half;
       }
-      posv = lane == k ? cur : posv;  // v_cmp + v_cndmask
+      // tight chain through the candidates: all exits folded into one test; headers stay
+      // inside the region (its 64-byte overlap only serves their bytes)
+      const uint32_t olim = (rbase + (uint32_t)IX_REG - wbase) < 64u ? rbase + (uint32_t)IX_REG - wbase : 64u;
+      uint32_t o = 0;
+      while (true) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)nxv, (int)o);
+        if (nx == 0xFFFFFFFFu) break;
+        const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)cnv, (int)o);
+        posv = lane == k ? cur : posv;
+        ++k;
+        acc += cn < n ? cn : n;
+        cur = nx;
+        o = cur - wbase;
+        if ((o >= olim) | (k >= 64u) | (acc >= n)) break;
+      }
+      if (k >= 64u || acc >= n || o >= olim) continue;  // batch full / done / window left
+      // header at cur in another form
+      if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
+      uint32_t nxt, cnt, inf, flg;
+      run_parse(sm.region, cur - rbase, cur, slen, (int)w, nxt, cnt, inf, flg);
+      nxt = rfl(nxt);
+      cnt = rfl(cnt);
+      stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
+      posv = lane == k ? cur : posv;
       ++k;
       acc += cnt < n ? cnt : n;
       cur = nxt;
-      if (stop || acc >= n) break;
     }
+    stamp(t_hop);
     if (k == 0) continue;  // region boundary: reload
     // ---- batch: lane l re-parses header l
     const bool in = lane < k;
@@ -415,7 +447,11 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
       carry_tile = le / RUN_TILE;
       carry_j = (let == carry_tile) ? (lt == carry_tile ? lj + 1 : 1u) : 0u;
     }
-    if (produced >= n) return 0;
+    stamp(t_batch);
+    if (produced >= n) {
+      flush();
+      return 0;
+    }
   }
 }
 

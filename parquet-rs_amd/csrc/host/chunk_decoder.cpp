@@ -388,15 +388,15 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   static const int dbg_env = getenv("PQG_DEBUG") ? atoi(getenv("PQG_DEBUG")) : 0;
   cp.debug = dbg_env;
   cp.dbgbuf = nullptr;
-  if (dbg_env & 16) {
-    const size_t need = (size_t)total_tiles * 4 * 16;
+  if (dbg_env & 48) {
+    const size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
       HIPCHK(hipMalloc(&ctx->dbgbuf, need), "hipMalloc dbg");
       ctx->dbg_cap = need;
     }
-    ctx->dbg_n = total_tiles * 4;
+    ctx->dbg_n = (dbg_env & 32) ? (uint32_t)npages : total_tiles * 4;
     cp.dbgbuf = ctx->dbgbuf;
   }
 
