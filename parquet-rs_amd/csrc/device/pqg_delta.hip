@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   const uint32_t off0 = (uint32_t)(S - G);
   const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
   const uint64_t below = (1ull << lane) - 1ull;
-  uint4 pf[9];
+  uint4 pf[IX_PF];
   uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
   uint32_t cur = q, b = 0;
   bool overflow = false;
@@ -163,34 +163,20 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
       __builtin_amdgcn_wave_barrier();
     }
     const uint32_t rbase = r * IX_REG - off0;  // stream offset of region byte 0
-    // header bytes from a register window (lane l holds region dword wb/4 + l): v_readlane
-    // and SALU per hop, an LDS read only when the chain leaves the window
     uint32_t posv = 0, k = 0;
-    uint32_t wb = 0x80000000u, vwin = 0;
-    auto win8 = [&](uint32_t o) -> uint64_t {  // 8 bytes at window offset o (o <= 243)
-      const int d = (int)(o >> 2);
-      const uint64_t a = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vwin, d) |
-                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vwin, d + 1) << 32);
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)vwin, d + 2);
-      const uint32_t sh = (o & 3u) * 8u;
-      return sh ? ((a >> sh) | ((uint64_t)c << (64 - sh))) : a;
-    };
     while (k < 64 && b + k < nblocks) {
       if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;  // 64-byte overlap holds the header
       const uint32_t rel = cur - rbase;
-      if (rel - wb >= 228u) {
-        wb = rel & ~3u;
-        const uint32_t wi = (wb >> 2) + lane;
-        vwin = wi < (uint32_t)IX_WORDS ? sm.region[wi] : 0u;
-      }
-      const uint32_t o = rel - wb;
-      const uint64_t lo = win8(o);
+      const uint64_t w0 = lload_u64(sm.region, rel);
+      const uint32_t x0 = rfl32((uint32_t)w0), x1 = rfl32((uint32_t)(w0 >> 32));
+      const uint64_t lo = ((uint64_t)x1 << 32) | x0;
       const uint64_t t8 = ~lo & 0x8080808080808080ull;
       posv = lane == k ? cur : posv;
       ++k;
       if (!t8 || nmb32 > 8) break;  // long varint / many widths: the batch finishes this block
       const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
-      const uint64_t wy = win8(o + vl);
+      const uint64_t w1 = lload_u64(sm.region, rel + vl);
+      const uint64_t wy = ((uint64_t)rfl32((uint32_t)(w1 >> 32)) << 32) | rfl32((uint32_t)w1);
       const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
       uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
       const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);

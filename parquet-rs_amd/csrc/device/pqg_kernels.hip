@@ -158,33 +158,6 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
   if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 
-struct LevelEmit {
-  int16_t* out;
-  int16_t max_level;
-  bool count;
-  uint64_t nonnull;
-  int32_t err;
-  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
-    if (count) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((mask >> j) & 1) nonnull += ((int16_t)v[j] == max_level) ? 1 : 0;
-    }
-    if (!out) return;  // diagnostics: no stores
-    if (mask == 0xFFu) {
-      uint4 pk;
-      pk.x = (v[0] & 0xFFFFu) | (v[1] << 16);
-      pk.y = (v[2] & 0xFFFFu) | (v[3] << 16);
-      pk.z = (v[4] & 0xFFFFu) | (v[5] << 16);
-      pk.w = (v[6] & 0xFFFFu) | (v[7] << 16);
-      *reinterpret_cast<uint4*>(out + g) = pk;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((mask >> j) & 1) out[g + j] = (int16_t)v[j];
-    }
-  }
-};
 
 // Quarter-tile descriptors of stream `sel` (one thread per quarter), read by the wave expand
 // kernels.
@@ -229,11 +202,9 @@ struct LevelsMaker {
                                                   int which, int16_t* __restrict__ out) {             \
     __shared__ TileSmem sm;                                                                       \
     LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount};  \
-    tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                  \
+    tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                   \
   }
-PQG_TEXPAND_LEVELS(k_texpand_levels, )
-PQG_TEXPAND_LEVELS(k_texpand_levels_e6, __attribute__((amdgpu_waves_per_eu(6, 8))))
-PQG_TEXPAND_LEVELS(k_texpand_levels_e8, __attribute__((amdgpu_waves_per_eu(8, 8))))
+PQG_TEXPAND_LEVELS(k_texpand_levels, __attribute__((amdgpu_waves_per_eu(8, 8))))
 
 // Tile expand of RLE_DICTIONARY indices with the dictionary gather. MODE 1 (diagnostics,
 // PQG_DEBUG bits 8-11 = 1) writes the index instead of gathering.
@@ -265,11 +236,9 @@ struct DictMaker {
     const PageWork& dp = pages[dict_page];                                                          \
     DictMaker<ES, MODE> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
                            out, pages, res};                                                        \
-    tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                    \
+    tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                     \
   }
 PQG_TEXPAND_DICT(k_texpand_dict, )
-PQG_TEXPAND_DICT(k_texpand_dict_e5, __attribute__((amdgpu_waves_per_eu(5, 8))))
-PQG_TEXPAND_DICT(k_texpand_dict_e6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
 // Tile expand of RLE booleans (data page v2 values).
 struct BoolMaker {
@@ -282,18 +251,7 @@ __global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__
                                                      uint32_t ntiles, RunTables rt, uint8_t* __restrict__ out) {
   __shared__ TileSmem sm;
   BoolMaker mk{out};
-  tile_loop(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);
-}
-
-// Persistent grid of a tile expand kernel: as many workgroups as fit on the chip at once.
-template <class K>
-static inline uint32_t tx_grid(K kernel, uint32_t ntiles) {
-  int cus = 0, dev = 0, per = 0;
-  hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WG, 0) != hipSuccess || per <= 0) per = 2;
-  const uint32_t g = (uint32_t)cus * (uint32_t)per;
-  return ntiles < g ? ntiles : g;
+  tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);
 }
 
 // Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
@@ -310,32 +268,6 @@ __global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint3
   if (threadIdx.x == 0) {
     if (field == 0) pages[p].nonnull = t;
     else pages[p].nbytes_out = t;
-  }
-}
-
-// Expand pass of a level stream (which: SS_DEF / SS_REP), one wave per quarter tile; def
-// levels also count the values read_batch will ask for (def == max_def, column/reader.rs:212-226).
-__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                       RunTables rt, ColumnParams cp, int which,
-                                                       int16_t* __restrict__ out) {
-  __shared__ WaveSmem sm;
-  const bool stamps = (cp.debug & 16) != 0;
-  const uint64_t c0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
-  const uint64_t c1 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-  LevelEmit em{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, 0, 0};
-  if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, sm, em);
-  const uint64_t c2 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-  if (which == SS_DEF) {
-    const uint32_t nn = wave_sum_u32((uint32_t)em.nonnull);
-    if ((threadIdx.x & 63) == 0) rt.qcount[blockIdx.x] = nn;
-  }
-  if (stamps && cp.dbgbuf) {
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t c3 = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) == 0)
-      reinterpret_cast<uint4*>(cp.dbgbuf)[blockIdx.x] =
-          make_uint4((uint32_t)(c1 - c0), (uint32_t)(c2 - c1), (uint32_t)(c3 - c2), (uint32_t)(c0 >> 8));
   }
 }
 
@@ -380,49 +312,6 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages,
 }
 
 // ------------------------------------------------------------------------------ dictionary
-
-template <int ES>
-struct DictEmit {
-  const uint8_t* dict;  // PLAIN dictionary page payload
-  uint32_t dict_len;
-  bool aligned;
-  uint8_t* out;
-  int32_t err;
-  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (!((mask >> j) & 1)) continue;
-      uint32_t idx = v[j];
-      if (idx >= dict_len) {  // dict[idx] out of bounds: the reference panics
-        err = ST_PANIC;
-        continue;
-      }
-      uint8_t* d = out + (g + (uint64_t)j) * ES;
-      const uint8_t* s = dict + (uint64_t)idx * ES;
-      if (ES == 4 && aligned) {
-        *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
-      } else if (ES == 8 && aligned) {
-        *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(s);
-      } else {
-        for (int k = 0; k < ES; ++k) d[k] = s[k];
-      }
-    }
-  }
-};
-
-template <int ES>
-__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, RunTables rt, int dict_page,
-                                                     uint8_t* __restrict__ out, ChunkResult* res) {
-  __shared__ WaveSmem sm;
-  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
-  if (!d.qhi) return;
-  const PageWork& dp = pages[dict_page];
-  DictEmit<ES> em{blob + dp.base, dp.num_values, ((dp.base % ES) == 0), out, 0};
-  wave_expand(blob, blob_len, d, rt.runs, sm, em);
-  const uint64_t bad = __ballot(em.err != 0);
-  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
-}
 
 // Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
 __global__ void k_dict_check(PageWork* pages, int dict_page, int es, ChunkResult* res) {
@@ -517,33 +406,6 @@ __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ b
   }
 }
 
-// RLE-encoded booleans of data page v2 (RleValueDecoder<Bool>, decoding.rs:323-384):
-// [i32 length][RLE hybrid, bit width 1].
-struct BoolEmit {
-  uint8_t* out;
-  int32_t err;
-  __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
-    if (mask == 0xFFu) {
-      uint2 pk;
-      pk.x = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
-      pk.y = (v[4] & 0xFF) | ((v[5] & 0xFF) << 8) | ((v[6] & 0xFF) << 16) | ((v[7] & 0xFF) << 24);
-      *reinterpret_cast<uint2*>(out + g) = pk;
-    } else {
-      for (int j = 0; j < 8; ++j)
-        if ((mask >> j) & 1) out[g + j] = (uint8_t)v[j];
-    }
-  }
-};
-
-__global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     RunTables rt, uint8_t* __restrict__ out) {
-  __shared__ WaveSmem sm;
-  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
-  if (!d.qhi) return;
-  BoolEmit em{out, 0};
-  wave_expand(blob, blob_len, d, rt.runs, sm, em);
-}
-
 // ------------------------------------------------------------------------------ finalize
 
 __global__ void k_finalize(PageWork* pages, ChunkResult* res) {
@@ -598,11 +460,7 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    switch ((cp.debug >> 8) & 15) {  // diagnostics variants (PQG_DEBUG bits 8-11)
-      case 2: hipLaunchKernelGGL(k_texpand_levels_e6, dim3(tx_grid(k_texpand_levels_e6, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
-      case 3: hipLaunchKernelGGL(k_texpand_levels_e8, dim3(tx_grid(k_texpand_levels_e8, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
-      default: hipLaunchKernelGGL(k_texpand_levels, dim3(tx_grid(k_texpand_levels, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out); break;
-    }
+    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();
@@ -624,17 +482,13 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   if (!ntiles) return hipGetLastError();
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
-  const dim3 g(tx_grid(k_texpand_dict<8>, ntiles));
+  const dim3 g(ntiles);
   switch (es) {
     case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 8:
       if (((cp.debug >> 8) & 15) == 1)  // diagnostics: no gather
         hipLaunchKernelGGL((k_texpand_dict<8, 1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
-      else if (((cp.debug >> 8) & 15) == 2)
-        hipLaunchKernelGGL((k_texpand_dict_e5<8>), dim3(tx_grid(k_texpand_dict_e5<8>, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
-      else if (((cp.debug >> 8) & 15) == 3)
-        hipLaunchKernelGGL((k_texpand_dict_e6<8>), dim3(tx_grid(k_texpand_dict_e6<8>, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
       else
         hipLaunchKernelGGL((k_texpand_dict<8>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
       break;
@@ -673,7 +527,7 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);
-    hipLaunchKernelGGL(k_texpand_bool, dim3(tx_grid(k_texpand_bool, ntiles)), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
+    hipLaunchKernelGGL(k_texpand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
   }
   return hipGetLastError();
 }

@@ -18,9 +18,13 @@
 #pragma once
 #include "pqg_device.hpp"
 
+#ifndef PQG_IX_REG
+#define PQG_IX_REG 32768
+#endif
+
 namespace pqg {
 
-constexpr int IX_REG = 8192;                  // index walker region (bytes)
+constexpr int IX_REG = PQG_IX_REG;            // index walker region (bytes)
 constexpr int IX_WORDS = (IX_REG + 64) / 4;
 constexpr int EX_STAGE = 10240;               // expand staging window (bytes)
 constexpr int EX_WORDS = (EX_STAGE + 64) / 4;
@@ -234,31 +238,32 @@ struct IndexSmem {
 };
 
 constexpr int IX_CHUNKS = (IX_REG + 64) / 16;  // 16-byte chunks per region (64-byte overlap)
+constexpr int IX_PF = (IX_CHUNKS + 63) / 64;     // 16-byte loads per lane per region
 
 // Region r of the walker's grid: bytes [G + r*IX_REG, G + (r+1)*IX_REG + 64), loaded by the
 // whole wave into registers (one wave-instruction per KiB, all in flight together).
 __device__ inline void ix_fetch(const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t A0,
-                                uint32_t lane, uint4 (&v)[9]) {
+                                uint32_t lane, uint4 (&v)[IX_PF]) {
   if (A0 + IX_REG + 64 <= blob_len) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
+    for (int k = 0; k < IX_PF; ++k) {
       const uint32_t c = lane + 64u * (uint32_t)k;
-      if (k < 8 || c < (uint32_t)IX_CHUNKS) v[k] = *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16);
+      if (k < IX_PF - 1 || c < (uint32_t)IX_CHUNKS) v[k] = *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16);
     }
   } else {  // blob tail: guarded byte loads (unrolled: v must stay in registers)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
+    for (int k = 0; k < IX_PF; ++k) {
       const uint32_t c = lane + 64u * (uint32_t)k;
-      if (k < 8 || c < (uint32_t)IX_CHUNKS) v[k] = gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
+      if (k < IX_PF - 1 || c < (uint32_t)IX_CHUNKS) v[k] = gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
     }
   }
 }
 
-__device__ inline void ix_install(uint32_t* region, uint32_t lane, const uint4 (&v)[9]) {
+__device__ inline void ix_install(uint32_t* region, uint32_t lane, const uint4 (&v)[IX_PF]) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
+  for (int k = 0; k < IX_PF; ++k) {
     const uint32_t c = lane + 64u * (uint32_t)k;
-    if (k < 8 || c < (uint32_t)IX_CHUNKS) reinterpret_cast<uint4*>(region)[c] = v[k];
+    if (k < IX_PF - 1 || c < (uint32_t)IX_CHUNKS) reinterpret_cast<uint4*>(region)[c] = v[k];
   }
 }
 
@@ -309,7 +314,7 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
   const uint32_t vb = (w + 7u) >> 3;
   const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
-  uint4 pf[9];
+  uint4 pf[IX_PF];
   uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
   uint32_t cur = 0;            // next header
   uint32_t produced = 0;       // outputs before `cur`'s run
@@ -332,54 +337,88 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
       stamp(t_fetch);
     }
     const uint32_t rbase = r * IX_REG - off0;  // stream offset of region byte 0
-    // ---- hop loop: follow up to 64 headers inside this region (uniform, scalar). The 64 lanes
-    // first decode a header at each of the 64 stream positions from the current one (one-byte
-    // form: next header and output count); the chain then takes two v_readlane and a few SALU
-    // ops per hop until it leaves those 64 bytes. Other header forms take run_parse.
+    // ---- hop loop: follow up to 64 headers inside this region (uniform, scalar). Sparse headers
+    // (bit widths > 2) take one LDS read per hop. Dense ones: the 64 lanes first decode a header
+    // at each of the 64 stream positions from the current one (one-byte form: next header and
+    // output count); the chain then takes two v_readlane and a few SALU ops per hop until it
+    // leaves those 64 bytes. Other header forms take run_parse.
     uint32_t posv = 0, k = 0;
     uint32_t acc = produced;  // < n before each add, so acc + min(cnt, n) < 2^32
-    bool stop = false;
-    while (k < 64 && !stop && acc < n) {
-      if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
-      // candidate headers at cur + lane (one-byte form); ~0u marks any other form
-      const uint32_t wbase = cur;
-      uint32_t nxv, cnv;
-      {
-        const uint32_t q = cur + lane;
-        const uint32_t rel = q - rbase;
-        const uint32_t b0 = (q < slen && rel < (uint32_t)(IX_REG + 60)) ? lbyte(sm.region, rel) : 0x80u;
-        const uint32_t half = b0 >> 1;
-        const bool fast = !(b0 & 0x80u) && vb <= 3u;
-        nxv = !fast ? 0xFFFFFFFFu : ((b0 & 1u) ? q + 1u + half * w : q + 1u + vb);
-        cnv = (b0 & 1u) ? half << 3 : half;
+    if (w > 2u) {  // sparse headers (runs of >= 64 bytes): one LDS read per hop
+      while (k < 64) {
+        if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
+        const uint32_t rel = cur - rbase;
+        const uint32_t wi = rel >> 2;
+        const uint32_t x = rfl(__builtin_amdgcn_alignbyte(sm.region[wi + 1], sm.region[wi], rel & 3u));
+        const uint32_t b0 = x & 0xFFu;
+        uint32_t cnt, nxt;
+        bool stop = false;
+        if (!(b0 & 0x80u) && vb <= 3u) {
+          const uint32_t half = b0 >> 1;
+          if (b0 & 1u) {
+            cnt = half << 3;
+            nxt = cur + 1u + half * w;
+          } else {
+            cnt = half;
+            nxt = cur + 1u + vb;
+          }
+        } else {
+          uint32_t inf, flg;
+          run_parse(sm.region, rel, cur, slen, (int)w, nxt, cnt, inf, flg);
+          nxt = rfl(nxt);
+          cnt = rfl(cnt);
+          stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
+        }
+        posv = lane == k ? cur : posv;  // v_cmp + v_cndmask
+        ++k;
+        acc += cnt < n ? cnt : n;
+        cur = nxt;
+        if (stop || acc >= n) break;
       }
-      // tight chain through the candidates: all exits folded into one test; headers stay
-      // inside the region (its 64-byte overlap only serves their bytes)
-      const uint32_t olim = (rbase + (uint32_t)IX_REG - wbase) < 64u ? rbase + (uint32_t)IX_REG - wbase : 64u;
-      uint32_t o = 0;
-      while (true) {
-        const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)nxv, (int)o);
-        if (nx == 0xFFFFFFFFu) break;
-        const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)cnv, (int)o);
+    } else {  // dense headers: candidate windows
+      bool stop = false;
+      while (k < 64 && !stop && acc < n) {
+        if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
+        // candidate headers at cur + lane (one-byte form); ~0u marks any other form
+        const uint32_t wbase = cur;
+        uint32_t nxv, cnv;
+        {
+          const uint32_t q = cur + lane;
+          const uint32_t rel = q - rbase;
+          const uint32_t b0 = (q < slen && rel < (uint32_t)(IX_REG + 60)) ? lbyte(sm.region, rel) : 0x80u;
+          const uint32_t half = b0 >> 1;
+          const bool fast = !(b0 & 0x80u) && vb <= 3u;
+          nxv = !fast ? 0xFFFFFFFFu : ((b0 & 1u) ? q + 1u + half * w : q + 1u + vb);
+          cnv = (b0 & 1u) ? half << 3 : half;
+        }
+        // tight chain through the candidates: all exits folded into one test; headers stay
+        // inside the region (its 64-byte overlap only serves their bytes)
+        const uint32_t olim = (rbase + (uint32_t)IX_REG - wbase) < 64u ? rbase + (uint32_t)IX_REG - wbase : 64u;
+        uint32_t o = 0;
+        while (true) {
+          const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)nxv, (int)o);
+          if (nx == 0xFFFFFFFFu) break;
+          const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)cnv, (int)o);
+          posv = lane == k ? cur : posv;
+          ++k;
+          acc += cn < n ? cn : n;
+          cur = nx;
+          o = cur - wbase;
+          if ((o >= olim) | (k >= 64u) | (acc >= n)) break;
+        }
+        if (k >= 64u || acc >= n || o >= olim) continue;  // batch full / done / window left
+        // header at cur in another form
+        if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
+        uint32_t nxt, cnt, inf, flg;
+        run_parse(sm.region, cur - rbase, cur, slen, (int)w, nxt, cnt, inf, flg);
+        nxt = rfl(nxt);
+        cnt = rfl(cnt);
+        stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
         posv = lane == k ? cur : posv;
         ++k;
-        acc += cn < n ? cn : n;
-        cur = nx;
-        o = cur - wbase;
-        if ((o >= olim) | (k >= 64u) | (acc >= n)) break;
+        acc += cnt < n ? cnt : n;
+        cur = nxt;
       }
-      if (k >= 64u || acc >= n || o >= olim) continue;  // batch full / done / window left
-      // header at cur in another form
-      if (cur >= slen || cur - rbase >= (uint32_t)IX_REG) break;
-      uint32_t nxt, cnt, inf, flg;
-      run_parse(sm.region, cur - rbase, cur, slen, (int)w, nxt, cnt, inf, flg);
-      nxt = rfl(nxt);
-      cnt = rfl(cnt);
-      stop = (rfl(flg) & (RF_EOF | RF_PANIC)) != 0;  // the batch reports it
-      posv = lane == k ? cur : posv;
-      ++k;
-      acc += cnt < n ? cnt : n;
-      cur = nxt;
     }
     stamp(t_hop);
     if (k == 0) continue;  // region boundary: reload

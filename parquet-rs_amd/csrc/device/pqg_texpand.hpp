@@ -250,58 +250,27 @@ __device__ inline void tx_rewalk(const uint8_t* __restrict__ blob, uint64_t blob
   __syncthreads();
 }
 
-// Persistent tile loop: workgroup b expands tiles b, b + grid, b + 2 grid, ... The loads of
-// the next tile (descriptor, then its records and payload into registers) are issued before
-// the current tile is expanded, so their latency hides behind its gathers and stores.
-// M::make(d) builds the tile's emitter, M::done(d, t, em) runs after it (per-wave counts).
+// One tile per workgroup (grid = ntiles): no state carried between tiles, so the fewest live
+// registers; the hardware overlaps tiles across workgroups instead.
 template <class M>
-__device__ inline void tile_loop(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                 const QDesc* __restrict__ desc, uint32_t ntiles,
-                                 const uint2* __restrict__ runs, TileSmem& sm, M& mk) {
-  uint32_t t = blockIdx.x;
+__device__ inline void tile_one(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                const QDesc* __restrict__ desc, uint32_t ntiles,
+                                const uint2* __restrict__ runs, TileSmem& sm, M& mk) {
+  const uint32_t t = blockIdx.x;
   if (t >= ntiles) return;
-  const uint32_t G = gridDim.x;
-  const uint32_t lane = threadIdx.x & 63;
-  // Descriptors travel as one dword per lane (lanes 0-15, one VGPR) two tiles ahead and are
-  // made uniform (v_readlane) when their tile's loads are issued, one tile ahead.
-  auto fetch = [&](uint32_t tt) -> uint32_t {
-    return (tt < ntiles && lane < 16) ? reinterpret_cast<const uint32_t*>(desc + tt)[lane] : 0u;
-  };
-  auto uniform = [&](uint32_t x) {
-    QDesc q;
-    uint32_t* o = reinterpret_cast<uint32_t*>(&q);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) o[k] = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
-    return q;
-  };
-  QDesc d = uniform(fetch(t));
-  uint32_t xn = fetch(t + G);
-  TileLoad f;
-  tx_issue(blob, blob_len, d, runs, f);
-  while (true) {
-    const bool single = d.qhi && d.rec != RUN_REWALK;
-    const uint32_t sb32 = (uint32_t)(f.A0 - d.S), staged = f.nchunks * 16u;
-    if (single) tx_install(d, f, sm);
+  const QDesc d = desc[t];
+  auto em = mk.make(d);
+  if (d.qhi && d.rec != RUN_REWALK) {
+    TileLoad f;
+    tx_issue(blob, blob_len, d, runs, f);
+    tx_install(d, f, sm);
     __syncthreads();
-    const uint32_t tn = t + G;
-    QDesc dn;
-    if (tn < ntiles) {
-      dn = uniform(xn);
-      xn = fetch(tn + G);
-      tx_issue(blob, blob_len, dn, runs, f);
-    }
-    auto em = mk.make(d);
-    if (single)
-      tx_range(sm, tx_nrec(d), d.qlo, d.qlo, d.qhi, d.w, sb32, staged, tx_wide(d), blob, blob_len,
-               d.S, em);
-    else if (d.qhi)
-      tx_rewalk(blob, blob_len, d, sm, em);
-    mk.done(d, t, em);
-    if (tn >= ntiles) break;
-    __syncthreads();
-    d = dn;
-    t = tn;
+    tx_range(sm, tx_nrec(d), d.qlo, d.qlo, d.qhi, d.w, (uint32_t)(f.A0 - d.S), f.nchunks * 16u,
+             tx_wide(d), blob, blob_len, d.S, em);
+  } else if (d.qhi) {
+    tx_rewalk(blob, blob_len, d, sm, em);
   }
+  mk.done(d, t, em);
 }
 
 // ------------------------------------------------------------------------------ emitters
