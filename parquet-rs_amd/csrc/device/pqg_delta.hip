@@ -56,6 +56,9 @@ extern "C" hipError_t pqg_launch_delta(const uint8_t* blob, uint64_t blob_len, P
 
 namespace pqg {
 
+// DeltaPage::tiled values set by k_delta_page (0 / 1 are the tiled path's own)
+constexpr uint32_t DP_DONE = 2u, DP_FALLBACK = 3u;
+
 __device__ inline uint32_t rfl32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
 // zigzag/ULEB128 from a wave-uniform 16-byte window (lo, hi): returns bytes used, 0 when the
@@ -81,6 +84,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   const uint32_t lane = threadIdx.x & 63;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (dt.page[p].tiled == DP_DONE) return;  // decoded by k_delta_page
   DeltaPage info{0, 0, 0, 0, 0};
   if (pw.status != 0) {
     if (lane == 0) dt.page[p] = info;
@@ -292,7 +296,7 @@ __device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __re
   if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) return false;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return false;
   info = dt.page[p];
-  if (!info.tiled) return false;
+  if (info.tiled != 1u) return false;
   const uint32_t n = (uint32_t)pw.nonnull;
   const uint32_t k = t - pw.ltile0;
   lo = k * DELTA_TILE;
@@ -424,11 +428,10 @@ __device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __re
 
 // Tile sums: wrapping sum of min_delta + delta over each tile's deltas -> dt.agg[t].
 template <int ES>
-__global__ void __launch_bounds__(WG) k_delta_sums(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                   PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                   uint32_t ntiles, DeltaTables dt) {
-  __shared__ DeltaExpandSmem sm;
-  const uint32_t t = blockIdx.x;
+__device__ inline void delta_sums_tile(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
+                                       uint64_t blob_len, PageWork* pages,
+                                       const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                       const DeltaTables& dt, uint32_t t) {
   int p;
   DeltaPage info;
   uint32_t lo, hi;
@@ -437,6 +440,20 @@ __global__ void __launch_bounds__(WG) k_delta_sums(const uint8_t* __restrict__ b
     return;
   const uint64_t T = block_sum_u64(s, sm.wsum);
   if (threadIdx.x == 0) dt.agg[t] = T;
+}
+
+// Grid-stride over the tiles (the pages k_delta_page decoded are skipped inside; with none left
+// for this path the kernel exits at once).
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_sums(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                   uint32_t ntiles, DeltaTables dt) {
+  __shared__ DeltaExpandSmem sm;
+  if (*dt.nfall == 0) return;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    delta_sums_tile<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t);
+    __syncthreads();
+  }
 }
 
 // Running value at each tile start: dt.inc[t] = first + the page's earlier tile sums (one
@@ -449,7 +466,7 @@ __global__ void __launch_bounds__(WG) k_delta_tscan(const PageWork* pages, Delta
   if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   const DeltaPage info = dt.page[p];
-  if (!info.tiled) return;
+  if (info.tiled != 1u) return;
   const uint32_t n = (uint32_t)pw.nonnull;
   const uint32_t nt = (n + DELTA_TILE - 1) / DELTA_TILE;
   if (threadIdx.x == 0) carry = info.first;
@@ -479,13 +496,11 @@ __global__ void __launch_bounds__(WG) k_delta_tscan(const PageWork* pages, Delta
 // threads [128h, 128h + 128) hold tile values [2048h, 2048h + 2048) and the half leaves as
 // 16-byte chunks, chunk c by thread c % 256.
 template <int ES>
-__global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                     uint32_t ntiles, DeltaTables dt,
-                                                     uint8_t* __restrict__ out) {
-  __shared__ DeltaExpandSmem sm;
+__device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
+                                         uint64_t blob_len, PageWork* pages,
+                                         const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                         const DeltaTables& dt, uint8_t* __restrict__ out, uint32_t t) {
   const int tid = threadIdx.x;
-  const uint32_t t = blockIdx.x;
   int p;
   DeltaPage info;
   uint32_t lo, hi;
@@ -556,6 +571,326 @@ __global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__
   }
 }
 
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                     uint32_t ntiles, DeltaTables dt,
+                                                     uint8_t* __restrict__ out) {
+  __shared__ DeltaExpandSmem sm;
+  if (*dt.nfall == 0) return;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    delta_expand_tile<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, out, t);
+    __syncthreads();
+  }
+}
+
+// ============================================================================ page pass
+//
+// k_delta_page: one 256-thread workgroup per page decodes the page's whole value stream tile by
+// tile, carrying the running value in registers, so no index pass, tile sums, tile scan or
+// cross-workgroup wait is needed. Tiles are 4096 deltas (value i = first + sum of deltas d < i,
+// decoding.rs:560-566; the tile of deltas [D0, D1) yields values [D0 + 1, D1 + 1)), and blocks
+// must divide the tile, so a block never spans two tiles. Per tile: wave 0 follows the block
+// header chain (one 8-byte LDS read per block for the varint length, one for the widths) and
+// then parses each block's header on its own lane (the checks of k_delta_index); every thread
+// unpacks 16 deltas of one mini-block (hoisted parameters, 32-bit bit offsets, one funnel shift
+// per delta), the workgroup scans, adds the carry and stores through an LDS transpose (quarters
+// of 1024 values). The next tile's bytes are loaded into registers while the current tile is
+// expanded. Anything else (an error the reference reports, a header or payload outside the
+// staged window, more than 8 mini-blocks, mini-blocks of a size not a multiple of 16, blocks
+// not dividing 4096) marks the page DP_FALLBACK for the tiled path, which reports errors exactly.
+constexpr int DPG_STAGE = 12288;
+constexpr int DPG_CH = DPG_STAGE / 16 / WG;  // 16-byte loads per thread per tile
+constexpr uint32_t DPG_T = 4096;             // deltas per tile
+constexpr int DPG_NB = 32;                   // blocks per tile (blocks of >= 128 values)
+
+struct DeltaPageSmem {
+  union {
+    uint32_t stage[(DPG_STAGE + 64) / 4];
+    uint4 stq[(DPG_STAGE + 64) / 16];
+  };
+  uint64_t mind[DPG_NB];
+  uint32_t pos[DPG_NB];
+  uint32_t mboff[DPG_NB][8];
+  uint32_t mbw[DPG_NB][8];
+  uint64_t wsum[WG / 64];
+  uint32_t ctl[4];  // 0: fallback, 1: header of the next tile's first block
+};
+
+template <int ES>
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG) k_delta_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, DeltaTables dt,
+                                                   uint8_t* __restrict__ out) {
+  __shared__ DeltaPageSmem sm;
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  const PageWork& pw = pages[p];
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
+  if (pw.status != 0) {
+    if (tid == 0) {
+      dt.page[p] = info;
+      atomicAdd(dt.nfall, 1u);
+    }
+    return;
+  }
+  const uint64_t S = pw.base + pw.val_off;
+  const uint32_t slen = pw.val_bytes;
+  const uint8_t* sp = blob + S;
+  uint64_t block_size, nmb, total, fz;
+  uint32_t q = 0;
+  bool bad = false;
+  int l;
+  if ((l = g_vlq(sp, q, slen, block_size)) <= 0) bad = true;
+  q += l > 0 ? l : 0;
+  if (!bad && (l = g_vlq(sp, q, slen, nmb)) <= 0) bad = true;
+  q += l > 0 ? l : 0;
+  if (!bad && (l = g_vlq(sp, q, slen, total)) <= 0) bad = true;
+  q += l > 0 ? l : 0;
+  if (!bad && (l = g_vlq(sp, q, slen, fz)) <= 0) bad = true;
+  q += l > 0 ? l : 0;
+  const uint64_t n = pw.nonnull;
+  uint64_t vpmb = 0;
+  if (!bad) {
+    if ((int64_t)nmb <= 0 || nmb > 8) bad = true;
+    else {
+      vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
+      if (vpmb % 16 != 0 || vpmb == 0 || vpmb * nmb < 128 || DPG_T % (vpmb * nmb) != 0) bad = true;
+    }
+  }
+  if (!bad && (total < n || n > 0x7FFFFFFFull || slen >= (1u << 28))) bad = true;
+  if (bad) {
+    if (tid == 0) {
+      dt.page[p] = info;
+      atomicAdd(dt.nfall, 1u);
+    }
+    return;
+  }
+  const uint32_t nmb32 = (uint32_t)nmb, vpmb32 = (uint32_t)vpmb, vpb = vpmb32 * nmb32;
+  const uint32_t nn = (uint32_t)n;
+  const uint32_t need = nn > 0 ? nn - 1 : 0u;  // deltas
+  const uint32_t wmax = ES == 4 ? 32u : 64u;
+  const uint64_t first = (uint64_t)unzigzag(fz);
+  uint8_t* const ob = out + pw.value_out * (uint64_t)ES;
+  if (tid == 0 && nn > 0) {  // value 0
+    if (ES == 8) *reinterpret_cast<uint64_t*>(ob) = first;
+    else *reinterpret_cast<uint32_t*>(ob) = (uint32_t)first;
+  }
+  uint4 pv[DPG_CH];
+  uint64_t SB = (S + q) & ~15ull;  // stage base of the current tile (absolute)
+  auto issue = [&](uint64_t base) {
+    const bool fast = base + DPG_STAGE <= blob_len;
+#pragma unroll
+    for (int c = 0; c < DPG_CH; ++c) {
+      const uint64_t a = base + (uint64_t)(tid + c * WG) * 16;
+      pv[c] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+    }
+  };
+  const uint32_t ntl = (need + DPG_T - 1) / DPG_T;
+  if (ntl) issue(SB);
+  uint32_t hdr = q;        // header of the current tile's first block (stream offset)
+  uint64_t carry = first;  // value before the tile's first delta
+  for (uint32_t k = 0; k < ntl; ++k) {
+    const uint32_t D0 = k * DPG_T;
+    const uint32_t D1 = D0 + DPG_T < need ? D0 + DPG_T : need;
+    const uint32_t nb = (D1 - D0 + vpb - 1) / vpb;  // blocks of the tile
+    // ---- install the staged bytes
+#pragma unroll
+    for (int c = 0; c < DPG_CH; ++c) sm.stq[tid + c * WG] = pv[c];
+    if (tid < 16) sm.stage[DPG_STAGE / 4 + tid] = 0;
+    __syncthreads();
+    const uint32_t sb = (uint32_t)(SB - S);  // stream offset of staged byte 0 (mod 2^32)
+    // ---- wave 0: block header chain, then one block header per lane
+    if (tid < 64) {
+      const uint32_t lane = (uint32_t)tid;
+      uint32_t hp = hdr, posv = 0;
+      bool fb = false;
+      for (uint32_t j = 0; j < nb; ++j) {
+        const uint32_t rel = hp - sb;
+        if (hp >= slen || rel + 24u > (uint32_t)DPG_STAGE) {
+          fb = true;
+          break;
+        }
+        posv = lane == j ? hp : posv;
+        const uint64_t lo8 = lload_u64(sm.stage, rel);
+        const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+        if (!t8) {
+          fb = true;
+          break;
+        }
+        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
+        const uint64_t wy = lload_u64(sm.stage, rel + vl);
+        const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
+        const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+        const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+        const uint64_t nx = (uint64_t)hp + vl + nmb32 + (uint64_t)(vpmb32 >> 3) * sumw;
+        hp = nx > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nx;
+      }
+      bool lfb = false;
+      if (!fb && lane < nb) {
+        const uint32_t pos = posv, rel = pos - sb, b = D0 / vpb + lane;
+        const uint64_t lo8 = lload_u64(sm.stage, rel), hi8 = lload_u64(sm.stage, rel + 8);
+        const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;  // t8 != 0 (chain above)
+        uint64_t y = lo8 & 0x7F7F7F7F7F7F7F7Full;
+        if (vl < 8) y &= (1ull << (8 * vl)) - 1ull;
+        y = (y & 0x007F007F007F007Full) | ((y & 0x7F007F007F007F00ull) >> 1);
+        y = (y & 0x00003FFF00003FFFull) | ((y & 0x3FFF00003FFF0000ull) >> 2);
+        const uint64_t zz = (y & 0x000000000FFFFFFFull) | ((y & 0x0FFFFFFF00000000ull) >> 4);
+        if ((uint64_t)pos + vl + nmb32 > slen) lfb = true;
+        const uint32_t payload = pos + vl + nmb32;
+        const uint32_t left = need - b * vpb;
+        const uint32_t inblk = left < vpb ? left : vpb;
+        const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
+        const uint32_t sh = vl * 8u;  // widths: bytes [vl, vl + nmb) of the 16-byte window
+        const uint64_t wv = sh < 64 ? ((lo8 >> sh) | (sh ? hi8 << (64 - sh) : 0ull)) : hi8;
+        uint32_t boff = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < 8; ++m) {
+          const uint32_t wdt = m < nmb32 ? (uint32_t)((wv >> (8 * m)) & 0xFFu) : 0u;
+          if (m < nmb32 && m < mneed &&
+              (wdt > wmax || (uint64_t)payload + boff + (vpmb32 * wdt) / 8 > slen)) lfb = true;
+          sm.mbw[lane][m] = wdt;
+          sm.mboff[lane][m] = boff;
+          boff += m < nmb32 ? (vpmb32 * wdt) / 8 : 0u;
+        }
+        sm.pos[lane] = payload;
+        sm.mind[lane] = (uint64_t)unzigzag(zz);
+      }
+      fb = fb || __ballot(lfb) != 0;
+      if (lane == 0) {
+        sm.ctl[0] = fb ? 1u : 0u;
+        sm.ctl[1] = hp;
+      }
+    }
+    __syncthreads();
+    if (sm.ctl[0]) {  // leave the page to the tiled path
+      if (tid == 0) {
+        dt.page[p] = info;
+        atomicAdd(dt.nfall, 1u);
+      }
+      return;
+    }
+    hdr = sm.ctl[1];
+    const uint64_t SBn = (S + hdr) & ~15ull;
+    if (k + 1 < ntl) issue(SBn);
+    // ---- 16 deltas of one mini-block per thread
+    const uint32_t lim = DPG_STAGE * 8u;
+    const uint32_t r0 = (uint32_t)tid * DPT;  // tile-relative first delta
+    uint64_t x[DPT];
+    uint64_t s = 0;
+    if (D0 + r0 < D1) {
+      const uint32_t bi = r0 / vpb, m = (r0 - bi * vpb) / vpmb32, kk = r0 - bi * vpb - m * vpmb32;
+      const uint32_t wdt = sm.mbw[bi][m];
+      const uint64_t mn = sm.mind[bi];
+      const uint32_t base = (sm.pos[bi] + sm.mboff[bi][m] - sb) * 8u + kk * wdt;  // bit offset in the window
+      const uint32_t cnt = D1 - D0 - r0 < (uint32_t)DPT ? D1 - D0 - r0 : (uint32_t)DPT;
+      const uint32_t wm = wdt >= 32 ? 0xFFFFFFFFu : (1u << wdt) - 1u;
+      if (wdt <= 32 && base + DPT * wdt <= lim) {
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+          const uint32_t bit = base + (uint32_t)j * wdt;
+          const uint32_t wi = bit >> 5;
+          const uint32_t r = __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
+          x[j] = (uint32_t)j < cnt ? mn + r : 0ull;
+          s += x[j];
+        }
+      } else {  // outside the window or wider than 32 bits: global reads
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+          uint64_t v = 0;
+          if ((uint32_t)j < cnt) {
+            const uint64_t gb = ((uint64_t)sm.pos[bi] + sm.mboff[bi][m]) * 8ull + (uint64_t)(kk + j) * wdt;
+            const uint64_t abs = S + (gb >> 3);
+            const uint32_t sh = (uint32_t)(gb & 7);
+            uint64_t r = gload_u64(blob, blob_len, abs) >> sh;
+            if (wdt + sh > 64) r |= gload_u64(blob, blob_len, abs + 8) << (64 - sh);
+            v = mn + (wdt >= 64 ? r : (r & ((1ull << wdt) - 1ull)));
+          }
+          x[j] = v;
+          s += v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < DPT; ++j) x[j] = 0;
+    }
+    // ---- workgroup scan; the barrier also ends every read of the stage and the tables
+    uint64_t incl = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y2 = __shfl_up(incl, off, 64);
+      if ((tid & 63) >= off) incl += y2;
+    }
+    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint64_t acc = carry + incl - s;
+    for (int wv = 0; wv < (tid >> 6); ++wv) acc += sm.wsum[wv];
+    carry += sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+    uint64_t val[DPT];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      acc += x[j];
+      val[j] = acc;
+    }
+    // ---- stores through the stage buffer: quarter qq = wave qq's values [1024 qq, + 1024)
+    const uint32_t cnt = D1 - D0;
+    uint8_t* const tb = ob + (uint64_t)(D0 + 1) * ES;
+    constexpr uint32_t CPT = DPT * ES / 16;  // 16-byte chunks per thread
+    constexpr uint32_t QV = DPG_T / 4;       // values per quarter
+    constexpr uint32_t NCH = QV * ES / 16;   // chunks per quarter
+#pragma unroll 1
+    for (int qq = 0; qq < 4; ++qq) {
+      if ((tid >> 6) == qq) {
+        const uint32_t tl = (uint32_t)tid & 63u;
+#pragma unroll
+        for (uint32_t c = 0; c < CPT; ++c) {
+          uint4 v4;
+          if (ES == 8)
+            v4 = make_uint4((uint32_t)val[2 * c], (uint32_t)(val[2 * c] >> 32), (uint32_t)val[2 * c + 1],
+                            (uint32_t)(val[2 * c + 1] >> 32));
+          else
+            v4 = make_uint4((uint32_t)val[4 * c], (uint32_t)val[4 * c + 1], (uint32_t)val[4 * c + 2],
+                            (uint32_t)val[4 * c + 3]);
+          const uint32_t ci = tl * CPT + c;
+          sm.stq[ci ^ (tl & 7u)] = v4;  // xor swizzle against bank conflicts
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < (NCH + WG - 1) / WG; ++r) {
+        const uint32_t ci = (uint32_t)tid + r * WG;
+        if (ci < NCH) {
+          const uint4 v4 = sm.stq[ci ^ ((ci / CPT) & 7u)];
+          const uint32_t v0 = (uint32_t)qq * QV + ci * (16 / ES);
+          uint8_t* dst = tb + (uint64_t)v0 * ES;
+          if (v0 + 16 / ES <= cnt) {
+            *reinterpret_cast<uint4*>(dst) = v4;
+          } else if (v0 < cnt) {
+            const uint32_t qa[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (uint32_t e = 0; e < 16 / ES; ++e) {
+              if (v0 + e >= cnt) break;
+              if (ES == 8) reinterpret_cast<uint64_t*>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
+              else reinterpret_cast<uint32_t*>(dst)[e] = qa[e];
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    SB = SBn;
+  }
+  if (tid == 0) {
+    info.first = first;
+    info.vpmb = vpmb32;
+    info.nmb = nmb32;
+    info.tiled = DP_DONE;
+    dt.page[p] = info;
+  }
+}
+
 // Per-page fallback for pages the tiled path does not take (k_delta with a page filter).
 template <int ES>
 __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -578,11 +913,13 @@ template <int ES>
 static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                         uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, uint8_t* out,
                         ChunkResult* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out);
   hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
   if (ntiles) {
-    hipLaunchKernelGGL(k_delta_sums<ES>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt);
+    const dim3 tg(ntiles < 4096u ? ntiles : 4096u);  // grid-stride over the tiles
+    hipLaunchKernelGGL(k_delta_sums<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt);
     hipLaunchKernelGGL(k_delta_tscan, dim3(npages), dim3(WG), 0, s, pages, dt);
-    hipLaunchKernelGGL(k_delta_expand<ES>, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, out);
+    hipLaunchKernelGGL(k_delta_expand<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, out);
   }
   hipLaunchKernelGGL(k_delta_rest<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
 }

@@ -199,6 +199,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dt.agg);
     hipFree(sl.dt.inc);
     hipFree(sl.dt.flag);
+    hipFree(sl.dt.nfall);
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   delete ctx;
@@ -526,6 +527,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
         hipFree(sl.dt.agg);
         hipFree(sl.dt.inc);
         hipFree(sl.dt.flag);
+        hipFree(sl.dt.nfall);
         sl.dt = DeltaTables{};
         sl.dt_tcap = sl.dt_pcap = 0;
         const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
@@ -534,6 +536,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
         HIPCHK(hipMalloc(&sl.dt.agg, tc * sizeof(uint64_t)), "hipMalloc delta agg");
         HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
         HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
+        HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
         HIPCHK(hipMemsetAsync(sl.dt.flag, 0, tc * sizeof(uint32_t), s), "memset delta flags");
         sl.dt_tcap = tc;
         sl.dt_pcap = pc;
@@ -543,6 +546,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
         HIPCHK(hipMemsetAsync(sl.dt.flag, 0, sl.dt_tcap * sizeof(uint32_t), s), "memset delta flags");
         ctx->epoch = 1;
       }
+      sl.dt.dbg = (cp.debug & 32) ? cp.dbgbuf : nullptr;
+      HIPCHK(hipMemsetAsync(sl.dt.nfall, 0, sizeof(uint32_t), s), "memset delta fallback count");
       HIPCHK(pqg_launch_delta_tiled(blob, blob_len, ctx->d_pages, np, nt, sl.tile_page, sl.dt, ctx->epoch,
                                     es, vo, ctx->d_res, s), "delta");
     }

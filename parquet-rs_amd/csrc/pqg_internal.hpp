@@ -142,6 +142,8 @@ struct DeltaTables {
   uint64_t* agg;      // [tiles] tile sums (decoupled look-back)
   uint64_t* inc;      // [tiles] inclusive prefixes
   uint32_t* flag;     // [tiles] epoch * 4 + {1 aggregate, 2 inclusive}
+  uint64_t* dbg;      // diagnostics: per-page phase cycles of k_delta_page (PQG_DEBUG bit 5)
+  uint32_t* nfall;    // pages k_delta_page left to the tiled path (0: its tile kernels exit at once)
 };
 
 struct ColumnParams {
