@@ -13,7 +13,7 @@
 //
 // All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
 // (index pass + grid-wide expand pass) is in pqg_runs.hpp.
-#include "pqg_texpand.hpp"
+#include "pqg_rlepage.hpp"
 
 namespace pqg {
 
@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
                                                   int dict_page, RunTables rt, ChunkResult* res) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
+  if (*rt.nfall == 0 || rt.pflag[p]) return;  // decoded by the page pass
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   Stream s;
@@ -176,7 +177,7 @@ __global__ void __launch_bounds__(WG) k_tile_desc(const uint8_t* __restrict__ bl
                                                   uint32_t ntiles, RunTables rt, ColumnParams cp,
                                                   int sel, int dict_page) {
   const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  if (t >= ntiles) return;
+  if (t >= ntiles || *rt.nfall == 0) return;
   rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, t, 0, RUN_TILE);
 }
 
@@ -189,8 +190,9 @@ struct LevelsMaker {
   bool count;
   uint32_t* qcount;
   __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
-  __device__ void done(const QDesc&, uint32_t t, TxLevels& em) {
-    if (!count) return;
+  const uint32_t* pflag;
+  __device__ void done(const QDesc& d, uint32_t t, TxLevels& em) {
+    if (!count || (!d.qhi && pflag[d.page])) return;  // the page pass wrote these counts
     const uint32_t nn = wave_sum_u32(em.nonnull);
     if ((threadIdx.x & 63) == 0) qcount[4 * t + (threadIdx.x >> 6)] = nn;
   }
@@ -201,8 +203,10 @@ struct LevelsMaker {
                                                   uint32_t ntiles, RunTables rt, ColumnParams cp,     \
                                                   int which, int16_t* __restrict__ out) {             \
     __shared__ TileSmem sm;                                                                       \
-    LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount};  \
-    tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                   \
+    if (*rt.nfall == 0) return;                                                                   \
+    LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount,     \
+                   rt.pflag};                                                                     \
+    if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);     \
   }
 PQG_TEXPAND_LEVELS(k_texpand_levels, __attribute__((amdgpu_waves_per_eu(8, 8))))
 
@@ -236,7 +240,8 @@ struct DictMaker {
     const PageWork& dp = pages[dict_page];                                                          \
     DictMaker<ES, MODE> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
                            out, pages, res};                                                        \
-    tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);                                     \
+    if (*rt.nfall == 0) return;                                                                     \
+    if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);       \
   }
 PQG_TEXPAND_DICT(k_texpand_dict, )
 
@@ -250,9 +255,106 @@ struct BoolMaker {
 __global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                      uint32_t ntiles, RunTables rt, uint8_t* __restrict__ out) {
   __shared__ TileSmem sm;
+  if (*rt.nfall == 0) return;
   BoolMaker mk{out};
-  tile_one(blob, blob_len, rt.desc, ntiles, rt.runs, sm, mk);
+  if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);
 }
+
+// ------------------------------------------------------------------------------ page pass
+// (pqg_rlepage.hpp) One workgroup per page; pages it cannot finish are flagged for the tiled
+// path above (rt.pflag = 0, rt.nfall counts them).
+
+struct LevelsPageMaker {
+  int16_t* out;  // page output base
+  int16_t maxl;
+  bool count;
+  uint32_t* qcount;
+  uint32_t t0;   // the page's first expand tile
+  __device__ TxLevels make(uint32_t) { return TxLevels{out, maxl, count, 0u}; }
+  __device__ void done(uint32_t k, TxLevels& em) {
+    if (!count) return;
+    const uint32_t nn = wave_sum_u32(em.nonnull);
+    if ((threadIdx.x & 63) == 0) qcount[4 * (t0 + k) + (threadIdx.x >> 6)] = nn;
+  }
+};
+
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
+k_rlepage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len, const PageWork* pages,
+                 ColumnParams cp, int which, RunTables rt, int16_t* __restrict__ out) {
+  __shared__ TileSmem sm;
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  Stream s;
+  bool done = false;
+  if (get_stream(blob, pw, which, cp, s)) {
+    if (pw.status == 0) {
+      LevelsPageMaker mk{out + s.out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF,
+                         rt.qcount, pw.ltile0};
+      done = rle_page(blob, blob_len, s, sm, mk);
+    }
+    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
+  }
+  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+}
+
+template <int ES>
+struct DictPageMaker {
+  const uint8_t* dict;
+  uint32_t ndict;
+  bool aligned;
+  uint8_t* out;  // page output base
+  int32_t err;
+  __device__ TxDict<ES> make(uint32_t) { return TxDict<ES>{dict, ndict, aligned, out, 0}; }
+  __device__ void done(uint32_t, TxDict<ES>& em) { err |= em.err; }
+};
+
+template <int ES>
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
+k_rlepage_dict(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages, ColumnParams cp,
+               int dict_page, RunTables rt, uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ TileSmem sm;
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  Stream s;
+  bool done = false;
+  if (get_stream(blob, pw, SS_DICT, cp, s)) {
+    if (pw.status == 0 && dict_page >= 0 && pages[dict_page].status == 0) {
+      const PageWork& dp = pages[dict_page];
+      DictPageMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
+                           out + s.out * (uint64_t)ES, 0};
+      done = rle_page(blob, blob_len, s, sm, mk);
+      if (done && __ballot(mk.err != 0) && (threadIdx.x & 63) == 0) report(pages, res, p, ST_PANIC);
+    }
+    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
+  }
+  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+}
+
+struct BoolPageMaker {
+  uint8_t* out;
+  __device__ TxBool make(uint32_t) { return TxBool{out}; }
+  __device__ void done(uint32_t, TxBool&) {}
+};
+
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
+k_rlepage_bool(const uint8_t* __restrict__ blob, uint64_t blob_len, const PageWork* pages,
+               ColumnParams cp, RunTables rt, uint8_t* __restrict__ out) {
+  __shared__ TileSmem sm;
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  Stream s;
+  bool done = false;
+  if (get_stream(blob, pw, SS_BOOL, cp, s)) {
+    if (pw.status == 0) {
+      BoolPageMaker mk{out + s.out};
+      done = rle_page(blob, blob_len, s, sm, mk);
+    }
+    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
+  }
+  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+}
+
+static inline dim3 tx_grid(uint32_t ntiles) { return dim3(ntiles); }  // one tile per workgroup
 
 // Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
 __global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint32_t* __restrict__ qcount,
@@ -455,12 +557,14 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
                              const uint32_t* tile_page, RunTables rt, int16_t* out,
                              ChunkResult* res, hipStream_t s) {
   const int sel = which ? SS_REP : SS_DEF;
+  if (cp.debug & PQG_DBG_PAGEPASS)
+    hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
                      -1, rt, res);
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
+    hipLaunchKernelGGL(k_texpand_levels, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();
@@ -477,12 +581,19 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
                            const uint32_t* tile_page, RunTables rt, uint8_t* out, ChunkResult* res,
                            hipStream_t s) {
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
+  if (cp.debug & PQG_DBG_PAGEPASS) switch (es) {
+    case 1: hipLaunchKernelGGL((k_rlepage_dict<1>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
+    case 4: hipLaunchKernelGGL((k_rlepage_dict<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
+    case 8: hipLaunchKernelGGL((k_rlepage_dict<8>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
+    case 12: hipLaunchKernelGGL((k_rlepage_dict<12>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
+    default: return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
-  const dim3 g(ntiles);
+  const dim3 g = tx_grid(ntiles);
   switch (es) {
     case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
@@ -522,12 +633,14 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
                                int npages, uint32_t ntiles, ColumnParams cp,
                                const uint32_t* tile_page, RunTables rt, uint8_t* out,
                                ChunkResult* res, hipStream_t s) {
+  if (cp.debug & PQG_DBG_PAGEPASS)
+    hipLaunchKernelGGL(k_rlepage_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, rt, out);
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
                      -1, rt, res);
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);
-    hipLaunchKernelGGL(k_texpand_bool, dim3(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
+    hipLaunchKernelGGL(k_texpand_bool, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
   }
   return hipGetLastError();
 }

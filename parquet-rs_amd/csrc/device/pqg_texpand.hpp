@@ -250,14 +250,12 @@ __device__ inline void tx_rewalk(const uint8_t* __restrict__ blob, uint64_t blob
   __syncthreads();
 }
 
-// One tile per workgroup (grid = ntiles): no state carried between tiles, so the fewest live
+// Tile t with the whole workgroup: no state carried between tiles, so the fewest live
 // registers; the hardware overlaps tiles across workgroups instead.
 template <class M>
 __device__ inline void tile_one(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                const QDesc* __restrict__ desc, uint32_t ntiles,
+                                const QDesc* __restrict__ desc, uint32_t t,
                                 const uint2* __restrict__ runs, TileSmem& sm, M& mk) {
-  const uint32_t t = blockIdx.x;
-  if (t >= ntiles) return;
   const QDesc d = desc[t];
   auto em = mk.make(d);
   if (d.qhi && d.rec != RUN_REWALK) {

@@ -75,6 +75,7 @@ struct Slot {
   uint32_t* tile_page = nullptr;
   RunTables rt[3] = {};  // def, rep, values (index-pass outputs)
   size_t tcap = 0;
+  size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
 };
@@ -448,9 +449,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       hipFree(r.nruns);
       hipFree(r.desc);
       hipFree(r.qcount);
+      hipFree(r.pflag);
+      hipFree(r.nfall);
       r = RunTables{};
     }
     sl.tcap = 0;
+    sl.pfcap = 0;
     size_t cap = (size_t)total_tiles + 1024;
     HIPCHK(hipMalloc(&sl.tile_page, cap * sizeof(uint32_t)), "hipMalloc tile_page");
     sl.tcap = cap;
@@ -464,8 +468,20 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (e == hipSuccess) e = hipMalloc(&r.nruns, sl.tcap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&r.desc, sl.tcap * 4 * sizeof(QDesc));
     if (e == hipSuccess) e = hipMalloc(&r.qcount, sl.tcap * 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&r.nfall, sizeof(uint32_t));
     return e;
   };
+  // page-pass flags, sized by pages (all stream kinds together)
+  if ((size_t)np > sl.pfcap) {
+    const size_t pc = (size_t)np < 4096 ? 4096 : (size_t)np * 2;
+    for (RunTables& r : sl.rt) {
+      hipFree(r.pflag);
+      r.pflag = nullptr;
+    }
+    sl.pfcap = 0;
+    for (RunTables& r : sl.rt) HIPCHK(hipMalloc(&r.pflag, pc * sizeof(uint32_t)), "hipMalloc page flags");
+    sl.pfcap = pc;
+  }
   const bool hybrid_values = enc_present[PQG_RLE_DICTIONARY] || (enc_present[PQG_RLE] && t == PQG_BOOLEAN);
   if (want_def) HIPCHK(tables(0), "hipMalloc run tables");
   if (want_rep) HIPCHK(tables(1), "hipMalloc run tables");
@@ -474,6 +490,14 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
+  // page-pass flags: with the page pass every stream starts "none left over"; without it the
+  // tiled passes take every page
+  const bool pagepass = (cp.debug & PQG_DBG_PAGEPASS) != 0;
+  for (int k = 0; k < 3; ++k) {
+    if (!sl.rt[k].nfall) continue;
+    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, pagepass ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
+    if (!pagepass && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+  }
   if (np && want_def)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              out->def_levels, ctx->d_res, s), "def levels");
@@ -494,6 +518,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (enc_present[PQG_RLE_DICTIONARY]) {
       HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
                                      ctx->d_res, s), "byte-array dictionary");
+      HIPCHK(hipMemsetAsync(sl.rt[2].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+      HIPCHK(hipMemsetAsync(sl.rt[2].nfall, 0xFF, sizeof(uint32_t), s), "memset fallback count");
       HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
                                   sl.rt[2], ctx->d_res, s), "dictionary index pass");
       HIPCHK(pqg_launch_tile_desc(blob, ctx->d_pages, nt, sl.tile_page, sl.rt[2], cp, 2, dict_page, s),

@@ -113,6 +113,8 @@ struct RunTables {
   uint32_t* nruns;  // [tiles]
   QDesc* desc;      // [tiles * 4]
   uint32_t* qcount; // [tiles * 4] per quarter-tile counts (def levels == max_def; byte totals)
+  uint32_t* pflag;  // [pages] 1: stream decoded by the page pass (k_rlepage_*)
+  uint32_t* nfall;  // streams the page pass left to the tiled path (0: its kernels exit at once)
 };
 
 // DELTA_BINARY_PACKED index-pass outputs (device/pqg_delta.hip). Tiles of DELTA_TILE values
@@ -145,6 +147,11 @@ struct DeltaTables {
   uint64_t* dbg;      // diagnostics: per-page phase cycles of k_delta_page (PQG_DEBUG bit 5)
   uint32_t* nfall;    // pages k_delta_page left to the tiled path (0: its tile kernels exit at once)
 };
+
+// ColumnParams::debug bit: decode RLE/bit-packed streams with the page pass (pqg_rlepage.hpp)
+// instead of the tiled index + expand passes (PQG_DEBUG=16384). Off by default: on the benchmark
+// pages the tiled passes are as fast (dictionary) or faster (levels).
+constexpr int32_t PQG_DBG_PAGEPASS = 0x4000;
 
 struct ColumnParams {
   int32_t physical_type;
