@@ -230,6 +230,25 @@ def pcie_inclusive(pqgpu, ctx, w, stream, iters=3):
             "note": "pinned H2D of page bytes + decode + D2H of decoded levels/values, best of %d" % iters}
 
 
+def pmc_traffic(kind, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this config
+    (profiles/<round>/<config>/kernels.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 +
+    WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). None when not profiled."""
+    base = kernel.split("<")[0]
+    for rnd in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True):
+        path = os.path.join(ROOT, "profiles", rnd, kind, "kernels.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            ks = json.load(open(path))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for k, e in ks.items():
+            if k.replace("pqg::", "").split("<")[0] == base and "traffic_bytes" in e:
+                return e["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def copy_ceiling_gbs(nbytes=4 << 30):
     import torch
     a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
@@ -276,16 +295,19 @@ def main():
     value = units * world / per_step
     step_bytes = w.in_bytes + w.out_bytes
 
-    # dominant kernel roofline (HIP events around each stage on the decode stream)
+    # dominant kernel roofline: HIP events around that kernel's launch on the decode stream
+    # (pqg_timings.{levels,values}_kernel_ms), algorithmic bytes of that kernel per launch
     if kind == "levels":
-        lev_b = w.level_bytes_in + 2 * w.levels
-        val_b = 2 * w.values * w.es
-        stages = [("k_rle_levels", tm.levels_ms, lev_b), ("k_plain_copy", tm.values_ms, val_b)]
-    elif kind == "dict":
-        stages = [("k_dict_gather<8>", tm.values_ms, w.in_bytes + w.out_bytes)]
-    else:
-        stages = [("k_delta<8>", tm.values_ms, w.in_bytes + w.out_bytes)]
+        lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
+        val_b = 2 * w.values * w.es               # PLAIN values in + out
+        stages = [("k_texpand_levels", tm.levels_kernel_ms, lev_b),
+                  ("k_plain_copy", tm.values_kernel_ms, val_b)]
+    elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
+        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
+    else:                  # deltas in + values out
+        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
     name, ms, nbytes = max(stages, key=lambda s: s[1])
+    traffic, traffic_src = pmc_traffic(kind, name)
     achieved = nbytes / (ms * 1e-3) / 1e9
 
     result = {
@@ -314,10 +336,11 @@ def main():
                    "mini_blocks": args.mini_blocks if kind == "delta" else None,
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_launch": nbytes, "avg_ms": ms},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms},
         "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
-                      "values": tm.values_ms, "total": tm.total_ms},
+                      "values": tm.values_ms, "total": tm.total_ms,
+                      "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},
     }
     if rank == 0:
         try:

@@ -912,8 +912,10 @@ __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ b
 template <int ES>
 static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                         uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, uint8_t* out,
-                        ChunkResult* res, hipStream_t s) {
+                        ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
+  if (kev) hipEventRecord(kev[0], s);
   hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out);
+  if (kev) hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
   if (ntiles) {
     const dim3 tg(ntiles < 4096u ? ntiles : 4096u);  // grid-stride over the tiles
@@ -927,10 +929,10 @@ static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
 extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                                              int npages, uint32_t ntiles, const uint32_t* tile_page,
                                              DeltaTables dt, uint32_t epoch, int es, uint8_t* out,
-                                             ChunkResult* res, hipStream_t s) {
+                                             ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
   (void)epoch;  // tile prefixes come from k_delta_tscan: no cross-workgroup flags
-  if (es == 8) delta_tiled<8>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s);
-  else if (es == 4) delta_tiled<4>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s);
+  if (es == 8) delta_tiled<8>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s, kev);
+  else if (es == 4) delta_tiled<4>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s, kev);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -25,11 +25,13 @@ hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnPa
 hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
                                 RunTables, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                             const uint32_t*, RunTables, int16_t*, ChunkResult*, hipStream_t);
+                             const uint32_t*, RunTables, int16_t*, ChunkResult*, hipStream_t,
+                             hipEvent_t*);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                           int, const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t);
+                           int, const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t,
+                           hipEvent_t*);
 hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
                                  uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
@@ -40,7 +42,8 @@ hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
-                                  DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t);
+                                  DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t,
+                                  hipEvent_t*);
 hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
                                    uint32_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, bool, uint64_t*, uint32_t*,
@@ -60,7 +63,8 @@ struct Slot {
   PageWork* h_pages = nullptr;  // pinned staging
   ChunkResult* d_res = nullptr;
   ChunkResult* h_res = nullptr;  // pinned
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the levels / values kernel
+  bool kl = false, kv = false;  // events 6-7 / 8-9 recorded by the last decode
   bool used = false;
   // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix;
   // per dictionary entry source address and length
@@ -92,7 +96,7 @@ struct pqg_ctx {
   hipStream_t stream = nullptr;
   bool timing = false;
   bool pending = false;
-  double acc_ms[5] = {};
+  double acc_ms[7] = {};
   uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
   uint64_t* dbgbuf = nullptr;  // diagnostics (PQG_DEBUG bit 4)
   size_t dbg_cap = 0;
@@ -105,6 +109,19 @@ struct pqg_ctx {
   uint64_t total_levels = 0;
   std::string msg;
 };
+
+// Adds the stage and kernel times of a finished decode to the accumulators.
+static void harvest_times(double* acc, const hipEvent_t* ev, bool kl, bool kv) {
+  float ms[7] = {};
+  hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+  hipEventElapsedTime(&ms[1], ev[1], ev[2]);
+  hipEventElapsedTime(&ms[2], ev[2], ev[3]);
+  hipEventElapsedTime(&ms[3], ev[3], ev[4]);
+  hipEventElapsedTime(&ms[4], ev[0], ev[5]);
+  if (kl) hipEventElapsedTime(&ms[5], ev[6], ev[7]);
+  if (kv) hipEventElapsedTime(&ms[6], ev[8], ev[9]);
+  for (int k = 0; k < 7; ++k) acc[k] += ms[k];
+}
 
 static int set_err(pqg_ctx* c, int st, const char* fmt, ...) {
   char buf[512];
@@ -307,13 +324,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (sl.used) {
     HIPCHK(hipEventSynchronize(sl.ev[5]), "slot wait");
     if (ctx->timing) {
-      float ms[5];
-      hipEventElapsedTime(&ms[0], sl.ev[0], sl.ev[1]);
-      hipEventElapsedTime(&ms[1], sl.ev[1], sl.ev[2]);
-      hipEventElapsedTime(&ms[2], sl.ev[2], sl.ev[3]);
-      hipEventElapsedTime(&ms[3], sl.ev[3], sl.ev[4]);
-      hipEventElapsedTime(&ms[4], sl.ev[0], sl.ev[5]);
-      for (int k = 0; k < 5; ++k) ctx->acc_ms[k] += ms[k];
+      harvest_times(ctx->acc_ms, sl.ev, sl.kl, sl.kv);
       ctx->acc_n++;
     }
     sl.used = false;
@@ -333,6 +344,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   ctx->d_res = sl.d_res;
   ctx->h_res = sl.h_res;
   ctx->ev = sl.ev;
+  sl.kl = sl.kv = false;
   int bad = -1, dict_page = -1;
   std::string why;
   int vst = validate_pages(col, pages, npages, &bad, &dict_page, why);
@@ -500,10 +512,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   }
   if (np && want_def)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
-                             out->def_levels, ctx->d_res, s), "def levels");
+                             out->def_levels, ctx->d_res, s, ctx->timing ? &sl.ev[6] : nullptr),
+           "def levels");
+  if (np && want_def) sl.kl = nt > 0 || (cp.debug & PQG_DBG_PAGEPASS);
   if (np && want_rep)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
-                             out->rep_levels, ctx->d_res, s), "rep levels");
+                             out->rep_levels, ctx->d_res, s, nullptr), "rep levels");
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
   HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
@@ -538,12 +552,18 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       if (t == PQG_BOOLEAN)
         HIPCHK(pqg_launch_plain_bool(blob, ctx->d_pages, np, max_page_vals, vo, ctx->d_res, s), "plain bool");
       else if (es > 0)
+      {
+        if (ctx->timing) hipEventRecord(sl.ev[8], s);
         HIPCHK(pqg_launch_plain_copy(blob, blob_len, ctx->d_pages, np, es, PQG_PLAIN, max_page_bytes, vo, ctx->d_res, s), "plain");
+        if (ctx->timing) hipEventRecord(sl.ev[9], s);
+        sl.kv = true;
+      }
     }
     if (enc_present[PQG_RLE_DICTIONARY]) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
       HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
-                             sl.rt[2], vo, ctx->d_res, s), "dict");
+                             sl.rt[2], vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "dict");
+      sl.kv = nt > 0;
     }
     if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
@@ -575,7 +595,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       sl.dt.dbg = (cp.debug & 32) ? cp.dbgbuf : nullptr;
       HIPCHK(hipMemsetAsync(sl.dt.nfall, 0, sizeof(uint32_t), s), "memset delta fallback count");
       HIPCHK(pqg_launch_delta_tiled(blob, blob_len, ctx->d_pages, np, nt, sl.tile_page, sl.dt, ctx->epoch,
-                                    es, vo, ctx->d_res, s), "delta");
+                                    es, vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "delta");
+      sl.kv = true;
     }
     if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
       ctx->values_kernel = PQG_RLE;
@@ -599,13 +620,8 @@ int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
   hipError_t e = hipEventSynchronize(ctx->ev[5]);
   ctx->pending = false;
   if (ctx->timing && e == hipSuccess) {
-    float ms[5];
-    hipEventElapsedTime(&ms[0], ctx->ev[0], ctx->ev[1]);
-    hipEventElapsedTime(&ms[1], ctx->ev[1], ctx->ev[2]);
-    hipEventElapsedTime(&ms[2], ctx->ev[2], ctx->ev[3]);
-    hipEventElapsedTime(&ms[3], ctx->ev[3], ctx->ev[4]);
-    hipEventElapsedTime(&ms[4], ctx->ev[0], ctx->ev[5]);
-    for (int k = 0; k < 5; ++k) ctx->acc_ms[k] += ms[k];
+    const Slot& cs = ctx->slot[ctx->cur];
+    harvest_times(ctx->acc_ms, ctx->ev, cs.kl, cs.kv);
     ctx->acc_n++;
     ctx->slot[ctx->cur].used = false;  // harvested
   }
@@ -644,6 +660,8 @@ int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
   t->scan_ms = (float)(ctx->acc_ms[2] / n);
   t->values_ms = (float)(ctx->acc_ms[3] / n);
   t->total_ms = (float)(ctx->acc_ms[4] / n);
+  t->levels_kernel_ms = (float)(ctx->acc_ms[5] / n);
+  t->values_kernel_ms = (float)(ctx->acc_ms[6] / n);
   t->values_kernel = ctx->values_kernel;
   return PQG_OK;
 }

@@ -53,7 +53,8 @@ class Output(C.Structure):
 
 class Timings(C.Structure):
     _fields_ = [("prepare_ms", C.c_float), ("levels_ms", C.c_float), ("scan_ms", C.c_float),
-                ("values_ms", C.c_float), ("total_ms", C.c_float), ("values_kernel", C.c_uint32)]
+                ("values_ms", C.c_float), ("total_ms", C.c_float), ("values_kernel", C.c_uint32),
+                ("levels_kernel_ms", C.c_float), ("values_kernel_ms", C.c_float)]
 
 
 class WorkloadInfo(C.Structure):
