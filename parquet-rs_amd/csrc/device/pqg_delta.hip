@@ -913,9 +913,9 @@ template <int ES>
 static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                         uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, uint8_t* out,
                         ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
-  if (kev) hipEventRecord(kev[0], s);
+  if (kev) (void)hipEventRecord(kev[0], s);
   hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out);
-  if (kev) hipEventRecord(kev[1], s);
+  if (kev) (void)hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
   if (ntiles) {
     const dim3 tg(ntiles < 4096u ? ntiles : 4096u);  // grid-stride over the tiles

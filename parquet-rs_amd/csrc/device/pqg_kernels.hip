@@ -559,18 +559,18 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   const bool pp = (cp.debug & PQG_DBG_PAGEPASS) != 0;  // kev brackets the dominant kernel
   const int sel = which ? SS_REP : SS_DEF;
   if (pp) {
-    if (kev) hipEventRecord(kev[0], s);
+    if (kev) (void)hipEventRecord(kev[0], s);
     hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
-    if (kev) hipEventRecord(kev[1], s);
+    if (kev) (void)hipEventRecord(kev[1], s);
   }
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
                      -1, rt, res);
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    if (kev && !pp) hipEventRecord(kev[0], s);
+    if (kev && !pp) (void)hipEventRecord(kev[0], s);
     hipLaunchKernelGGL(k_texpand_levels, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
-    if (kev && !pp) hipEventRecord(kev[1], s);
+    if (kev && !pp) (void)hipEventRecord(kev[1], s);
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();
@@ -588,7 +588,7 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
                            hipStream_t s, hipEvent_t* kev) {
   const bool pp = (cp.debug & PQG_DBG_PAGEPASS) != 0;  // kev brackets the dominant kernel
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
-  if (kev && pp) hipEventRecord(kev[0], s);
+  if (kev && pp) (void)hipEventRecord(kev[0], s);
   if (pp) switch (es) {
     case 1: hipLaunchKernelGGL((k_rlepage_dict<1>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
     case 4: hipLaunchKernelGGL((k_rlepage_dict<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
@@ -596,14 +596,14 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
     case 12: hipLaunchKernelGGL((k_rlepage_dict<12>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
     default: return hipErrorInvalidValue;
   }
-  if (kev && pp) hipEventRecord(kev[1], s);
+  if (kev && pp) (void)hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
   const dim3 g = tx_grid(ntiles);
-  if (kev && !pp) hipEventRecord(kev[0], s);
+  if (kev && !pp) (void)hipEventRecord(kev[0], s);
   switch (es) {
     case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
@@ -616,7 +616,7 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
     case 12: hipLaunchKernelGGL((k_texpand_dict<12>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
-  if (kev && !pp) hipEventRecord(kev[1], s);
+  if (kev && !pp) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();
 }
 

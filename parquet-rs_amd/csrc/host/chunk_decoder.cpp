@@ -211,6 +211,8 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
       hipFree(t.nruns);
       hipFree(t.desc);
       hipFree(t.qcount);
+      hipFree(t.pflag);
+      hipFree(t.nfall);
     }
     hipFree(sl.dt.page);
     hipFree(sl.dt.blocks);
