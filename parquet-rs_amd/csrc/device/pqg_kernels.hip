@@ -138,10 +138,11 @@ __global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
 // Index pass over stream `sel` of every page (one wave per page), pqg_runs.hpp.
 __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                   PageWork* pages, ColumnParams cp, int sel,
-                                                  int dict_page, RunTables rt, ChunkResult* res) {
+                                                  int dict_page, RunTables rt, ChunkResult* res,
+                                                  int bailed_only = 0) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
-  if (*rt.nfall == 0 || rt.pflag[p]) return;  // decoded by the page pass
+  if (bailed_only ? rt.pflag[p] != PF_BAIL : (*rt.nfall == 0 || rt.pflag[p] == PF_PAGE)) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   Stream s;
@@ -159,6 +160,30 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
   if (st && threadIdx.x == 0) report(pages, res, p, st);
 }
 
+
+// Index pass of dense level / boolean streams: run_index_par with a 256-thread workgroup per
+// page; the streams it hands back are flagged PF_BAIL for k_run_index(bailed_only).
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2, 2))) k_run_index_par(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                      PageWork* pages, ColumnParams cp, int sel,
+                                                      RunTables rt, ChunkResult* res) {
+  __shared__ ParIndexSmem sm;
+  const int p = blockIdx.x;
+  if (*rt.nfall == 0 || rt.pflag[p] == PF_PAGE) return;  // decoded by the page pass
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  Stream s;
+  if (!get_stream(blob, pw, sel, cp, s)) return;
+  RunCkpt* ck = rt.ck + pw.ltile0;
+  uint2* runs = rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT;
+  uint32_t* nr = rt.nruns + pw.ltile0;
+  const int32_t st = run_index_par(blob, blob_len, s, ck, runs, nr, sm,
+                                   (cp.debug & 32) && cp.dbgbuf ? cp.dbgbuf + 2 * p : nullptr);
+  if (st == PR_BAIL) {  // k_run_index (bailed_only) walks it
+    if (threadIdx.x == 0) rt.pflag[p] = PF_BAIL;
+    return;
+  }
+  if (st && threadIdx.x == 0) report(pages, res, p, st);
+}
 
 // Quarter-tile descriptors of stream `sel` (one thread per quarter), read by the wave expand
 // kernels.
@@ -192,7 +217,7 @@ struct LevelsMaker {
   __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
   const uint32_t* pflag;
   __device__ void done(const QDesc& d, uint32_t t, TxLevels& em) {
-    if (!count || (!d.qhi && pflag[d.page])) return;  // the page pass wrote these counts
+    if (!count || (!d.qhi && pflag[d.page] == PF_PAGE)) return;  // the page pass wrote these counts
     const uint32_t nn = wave_sum_u32(em.nonnull);
     if ((threadIdx.x & 63) == 0) qcount[4 * t + (threadIdx.x >> 6)] = nn;
   }
@@ -294,7 +319,7 @@ k_rlepage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len, const Page
     }
     if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
   }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
 }
 
 template <int ES>
@@ -327,7 +352,7 @@ k_rlepage_dict(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pa
     }
     if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
   }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
 }
 
 struct BoolPageMaker {
@@ -351,7 +376,7 @@ k_rlepage_bool(const uint8_t* __restrict__ blob, uint64_t blob_len, const PageWo
     }
     if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
   }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? 1u : 0u;
+  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
 }
 
 static inline dim3 tx_grid(uint32_t ntiles) { return dim3(ntiles); }  // one tile per workgroup
@@ -563,8 +588,13 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
     hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
     if (kev) (void)hipEventRecord(kev[1], s);
   }
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
-                     -1, rt, res);
+  if (cp.debug & PQG_DBG_SERIAL_INDEX)
+    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
+                       -1, rt, res);
+  else {
+    hipLaunchKernelGGL(k_run_index_par, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, res);
+    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel, -1, rt, res, 1);
+  }
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
@@ -646,8 +676,15 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
                                ChunkResult* res, hipStream_t s) {
   if (cp.debug & PQG_DBG_PAGEPASS)
     hipLaunchKernelGGL(k_rlepage_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, rt, out);
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
-                     -1, rt, res);
+  if (cp.debug & PQG_DBG_SERIAL_INDEX)
+    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
+                       -1, rt, res);
+  else {
+    hipLaunchKernelGGL(k_run_index_par, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp,
+                       (int)SS_BOOL, rt, res);
+    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
+                       -1, rt, res, 1);
+  }
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);

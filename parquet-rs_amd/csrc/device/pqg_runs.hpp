@@ -269,6 +269,91 @@ __device__ inline void ix_install(uint32_t* region, uint32_t lane, const uint4 (
 
 __device__ inline uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
+// One batch of k <= 64 consecutive headers of the chain (lane l: header at stream offset posv,
+// staged at region index posv - rbase): parse, prefix-sum output counts, make every check the
+// reference makes while reading them and write the run records, tile checkpoints and per-tile
+// run counts. Headers whose first output is at or past n are not read by the reference and are
+// ignored. Returns a status (0: fine); cy carries the position in the output across batches.
+struct IxCarry {
+  uint32_t produced;    // outputs before the next batch's first header
+  uint32_t carry_tile;  // tile of output `produced`
+  uint32_t carry_j;     // records already written for carry_tile
+};
+
+__device__ inline int32_t ix_batch(const uint32_t* region, uint32_t rbase, uint32_t posv, uint32_t k,
+                                   uint32_t slen, uint32_t n, uint32_t w, RunCkpt* __restrict__ ck,
+                                   uint2* __restrict__ runs, uint32_t* __restrict__ nruns, IxCarry& cy) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_below = (1ull << lane) - 1ull;
+  const uint32_t produced = cy.produced, carry_tile = cy.carry_tile, carry_j = cy.carry_j;
+  const bool in0 = lane < k;
+  uint32_t nx, cnt = 0, inf = 0, flg = 0;
+  if (in0) run_parse(region, posv - rbase, posv, slen, (int)w, nx, cnt, inf, flg);
+  // exclusive scan of counts
+  uint64_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint64_t before = (uint64_t)produced + incl - cnt;
+  const bool in = in0 && before < n;
+  const uint32_t need = before >= n ? 0u : (uint32_t)((uint64_t)cnt < n - before ? cnt : n - before);
+  const bool bp = (flg & RF_BP) != 0;
+  int32_t e = 0;
+  if (in) {
+    if (flg & (RF_EOF | RF_PANIC)) e = (flg & RF_PANIC) ? ST_PANIC : ST_EOF;
+    else if (need && bp && w > 32) e = ST_PANIC;  // BitReader::get_batch asserts num_bits <= 32
+    else if (need && bp && (uint64_t)inf * 8ull + (uint64_t)need * w > (uint64_t)slen * 8ull)
+      e = ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
+  }
+  const uint64_t emask = __ballot(e != 0);
+  if (emask) return __shfl(e, __builtin_ctzll(emask), 64);
+  // records: lanes whose run yields outputs
+  const bool valid = in && need > 0;
+  const uint64_t V = __ballot(valid);
+  const uint32_t tile = (uint32_t)(before / RUN_TILE);
+  const uint32_t end_level = (uint32_t)before + need;          // one past the run's last output
+  const uint32_t end_tile = (end_level - 1u) / RUN_TILE;        // tile of its last output
+  // previous valid lane (its tile decides whether this lane starts a tile group)
+  const uint64_t vb_below = V & lanes_below;
+  const int prev = vb_below ? 63 - __builtin_clzll(vb_below) : -1;
+  const uint32_t prev_tile = __shfl(tile, prev < 0 ? 0 : prev, 64);
+  const bool head = valid && (prev < 0 || prev_tile != tile);
+  const uint64_t H = __ballot(head);
+  const uint64_t hb = H & (lanes_below | (1ull << lane));
+  const int hl = hb ? 63 - __builtin_clzll(hb) : 0;             // head lane of this lane's group
+  const uint32_t rank = (uint32_t)__builtin_popcountll(V & lanes_below & ~((1ull << hl) - 1ull));
+  const uint32_t head_before = __shfl((uint32_t)before, hl, 64);
+  const uint32_t base = tile == carry_tile ? carry_j : (head_before > tile * RUN_TILE ? 1u : 0u);
+  const uint32_t j = base + rank;
+  const uint32_t info = bp ? inf : (R_RLE | (inf > 0x7FFFFFFFu ? 0x7FFFFFFFu : inf));
+  if (valid) {
+    if (j == 0) ck[tile] = RunCkpt{posv, (uint32_t)before};
+    if (j < RUN_CAPT) runs[(uint64_t)tile * RUN_CAPT + j] = make_uint2((uint32_t)before, info);
+    const bool done_tile = end_tile > tile || end_level == (tile + 1) * RUN_TILE || end_level >= n;
+    if (done_tile) nruns[tile] = j + 1;
+    for (uint32_t t = tile + 1; t <= end_tile; ++t) {  // the run continues into later tiles
+      ck[t] = RunCkpt{posv, (uint32_t)before};
+      runs[(uint64_t)t * RUN_CAPT] = make_uint2((uint32_t)before, info);
+      if (t < end_tile || end_level == (t + 1) * RUN_TILE || end_level >= n) nruns[t] = 1;
+    }
+  }
+  // carry to the next batch (from the last valid lane)
+  if (V) {
+    const int L = 63 - __builtin_clzll(V);
+    const uint32_t lt = rfl(__shfl(tile, L, 64));
+    const uint32_t lj = rfl(__shfl(j, L, 64));
+    const uint32_t le = rfl(__shfl(end_level, L, 64));
+    const uint32_t let = rfl(__shfl(end_tile, L, 64));
+    const uint32_t nt = le / RUN_TILE;
+    cy.produced = le;
+    cy.carry_tile = nt;
+    cy.carry_j = (let == nt) ? (lt == nt ? lj + 1 : 1u) : 0u;
+  }
+  return 0;
+}
+
 // Walks stream s of one page with one wave and writes, per expand tile k of the stream:
 // ck[k] = header of the run holding the tile's first output; runs[k*RUN_CAPT + j] = the tile's
 // runs (page-relative first output, RLE value | payload offset); nruns[k] = their count
@@ -313,13 +398,11 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
   const uint32_t off0 = (uint32_t)(S - G);  // stream byte 0 in grid coordinates
   const uint32_t vb = (w + 7u) >> 3;
   const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
-  const uint64_t lanes_below = (1ull << lane) - 1ull;
   uint4 pf[IX_PF];
   uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
   uint32_t cur = 0;            // next header
-  uint32_t produced = 0;       // outputs before `cur`'s run
-  uint32_t carry_tile = 0;     // tile of output `produced`
-  uint32_t carry_j = 0;        // records already written for carry_tile
+  IxCarry cy{0u, 0u, 0u};
+  const uint32_t& produced = cy.produced;
   while (true) {
     if (cur >= slen) return ST_EOF;  // reload() finds no more data: the reference stalls (A.4)
     const uint32_t r = (off0 + cur) / IX_REG;
@@ -423,74 +506,302 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
     stamp(t_hop);
     if (k == 0) continue;  // region boundary: reload
     // ---- batch: lane l re-parses header l
-    const bool in = lane < k;
-    uint32_t nx, cnt = 0, inf = 0, flg = 0;
-    if (in) run_parse(sm.region, posv - rbase, posv, slen, (int)w, nx, cnt, inf, flg);
-    // exclusive scan of counts
-    uint64_t incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t y = __shfl_up(incl, d, 64);
-      if (lane >= (uint32_t)d) incl += y;
-    }
-    const uint64_t before = (uint64_t)produced + incl - cnt;
-    const uint32_t need = before >= n ? 0u : (uint32_t)((uint64_t)cnt < n - before ? cnt : n - before);
-    const bool bp = (flg & RF_BP) != 0;
-    int32_t e = 0;
-    if (in) {
-      if (flg & (RF_EOF | RF_PANIC)) e = (flg & RF_PANIC) ? ST_PANIC : ST_EOF;
-      else if (need && bp && w > 32) e = ST_PANIC;  // BitReader::get_batch asserts num_bits <= 32
-      else if (need && bp && (uint64_t)inf * 8ull + (uint64_t)need * w > (uint64_t)slen * 8ull)
-        e = ST_EOF;  // truncated bit-packed run: the reference spins (A.4)
-    }
-    const uint64_t emask = __ballot(e != 0);
-    if (emask) return __shfl(e, __builtin_ctzll(emask), 64);
-    // records: lanes whose run yields outputs
-    const bool valid = in && need > 0;
-    const uint64_t V = __ballot(valid);
-    const uint32_t tile = (uint32_t)(before / RUN_TILE);
-    const uint32_t end_level = (uint32_t)before + need;          // one past the run's last output
-    const uint32_t end_tile = (end_level - 1u) / RUN_TILE;        // tile of its last output
-    // previous valid lane (its tile decides whether this lane starts a tile group)
-    const uint64_t vb_below = V & lanes_below;
-    const int prev = vb_below ? 63 - __builtin_clzll(vb_below) : -1;
-    const uint32_t prev_tile = __shfl(tile, prev < 0 ? 0 : prev, 64);
-    const bool head = valid && (prev < 0 || prev_tile != tile);
-    const uint64_t H = __ballot(head);
-    const uint64_t hb = H & (lanes_below | (1ull << lane));
-    const int hl = hb ? 63 - __builtin_clzll(hb) : 0;             // head lane of this lane's group
-    const uint32_t rank = (uint32_t)__builtin_popcountll(V & lanes_below & ~((1ull << hl) - 1ull));
-    const uint32_t head_before = __shfl((uint32_t)before, hl, 64);
-    const uint32_t base = tile == carry_tile ? carry_j : (head_before > tile * RUN_TILE ? 1u : 0u);
-    const uint32_t j = base + rank;
-    const uint32_t info = bp ? inf : (R_RLE | (inf > 0x7FFFFFFFu ? 0x7FFFFFFFu : inf));
-    if (valid) {
-      if (j == 0) ck[tile] = RunCkpt{posv, (uint32_t)before};
-      if (j < RUN_CAPT) runs[(uint64_t)tile * RUN_CAPT + j] = make_uint2((uint32_t)before, info);
-      const bool done_tile = end_tile > tile || end_level == (tile + 1) * RUN_TILE || end_level >= n;
-      if (done_tile) nruns[tile] = j + 1;
-      for (uint32_t t = tile + 1; t <= end_tile; ++t) {  // the run continues into later tiles
-        ck[t] = RunCkpt{posv, (uint32_t)before};
-        runs[(uint64_t)t * RUN_CAPT] = make_uint2((uint32_t)before, info);
-        if (t < end_tile || end_level == (t + 1) * RUN_TILE || end_level >= n) nruns[t] = 1;
-      }
-    }
-    // carry to the next batch (from the last valid lane)
-    if (V) {
-      const int L = 63 - __builtin_clzll(V);
-      const uint32_t lt = rfl(__shfl(tile, L, 64));
-      const uint32_t lj = rfl(__shfl(j, L, 64));
-      const uint32_t le = rfl(__shfl(end_level, L, 64));
-      const uint32_t let = rfl(__shfl(end_tile, L, 64));
-      produced = le;
-      carry_tile = le / RUN_TILE;
-      carry_j = (let == carry_tile) ? (lt == carry_tile ? lj + 1 : 1u) : 0u;
+    {
+      const int32_t e = ix_batch(sm.region, rbase, posv, k, slen, n, w, ck, runs, nruns, cy);
+      if (e) return e;
     }
     stamp(t_batch);
-    if (produced >= n) {
+    if (cy.produced >= n) {
       flush();
       return 0;
     }
+  }
+}
+
+// ------------------------------------------------------------------------------ parallel index pass
+//
+// Dense streams (bit widths <= 8: levels, booleans, small dictionaries) have a header every few
+// bytes, so the one-wave chain walk above pays one dependent step per header. run_index_par
+// walks the same chain with a 256-thread workgroup per stream, PR_REG bytes at a time:
+//   A  every byte position p of the staged region is a candidate header (one- and two-byte
+//      forms); thread t owns the 64-byte segment t, holds its bytes in registers and, right to
+//      left, records in E[p] where the chain from p leaves the segment, or the first position
+//      on it whose header it cannot take (a stop)
+//   B  the same, in place, for 256-byte blocks: E[p] := where the chain from p leaves p's block
+//      (blocks' segments right to left, one position per thread and step)
+//   C  wave 0 follows the true chain one block per step through E, noting each block's entry
+//   D  lane u of wave 0 lists the true headers of block u from its entry; a wave scan orders
+//      them into pos[]
+//   E  wave 0 runs ix_batch over pos[] (64 headers per batch): the same parse, checks and
+//      records as run_index.
+// E is stored transposed (position p at (p % 64) * 256 + p / 64) so the per-position passes
+// hit distinct LDS banks. A stop ends the region's listing at that header; the walk resumes
+// after it. Streams this pass does not take (bit widths > 8, more than PR_POSCAP headers in a
+// region) return PR_BAIL and the caller walks them with run_index.
+constexpr int PR_REG = 16384;
+constexpr int PR_SEG = 64;
+constexpr int PR_NSEG = PR_REG / PR_SEG;  // == threads per workgroup
+constexpr int PR_BLK = 256;               // block (bytes) of the chain walk
+constexpr int PR_NBLK = PR_REG / PR_BLK;  // == 64 lanes
+constexpr int PR_POSCAP = 8192;
+constexpr int PR_ROW = PR_NSEG + 2;  // E row stride (u16)
+constexpr int PR_CHUNKS = (PR_REG + 64) / 16;
+constexpr int PR_PF = (PR_CHUNKS + PR_NSEG - 1) / PR_NSEG;
+constexpr uint32_t PR_STOP = 0x8000u, PR_NONE = 0xFFFFu, PR_BAD = 0xFFFFFFFFu;
+constexpr int32_t PR_BAIL = 0x7FFF0000;
+static_assert(PR_NSEG == 256 && PR_NBLK == 64, "one segment per thread, one block per lane");
+
+struct ParIndexSmem {
+  uint32_t region[(PR_REG + 64) / 4];
+  uint16_t E[64 * PR_ROW];  // transposed, see pr_eix
+  uint16_t pos[PR_POSCAP];
+  uint32_t ctl[8];
+};
+
+// E of region index p (segment p / 64, offset p % 64) sits at row p % 64, column p / 64; rows
+// are padded to an odd word count so that lanes reading one offset of consecutive segments and
+// lanes reading consecutive offsets of one segment both hit distinct banks.
+__device__ inline uint32_t pr_eix(uint32_t p) { return (p & 63u) * (uint32_t)PR_ROW + (p >> 6); }
+
+// Next header after a candidate header at region index p (stream offset so < slen) with first
+// bytes b0, b1: one- or two-byte header forms only, the same next position run_parse finds for
+// them; PR_BAD for any other form, a header or RLE value running past the stream, or a next
+// position >= 0x8000.
+__device__ inline uint32_t pr_next2(uint32_t b0, uint32_t b1, uint32_t p, uint32_t so, uint32_t slen,
+                                    uint32_t w, uint32_t vb) {
+  uint32_t hl = 1, ind = b0;
+  if (b0 & 0x80u) {
+    if (so + 1u >= slen || (b1 & 0x80u)) return PR_BAD;
+    hl = 2;
+    ind = (b0 & 0x7Fu) | (b1 << 7);
+  }
+  uint32_t nx;
+  if (ind & 1u) {
+    nx = p + hl + (ind >> 1) * w;
+  } else {
+    if ((uint64_t)so + hl + vb > slen) return PR_BAD;
+    nx = p + hl + vb;
+  }
+  return nx < 0x8000u ? nx : PR_BAD;
+}
+
+__device__ inline uint32_t pr_next(const uint32_t* region, uint32_t p, uint32_t so, uint32_t slen,
+                                   uint32_t w, uint32_t vb) {
+  const uint32_t x = lload_u32(region, p);
+  return pr_next2(x & 0xFFu, (x >> 8) & 0xFFu, p, so, slen, w, vb);
+}
+
+// Workgroup barrier for LDS only: global loads in flight (the next region's prefetch) stay in
+// flight across it.
+__device__ inline void pr_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Whole workgroup (PR_NSEG threads). Returns the stream's status in every thread, or PR_BAIL.
+__device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                        const Stream& s, RunCkpt* __restrict__ ck,
+                                        uint2* __restrict__ runs, uint32_t* __restrict__ nruns,
+                                        ParIndexSmem& sm, uint64_t* stamps = nullptr) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // diagnostics (PQG_DEBUG bit 5): s_memtime cycles in fetch + exits, chain + listing, batches
+  uint64_t t_ab = 0, t_chain = 0, t_list = 0, t0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](uint64_t& acc) {
+    if (stamps) {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      acc += t1 - t0;
+      t0 = t1;
+    }
+  };
+  if (s.err) return s.err;
+  const uint32_t n = s.n;
+  if (n == 0) return 0;
+  const uint32_t w = (uint32_t)s.w;
+  if (s.kind == LK_BIT_PACKED) {  // one header-less run (levels.rs:203-209)
+    if ((uint64_t)n * (uint64_t)w > (uint64_t)s.slen * 8ull) return ST_EOF;
+    if (w > 32) return ST_PANIC;
+    return 0;
+  }
+  if (w == 0 || w > 8) return PR_BAIL;
+  const uint64_t S = s.S;
+  const uint32_t slen = s.slen;
+  const uint64_t G = S & ~15ull;
+  const uint32_t off0 = (uint32_t)(S - G);
+  const uint32_t vb = (w + 7u) >> 3;
+  const uint32_t nregions = (off0 + slen + PR_REG - 1) / PR_REG;
+  uint4 pf[PR_PF];
+  auto fetch = [&](uint32_t r) {
+    const uint64_t A0 = G + (uint64_t)r * PR_REG;
+    const bool fast = A0 + PR_REG + 64 <= blob_len;
+#pragma unroll
+    for (int k = 0; k < PR_PF; ++k) {
+      const uint32_t c = tid + PR_NSEG * (uint32_t)k;
+      if (c < (uint32_t)PR_CHUNKS)
+        pf[k] = fast ? *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16)
+                     : gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
+    }
+  };
+  uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
+  uint32_t cur = 0;
+  IxCarry cy{0u, 0u, 0u};  // meaningful in wave 0
+  const uint32_t seg0 = tid * PR_SEG, seg1 = seg0 + PR_SEG;
+  while (true) {
+    if (cur >= slen) return ST_EOF;  // the reference stalls at the end of the data (A.4)
+    const uint32_t r = (off0 + cur) / PR_REG;
+    const uint32_t rbase = r * PR_REG - off0;  // stream offset of region byte 0 (mod 2^32)
+    if (r != cur_r) {
+      if (r != pf_r) fetch(r);
+#pragma unroll
+      for (int k = 0; k < PR_PF; ++k) {
+        const uint32_t c = tid + PR_NSEG * (uint32_t)k;
+        if (c < (uint32_t)PR_CHUNKS) reinterpret_cast<uint4*>(sm.region)[c] = pf[k];
+      }
+      cur_r = r;
+      pf_r = 0xFFFFFFFFu;
+      if (r + 1 < nregions) {
+        fetch(r + 1);
+        pf_r = r + 1;
+      }
+      pr_sync();
+      // ---- A: segment exits, right to left, bytes in registers, in segment-local offsets
+      // (position seg0 + i is a stream position iff i < lim; E of local offset o sits at
+      // E[o * 256 + tid])
+      uint32_t bw[PR_SEG / 4 + 1];
+#pragma unroll
+      for (int k = 0; k <= PR_SEG / 4; ++k) bw[k] = sm.region[(seg0 >> 2) + (uint32_t)k];
+      const int64_t lim64 = (int64_t)slen - ((int64_t)r * PR_REG + seg0 - off0);
+      const int32_t lim = lim64 < -1 ? -1 : lim64 > PR_SEG + 8 ? PR_SEG + 8 : (int32_t)lim64;
+      const int32_t m = lim < PR_SEG ? lim : PR_SEG;  // local offsets >= m leave the segment
+      const int32_t omax = 0x8000 - (int32_t)seg0;    // exits must stay below 0x8000
+      uint16_t* Et = sm.E + tid;
+#pragma unroll
+      for (int i = PR_SEG - 1; i >= 0; --i) {
+        const uint32_t b0 = (bw[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        const uint32_t b1 = (bw[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu;
+        const uint32_t two = b0 >> 7;
+        const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
+        const uint32_t hl = 1u + two;
+        const uint32_t bpf = ind & 1u;
+        const int32_t o = i + (int32_t)hl + (int32_t)(bpf ? (ind >> 1) * w : vb);
+        const uint32_t bad = (uint32_t)(i >= lim) | (two & ((b1 >> 7) | (uint32_t)(i + 1 >= lim))) |
+                             ((bpf ^ 1u) & (uint32_t)(i + (int32_t)(hl + vb) > lim)) | (uint32_t)(o >= omax);
+        const uint32_t leave = (uint32_t)(o >= m);
+        const uint32_t via = Et[(bad | leave) ? i * PR_ROW : o * PR_ROW];
+        Et[i * PR_ROW] = (uint16_t)(bad ? (PR_STOP | (seg0 + (uint32_t)i)) : leave ? seg0 + (uint32_t)o : via);
+      }
+      pr_sync();
+      stamp(t_ab);
+      // ---- B: block exits, in place (lane = block, wave + 4 * j = offset in the segment)
+#pragma unroll
+      for (int k = PR_BLK / PR_SEG - 2; k >= 0; --k) {
+#pragma unroll 4
+        for (int j = 0; j < PR_SEG / 4; ++j) {
+          const uint32_t p = lane * PR_BLK + (uint32_t)k * PR_SEG + wave + 4u * (uint32_t)j;
+          const uint32_t q = sm.E[pr_eix(p)];
+          const bool hop = !(q & PR_STOP) && q < (lane + 1) * (uint32_t)PR_BLK && rbase + q < slen;
+          const uint32_t v = sm.E[pr_eix(hop ? q : p)];
+          sm.E[pr_eix(p)] = (uint16_t)(hop ? v : q);
+        }
+        pr_sync();
+      }
+    }
+    stamp(t_ab);
+    // ---- C + D + E: wave 0
+    if (wave == 0) {
+      // C: follow the chain block by block; lane u keeps block u's entry. Lane l holds the
+      // block exits of offsets l < 64 of every block (entries after short jumps land there),
+      // so most steps are a v_readlane; other entries read E.
+      uint32_t xv[PR_NBLK];
+#pragma unroll
+      for (int k = 0; k < PR_NBLK; ++k) xv[k] = sm.E[pr_eix((uint32_t)k * PR_BLK + lane)];
+      uint32_t e = cur - rbase, kind = 2, at = 0, bent = PR_NONE;
+      if (rbase + e >= slen) {
+        kind = 0;
+        at = rbase + e;
+      }
+#pragma unroll
+      for (int k = 0; k < PR_NBLK; ++k) {
+        if (kind == 2 && e < (uint32_t)(k + 1) * PR_BLK) {  // e is in block k
+          bent = lane == (uint32_t)k ? e : bent;
+          const uint32_t off = e - (uint32_t)k * PR_BLK;
+          const uint32_t q = off < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)xv[k], (int)off)
+                                       : rfl(sm.E[pr_eix(e)]);
+          if (q & PR_STOP) {
+            kind = 1;  // stop at region index `at`
+            at = q & 0x7FFFu;
+          } else {
+            e = q;
+            if (rbase + e >= slen || e >= (uint32_t)PR_REG) {
+              kind = 0;  // left the region / the stream at stream offset `at`
+              at = rbase + e;
+            }
+          }
+        }
+      }
+      // D: lane u lists block u's headers
+      const uint32_t stop_at = kind == 1 ? at : 0xFFFFFFFFu;
+      const uint32_t b1e = (lane + 1) * (uint32_t)PR_BLK;
+      auto walk = [&](auto&& put) {
+        if (bent == PR_NONE) return;
+        uint32_t p = bent;
+        while (true) {
+          put(p);
+          if (p == stop_at) break;
+          p = pr_next(sm.region, p, rbase + p, slen, w, vb);
+          if (p >= b1e || rbase + p >= slen) break;
+        }
+      };
+      uint32_t c = 0;
+      walk([&](uint32_t) { ++c; });
+      uint32_t incl = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+      }
+      const uint32_t H = rfl(__shfl(incl, 63, 64));
+      int32_t st = PR_BAIL;
+      uint32_t done = 1, nxt = at;
+      stamp(t_chain);
+      if (H <= (uint32_t)PR_POSCAP) {
+        uint32_t base = incl - c;
+        walk([&](uint32_t p) { sm.pos[base++] = (uint16_t)p; });
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        // E: batches
+        st = 0;
+        done = 0;
+        for (uint32_t b = 0; b < H; b += 64) {
+          const uint32_t k = H - b < 64u ? H - b : 64u;
+          const uint32_t posv = lane < k ? rbase + sm.pos[b + lane] : 0u;
+          st = ix_batch(sm.region, rbase, posv, k, slen, n, w, ck, runs, nruns, cy);
+          if (st || cy.produced >= n) {
+            done = 1;
+            break;
+          }
+        }
+        if (!done && kind == 1) {  // resume after the stop header
+          uint32_t nx, cnt, inf, flg;
+          run_parse(sm.region, at, rbase + at, slen, (int)w, nx, cnt, inf, flg);
+          nxt = rfl(nx);
+        }
+      }
+      if (lane == 0) {
+        sm.ctl[2] = done;
+        sm.ctl[3] = (uint32_t)st;
+        sm.ctl[4] = nxt;
+      }
+      stamp(t_list);
+    }
+    pr_sync();
+    if (sm.ctl[2]) {
+      if (stamps && tid == 0)
+        *reinterpret_cast<uint4*>(stamps) = make_uint4((uint32_t)t_ab, (uint32_t)t_chain, (uint32_t)t_list, 0u);
+      return (int32_t)sm.ctl[3];
+    }
+    cur = sm.ctl[4];
+    pr_sync();  // ctl reuse
   }
 }
 
@@ -968,7 +1279,7 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   const PageWork& pw = pages[p];
   d.page = p;
   if (pw.status != 0) return d;
-  if (rt.pflag && rt.pflag[p]) return d;  // decoded by the page pass
+  if (rt.pflag && rt.pflag[p] == PF_PAGE) return d;  // decoded by the page pass
   if (sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0)) return d;
   Stream s;
   if (!get_stream(blob, pw, sel, cp, s) || s.err) return d;

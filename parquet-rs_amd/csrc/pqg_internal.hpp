@@ -152,6 +152,9 @@ struct DeltaTables {
 // instead of the tiled index + expand passes (PQG_DEBUG=16384). Off by default: on the benchmark
 // pages the tiled passes are as fast (dictionary) or faster (levels).
 constexpr int32_t PQG_DBG_PAGEPASS = 0x4000;
+constexpr int32_t PQG_DBG_SERIAL_INDEX = 0x8000;  // one-wave index walker for every stream
+// RunTables::pflag values: stream decoded by the page pass / handed back by the parallel index walker
+constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u;
 
 struct ColumnParams {
   int32_t physical_type;
