@@ -14,6 +14,7 @@
 // All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
 // (index pass + grid-wide expand pass) is in pqg_runs.hpp.
 #include "pqg_rlepage.hpp"
+#include "pqg_parpage.hpp"
 
 namespace pqg {
 
@@ -322,6 +323,41 @@ k_rlepage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len, const Page
   if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
 }
 
+// Fused page pass of level streams (pqg_parpage.hpp). Def levels: the page's non-null count
+// goes to its first tile's four quarter counts (zeros in the rest) for k_page_counts.
+struct ParLevelsMaker {
+  int16_t* out;  // page output base
+  int16_t maxl;
+  bool count;
+  uint32_t nn;
+  __device__ TxLevels make(uint32_t) { return TxLevels{out, maxl, count, 0u}; }
+  __device__ void done(uint32_t, TxLevels& em) { nn += em.nonnull; }
+};
+
+__global__ void __launch_bounds__(WG) k_parpage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                       const PageWork* pages, ColumnParams cp, int which,
+                                                       RunTables rt, int16_t* __restrict__ out) {
+  __shared__ ParPageSmem sm;
+  const int p = blockIdx.x;
+  const PageWork& pw = pages[p];
+  Stream s;
+  bool done = false;
+  if (get_stream(blob, pw, which, cp, s)) {
+    if (pw.status == 0) {
+      const bool count = which == SS_DEF;
+      ParLevelsMaker mk{out + s.out, which == SS_DEF ? cp.max_def : cp.max_rep, count, 0u};
+      done = par_page(blob, blob_len, s, sm, mk);
+      if (done && count && pw.ntiles) {
+        for (uint32_t i = 4 + threadIdx.x; i < 4 * pw.ntiles; i += WG) rt.qcount[4 * pw.ltile0 + i] = 0;
+        const uint32_t nn = wave_sum_u32(mk.nn);
+        if ((threadIdx.x & 63) == 0) rt.qcount[4 * pw.ltile0 + (threadIdx.x >> 6)] = nn;
+      }
+    }
+    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
+  }
+  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
+}
+
 template <int ES>
 struct DictPageMaker {
   const uint8_t* dict;
@@ -581,11 +617,16 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
                              int npages, uint32_t ntiles, ColumnParams cp, int which,
                              const uint32_t* tile_page, RunTables rt, int16_t* out,
                              ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
-  const bool pp = (cp.debug & PQG_DBG_PAGEPASS) != 0;  // kev brackets the dominant kernel
+  // optional page pass first (PQG_DBG_PAGEPASS: k_rlepage_levels; PQG_DBG_FUSED: k_parpage_levels),
+  // the tiled passes then take the streams it left (none: they exit at once)
+  const bool pp = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED)) != 0;
   const int sel = which ? SS_REP : SS_DEF;
-  if (pp) {
+  if (pp) {  // kev brackets the dominant kernel
     if (kev) (void)hipEventRecord(kev[0], s);
-    hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
+    if (cp.debug & PQG_DBG_PAGEPASS)
+      hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
+    else
+      hipLaunchKernelGGL(k_parpage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
     if (kev) (void)hipEventRecord(kev[1], s);
   }
   if (cp.debug & PQG_DBG_SERIAL_INDEX)

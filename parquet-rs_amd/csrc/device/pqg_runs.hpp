@@ -518,78 +518,31 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
   }
 }
 
-// ------------------------------------------------------------------------------ parallel index pass
+// ------------------------------------------------------------------------------ parallel chain walk
 //
 // Dense streams (bit widths <= 8: levels, booleans, small dictionaries) have a header every few
-// bytes, so the one-wave chain walk above pays one dependent step per header. run_index_par
-// walks the same chain with a 256-thread workgroup per stream, PR_REG bytes at a time:
-//   A  every byte position p of the staged region is a candidate header (one- and two-byte
-//      forms); thread t owns the 64-byte segment t, holds its bytes in registers and, right to
-//      left, records in E[p] where the chain from p leaves the segment, or the first position
-//      on it whose header it cannot take (a stop)
-//   B  the same, in place, for 256-byte blocks: E[p] := where the chain from p leaves p's block
-//      (blocks' segments right to left, one position per thread and step)
-//   C  wave 0 follows the true chain one block per step through E, noting each block's entry
-//   D  lane u of wave 0 lists the true headers of block u from its entry; a wave scan orders
-//      them into pos[]
-//   E  wave 0 runs ix_batch over pos[] (64 headers per batch): the same parse, checks and
-//      records as run_index.
-// E is stored transposed (position p at (p % 64) * 256 + p / 64) so the per-position passes
-// hit distinct LDS banks. A stop ends the region's listing at that header; the walk resumes
-// after it. Streams this pass does not take (bit widths > 8, more than PR_POSCAP headers in a
-// region) return PR_BAIL and the caller walks them with run_index.
-constexpr int PR_REG = 16384;
-constexpr int PR_SEG = 64;
-constexpr int PR_NSEG = PR_REG / PR_SEG;  // == threads per workgroup
-constexpr int PR_BLK = 256;               // block (bytes) of the chain walk
-constexpr int PR_NBLK = PR_REG / PR_BLK;  // == 64 lanes
-constexpr int PR_POSCAP = 8192;
-constexpr int PR_ROW = PR_NSEG + 2;  // E row stride (u16)
-constexpr int PR_CHUNKS = (PR_REG + 64) / 16;
-constexpr int PR_PF = (PR_CHUNKS + PR_NSEG - 1) / PR_NSEG;
-constexpr uint32_t PR_STOP = 0x8000u, PR_NONE = 0xFFFFu, PR_BAD = 0xFFFFFFFFu;
-constexpr int32_t PR_BAIL = 0x7FFF0000;
-static_assert(PR_NSEG == 256 && PR_NBLK == 64, "one segment per thread, one block per lane");
-
-struct ParIndexSmem {
-  uint32_t region[(PR_REG + 64) / 4];
-  uint16_t E[64 * PR_ROW];  // transposed, see pr_eix
-  uint16_t pos[PR_POSCAP];
-  uint32_t ctl[8];
+// bytes, so a one-wave chain walk pays one dependent step per header. The parallel walk finds
+// the chain inside a staged region of REG stream bytes with a 256-thread workgroup:
+//   A  every byte position p is a candidate header (one- and two-byte forms); thread t owns the
+//      segment [t * SEG, (t + 1) * SEG), holds its bytes in registers and, right to left,
+//      records in E[p] where the chain from p leaves the segment, or the first position on it
+//      whose header it cannot take (a stop)
+//   B  the same, in place, for blocks of 4 segments (REG / 64 bytes, one per lane): E[p] :=
+//      where the chain from p leaves p's block
+//   C  wave 0 follows the true chain block by block through E (a v_readlane per step for
+//      entries in a block's first 64 bytes); lane u keeps block u's entry
+//   D  lane u walks the true headers of block u from that entry.
+// E is stored transposed (segment offset major, rows padded to an odd word count) so both the
+// per-segment pass (lanes = segments) and the block pass hit distinct LDS banks.
+template <int REG>
+struct PC {
+  static constexpr int SEG = REG / 256;
+  static constexpr int BLK = REG / 64;
+  static constexpr int ROW = 256 + 2;
+  static constexpr int ESZ = SEG * ROW;  // u16 entries of E
+  static __device__ uint32_t eix(uint32_t p) { return (p % SEG) * ROW + p / SEG; }
 };
-
-// E of region index p (segment p / 64, offset p % 64) sits at row p % 64, column p / 64; rows
-// are padded to an odd word count so that lanes reading one offset of consecutive segments and
-// lanes reading consecutive offsets of one segment both hit distinct banks.
-__device__ inline uint32_t pr_eix(uint32_t p) { return (p & 63u) * (uint32_t)PR_ROW + (p >> 6); }
-
-// Next header after a candidate header at region index p (stream offset so < slen) with first
-// bytes b0, b1: one- or two-byte header forms only, the same next position run_parse finds for
-// them; PR_BAD for any other form, a header or RLE value running past the stream, or a next
-// position >= 0x8000.
-__device__ inline uint32_t pr_next2(uint32_t b0, uint32_t b1, uint32_t p, uint32_t so, uint32_t slen,
-                                    uint32_t w, uint32_t vb) {
-  uint32_t hl = 1, ind = b0;
-  if (b0 & 0x80u) {
-    if (so + 1u >= slen || (b1 & 0x80u)) return PR_BAD;
-    hl = 2;
-    ind = (b0 & 0x7Fu) | (b1 << 7);
-  }
-  uint32_t nx;
-  if (ind & 1u) {
-    nx = p + hl + (ind >> 1) * w;
-  } else {
-    if ((uint64_t)so + hl + vb > slen) return PR_BAD;
-    nx = p + hl + vb;
-  }
-  return nx < 0x8000u ? nx : PR_BAD;
-}
-
-__device__ inline uint32_t pr_next(const uint32_t* region, uint32_t p, uint32_t so, uint32_t slen,
-                                   uint32_t w, uint32_t vb) {
-  const uint32_t x = lload_u32(region, p);
-  return pr_next2(x & 0xFFu, (x >> 8) & 0xFFu, p, so, slen, w, vb);
-}
+constexpr uint32_t PR_STOP = 0x8000u, PR_NONE = 0xFFFFu;
 
 // Workgroup barrier for LDS only: global loads in flight (the next region's prefetch) stay in
 // flight across it.
@@ -599,7 +552,143 @@ __device__ inline void pr_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Whole workgroup (PR_NSEG threads). Returns the stream's status in every thread, or PR_BAIL.
+// Next header after a true header at region index p (stream offset so): one- or two-byte forms
+// (the only ones the exits pass follows), as run_parse finds it.
+__device__ inline uint32_t pr_next(const uint32_t* region, uint32_t p, uint32_t w, uint32_t vb) {
+  const uint32_t x = lload_u32(region, p);
+  const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu;
+  const uint32_t two = b0 >> 7;
+  const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
+  return p + 1u + two + ((ind & 1u) ? (ind >> 1) * w : vb);
+}
+
+// A + B over region r (stream offset of region byte 0: rbase) staged in `region`; whole
+// workgroup, LDS barrier at the end.
+template <int REG>
+__device__ inline void pc_exits(const uint32_t* region, uint16_t* E, uint32_t r, uint32_t rbase,
+                                uint32_t off0, uint32_t slen, uint32_t w, uint32_t vb) {
+  using G = PC<REG>;
+  constexpr int SEG = G::SEG, ROW = G::ROW, BLK = G::BLK;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t seg0 = tid * SEG;
+  // ---- A: segment exits, right to left, bytes in registers, segment-local offsets (position
+  // seg0 + i is a stream position iff i < lim; E of local offset o sits at E[o * ROW + tid])
+  uint32_t bw[SEG / 4 + 1];
+#pragma unroll
+  for (int k = 0; k <= SEG / 4; ++k) bw[k] = region[(seg0 >> 2) + (uint32_t)k];
+  const int64_t lim64 = (int64_t)slen - ((int64_t)r * REG + seg0 - off0);
+  const int32_t lim = lim64 < -1 ? -1 : lim64 > SEG + 8 ? SEG + 8 : (int32_t)lim64;
+  const int32_t m = lim < SEG ? lim : SEG;        // local offsets >= m leave the segment
+  const int32_t omax = 0x8000 - (int32_t)seg0;    // exits must stay below 0x8000
+  uint16_t* Et = E + tid;
+#pragma unroll
+  for (int i = SEG - 1; i >= 0; --i) {
+    const uint32_t b0 = (bw[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    const uint32_t b1 = (bw[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu;
+    const uint32_t two = b0 >> 7;
+    const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
+    const uint32_t hl = 1u + two;
+    const uint32_t bpf = ind & 1u;
+    const int32_t o = i + (int32_t)hl + (int32_t)(bpf ? (ind >> 1) * w : vb);
+    // not a stream position / longer header / header or RLE value past the stream / far exit
+    const uint32_t bad = (uint32_t)(i >= lim) | (two & ((b1 >> 7) | (uint32_t)(i + 1 >= lim))) |
+                         ((bpf ^ 1u) & (uint32_t)(i + (int32_t)(hl + vb) > lim)) | (uint32_t)(o >= omax);
+    const uint32_t leave = (uint32_t)(o >= m);
+    const uint32_t via = Et[(bad | leave) ? i * ROW : o * ROW];
+    Et[i * ROW] = (uint16_t)(bad ? (PR_STOP | (seg0 + (uint32_t)i)) : leave ? seg0 + (uint32_t)o : via);
+  }
+  pr_sync();
+  // ---- B: block exits, in place (lane = block, wave + 4 * j = offset in the segment)
+#pragma unroll
+  for (int k = BLK / SEG - 2; k >= 0; --k) {
+#pragma unroll 4
+    for (int j = 0; j < SEG / 4; ++j) {
+      const uint32_t p = lane * BLK + (uint32_t)k * SEG + wave + 4u * (uint32_t)j;
+      const uint32_t q = E[G::eix(p)];
+      const bool hop = !(q & PR_STOP) && q < (lane + 1) * (uint32_t)BLK && rbase + q < slen;
+      const uint32_t v = E[G::eix(hop ? q : p)];
+      E[G::eix(p)] = (uint16_t)(hop ? v : q);
+    }
+    pr_sync();
+  }
+}
+
+// C (wave 0): the chain from region index e0 (a stream position). Returns block `lane`'s entry
+// (PR_NONE if the chain skips it); kind 0: the chain leaves the region / stream at stream
+// offset `at`; kind 1: stop at region index `at`.
+template <int REG>
+__device__ inline uint32_t pc_chain(const uint16_t* E, uint32_t e0, uint32_t rbase, uint32_t slen,
+                                    uint32_t& kind, uint32_t& at) {
+  using G = PC<REG>;
+  constexpr int BLK = G::BLK;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t xv[64];  // block k's exits for entry offsets lane < 64
+#pragma unroll
+  for (int k = 0; k < 64; ++k) xv[k] = E[G::eix((uint32_t)k * BLK + lane)];
+  uint32_t e = e0, bent = PR_NONE;
+  kind = 2;
+  at = 0;
+  if (rbase + e >= slen) {
+    kind = 0;
+    at = rbase + e;
+  }
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    if (kind == 2 && e < (uint32_t)(k + 1) * BLK) {  // e is in block k
+      bent = lane == (uint32_t)k ? e : bent;
+      const uint32_t off = e - (uint32_t)k * BLK;
+      const uint32_t q = off < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)xv[k], (int)off) : rfl(E[G::eix(e)]);
+      if (q & PR_STOP) {
+        kind = 1;
+        at = q & 0x7FFFu;
+      } else {
+        e = q;
+        if (rbase + e >= slen || e >= (uint32_t)REG) {
+          kind = 0;
+          at = rbase + e;
+        }
+      }
+    }
+  }
+  return bent;
+}
+
+// D (wave 0, lane u = block u): calls put(p) for the true headers of the block in order.
+template <int REG, class F>
+__device__ inline void pc_walk(const uint32_t* region, uint32_t bent, uint32_t stop_at, uint32_t rbase,
+                               uint32_t slen, uint32_t w, uint32_t vb, F&& put) {
+  if (bent == PR_NONE) return;
+  const uint32_t b1e = ((threadIdx.x & 63) + 1) * (uint32_t)PC<REG>::BLK;
+  uint32_t p = bent;
+  while (true) {
+    put(p);
+    if (p == stop_at) break;
+    p = pr_next(region, p, w, vb);
+    if (p >= b1e || rbase + p >= slen) break;
+  }
+}
+
+// ------------------------------------------------------------------------------ parallel index pass
+//
+// run_index_par: the index pass of a dense stream with the parallel chain walk, PR_REG bytes per
+// region; the listed headers go through ix_batch (wave 0, 64 per batch): the same parse, checks
+// and records as run_index. A stop ends the region's listing at that header; the walk resumes
+// after it. Streams it does not take (bit widths > 8, more than PR_POSCAP headers in a region)
+// return PR_BAIL and are walked by run_index.
+constexpr int PR_REG = 16384;
+constexpr int PR_POSCAP = 8192;
+constexpr int PR_CHUNKS = (PR_REG + 64) / 16;
+constexpr int PR_PF = (PR_CHUNKS + WG - 1) / WG;
+constexpr int32_t PR_BAIL = 0x7FFF0000;
+
+struct ParIndexSmem {
+  uint32_t region[(PR_REG + 64) / 4];
+  uint16_t E[PC<PR_REG>::ESZ];
+  uint16_t pos[PR_POSCAP];
+  uint32_t ctl[8];
+};
+
+// Whole workgroup (WG threads). Returns the stream's status in every thread, or PR_BAIL.
 __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                         const Stream& s, RunCkpt* __restrict__ ck,
                                         uint2* __restrict__ runs, uint32_t* __restrict__ nruns,
@@ -636,7 +725,7 @@ __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64
     const bool fast = A0 + PR_REG + 64 <= blob_len;
 #pragma unroll
     for (int k = 0; k < PR_PF; ++k) {
-      const uint32_t c = tid + PR_NSEG * (uint32_t)k;
+      const uint32_t c = tid + WG * (uint32_t)k;
       if (c < (uint32_t)PR_CHUNKS)
         pf[k] = fast ? *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16)
                      : gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
@@ -645,7 +734,6 @@ __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64
   uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
   uint32_t cur = 0;
   IxCarry cy{0u, 0u, 0u};  // meaningful in wave 0
-  const uint32_t seg0 = tid * PR_SEG, seg1 = seg0 + PR_SEG;
   while (true) {
     if (cur >= slen) return ST_EOF;  // the reference stalls at the end of the data (A.4)
     const uint32_t r = (off0 + cur) / PR_REG;
@@ -654,7 +742,7 @@ __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64
       if (r != pf_r) fetch(r);
 #pragma unroll
       for (int k = 0; k < PR_PF; ++k) {
-        const uint32_t c = tid + PR_NSEG * (uint32_t)k;
+        const uint32_t c = tid + WG * (uint32_t)k;
         if (c < (uint32_t)PR_CHUNKS) reinterpret_cast<uint4*>(sm.region)[c] = pf[k];
       }
       cur_r = r;
@@ -664,96 +752,16 @@ __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64
         pf_r = r + 1;
       }
       pr_sync();
-      // ---- A: segment exits, right to left, bytes in registers, in segment-local offsets
-      // (position seg0 + i is a stream position iff i < lim; E of local offset o sits at
-      // E[o * 256 + tid])
-      uint32_t bw[PR_SEG / 4 + 1];
-#pragma unroll
-      for (int k = 0; k <= PR_SEG / 4; ++k) bw[k] = sm.region[(seg0 >> 2) + (uint32_t)k];
-      const int64_t lim64 = (int64_t)slen - ((int64_t)r * PR_REG + seg0 - off0);
-      const int32_t lim = lim64 < -1 ? -1 : lim64 > PR_SEG + 8 ? PR_SEG + 8 : (int32_t)lim64;
-      const int32_t m = lim < PR_SEG ? lim : PR_SEG;  // local offsets >= m leave the segment
-      const int32_t omax = 0x8000 - (int32_t)seg0;    // exits must stay below 0x8000
-      uint16_t* Et = sm.E + tid;
-#pragma unroll
-      for (int i = PR_SEG - 1; i >= 0; --i) {
-        const uint32_t b0 = (bw[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        const uint32_t b1 = (bw[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu;
-        const uint32_t two = b0 >> 7;
-        const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
-        const uint32_t hl = 1u + two;
-        const uint32_t bpf = ind & 1u;
-        const int32_t o = i + (int32_t)hl + (int32_t)(bpf ? (ind >> 1) * w : vb);
-        const uint32_t bad = (uint32_t)(i >= lim) | (two & ((b1 >> 7) | (uint32_t)(i + 1 >= lim))) |
-                             ((bpf ^ 1u) & (uint32_t)(i + (int32_t)(hl + vb) > lim)) | (uint32_t)(o >= omax);
-        const uint32_t leave = (uint32_t)(o >= m);
-        const uint32_t via = Et[(bad | leave) ? i * PR_ROW : o * PR_ROW];
-        Et[i * PR_ROW] = (uint16_t)(bad ? (PR_STOP | (seg0 + (uint32_t)i)) : leave ? seg0 + (uint32_t)o : via);
-      }
-      pr_sync();
-      stamp(t_ab);
-      // ---- B: block exits, in place (lane = block, wave + 4 * j = offset in the segment)
-#pragma unroll
-      for (int k = PR_BLK / PR_SEG - 2; k >= 0; --k) {
-#pragma unroll 4
-        for (int j = 0; j < PR_SEG / 4; ++j) {
-          const uint32_t p = lane * PR_BLK + (uint32_t)k * PR_SEG + wave + 4u * (uint32_t)j;
-          const uint32_t q = sm.E[pr_eix(p)];
-          const bool hop = !(q & PR_STOP) && q < (lane + 1) * (uint32_t)PR_BLK && rbase + q < slen;
-          const uint32_t v = sm.E[pr_eix(hop ? q : p)];
-          sm.E[pr_eix(p)] = (uint16_t)(hop ? v : q);
-        }
-        pr_sync();
-      }
+      pc_exits<PR_REG>(sm.region, sm.E, r, rbase, off0, slen, w, vb);
     }
     stamp(t_ab);
-    // ---- C + D + E: wave 0
+    // ---- chain, listing and batches: wave 0
     if (wave == 0) {
-      // C: follow the chain block by block; lane u keeps block u's entry. Lane l holds the
-      // block exits of offsets l < 64 of every block (entries after short jumps land there),
-      // so most steps are a v_readlane; other entries read E.
-      uint32_t xv[PR_NBLK];
-#pragma unroll
-      for (int k = 0; k < PR_NBLK; ++k) xv[k] = sm.E[pr_eix((uint32_t)k * PR_BLK + lane)];
-      uint32_t e = cur - rbase, kind = 2, at = 0, bent = PR_NONE;
-      if (rbase + e >= slen) {
-        kind = 0;
-        at = rbase + e;
-      }
-#pragma unroll
-      for (int k = 0; k < PR_NBLK; ++k) {
-        if (kind == 2 && e < (uint32_t)(k + 1) * PR_BLK) {  // e is in block k
-          bent = lane == (uint32_t)k ? e : bent;
-          const uint32_t off = e - (uint32_t)k * PR_BLK;
-          const uint32_t q = off < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)xv[k], (int)off)
-                                       : rfl(sm.E[pr_eix(e)]);
-          if (q & PR_STOP) {
-            kind = 1;  // stop at region index `at`
-            at = q & 0x7FFFu;
-          } else {
-            e = q;
-            if (rbase + e >= slen || e >= (uint32_t)PR_REG) {
-              kind = 0;  // left the region / the stream at stream offset `at`
-              at = rbase + e;
-            }
-          }
-        }
-      }
-      // D: lane u lists block u's headers
+      uint32_t kind, at;
+      const uint32_t bent = pc_chain<PR_REG>(sm.E, cur - rbase, rbase, slen, kind, at);
       const uint32_t stop_at = kind == 1 ? at : 0xFFFFFFFFu;
-      const uint32_t b1e = (lane + 1) * (uint32_t)PR_BLK;
-      auto walk = [&](auto&& put) {
-        if (bent == PR_NONE) return;
-        uint32_t p = bent;
-        while (true) {
-          put(p);
-          if (p == stop_at) break;
-          p = pr_next(sm.region, p, rbase + p, slen, w, vb);
-          if (p >= b1e || rbase + p >= slen) break;
-        }
-      };
       uint32_t c = 0;
-      walk([&](uint32_t) { ++c; });
+      pc_walk<PR_REG>(sm.region, bent, stop_at, rbase, slen, w, vb, [&](uint32_t) { ++c; });
       uint32_t incl = c;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -766,10 +774,10 @@ __device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64
       stamp(t_chain);
       if (H <= (uint32_t)PR_POSCAP) {
         uint32_t base = incl - c;
-        walk([&](uint32_t p) { sm.pos[base++] = (uint16_t)p; });
+        pc_walk<PR_REG>(sm.region, bent, stop_at, rbase, slen, w, vb,
+                        [&](uint32_t p) { sm.pos[base++] = (uint16_t)p; });
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
-        // E: batches
         st = 0;
         done = 0;
         for (uint32_t b = 0; b < H; b += 64) {

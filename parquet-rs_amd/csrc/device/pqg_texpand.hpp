@@ -33,8 +33,10 @@ struct TileSmem {
   uint32_t ctl[4];
 };
 
-// Run holding page-relative output o: binary search over sm.start[0, nr).
-__device__ inline uint32_t tx_find(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t o) {
+// Run holding page-relative output o: binary search over sm.start[0, nr). SM: any LDS layout
+// with start[], info[] (run list) and stage[] (payload window) members.
+template <class SM>
+__device__ inline uint32_t tx_find(const SM& sm, uint32_t nr, uint32_t lgn, uint32_t o) {
   uint32_t a = 0;
   for (uint32_t step = lgn; step; step >>= 1)
     if (a + step < nr && sm.start[a + step] <= o) a += step;
@@ -44,8 +46,8 @@ __device__ inline uint32_t tx_find(const TileSmem& sm, uint32_t nr, uint32_t lgn
 // Fast path for the V outputs [g, g + V): all inside the segment (caller checks), in at most
 // two runs, bit-packed payload inside the LDS window (lim = staged bits). Values go to v;
 // returns false when any of that does not hold (the slow path then produces the group).
-template <int V>
-__device__ inline bool tx_fast(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t g,
+template <int V, class SM>
+__device__ inline bool tx_fast(const SM& sm, uint32_t nr, uint32_t lgn, uint32_t g,
                                uint32_t seg_hi, uint32_t w, uint32_t wm, uint32_t sb32,
                                uint32_t lim, uint32_t (&v)[V]) {
   const uint32_t a = tx_find(sm, nr, lgn, g);
@@ -72,7 +74,8 @@ __device__ inline bool tx_fast(const TileSmem& sm, uint32_t nr, uint32_t lgn, ui
 }
 
 // One output, any case: LDS window or global memory (64-bit offsets).
-__device__ inline uint32_t tx_one(const TileSmem& sm, uint32_t nr, uint32_t lgn, uint32_t o,
+template <class SM>
+__device__ inline uint32_t tx_one(const SM& sm, uint32_t nr, uint32_t lgn, uint32_t o,
                                   uint32_t w, uint32_t wm, uint32_t sb32, uint32_t lim,
                                   const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t S) {
   const uint32_t a = tx_find(sm, nr, lgn, o);
@@ -90,8 +93,8 @@ __device__ inline uint32_t tx_one(const TileSmem& sm, uint32_t nr, uint32_t lgn,
 // Expand outputs [seg_lo, seg_hi) of the tile starting at page-relative output lo. Groups
 // that take the fast path are handed to the emitter E::PG at a time (put: all-or-nothing
 // masks); the others are produced one output at a time (put1) in a rolled loop.
-template <class E>
-__device__ inline void tx_range(const TileSmem& sm, uint32_t nr, uint32_t lo, uint32_t seg_lo,
+template <class E, class SM>
+__device__ inline void tx_range(const SM& sm, uint32_t nr, uint32_t lo, uint32_t seg_lo,
                                 uint32_t seg_hi, uint32_t w, uint32_t sb32, uint32_t staged,
                                 bool wide, const uint8_t* __restrict__ blob, uint64_t blob_len,
                                 uint64_t S, E& em) {

@@ -507,16 +507,18 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   // page-pass flags: with the page pass every stream starts "none left over"; without it the
   // tiled passes take every page
   const bool pagepass = (cp.debug & PQG_DBG_PAGEPASS) != 0;
+  const bool fused = (cp.debug & PQG_DBG_FUSED) != 0;  // level streams: fused page pass first
   for (int k = 0; k < 3; ++k) {
     if (!sl.rt[k].nfall) continue;
-    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, pagepass ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
-    if (!pagepass && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+    const bool pm = pagepass || (k < 2 && fused);
+    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, pm ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
+    if (!pm && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
   }
   if (np && want_def)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              out->def_levels, ctx->d_res, s, ctx->timing ? &sl.ev[6] : nullptr),
            "def levels");
-  if (np && want_def) sl.kl = nt > 0 || (cp.debug & PQG_DBG_PAGEPASS);
+  if (np && want_def) sl.kl = nt > 0 || pagepass || fused;
   if (np && want_rep)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
                              out->rep_levels, ctx->d_res, s, nullptr), "rep levels");
