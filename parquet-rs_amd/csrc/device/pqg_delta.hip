@@ -143,7 +143,6 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   const uint64_t G = S & ~15ull;
   const uint32_t off0 = (uint32_t)(S - G);
   const uint32_t nregions = (off0 + slen + IX_REG - 1) / IX_REG;
-  const uint64_t below = (1ull << lane) - 1ull;
   uint4 pf[IX_PF];
   uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
   uint32_t cur = q, b = 0;

@@ -1332,8 +1332,8 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   for (uint32_t r = a0; r <= a1; ++r) {
     const uint2 x = recs[r];
     if (x.y & R_RLE) continue;
-    const uint32_t st = x.x, en = r + 1 < nrec ? recs[r + 1].x : hi;
-    const uint32_t u = lo > st ? lo : st, v = hi < en ? hi : en;
+    const uint32_t st = x.x;
+    const uint32_t u = lo > st ? lo : st;
     blo = (uint32_t)min((uint64_t)blo, (uint64_t)x.y + (((uint64_t)(u - st) * w) >> 3));
     break;
   }
