@@ -334,6 +334,39 @@ struct ParLevelsMaker {
   __device__ void done(uint32_t, TxLevels& em) { nn += em.nonnull; }
 };
 
+// Header density of a level stream from its first headers (at most 16, or until 1024 levels are
+// covered): true when they average fewer than 24 levels per header (p_null 0.1 streams: ~18;
+// p_null 0.5: ~70, where index + expand is faster). The hybrid header layout is
+// RleDecoder::reload's (rle.rs:489-513): ULEB128 h, h & 1 -> (h >> 1) groups of 8 bit-packed
+// values, else an RLE run of h >> 1 with a ceil(w / 8)-byte value. Anything unusual answers
+// false, which leaves the page to the tiled passes (they own the error reporting).
+__device__ inline bool dense_headers(const uint8_t* __restrict__ blob, const Stream& s) {
+  if (s.kind != LK_RLE || s.err || s.w <= 0 || s.w > 8) return false;
+  const uint8_t* p = blob + s.S;
+  uint64_t pos = 0, covered = 0;
+  uint32_t hops = 0;
+  while (hops < 16 && covered < 1024 && covered < s.n) {
+    uint64_t h = 0;
+    int sh = 0;
+    uint8_t b;
+    do {
+      if (pos >= s.slen || sh > 35) return false;
+      b = p[pos++];
+      h |= (uint64_t)(b & 0x7F) << sh;
+      sh += 7;
+    } while (b & 0x80);
+    if (h & 1) {
+      covered += (h >> 1) * 8;
+      pos += (h >> 1) * (uint64_t)s.w;
+    } else {
+      covered += h >> 1;
+      pos += 1;  // w <= 8: one value byte
+    }
+    ++hops;
+  }
+  return (uint64_t)hops * 24 > covered;
+}
+
 __global__ void __launch_bounds__(WG) k_parpage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                        const PageWork* pages, ColumnParams cp, int which,
                                                        RunTables rt, int16_t* __restrict__ out) {
@@ -343,7 +376,7 @@ __global__ void __launch_bounds__(WG) k_parpage_levels(const uint8_t* __restrict
   Stream s;
   bool done = false;
   if (get_stream(blob, pw, which, cp, s)) {
-    if (pw.status == 0) {
+    if (pw.status == 0 && ((cp.debug & PQG_DBG_FUSED) || dense_headers(blob, s))) {
       const bool count = which == SS_DEF;
       ParLevelsMaker mk{out + s.out, which == SS_DEF ? cp.max_def : cp.max_rep, count, 0u};
       done = par_page(blob, blob_len, s, sm, mk);
@@ -619,15 +652,17 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
                              ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
   // optional page pass first (PQG_DBG_PAGEPASS: k_rlepage_levels; PQG_DBG_FUSED: k_parpage_levels),
   // the tiled passes then take the streams it left (none: they exit at once)
-  const bool pp = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED)) != 0;
+  const bool pp = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED | PQG_DBG_AUTO)) != 0;
   const int sel = which ? SS_REP : SS_DEF;
-  if (pp) {  // kev brackets the dominant kernel
-    if (kev) (void)hipEventRecord(kev[0], s);
+  // kev brackets the dominant kernel: the page pass when forced for every page, else the expand
+  const bool ppall = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED)) != 0;
+  if (pp) {
+    if (kev && ppall) (void)hipEventRecord(kev[0], s);
     if (cp.debug & PQG_DBG_PAGEPASS)
       hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
     else
       hipLaunchKernelGGL(k_parpage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
-    if (kev) (void)hipEventRecord(kev[1], s);
+    if (kev && ppall) (void)hipEventRecord(kev[1], s);
   }
   if (cp.debug & PQG_DBG_SERIAL_INDEX)
     hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
@@ -639,9 +674,9 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    if (kev && !pp) (void)hipEventRecord(kev[0], s);
+    if (kev && !ppall) (void)hipEventRecord(kev[0], s);
     hipLaunchKernelGGL(k_texpand_levels, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
-    if (kev && !pp) (void)hipEventRecord(kev[1], s);
+    if (kev && !ppall) (void)hipEventRecord(kev[1], s);
     if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
   }
   return hipGetLastError();

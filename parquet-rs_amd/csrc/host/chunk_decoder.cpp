@@ -507,7 +507,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   // page-pass flags: with the page pass every stream starts "none left over"; without it the
   // tiled passes take every page
   const bool pagepass = (cp.debug & PQG_DBG_PAGEPASS) != 0;
-  const bool fused = (cp.debug & PQG_DBG_FUSED) != 0;  // level streams: fused page pass first
+  // level streams: fused page pass first, for every page (PQG_DBG_FUSED) or the dense ones (PQG_DBG_AUTO)
+  const bool fused = (cp.debug & (PQG_DBG_FUSED | PQG_DBG_AUTO)) != 0;
   for (int k = 0; k < 3; ++k) {
     if (!sl.rt[k].nfall) continue;
     const bool pm = pagepass || (k < 2 && fused);

@@ -153,7 +153,11 @@ struct DeltaTables {
 // pages the tiled passes are as fast (dictionary) or faster (levels).
 constexpr int32_t PQG_DBG_PAGEPASS = 0x4000;
 constexpr int32_t PQG_DBG_SERIAL_INDEX = 0x8000;  // one-wave index walker for every stream
-constexpr int32_t PQG_DBG_FUSED = 0x10000;        // level streams: fused page pass first (k_parpage_levels)
+constexpr int32_t PQG_DBG_FUSED = 0x10000;        // level streams: fused page pass for every page
+// Level streams, optional (PQG_DEBUG=131072): the fused page pass takes only the pages whose
+// first headers are dense (< 24 levels per header) and leaves the rest to the tiled passes. Off by
+// default: measured slower than either pure mode when the pages split between the two.
+constexpr int32_t PQG_DBG_AUTO = 0x20000;
 // RunTables::pflag values: stream decoded by the page pass / handed back by the parallel index walker
 constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u;
 
