@@ -5,18 +5,22 @@
 
 A step is one decode of the whole synthetic column (BASELINE.json configs[1..3], 1e9
 levels/values per GPU) through the C ABI (pqg_decode_chunk), with the page bytes already
-resident in HBM. For N > 1 the driver launches one rank per GPU via torch.distributed.run;
+resident in HBM. With --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
+N ranks through torch.distributed.run (before touching the GPU) and exits with their status;
 every rank decodes its own partition (its own row groups, seed + rank): weak scaling, no
 collective on the data path. Rank 0 prints one JSON line.
 
 The reported roofline is for the dominant kernel, timed with HIP events on the decode stream
 over the timed steps; the CPU baseline is the C restatement of parquet-rs's decode loop
-(oracle/, kind "port") on a bounded sample, one decoder per thread.
+(oracle/, kind "port") on a bounded sample, one decoder per thread, at 1 thread and at every
+host core, batch sizes 32/64/128/1024 (benches/decoding.rs:103-123, record/reader.rs:33).
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,11 +28,14 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_ACHIEVABLE_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
+METRIC = "decoded values/s + GB/s, device-resident page decode, 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -44,42 +51,67 @@ def parse():
     ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0 / 0.1 variants")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--pcie", type=int, default=1, help="also time the host-to-host (PCIe) rate")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--threads", type=int, default=16, help="host threads (box CPU share: 16)")
     ap.add_argument("--seed", type=int, default=0x5EED0000)
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
+    return ap.parse_args(argv)
 
 
-from sharding import shard_seed  # noqa: E402  (row-group partition per rank)
+from sharding import max_over_ranks, shard_seed  # noqa: E402  (row-group partition per rank)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """One process per GPU through torch.distributed.run, started before this process touches
+    the GPU; returns their exit status (rank 0 prints the JSON line)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 class Workload:
     """Synthetic pages generated on the host by the reference-identical writers of
-    libpqgpu.so (encoders.cpp) and uploaded once to HBM."""
+    libpqgtools.so (tools/gen) and uploaded once to HBM."""
 
     def __init__(self, pqgpu, args, rank, kind, p_null=None):
         import torch
-        L = pqgpu.lib()
-        info = pqgpu.WorkloadInfo()
+        import pqgtools
+        L = pqgtools.lib()
+        info = pqgtools.WorkloadInfo()
         n = int(args.n)
-        seed = shard_seed(args.seed + 2, rank)
+        self.n = n
         self.kind = kind
         self.p_null = p_null
+        self.page_values = args.page_values
+        self.dict_size, self.delta_bits = args.dict_size, args.delta_bits
         if kind == "levels":
+            self.seed = shard_seed(args.seed + 2, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_levels_plain(
-                n, p_null, args.page_values, seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+                n, p_null, args.page_values, self.seed, args.threads, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
             self.es = 4
         elif kind == "dict":
-            seed = shard_seed(args.seed + 3, rank)
+            self.seed = shard_seed(args.seed + 3, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64(
-                n, args.dict_size, args.page_values, seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+                n, args.dict_size, args.page_values, self.seed, args.threads, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
         else:
-            seed = shard_seed(args.seed + 4, rank)
+            self.seed = shard_seed(args.seed + 4, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64(
-                n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, seed,
+                n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, self.seed,
                 args.threads, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
@@ -111,11 +143,11 @@ class Workload:
                 self.level_bytes_in += int.from_bytes(self.host[self.pages[i].offset:self.pages[i].offset + 4].tobytes(), "little") + 4
         self.out_bytes = (2 * nlev if self.col.max_def > 0 else 0) + self.values * self.es
 
-    def page_specs(self, count):
-        """First `count` pages as oracle page specs (CPU baseline leg only)."""
+    def page_specs(self, count, first=0):
+        """Pages [first, first + count) as oracle page specs (CPU baseline leg only)."""
         import pyoracle
         specs = []
-        for i in range(count):
+        for i in range(first, first + count):
             p = self.pages[i]
             buf = self.host[p.offset:p.offset + p.nbytes].tobytes()
             specs.append(pyoracle.PageSpec(p.page_type, buf, p.num_values, p.encoding, p.def_encoding,
@@ -123,31 +155,54 @@ class Workload:
         return specs
 
 
-def decode_once(pqgpu, ctx, w, stream):
+def decode_once(ctx, w, stream):
     ctx.decode_async(w.col, w.d_blob.data_ptr(), w.blob_len, w.pages, w.out, stream, npages=w.npages)
 
 
-def spot_check(pqgpu, ctx, w, stream):
-    """Sanity check before timing (parity itself is established by tests/ against the
-    oracle): the decode succeeds, yields exactly the generator's value count, and for
-    config 2 the number of def levels equal to max_def matches the value count."""
-    import torch
-    decode_once(pqgpu, ctx, w, stream)
+def check_values(ctx, w, stream):
+    """Decode once and compare sampled pages (first, middle, last) with the generator's own
+    content (pqg_truth_*: the levels and values the pages were written from), plus the status
+    and the value count. Parity itself is established by tests/ against the oracle."""
+    import pqgtools
+    L = pqgtools.lib()
+    decode_once(ctx, w, stream)
     st, bad = ctx.sync()
-    if os.environ.get("PQG_DEBUG"):  # diagnostics builds skip work: no result to check
-        return True
     assert st == 0, (st, bad, ctx.error_message())
     assert w.out.num_values == w.values, (w.out.num_values, w.values)
+    first = 1 if w.kind == "dict" else 0
+    ndata = w.npages - first
+    checked = 0
+    for k in sorted({0, ndata // 2, ndata - 1}):
+        cnt = w.pages[first + k].num_values
+        lo = k * w.page_values  # every page but the last holds page_values levels/values
+        if w.kind == "levels":
+            lv = np.zeros(cnt, np.int16)
+            vals = np.zeros(cnt, np.int32)
+            nn = L.pqg_truth_levels_plain(w.n, w.p_null, w.page_values, w.seed, k, lv.ctypes.data, vals.ctypes.data)
+            got_lv = w.d_def[lo:lo + cnt].cpu().numpy()
+            assert np.array_equal(got_lv, lv), f"def levels of page {k} differ from the generator"
+            voff = int((w.d_def[:lo] == 1).sum().item())
+            got_v = w.d_val[4 * voff:4 * (voff + nn)].cpu().numpy().view(np.int32)
+            assert np.array_equal(got_v, vals[:nn]), f"values of page {k} differ from the generator"
+        else:
+            vals = np.zeros(cnt, np.int64)
+            if w.kind == "dict":
+                L.pqg_truth_dict_int64(w.n, w.dict_size, w.page_values, w.seed, k, vals.ctypes.data)
+            else:
+                L.pqg_truth_delta_int64(w.n, w.delta_bits, w.page_values, w.seed, k, vals.ctypes.data)
+            got_v = w.d_val[8 * lo:8 * (lo + cnt)].cpu().numpy().view(np.int64)
+            assert np.array_equal(got_v, vals), f"values of page {k} differ from the generator"
+        checked += 1
     if w.d_def is not None:
         nn = int((w.d_def[: w.levels] == 1).sum().item())
         assert nn == w.values, (nn, w.values)
-    return True
+    return {"pages_checked": checked, "status": st, "values": int(w.out.num_values)}
 
 
 def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
     import torch
     for _ in range(warmup):
-        decode_once(pqgpu, ctx, w, stream)
+        decode_once(ctx, w, stream)
     ctx.sync()
     pqgpu.lib().pqg_reset_timings(ctx.h)
     if dist is not None:
@@ -155,53 +210,72 @@ def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        decode_once(pqgpu, ctx, w, stream)
+        decode_once(ctx, w, stream)
     st, bad = ctx.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    assert st == 0 or os.environ.get("PQG_DEBUG"), (st, bad, ctx.error_message())
+    assert st == 0, (st, bad, ctx.error_message())
     return (t1 - t0) / steps, ctx.timings()
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(w, seconds, threads):
-    """parquet-rs decode loop restated in C (oracle, kind "port"), one read_batch(1024)
-    column reader per thread over disjoint pages (the reference's Rc types are !Send, so
-    one reader per row group/thread is its only parallelism)."""
+    """parquet-rs's decode loop restated in C (oracle, kind "port"): ColumnReaderImpl::
+    read_batch(batch) per reader, one reader per thread over disjoint pages (the reference's Rc
+    types are !Send, so one reader per row group / thread is its only parallelism). Timed at 1
+    thread and at `threads` threads, batch sizes 32/64/128/1024, on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from concurrent.futures import ThreadPoolExecutor
     first = 1 if w.kind == "dict" else 0
     dict_spec = w.page_specs(1)[0] if w.kind == "dict" else None
-    # time one page to size the sample
-    sp = w.page_specs(first + 1)[first:]
-    t0 = time.perf_counter()
-    r = pyoracle.read_column(w.col.physical_type, ([dict_spec] if dict_spec else []) + sp,
-                             max_def=w.col.max_def, batch_size=1024)
-    one = time.perf_counter() - t0
-    assert r["status"] == 0
-    npg = max(threads, min(w.npages - first, int(seconds * threads / max(one, 1e-6))))
-    npg = min(npg, w.npages - first)
-    specs = w.page_specs(first + npg)[first:]
-    groups = [specs[i::threads] for i in range(threads)]
+    batches = (32, 64, 128, 1024)
+    legs = [(1, b) for b in batches] + [(threads, b) for b in batches]
+    budget = seconds / len(legs)
 
-    def run(g):
+    def run(g, b):
         pages = ([dict_spec] if dict_spec else []) + g
-        rr = pyoracle.read_column(w.col.physical_type, pages, max_def=w.col.max_def, batch_size=1024)
+        rr = pyoracle.read_column(w.col.physical_type, pages, max_def=w.col.max_def, batch_size=b)
         assert rr["status"] == 0, rr["message"]
         return sum(p.num_values for p in g)
 
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        n = sum(ex.map(run, groups))
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "values/s", "cores": threads, "kind": "port",
-            "sample": f"{npg} of {w.npages} pages ({n} levels/values), read_batch(1024) per "
-                      f"thread-owned reader, {dt:.1f}s wall"}
+    one = {}
+    for b in batches:  # time one page per batch size to size the samples
+        sp = w.page_specs(1, first)
+        t0 = time.perf_counter()
+        run(sp, b)
+        one[b] = time.perf_counter() - t0
+    res = {}
+    for th, b in legs:
+        npg = max(th, min(w.npages - first, int(budget * th / max(one[b], 1e-6))))
+        npg = min(npg, w.npages - first)
+        specs = w.page_specs(npg, first)
+        groups = [specs[i::th] for i in range(th)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(th) as ex:
+            n = sum(ex.map(lambda g: run(g, b), groups))
+        dt = time.perf_counter() - t0
+        res[(th, b)] = (n / dt, npg, n, dt)
+    head = res[(threads, 1024)]
+    return {"value": head[0], "unit": "values/s" if w.kind != "levels" else "levels/s",
+            "cores": threads, "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"{head[1]} of {w.npages} pages ({head[2]} levels/values), read_batch(1024), "
+                      f"one reader per thread, {head[3]:.1f}s wall",
+            "by_threads_batch": {f"{th}t_b{b}": round(v[0], 1) for (th, b), v in res.items()}}
 
 
-def pcie_inclusive(pqgpu, ctx, w, stream, iters=3):
+def pcie_inclusive(ctx, w, stream, iters=3):
     """Host-to-host rate of the same decode (north_star): pinned page bytes -> HBM, decode,
     decoded levels/values -> pinned host memory, all on the decode stream."""
     import torch
@@ -215,7 +289,7 @@ def pcie_inclusive(pqgpu, ctx, w, stream, iters=3):
         t0 = time.perf_counter()
         with torch.cuda.stream(s):
             w.d_blob.copy_(h_blob, non_blocking=True)
-            decode_once(pqgpu, ctx, w, stream)
+            decode_once(ctx, w, stream)
             if h_def is not None:
                 h_def.copy_(w.d_def[: w.levels], non_blocking=True)
             h_val.copy_(w.d_val[: w.values * w.es], non_blocking=True)
@@ -250,29 +324,56 @@ def pmc_traffic(kind, kernel):
 
 
 def copy_ceiling_gbs(nbytes=4 << 30):
-    import torch
-    a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
-    b = torch.empty_like(a)
-    for _ in range(3):
-        b.copy_(a)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 10
-    del a, b
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    """Achievable HBM rate on this device: a 16-byte-per-lane copy kernel
+    (tools/ubench/copy_ceiling.hip), best of plain and non-temporal."""
+    L = C.CDLL(os.path.join(ROOT, "tools", "ubench", "libpqgcopy.so"))
+    L.pqg_copy_ceiling_gbs.restype = C.c_double
+    L.pqg_copy_ceiling_gbs.argtypes = [C.c_uint64, C.c_int]
+    return L.pqg_copy_ceiling_gbs(nbytes, 10)
 
 
-def main():
-    args = parse()
-    import torch
+def dry_run(args, world, rank, dist):
+    """Launcher / partition / reduction plumbing without a GPU: every rank derives its own
+    partition seed, the max-over-ranks step time is reduced over gloo, rank 0 prints a line
+    marked dry_run with no value."""
+    seed = shard_seed(args.seed + 2, rank)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    per_step = max_over_ranks(time.perf_counter() - t0, dist)
+    seeds = [seed]
+    if dist is not None:
+        seeds = [None] * world
+        dist.all_gather_object(seeds, seed)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "values/s", "n_gpus": world,
+                          "steps": 0, "warmup": 0, "ms_per_step": per_step * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dry_run": True,
+                          "config": {"workload": args.config, "partition_seeds": seeds,
+                                     "parallelism": f"row-group partitions x{world}, no collective"}}),
+              flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if os.environ.get("PQG_DEBUG"):
+        sys.exit("bench.py: PQG_DEBUG is set; diagnostic modes are not a valid measurement")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dist = None
+        if world > 1:
+            import torch.distributed as td
+            td.init_process_group("gloo")
+            dist = td
+        dry_run(args, world, rank, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as td
@@ -282,15 +383,14 @@ def main():
     else:
         torch.cuda.set_device(0)
     import pqgpu
-    import sharding
     ctx = pqgpu.Context(torch.cuda.current_device(), timing=True)
     stream = torch.cuda.current_stream().cuda_stream
 
     kind = args.config
     w = Workload(pqgpu, args, rank, kind, p_null=args.p_null if kind == "levels" else None)
-    spot_check(pqgpu, ctx, w, stream)
+    checked = check_values(ctx, w, stream)
     per_step, tm = time_steps(pqgpu, ctx, w, stream, args.steps, args.warmup, dist)
-    per_step = sharding.max_over_ranks(per_step, dist, device="cuda")
+    per_step = max_over_ranks(per_step, dist, device="cuda")
     units = w.levels if kind == "levels" else w.values
     value = units * world / per_step
     step_bytes = w.in_bytes + w.out_bytes
@@ -311,7 +411,7 @@ def main():
     achieved = nbytes / (ms * 1e-3) / 1e9
 
     result = {
-        "metric": "decoded values/s + GB/s, device-resident page decode, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": value,
         "unit": "values/s",
         "n_gpus": world,
@@ -337,10 +437,12 @@ def main():
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms},
+                     "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms,
+                     "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
         "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
                       "values": tm.values_ms, "total": tm.total_ms,
                       "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},
+        "value_check": checked,
     }
     if rank == 0:
         try:
@@ -348,7 +450,7 @@ def main():
         except Exception as e:  # pragma: no cover
             result["copy_ceiling_gbs"] = str(e)
     if rank == 0 and args.pcie and world == 1:
-        result["pcie_inclusive"] = pcie_inclusive(pqgpu, ctx, w, stream)
+        result["pcie_inclusive"] = pcie_inclusive(ctx, w, stream)
     if rank == 0 and args.cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, min(args.threads, os.cpu_count() or 1))
     if kind == "levels" and args.variants and world == 1:
@@ -357,18 +459,14 @@ def main():
             del w
             torch.cuda.empty_cache()
             wv = Workload(pqgpu, args, rank, "levels", p_null=p)
-            spot_check(pqgpu, ctx, wv, stream)
+            check_values(ctx, wv, stream)
             ps, tv = time_steps(pqgpu, ctx, wv, stream, max(3, args.steps // 2), 2)
             var[f"p_null={p}"] = {"levels_per_s": wv.levels / ps, "ms_per_step": ps * 1e3,
                                   "gbps": (wv.in_bytes + wv.out_bytes) / ps / 1e9,
-                                  "levels_ms": tv.levels_ms, "values_ms": tv.values_ms}
+                                  "levels_ms": tv.levels_ms, "values_ms": tv.values_ms,
+                                  "levels_kernel_ms": tv.levels_kernel_ms}
             w = wv
         result["variants"] = var
-    if os.environ.get("PQG_DEBUG") and int(os.environ["PQG_DEBUG"]) & 48:
-        st4 = (C.c_double * 4)()
-        pqgpu.lib().pqg_debug_stamps(ctx.h, st4)
-        result["debug_stamps"] = {"waves": st4[3], "desc_cyc": st4[0], "expand_cyc": st4[1],
-                                  "tail_cyc": st4[2]}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

@@ -1521,8 +1521,15 @@ static uint64_t delta_sub_u64(int t, int64_t l, int64_t r) {
   return (uint64_t)l - (uint64_t)r;
 }
 
-size_t or_delta_encode(int t, const void *values, size_t n, uint8_t *out, size_t cap) {
-  const size_t block_size = 128, num_mini_blocks = 4, mini = 32;
+/* Block shape: the reference encoder always writes 128 / 4 x 32 (encoding.rs:508-509); the
+ * decoder accepts any block with values_per_mini_block % 8 == 0 (decoding.rs:529-530), so the
+ * generator also takes other shapes (BASELINE config 4: 512 / 4 x 128). */
+size_t or_delta_encode_shape(int t, const void *values, size_t n, size_t block_size,
+                             size_t num_mini_blocks, uint8_t *out, size_t cap) {
+  if (block_size == 0 || num_mini_blocks == 0 || block_size % num_mini_blocks ||
+      (block_size / num_mini_blocks) % 8 || block_size > 65536)
+    return (size_t)-1;
+  const size_t mini = block_size / num_mini_blocks;
   uint8_t hdr[32];
   or_bit_writer hw;
   memset(hdr, 0, sizeof(hdr));
@@ -1531,7 +1538,7 @@ size_t or_delta_encode(int t, const void *values, size_t n, uint8_t *out, size_t
   uint8_t *body = (uint8_t *)calloc(body_cap ? body_cap : 1, 1);
   or_bit_writer w;
   bw_init(&w, body, body_cap, 0);
-  int64_t deltas[128];
+  int64_t *deltas = (int64_t *)malloc(block_size * sizeof(int64_t));
   size_t in_block = 0;
   int64_t first = 0, cur = 0;
   int ok = 1;
@@ -1583,6 +1590,7 @@ size_t or_delta_encode(int t, const void *values, size_t n, uint8_t *out, size_t
   ok &= bw_flush(&hw);
   ok &= bw_flush(&w);
   size_t total = hw.byte_offset + w.byte_offset;
+  free(deltas);
   if (!ok || total > cap) {
     free(body);
     return (size_t)-1;
@@ -1591,6 +1599,10 @@ size_t or_delta_encode(int t, const void *values, size_t n, uint8_t *out, size_t
   memcpy(out + hw.byte_offset, body, w.byte_offset);
   free(body);
   return total;
+}
+
+size_t or_delta_encode(int t, const void *values, size_t n, uint8_t *out, size_t cap) {
+  return or_delta_encode_shape(t, values, n, 128, 4, out, cap);
 }
 
 /* DeltaLengthByteArrayEncoder, encoding.rs:796-859 */

@@ -203,6 +203,9 @@ size_t or_plain_encode(int physical_type, const void *values, size_t n, uint8_t 
                        size_t cap);
 size_t or_delta_encode(int physical_type, const void *values, size_t n, uint8_t *out,
                        size_t cap);
+/* Same with any block shape (block_size / num_mini_blocks values per mini-block, a multiple of 8). */
+size_t or_delta_encode_shape(int physical_type, const void *values, size_t n, size_t block_size,
+                             size_t num_mini_blocks, uint8_t *out, size_t cap);
 /* DictEncoder (encoding.rs:200-387): returns number of uniques; writes the PLAIN dict page
  * to dict_out (*dict_len) and [bit_width][RLE] indices to idx_out (*idx_len). For
  * fixed-width types only (elem_size bytes per value). */

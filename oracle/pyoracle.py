@@ -94,6 +94,7 @@ def _declare(L):
         ("or_level_encode", [C.c_int, C.c_int, C.c_int16, vp, sz, vp, sz]),
         ("or_plain_encode", [C.c_int, vp, sz, vp, sz]),
         ("or_delta_encode", [C.c_int, vp, sz, vp, sz]),
+        ("or_delta_encode_shape", [C.c_int, vp, sz, sz, sz, vp, sz]),
         ("or_dict_encode", [vp, sz, sz, vp, sz, szp, vp, sz, szp]),
         ("or_rle_bool_encode", [vp, sz, vp, sz]),
         ("or_plain_encode_ba", [vp, vp, sz, C.c_int, vp, sz]),
@@ -228,10 +229,14 @@ def plain_encode(ptype, values):
     return _enc(lib().or_plain_encode, ptype, _ptr(v), len(v), cap=cap)
 
 
-def delta_encode(ptype, values):
+def delta_encode(ptype, values, block_size=128, mini_blocks=4):
+    """DeltaBitPackEncoder (encoding.rs:534-714); the reference writes 128 / 4 x 32 blocks,
+    other shapes exercise what the decoder accepts (decoding.rs:501-533)."""
     v = np.ascontiguousarray(values, dtype=np.int32 if ptype == INT32 else np.int64)
-    cap = len(v) * 10 + 256
-    return _enc(lib().or_delta_encode, ptype, _ptr(v), len(v), cap=cap)
+    cap = len(v) * 10 + 256 + 16 * (len(v) // max(block_size, 1) + 2)
+    if (block_size, mini_blocks) == (128, 4):
+        return _enc(lib().or_delta_encode, ptype, _ptr(v), len(v), cap=cap)
+    return _enc(lib().or_delta_encode_shape, ptype, _ptr(v), len(v), block_size, mini_blocks, cap=cap)
 
 
 def dict_encode(values):

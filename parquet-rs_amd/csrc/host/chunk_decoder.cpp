@@ -305,13 +305,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
                      const pqg_page* pages, uint32_t npages, pqg_output* out, void* stream_v) {
   if (!ctx || !col || !out || (npages && !pages)) return PQG_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream_v;
-  HIPCHK(hipSetDevice(ctx->device), "hipSetDevice");
-  ctx->msg.clear();
-  ctx->host_status = 0;
-  ctx->host_bad_page = -1;
-  ctx->out = out;
-  ctx->stream = s;
-  out->num_levels = out->num_values = out->num_bytes = 0;
+  // ---- argument checks first: a rejected call leaves the context (and a decode still in
+  // flight on it) untouched, so a later pqg_sync reports that decode's own status
   auto misaligned = [](const void* p) { return p && ((uintptr_t)p & 15u); };
   if (misaligned(out->def_levels) || misaligned(out->rep_levels) || misaligned(out->values))
     return set_err(ctx, PQG_ERR_INVALID, "output buffers must be 16-byte aligned");
@@ -319,6 +314,21 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (t < 0 || t > 7) return set_err(ctx, PQG_ERR_INVALID, "bad physical type %d", t);
   if (t == PQG_FIXED_LEN_BYTE_ARRAY && col->type_length <= 0)
     return set_err(ctx, PQG_ERR_PANIC, "FLBA requires type_length > 0");
+  if ((t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) && out->values) {
+    uint64_t nlev = 0;
+    for (uint32_t i = 0; i < npages; ++i)
+      if (pages[i].page_type == PQG_PAGE_DATA || pages[i].page_type == PQG_PAGE_DATA_V2)
+        nlev += pages[i].num_values;
+    if (!out->offsets || out->offsets_capacity < nlev + 1)
+      return set_err(ctx, PQG_ERR_INVALID, "BYTE_ARRAY/FLBA output needs offsets[num_levels + 1]");
+  }
+  HIPCHK(hipSetDevice(ctx->device), "hipSetDevice");
+  ctx->msg.clear();
+  ctx->host_status = 0;
+  ctx->host_bad_page = -1;
+  ctx->out = out;
+  ctx->stream = s;
+  out->num_levels = out->num_values = out->num_bytes = 0;
 
   // ---- staging slot: wait until its previous decode has finished, harvest its timings
   ctx->cur ^= 1;
@@ -401,7 +411,13 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
   cp.want_def = want_def;
   cp.want_rep = want_rep;
+  // Diagnostic kernel modes exist only in a PQG_DIAG build (make DIAG=1); the shipped library
+  // never reads the environment and always runs the production path.
+#ifdef PQG_DIAG
   static const int dbg_env = getenv("PQG_DEBUG") ? atoi(getenv("PQG_DEBUG")) : 0;
+#else
+  const int dbg_env = 0;
+#endif
   cp.debug = dbg_env;
   cp.dbgbuf = nullptr;
   if (dbg_env & 48) {
@@ -428,8 +444,6 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   const int es = is_ba ? 0 : value_size(t, col->type_length);
   const int np = (int)npages;
   if (is_ba && out->values) {
-    if (!out->offsets || out->offsets_capacity < lev_needed + 1)
-      return set_err(ctx, PQG_ERR_INVALID, "BYTE_ARRAY/FLBA output needs offsets[num_levels + 1]");
     size_t need = lev_needed ? lev_needed : 1;
     if (need > sl.vcap) {
       hipFree(sl.vsrc);

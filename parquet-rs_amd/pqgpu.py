@@ -57,20 +57,13 @@ class Timings(C.Structure):
                 ("levels_kernel_ms", C.c_float), ("values_kernel_ms", C.c_float)]
 
 
-class WorkloadInfo(C.Structure):
-    _fields_ = [("blob_len", C.c_uint64), ("npages", C.c_uint32), ("total_levels", C.c_uint64),
-                ("total_values", C.c_uint64)]
-
-
 EXPORTS = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_sync",
     "pqg_get_timings", "pqg_reset_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
     "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
-    "pqg_column_reader_read_batch", "pqg_encode_rle", "pqg_encode_levels_v1", "pqg_encode_delta",
-    "pqg_encode_dict_indices", "pqg_gen_levels_plain", "pqg_gen_dict_int64",
-    "pqg_gen_delta_int64",
+    "pqg_column_reader_read_batch",
 ]
 
 _lib = None
@@ -115,21 +108,6 @@ def lib():
         L.pqg_column_reader_close.restype = None
         L.pqg_column_reader_read_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, u64, vp,
                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
-        for name in ("pqg_gen_levels_plain",):
-            getattr(L, name).argtypes = [u64, C.c_double, C.c_uint32, u64, i32, vp, u64,
-                                         C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
-        L.pqg_gen_dict_int64.argtypes = [u64, C.c_uint32, C.c_uint32, u64, i32, vp, u64,
-                                         C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
-        L.pqg_gen_delta_int64.argtypes = [u64, i32, C.c_uint32, i32, i32, u64, i32, vp, u64,
-                                          C.POINTER(Page), C.c_uint32, C.POINTER(WorkloadInfo)]
-        L.pqg_encode_rle.restype = u64
-        L.pqg_encode_rle.argtypes = [vp, u64, i32, vp, u64]
-        L.pqg_encode_levels_v1.restype = u64
-        L.pqg_encode_levels_v1.argtypes = [vp, u64, C.c_int16, vp, u64]
-        L.pqg_encode_delta.restype = u64
-        L.pqg_encode_delta.argtypes = [i32, vp, u64, i32, i32, vp, u64]
-        L.pqg_encode_dict_indices.restype = u64
-        L.pqg_encode_dict_indices.argtypes = [vp, u64, i32, vp, u64]
         _lib = L
     return _lib
 

@@ -4,7 +4,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "parquet-rs_amd")):
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "parquet-rs_amd"),
+          os.path.join(ROOT, "tools", "gen")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

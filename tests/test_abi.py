@@ -22,7 +22,9 @@ def declared_functions():
 def test_header_declares_entry_points():
     names = declared_functions()
     assert "pqg_decode_chunk" in names and "pqg_column_reader_read_batch" in names
-    assert len(names) >= 25
+    assert len(names) >= 20
+    # bench/test writers live in the tools library, not in the decode library's ABI
+    assert not any(n.startswith(("pqg_gen_", "pqg_encode_", "pqg_truth_")) for n in names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -43,11 +45,27 @@ def test_status_codes_match_header():
     assert int(codes["PQG_ERR_HIP"]) == pqgpu.HIP
 
 
+def test_decode_library_has_no_tooling_symbols():
+    """Workload generators and writers are tooling (tools/gen/libpqgtools.so): the product
+    library neither exports nor links them."""
+    import pqgpu
+    lib = ctypes.CDLL(pqgpu.LIB_PATH)
+    for name in ("pqg_gen_levels_plain", "pqg_encode_rle", "pqg_truth_delta_int64"):
+        assert not hasattr(lib, name), name
+
+
+def test_tools_library_exports():
+    import pqgtools
+    lib = pqgtools.lib()
+    for name in pqgtools.EXPORTS:
+        assert hasattr(lib, name), name
+
+
 def test_no_gpu_needed_for_host_entry_points():
     """Host-only entry points (writers, file reader) run without a device."""
     import numpy as np
-    import pqgpu
-    L = pqgpu.lib()
+    import pqgtools
+    L = pqgtools.lib()
     vals = np.arange(100, dtype=np.uint64) % 4
     out = np.zeros(256, np.uint8)
     n = L.pqg_encode_rle(vals.ctypes.data, 100, 2, out.ctypes.data, 256)

@@ -1,5 +1,5 @@
-"""CPU tests: the product's reference-identical writers and workload generators
-(parquet-rs_amd/csrc/host/encoders.cpp) against the oracle's restated writers/decoders."""
+"""CPU tests: the tooling's reference-identical writers and workload generators
+(tools/gen/pqg_gen.cpp, libpqgtools.so) against the oracle's restated writers/decoders."""
 import ctypes as C
 
 import numpy as np
@@ -9,7 +9,9 @@ import pytest
 @pytest.fixture(scope="module")
 def pq():
     import pqgpu
-    return pqgpu
+    import pqgtools
+    pqgtools.Page = pqgpu.Page
+    return pqgtools
 
 
 def _enc(fn, *args, cap):
@@ -126,3 +128,39 @@ def test_gen_delta(pq, oracle, bs, nmb):
         for s in specs:
             st, v, off, tot = oracle.delta_decode(oracle.INT64, s.buf, s.num_values)
             assert oracle.delta_encode(oracle.INT64, v) == s.buf
+
+
+@pytest.mark.parametrize("kind", ["levels", "dict", "delta"])
+def test_truth_matches_generated_pages(pq, oracle, kind):
+    """pqg_truth_* (the bench's value check) regenerates exactly what the generator encoded:
+    the oracle's decode of generated page k equals the truth of page k."""
+    L = pq.lib()
+    n, pv = 200000, 65536
+    if kind == "levels":
+        blob, pages, info = _gen(pq, "levels", n=n, p=0.3, pv=pv)
+    elif kind == "dict":
+        blob, pages, info = _gen(pq, "dict", n=n, dict=4096, pv=pv)
+    else:
+        blob, pages, info = _gen(pq, "delta", n=n, pv=pv)
+    specs = _specs(oracle, blob, pages)
+    first = 1 if kind == "dict" else 0
+    for k in (0, len(specs) - first - 1):
+        sel = ([specs[0]] if first else []) + [specs[first + k]]
+        r = oracle.read_column(oracle.INT32 if kind == "levels" else oracle.INT64, sel,
+                               max_def=1 if kind == "levels" else 0)
+        assert r["status"] == 0
+        cnt = specs[first + k].num_values
+        if kind == "levels":
+            lv = np.zeros(cnt, np.int16)
+            vals = np.zeros(cnt, np.int32)
+            nn = L.pqg_truth_levels_plain(n, 0.3, pv, 7, k, lv.ctypes.data, vals.ctypes.data)
+            np.testing.assert_array_equal(r["def"], lv)
+            np.testing.assert_array_equal(r["values"], vals[:nn])
+        else:
+            vals = np.zeros(cnt, np.int64)
+            if kind == "dict":
+                got = L.pqg_truth_dict_int64(n, 4096, pv, 7, k, vals.ctypes.data)
+            else:
+                got = L.pqg_truth_delta_int64(n, 16, pv, 7, k, vals.ctypes.data)
+            assert got == cnt
+            np.testing.assert_array_equal(r["values"], vals)

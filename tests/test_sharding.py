@@ -58,3 +58,33 @@ def test_gloo_world2_partition_and_max():
         assert flat == list(range(33))
         assert abs(t - 0.020) < 1e-12  # slowest rank
         assert len(set(seeds)) == world
+
+
+@pytest.mark.timeout(240)
+def test_bench_launches_n_ranks_dry_run():
+    """bench.py --gpus 2 starts two ranks itself (torch.distributed.run, 127.0.0.1) when no
+    WORLD_SIZE is set; on the gloo dry path rank 0 prints one line with n_gpus 2 and both
+    ranks' distinct partition seeds."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=220, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["dry_run"] is True and res["value"] is None
+    assert len(set(res["config"]["partition_seeds"])) == 2
+
+
+def test_bench_refuses_debug_env():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PQG_DEBUG="256")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "PQG_DEBUG" in r.stderr

@@ -1,4 +1,5 @@
-// encoders.cpp — reference-identical page writers and the synthetic workload generators.
+// pqg_gen.cpp — reference-identical page writers and the synthetic workload generators
+// (libpqgtools.so: bench and test tooling, not part of the decode library libpqgpu.so).
 //
 // The writers restate parquet-rs's encoders so the generated pages are byte-for-byte what
 // the reference would write:
@@ -8,8 +9,9 @@
 //   DictEncoder indices  encodings/encoding.rs:338-355 ([bit width][RLE hybrid])
 //   DeltaBitPackEncoder  encodings/encoding.rs:534-714 (block size / mini-block count are
 //                        parameters; the reference fixes 128 / 4, encoding.rs:508-509)
-// The generators build BASELINE.json configs 2-4 page by page on host threads (pages are
-// independent) for bench.py; see DESIGN.md §4.
+// The generators build BASELINE.json configs 2-5 page by page on host threads (pages are
+// independent) for bench.py; the pqg_truth_* entry points regenerate one page's raw
+// levels / values so the bench can check decoded output against the generator.
 #include <stdint.h>
 #include <string.h>
 
@@ -17,7 +19,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../../include/pqgpu.h"
+#include "pqg_gen.h"
 
 namespace {
 
@@ -314,6 +316,26 @@ uint64_t pqg_encode_dict_indices(const uint32_t* idx, uint64_t n, int bit_width,
 }
 
 // ------------------------------------------------------------------ config 2
+// Raw content of config-2 page p: levels (1 = non-null) and the non-null INT32 values.
+static uint64_t levels_page(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed, uint32_t p,
+                            std::vector<int16_t>& lv, int32_t* vals) {
+  const uint64_t cnt = std::min<uint64_t>(page_levels, n - (uint64_t)p * page_levels);
+  // a level is null with probability p_null: compare 53-bit uniforms against the threshold
+  const uint64_t thresh = (uint64_t)(p_null * 9007199254740992.0);
+  uint64_t s = page_seed(seed, p);
+  lv.resize(cnt);
+  uint64_t nn = 0;
+  for (uint64_t i = 0; i < cnt; ++i) {
+    lv[i] = (splitmix64(s) >> 11) >= thresh ? 1 : 0;
+    nn += (uint64_t)lv[i];
+  }
+  for (uint64_t i = 0; i < nn; ++i) {
+    int32_t x = (int32_t)(uint32_t)splitmix64(s);
+    memcpy((uint8_t*)vals + 4 * i, &x, 4);  // unaligned PLAIN section
+  }
+  return nn;
+}
+
 int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
                          int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
                          uint32_t pages_cap, pqg_workload_info* info) {
@@ -326,25 +348,15 @@ int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64
   info->total_values = 0;
   if (!blob) return PQG_OK;
   if (blob_cap < slot * np || pages_cap < np) return PQG_ERR_CAPACITY;
-  // a level is null with probability p_null: compare 53-bit uniforms against the threshold
-  const uint64_t thresh = (uint64_t)(p_null * 9007199254740992.0);
   std::vector<uint64_t> nonnull(np);
   parallel_pages(np, threads, [&](uint32_t p) {
-    const uint64_t cnt = std::min<uint64_t>(page_levels, n - (uint64_t)p * page_levels);
     uint8_t* out = blob + (uint64_t)p * slot;
-    uint64_t s = page_seed(seed, p);
-    std::vector<int16_t> lv(cnt);
-    uint64_t nn = 0;
-    for (uint64_t i = 0; i < cnt; ++i) {
-      lv[i] = (splitmix64(s) >> 11) >= thresh ? 1 : 0;
-      nn += (uint64_t)lv[i];
-    }
+    std::vector<int16_t> lv;
+    std::vector<int32_t> vals(page_levels);
+    const uint64_t nn = levels_page(n, p_null, page_levels, seed, p, lv, vals.data());
+    const uint64_t cnt = lv.size();
     uint64_t ll = pqg_encode_levels_v1(lv.data(), cnt, 1, out, slot - 4 * cnt);
-    int32_t* vals = reinterpret_cast<int32_t*>(out + ll);  // PLAIN INT32 (unaligned ok on x86)
-    for (uint64_t i = 0; i < nn; ++i) {
-      int32_t x = (int32_t)(uint32_t)splitmix64(s);
-      memcpy((uint8_t*)vals + 4 * i, &x, 4);
-    }
+    memcpy(out + ll, vals.data(), 4 * nn);
     pqg_page& pg = pages[p];
     pg.offset = (uint64_t)p * slot;
     pg.nbytes = (uint32_t)(ll + 4 * nn);
@@ -360,7 +372,32 @@ int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64
   return PQG_OK;
 }
 
+uint64_t pqg_truth_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
+                                uint32_t page, int16_t* levels, int32_t* values) {
+  std::vector<int16_t> lv;
+  const uint64_t nn = levels_page(n, p_null, page_levels, seed, page, lv, values);
+  memcpy(levels, lv.data(), lv.size() * 2);
+  return nn;
+}
+
 // ------------------------------------------------------------------ config 3
+static void dict_values(uint32_t dict_size, uint64_t seed, uint8_t* out) {
+  // distinct values (SplitMix64 of distinct counters is a bijection)
+  uint64_t ds = seed ^ 0xD1C7D1C7ull;
+  for (uint32_t i = 0; i < dict_size; ++i) {
+    uint64_t x = splitmix64(ds);
+    memcpy(out + 8ull * i, &x, 8);
+  }
+}
+
+static void dict_page_indices(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                              uint32_t p, std::vector<uint32_t>& idx) {
+  const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+  uint64_t s = page_seed(seed, p);
+  idx.resize(cnt);
+  for (uint64_t i = 0; i < cnt; ++i) idx[i] = (uint32_t)((splitmix64(s) >> 32) * dict_size >> 32);
+}
+
 int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
                        int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
                        uint32_t pages_cap, pqg_workload_info* info) {
@@ -375,28 +412,46 @@ int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uin
   info->total_values = n;
   if (!blob) return PQG_OK;
   if (blob_cap < info->blob_len || pages_cap < ndata + 1) return PQG_ERR_CAPACITY;
-  // dictionary: distinct values (SplitMix64 of distinct counters is a bijection)
-  uint64_t ds = seed ^ 0xD1C7D1C7ull;
-  for (uint32_t i = 0; i < dict_size; ++i) {
-    uint64_t x = splitmix64(ds);
-    memcpy(blob + 8ull * i, &x, 8);
-  }
+  dict_values(dict_size, seed, blob);
   pages[0] = pqg_page{0, 8u * dict_size, dict_size, PQG_PAGE_DICTIONARY, PQG_PLAIN_DICTIONARY,
                       PQG_RLE, PQG_RLE, 0, 0};
   parallel_pages(ndata, threads, [&](uint32_t p) {
-    const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
     uint8_t* out = blob + dslot + (uint64_t)p * slot;
-    uint64_t s = page_seed(seed, p);
-    std::vector<uint32_t> idx(cnt);
-    for (uint64_t i = 0; i < cnt; ++i) idx[i] = (uint32_t)((splitmix64(s) >> 32) * dict_size >> 32);
-    uint64_t l = pqg_encode_dict_indices(idx.data(), cnt, bw, out, slot);
-    pages[p + 1] = pqg_page{dslot + (uint64_t)p * slot, (uint32_t)l, (uint32_t)cnt, PQG_PAGE_DATA,
+    std::vector<uint32_t> idx;
+    dict_page_indices(n, dict_size, page_values, seed, p, idx);
+    uint64_t l = pqg_encode_dict_indices(idx.data(), idx.size(), bw, out, slot);
+    pages[p + 1] = pqg_page{dslot + (uint64_t)p * slot, (uint32_t)l, (uint32_t)idx.size(), PQG_PAGE_DATA,
                             PQG_PLAIN_DICTIONARY, PQG_RLE, PQG_BIT_PACKED, 0, 0};
   });
   return PQG_OK;
 }
 
+uint64_t pqg_truth_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                              uint32_t page, int64_t* values) {
+  std::vector<uint8_t> d(8ull * dict_size);
+  dict_values(dict_size, seed, d.data());
+  std::vector<uint32_t> idx;
+  dict_page_indices(n, dict_size, page_values, seed, page, idx);
+  for (size_t i = 0; i < idx.size(); ++i) memcpy(values + i, d.data() + 8ull * idx[i], 8);
+  return idx.size();
+}
+
 // ------------------------------------------------------------------ config 4
+static void delta_page_values(uint64_t n, int delta_bits, uint32_t page_values, uint64_t seed,
+                              uint32_t p, std::vector<int64_t>& v) {
+  const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+  uint64_t s = page_seed(seed, p);
+  v.resize(cnt);
+  uint64_t acc = splitmix64(s);
+  const uint64_t span = 1ull << delta_bits;
+  const int64_t half = (int64_t)(span >> 1);
+  for (uint64_t i = 0; i < cnt; ++i) {
+    v[i] = (int64_t)acc;
+    int64_t d = (int64_t)((splitmix64(s) >> (64 - delta_bits))) - half;
+    acc += (uint64_t)d;  // wrapping prefix sum
+  }
+}
+
 int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
                         int mini_blocks, uint64_t seed, int threads, uint8_t* blob,
                         uint64_t blob_cap, pqg_page* pages, uint32_t pages_cap,
@@ -413,24 +468,23 @@ int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int bl
   if (blob_cap < info->blob_len || pages_cap < np) return PQG_ERR_CAPACITY;
   int rc = PQG_OK;
   parallel_pages(np, threads, [&](uint32_t p) {
-    const uint64_t cnt = std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
-    uint64_t s = page_seed(seed, p);
-    std::vector<int64_t> v(cnt);
-    uint64_t acc = splitmix64(s);
-    const uint64_t span = 1ull << delta_bits;
-    const int64_t half = (int64_t)(span >> 1);
-    for (uint64_t i = 0; i < cnt; ++i) {
-      v[i] = (int64_t)acc;
-      int64_t d = (int64_t)((splitmix64(s) >> (64 - delta_bits))) - half;
-      acc += (uint64_t)d;  // wrapping prefix sum
-    }
+    std::vector<int64_t> v;
+    delta_page_values(n, delta_bits, page_values, seed, p, v);
     uint8_t* out = blob + (uint64_t)p * slot;
-    uint64_t l = delta_encode(v.data(), cnt, block_size, mini_blocks, out, slot);
+    uint64_t l = delta_encode(v.data(), v.size(), block_size, mini_blocks, out, slot);
     if (!l) rc = PQG_ERR_CAPACITY;
-    pages[p] = pqg_page{(uint64_t)p * slot, (uint32_t)l, (uint32_t)cnt, PQG_PAGE_DATA,
+    pages[p] = pqg_page{(uint64_t)p * slot, (uint32_t)l, (uint32_t)v.size(), PQG_PAGE_DATA,
                         PQG_DELTA_BINARY_PACKED, PQG_RLE, PQG_BIT_PACKED, 0, 0};
   });
   return rc;
+}
+
+uint64_t pqg_truth_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, uint64_t seed,
+                               uint32_t page, int64_t* values) {
+  std::vector<int64_t> v;
+  delta_page_values(n, delta_bits, page_values, seed, page, v);
+  memcpy(values, v.data(), v.size() * 8);
+  return v.size();
 }
 
 }  // extern "C"
