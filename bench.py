@@ -400,7 +400,8 @@ def main(argv=None):
     if kind == "levels":
         lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
         val_b = 2 * w.values * w.es               # PLAIN values in + out
-        stages = [("k_texpand_levels", tm.levels_kernel_ms, lev_b),
+        # the def-level path (pqg_levels.hip kernels) and the PLAIN copy
+        stages = [("k_lv_emit", tm.levels_kernel_ms, lev_b),
                   ("k_plain_copy", tm.values_kernel_ms, val_b)]
     elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
         stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]

@@ -128,7 +128,7 @@ typedef struct pqg_ctx pqg_ctx;
 typedef struct {
   float prepare_ms, levels_ms, scan_ms, values_ms, total_ms;
   uint32_t values_kernel; /* encoding whose kernel dominated values_ms */
-  float levels_kernel_ms; /* the def-level expand (or page) kernel alone, 0 if none */
+  float levels_kernel_ms; /* the def-level path kernels alone, 0 if none */
   float values_kernel_ms; /* the values stage's dominant kernel alone, 0 if none */
 } pqg_timings;
 

@@ -2,19 +2,20 @@
 //
 //   k_prepare        page layout: level streams + value section per page
 //                    (column/reader.rs:269-380, levels.rs:191-233)
-//   k_rle_levels     RLE/bit-packing hybrid -> i16 def/rep levels + non-null count
-//                    (rle.rs:398-434, levels.rs:249-271, column/reader.rs:212-226)
+//   k_run_index, k_tile_desc, k_texpand_*  the general RLE/bit-packing hybrid decoder
+//                    (rle.rs:398-487, levels.rs:249-271): dictionary indices, and the level /
+//                    boolean streams the level path hands back
 //   k_scan_values    dense value offsets per page (column/reader.rs:252-253)
-//   k_dict_gather    RLE_DICTIONARY indices -> dictionary gather (rle.rs:437-487,
+//   k_texpand_dict   RLE_DICTIONARY indices -> dictionary gather (rle.rs:437-487,
 //                    decoding.rs:256-315)
 //   k_plain_copy     PLAIN fixed-width values (decoding.rs:138-186, 228-247)
 //   k_plain_bool     PLAIN booleans (decoding.rs:188-204)
 //   k_finalize       chunk status
 //
-// All work is integer/byte movement bound by HBM: no MFMA. The RLE/bit-packed hybrid decoder
-// (index pass + grid-wide expand pass) is in pqg_runs.hpp.
-#include "pqg_rlepage.hpp"
-#include "pqg_parpage.hpp"
+// All work is integer/byte movement bound by HBM: no MFMA. The general RLE/bit-packing hybrid
+// decoder (index pass + grid-wide expand pass) is in pqg_runs.hpp / pqg_texpand.hpp; level
+// streams and RLE booleans take the fast path of pqg_levels.hip first.
+#include "pqg_texpand.hpp"
 
 namespace pqg {
 
@@ -162,30 +163,6 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
 }
 
 
-// Index pass of dense level / boolean streams: run_index_par with a 256-thread workgroup per
-// page; the streams it hands back are flagged PF_BAIL for k_run_index(bailed_only).
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2, 2))) k_run_index_par(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                      PageWork* pages, ColumnParams cp, int sel,
-                                                      RunTables rt, ChunkResult* res) {
-  __shared__ ParIndexSmem sm;
-  const int p = blockIdx.x;
-  if (*rt.nfall == 0 || rt.pflag[p] == PF_PAGE) return;  // decoded by the page pass
-  const PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  Stream s;
-  if (!get_stream(blob, pw, sel, cp, s)) return;
-  RunCkpt* ck = rt.ck + pw.ltile0;
-  uint2* runs = rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT;
-  uint32_t* nr = rt.nruns + pw.ltile0;
-  const int32_t st = run_index_par(blob, blob_len, s, ck, runs, nr, sm,
-                                   (cp.debug & 32) && cp.dbgbuf ? cp.dbgbuf + 2 * p : nullptr);
-  if (st == PR_BAIL) {  // k_run_index (bailed_only) walks it
-    if (threadIdx.x == 0) rt.pflag[p] = PF_BAIL;
-    return;
-  }
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
-}
-
 // Quarter-tile descriptors of stream `sel` (one thread per quarter), read by the wave expand
 // kernels.
 __global__ void __launch_bounds__(WG) k_quarter_desc(const uint8_t* __restrict__ blob, const PageWork* pages,
@@ -236,9 +213,8 @@ struct LevelsMaker {
   }
 PQG_TEXPAND_LEVELS(k_texpand_levels, __attribute__((amdgpu_waves_per_eu(8, 8))))
 
-// Tile expand of RLE_DICTIONARY indices with the dictionary gather. MODE 1 (diagnostics,
-// PQG_DEBUG bits 8-11 = 1) writes the index instead of gathering.
-template <int ES, int MODE>
+// Tile expand of RLE_DICTIONARY indices with the dictionary gather.
+template <int ES>
 struct DictMaker {
   const uint8_t* dict;
   uint32_t ndict;
@@ -246,17 +222,17 @@ struct DictMaker {
   uint8_t* out;
   PageWork* pages;
   ChunkResult* res;
-  __device__ TxDict<ES, MODE> make(const QDesc& d) {
-    return TxDict<ES, MODE>{dict, ndict, aligned, out + d.out * (uint64_t)ES, 0};
+  __device__ TxDict<ES> make(const QDesc& d) {
+    return TxDict<ES>{dict, ndict, aligned, out + d.out * (uint64_t)ES, 0};
   }
-  __device__ void done(const QDesc& d, uint32_t, TxDict<ES, MODE>& em) {
+  __device__ void done(const QDesc& d, uint32_t, TxDict<ES>& em) {
     const uint64_t bad = __ballot(em.err != 0);
     if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
   }
 };
 
 #define PQG_TEXPAND_DICT(NAME, ATTR)                                                                  \
-  template <int ES, int MODE = 0>                                                                     \
+  template <int ES>                                                                                   \
   __global__ void ATTR __launch_bounds__(WG) NAME(const uint8_t* __restrict__ blob, uint64_t blob_len, \
                                                   uint32_t ntiles, PageWork* pages, RunTables rt,     \
                                                   int dict_page, uint8_t* __restrict__ out,           \
@@ -264,7 +240,7 @@ struct DictMaker {
     __shared__ TileSmem sm;                                                                         \
     if (dict_page < 0) return;                                                                      \
     const PageWork& dp = pages[dict_page];                                                          \
-    DictMaker<ES, MODE> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
+    DictMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
                            out, pages, res};                                                        \
     if (*rt.nfall == 0) return;                                                                     \
     if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);       \
@@ -286,177 +262,18 @@ __global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__
   if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);
 }
 
-// ------------------------------------------------------------------------------ page pass
-// (pqg_rlepage.hpp) One workgroup per page; pages it cannot finish are flagged for the tiled
-// path above (rt.pflag = 0, rt.nfall counts them).
-
-struct LevelsPageMaker {
-  int16_t* out;  // page output base
-  int16_t maxl;
-  bool count;
-  uint32_t* qcount;
-  uint32_t t0;   // the page's first expand tile
-  __device__ TxLevels make(uint32_t) { return TxLevels{out, maxl, count, 0u}; }
-  __device__ void done(uint32_t k, TxLevels& em) {
-    if (!count) return;
-    const uint32_t nn = wave_sum_u32(em.nonnull);
-    if ((threadIdx.x & 63) == 0) qcount[4 * (t0 + k) + (threadIdx.x >> 6)] = nn;
-  }
-};
-
-__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
-k_rlepage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len, const PageWork* pages,
-                 ColumnParams cp, int which, RunTables rt, int16_t* __restrict__ out) {
-  __shared__ TileSmem sm;
-  const int p = blockIdx.x;
-  const PageWork& pw = pages[p];
-  Stream s;
-  bool done = false;
-  if (get_stream(blob, pw, which, cp, s)) {
-    if (pw.status == 0) {
-      LevelsPageMaker mk{out + s.out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF,
-                         rt.qcount, pw.ltile0};
-      done = rle_page(blob, blob_len, s, sm, mk);
-    }
-    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
-  }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
-}
-
-// Fused page pass of level streams (pqg_parpage.hpp). Def levels: the page's non-null count
-// goes to its first tile's four quarter counts (zeros in the rest) for k_page_counts.
-struct ParLevelsMaker {
-  int16_t* out;  // page output base
-  int16_t maxl;
-  bool count;
-  uint32_t nn;
-  __device__ TxLevels make(uint32_t) { return TxLevels{out, maxl, count, 0u}; }
-  __device__ void done(uint32_t, TxLevels& em) { nn += em.nonnull; }
-};
-
-// Header density of a level stream from its first headers (at most 16, or until 1024 levels are
-// covered): true when they average fewer than 24 levels per header (p_null 0.1 streams: ~18;
-// p_null 0.5: ~70, where index + expand is faster). The hybrid header layout is
-// RleDecoder::reload's (rle.rs:489-513): ULEB128 h, h & 1 -> (h >> 1) groups of 8 bit-packed
-// values, else an RLE run of h >> 1 with a ceil(w / 8)-byte value. Anything unusual answers
-// false, which leaves the page to the tiled passes (they own the error reporting).
-__device__ inline bool dense_headers(const uint8_t* __restrict__ blob, const Stream& s) {
-  if (s.kind != LK_RLE || s.err || s.w <= 0 || s.w > 8) return false;
-  const uint8_t* p = blob + s.S;
-  uint64_t pos = 0, covered = 0;
-  uint32_t hops = 0;
-  while (hops < 16 && covered < 1024 && covered < s.n) {
-    uint64_t h = 0;
-    int sh = 0;
-    uint8_t b;
-    do {
-      if (pos >= s.slen || sh > 35) return false;
-      b = p[pos++];
-      h |= (uint64_t)(b & 0x7F) << sh;
-      sh += 7;
-    } while (b & 0x80);
-    if (h & 1) {
-      covered += (h >> 1) * 8;
-      pos += (h >> 1) * (uint64_t)s.w;
-    } else {
-      covered += h >> 1;
-      pos += 1;  // w <= 8: one value byte
-    }
-    ++hops;
-  }
-  return (uint64_t)hops * 24 > covered;
-}
-
-__global__ void __launch_bounds__(WG) k_parpage_levels(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                       const PageWork* pages, ColumnParams cp, int which,
-                                                       RunTables rt, int16_t* __restrict__ out) {
-  __shared__ ParPageSmem sm;
-  const int p = blockIdx.x;
-  const PageWork& pw = pages[p];
-  Stream s;
-  bool done = false;
-  if (get_stream(blob, pw, which, cp, s)) {
-    if (pw.status == 0 && ((cp.debug & PQG_DBG_FUSED) || dense_headers(blob, s))) {
-      const bool count = which == SS_DEF;
-      ParLevelsMaker mk{out + s.out, which == SS_DEF ? cp.max_def : cp.max_rep, count, 0u};
-      done = par_page(blob, blob_len, s, sm, mk);
-      if (done && count && pw.ntiles) {
-        for (uint32_t i = 4 + threadIdx.x; i < 4 * pw.ntiles; i += WG) rt.qcount[4 * pw.ltile0 + i] = 0;
-        const uint32_t nn = wave_sum_u32(mk.nn);
-        if ((threadIdx.x & 63) == 0) rt.qcount[4 * pw.ltile0 + (threadIdx.x >> 6)] = nn;
-      }
-    }
-    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
-  }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
-}
-
-template <int ES>
-struct DictPageMaker {
-  const uint8_t* dict;
-  uint32_t ndict;
-  bool aligned;
-  uint8_t* out;  // page output base
-  int32_t err;
-  __device__ TxDict<ES> make(uint32_t) { return TxDict<ES>{dict, ndict, aligned, out, 0}; }
-  __device__ void done(uint32_t, TxDict<ES>& em) { err |= em.err; }
-};
-
-template <int ES>
-__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
-k_rlepage_dict(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages, ColumnParams cp,
-               int dict_page, RunTables rt, uint8_t* __restrict__ out, ChunkResult* res) {
-  __shared__ TileSmem sm;
-  const int p = blockIdx.x;
-  const PageWork& pw = pages[p];
-  Stream s;
-  bool done = false;
-  if (get_stream(blob, pw, SS_DICT, cp, s)) {
-    if (pw.status == 0 && dict_page >= 0 && pages[dict_page].status == 0) {
-      const PageWork& dp = pages[dict_page];
-      DictPageMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
-                           out + s.out * (uint64_t)ES, 0};
-      done = rle_page(blob, blob_len, s, sm, mk);
-      if (done && __ballot(mk.err != 0) && (threadIdx.x & 63) == 0) report(pages, res, p, ST_PANIC);
-    }
-    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
-  }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
-}
-
-struct BoolPageMaker {
-  uint8_t* out;
-  __device__ TxBool make(uint32_t) { return TxBool{out}; }
-  __device__ void done(uint32_t, TxBool&) {}
-};
-
-__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
-k_rlepage_bool(const uint8_t* __restrict__ blob, uint64_t blob_len, const PageWork* pages,
-               ColumnParams cp, RunTables rt, uint8_t* __restrict__ out) {
-  __shared__ TileSmem sm;
-  const int p = blockIdx.x;
-  const PageWork& pw = pages[p];
-  Stream s;
-  bool done = false;
-  if (get_stream(blob, pw, SS_BOOL, cp, s)) {
-    if (pw.status == 0) {
-      BoolPageMaker mk{out + s.out};
-      done = rle_page(blob, blob_len, s, sm, mk);
-    }
-    if (!done && threadIdx.x == 0) atomicAdd(rt.nfall, 1u);
-  }
-  if (threadIdx.x == 0) rt.pflag[p] = done ? PF_PAGE : 0u;
-}
-
 static inline dim3 tx_grid(uint32_t ntiles) { return dim3(ntiles); }  // one tile per workgroup
 
 // Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
 __global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint32_t* __restrict__ qcount,
-                                                    int field) {
+                                                    const uint32_t* __restrict__ pflag,
+                                                    const uint32_t* __restrict__ nfall, int field) {
   __shared__ uint64_t red[WG / 64];
+  if (*nfall == 0) return;  // every stream done by the level path, which set the counts
   const int p = blockIdx.x;
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pflag[p] == PF_PAGE) return;
   const uint32_t q0 = pw.ltile0 * 4u, nq = pw.ntiles * 4u;
   uint64_t s = 0;
   for (uint32_t i = threadIdx.x; i < nq; i += WG) s += qcount[q0 + i];
@@ -614,6 +431,9 @@ __global__ void k_finalize(PageWork* pages, ChunkResult* res) {
 
 extern "C" {
 
+hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                         ColumnParams cp, int sel, RunTables rt, LevelTables lt, void* out, hipStream_t s);
+
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                               int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
                               hipStream_t s) {
@@ -640,44 +460,29 @@ hipError_t pqg_launch_tile_desc(const uint8_t* blob, PageWork* pages, uint32_t n
 }
 
 hipError_t pqg_launch_page_counts(PageWork* pages, int npages, RunTables rt, int field, hipStream_t s) {
-  hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, field);
+  hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, field);
   return hipGetLastError();
 }
 
-// Level stream `which` (0 def, 1 rep): index pass, tile descriptors, wave expand pass, and for
-// def levels the per-page non-null counts.
+// Level stream `which` (0 def, 1 rep): the window-parallel level path (levels + per-page non-null
+// counts, pqg_levels.hip), then the general hybrid decoder for the streams it hands back
+// (k_run_index walks only those; the tiled kernels exit at once when there are none).
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                              int npages, uint32_t ntiles, ColumnParams cp, int which,
-                             const uint32_t* tile_page, RunTables rt, int16_t* out,
+                             const uint32_t* tile_page, RunTables rt, LevelTables lt, int16_t* out,
                              ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
-  // optional page pass first (PQG_DBG_PAGEPASS: k_rlepage_levels; PQG_DBG_FUSED: k_parpage_levels),
-  // the tiled passes then take the streams it left (none: they exit at once)
-  const bool pp = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED | PQG_DBG_AUTO)) != 0;
   const int sel = which ? SS_REP : SS_DEF;
-  // kev brackets the dominant kernel: the page pass when forced for every page, else the expand
-  const bool ppall = (cp.debug & (PQG_DBG_PAGEPASS | PQG_DBG_FUSED)) != 0;
-  if (pp) {
-    if (kev && ppall) (void)hipEventRecord(kev[0], s);
-    if (cp.debug & PQG_DBG_PAGEPASS)
-      hipLaunchKernelGGL(k_rlepage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
-    else
-      hipLaunchKernelGGL(k_parpage_levels, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, out);
-    if (kev && ppall) (void)hipEventRecord(kev[1], s);
-  }
-  if (cp.debug & PQG_DBG_SERIAL_INDEX)
-    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
-                       -1, rt, res);
-  else {
-    hipLaunchKernelGGL(k_run_index_par, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, sel, rt, res);
-    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel, -1, rt, res, 1);
-  }
+  if (kev) (void)hipEventRecord(kev[0], s);
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, rt, lt, out, s);
+  if (kev) (void)hipEventRecord(kev[1], s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel, -1, rt, res, 1);
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    if (kev && !ppall) (void)hipEventRecord(kev[0], s);
     hipLaunchKernelGGL(k_texpand_levels, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
-    if (kev && !ppall) (void)hipEventRecord(kev[1], s);
-    if (sel == SS_DEF) hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, 0);
+    if (sel == SS_DEF)
+      hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, 0);
   }
   return hipGetLastError();
 }
@@ -692,37 +497,22 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
                            uint32_t ntiles, ColumnParams cp, int dict_page, int es,
                            const uint32_t* tile_page, RunTables rt, uint8_t* out, ChunkResult* res,
                            hipStream_t s, hipEvent_t* kev) {
-  const bool pp = (cp.debug & PQG_DBG_PAGEPASS) != 0;  // kev brackets the dominant kernel
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
-  if (kev && pp) (void)hipEventRecord(kev[0], s);
-  if (pp) switch (es) {
-    case 1: hipLaunchKernelGGL((k_rlepage_dict<1>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
-    case 4: hipLaunchKernelGGL((k_rlepage_dict<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
-    case 8: hipLaunchKernelGGL((k_rlepage_dict<8>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
-    case 12: hipLaunchKernelGGL((k_rlepage_dict<12>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, dict_page, rt, out, res); break;
-    default: return hipErrorInvalidValue;
-  }
-  if (kev && pp) (void)hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res);
   if (!ntiles) return hipGetLastError();
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
   const dim3 g = tx_grid(ntiles);
-  if (kev && !pp) (void)hipEventRecord(kev[0], s);
+  if (kev) (void)hipEventRecord(kev[0], s);
   switch (es) {
     case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
-    case 8:
-      if (((cp.debug >> 8) & 15) == 1)  // diagnostics: no gather
-        hipLaunchKernelGGL((k_texpand_dict<8, 1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
-      else
-        hipLaunchKernelGGL((k_texpand_dict<8>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res);
-      break;
+    case 8: hipLaunchKernelGGL((k_texpand_dict<8>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 12: hipLaunchKernelGGL((k_texpand_dict<12>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     default: return hipErrorInvalidValue;
   }
-  if (kev && !pp) (void)hipEventRecord(kev[1], s);
+  if (kev) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();
 }
 
@@ -746,21 +536,16 @@ hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npage
   return hipGetLastError();
 }
 
+// RLE booleans (data page v2 values, RleValueDecoder<bool>): the level path (one byte per value)
+// with the general hybrid decoder for the streams it hands back.
 hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                                int npages, uint32_t ntiles, ColumnParams cp,
-                               const uint32_t* tile_page, RunTables rt, uint8_t* out,
+                               const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
                                ChunkResult* res, hipStream_t s) {
-  if (cp.debug & PQG_DBG_PAGEPASS)
-    hipLaunchKernelGGL(k_rlepage_bool, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp, rt, out);
-  if (cp.debug & PQG_DBG_SERIAL_INDEX)
-    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
-                       -1, rt, res);
-  else {
-    hipLaunchKernelGGL(k_run_index_par, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, cp,
-                       (int)SS_BOOL, rt, res);
-    hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
-                       -1, rt, res, 1);
-  }
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_BOOL, rt, lt, out, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
+                     -1, rt, res, 1);
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, (int)SS_BOOL, -1);

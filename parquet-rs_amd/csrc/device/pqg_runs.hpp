@@ -1,20 +1,15 @@
-// pqg_runs.hpp — RLE/bit-packing hybrid decode (rle.rs:320-509) as two grid-wide passes.
-//
-// Run headers sit at data-dependent byte offsets, so finding them is a serial walk, while
-// expanding runs into outputs is embarrassingly parallel. The decode is split accordingly:
+// pqg_runs.hpp — the general RLE/bit-packing hybrid decoder (rle.rs:320-509): index pass +
+// tiled expand (pqg_texpand.hpp). It takes every stream: dictionary indices of any width, and
+// the level / boolean streams the fast level path (pqg_levels.hip) hands back (malformed
+// input, unusual header forms), reproducing every reference error on them.
 //
 //   index  (run_index, one wave per stream): walks the header chain of a page's stream inside
-//          LDS-staged 8 KiB regions, checks everything the reference checks while reading
-//          (Err / panic / endless loop), and writes one checkpoint per
-//          expand tile: the header position of the run holding the tile's first output.
-//   expand (run_expand, one 256-thread workgroup per tile of RUN_TILE outputs, all pages of
-//          the chunk in one grid): stages the tile's stream bytes in LDS, re-walks the few
-//          runs of the tile from its checkpoint into an LDS run list, then every lane expands
-//          8 consecutive outputs twice (two coalesced 2048-output halves) through an Emit
-//          functor (levels, dictionary gather, booleans, byte-array dictionary slices).
-//
-// The walk is the only serial part and it touches header bytes only; the expansion runs over
-// the whole chunk at once, so its cost is the output bandwidth.
+//          LDS-staged regions, checks everything the reference checks while reading
+//          (Err / panic / endless loop), and writes per expand tile a
+//          checkpoint (the header of the run holding the tile's first output) and the tile's
+//          run records.
+//   expand (pqg_texpand.hpp tile_one, one 256-thread workgroup per tile of RUN_TILE outputs,
+//          all pages of the chunk in one grid; wave_expand below for byte-array dictionaries).
 #pragma once
 #include "pqg_device.hpp"
 
@@ -26,9 +21,6 @@ namespace pqg {
 
 constexpr int IX_REG = PQG_IX_REG;            // index walker region (bytes)
 constexpr int IX_WORDS = (IX_REG + 64) / 4;
-constexpr int EX_STAGE = 10240;               // expand staging window (bytes)
-constexpr int EX_WORDS = (EX_STAGE + 64) / 4;
-constexpr int EX_RCAP = 512;                  // runs per expand batch
 constexpr uint32_t RF_BP = 1u, RF_EOF = 2u, RF_PANIC = 4u;
 constexpr uint32_t R_RLE = 0x80000000u;
 
@@ -516,569 +508,6 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
       return 0;
     }
   }
-}
-
-// ------------------------------------------------------------------------------ parallel chain walk
-//
-// Dense streams (bit widths <= 8: levels, booleans, small dictionaries) have a header every few
-// bytes, so a one-wave chain walk pays one dependent step per header. The parallel walk finds
-// the chain inside a staged region of REG stream bytes with a 256-thread workgroup:
-//   A  every byte position p is a candidate header (one- and two-byte forms); thread t owns the
-//      segment [t * SEG, (t + 1) * SEG), holds its bytes in registers and, right to left,
-//      records in E[p] where the chain from p leaves the segment, or the first position on it
-//      whose header it cannot take (a stop)
-//   B  the same, in place, for blocks of 4 segments (REG / 64 bytes, one per lane): E[p] :=
-//      where the chain from p leaves p's block
-//   C  wave 0 follows the true chain block by block through E (a v_readlane per step for
-//      entries in a block's first 64 bytes); lane u keeps block u's entry
-//   D  lane u walks the true headers of block u from that entry.
-// E is stored transposed (segment offset major, rows padded to an odd word count) so both the
-// per-segment pass (lanes = segments) and the block pass hit distinct LDS banks.
-template <int REG>
-struct PC {
-  static constexpr int SEG = REG / 256;
-  static constexpr int BLK = REG / 64;
-  static constexpr int ROW = 256 + 2;
-  static constexpr int ESZ = SEG * ROW;  // u16 entries of E
-  static __device__ uint32_t eix(uint32_t p) { return (p % SEG) * ROW + p / SEG; }
-};
-constexpr uint32_t PR_STOP = 0x8000u, PR_NONE = 0xFFFFu;
-
-// Workgroup barrier for LDS only: global loads in flight (the next region's prefetch) stay in
-// flight across it.
-__device__ inline void pr_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Next header after a true header at region index p (stream offset so): one- or two-byte forms
-// (the only ones the exits pass follows), as run_parse finds it.
-__device__ inline uint32_t pr_next(const uint32_t* region, uint32_t p, uint32_t w, uint32_t vb) {
-  const uint32_t x = lload_u32(region, p);
-  const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu;
-  const uint32_t two = b0 >> 7;
-  const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
-  return p + 1u + two + ((ind & 1u) ? (ind >> 1) * w : vb);
-}
-
-// A + B over region r (stream offset of region byte 0: rbase) staged in `region`; whole
-// workgroup, LDS barrier at the end.
-template <int REG>
-__device__ inline void pc_exits(const uint32_t* region, uint16_t* E, uint32_t r, uint32_t rbase,
-                                uint32_t off0, uint32_t slen, uint32_t w, uint32_t vb) {
-  using G = PC<REG>;
-  constexpr int SEG = G::SEG, ROW = G::ROW, BLK = G::BLK;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t seg0 = tid * SEG;
-  // ---- A: segment exits, right to left, bytes in registers, segment-local offsets (position
-  // seg0 + i is a stream position iff i < lim; E of local offset o sits at E[o * ROW + tid])
-  uint32_t bw[SEG / 4 + 1];
-#pragma unroll
-  for (int k = 0; k <= SEG / 4; ++k) bw[k] = region[(seg0 >> 2) + (uint32_t)k];
-  const int64_t lim64 = (int64_t)slen - ((int64_t)r * REG + seg0 - off0);
-  const int32_t lim = lim64 < -1 ? -1 : lim64 > SEG + 8 ? SEG + 8 : (int32_t)lim64;
-  const int32_t m = lim < SEG ? lim : SEG;        // local offsets >= m leave the segment
-  const int32_t omax = 0x8000 - (int32_t)seg0;    // exits must stay below 0x8000
-  uint16_t* Et = E + tid;
-#pragma unroll
-  for (int i = SEG - 1; i >= 0; --i) {
-    const uint32_t b0 = (bw[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-    const uint32_t b1 = (bw[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu;
-    const uint32_t two = b0 >> 7;
-    const uint32_t ind = two ? ((b0 & 0x7Fu) | (b1 << 7)) : b0;
-    const uint32_t hl = 1u + two;
-    const uint32_t bpf = ind & 1u;
-    const int32_t o = i + (int32_t)hl + (int32_t)(bpf ? (ind >> 1) * w : vb);
-    // not a stream position / longer header / header or RLE value past the stream / far exit
-    const uint32_t bad = (uint32_t)(i >= lim) | (two & ((b1 >> 7) | (uint32_t)(i + 1 >= lim))) |
-                         ((bpf ^ 1u) & (uint32_t)(i + (int32_t)(hl + vb) > lim)) | (uint32_t)(o >= omax);
-    const uint32_t leave = (uint32_t)(o >= m);
-    const uint32_t via = Et[(bad | leave) ? i * ROW : o * ROW];
-    Et[i * ROW] = (uint16_t)(bad ? (PR_STOP | (seg0 + (uint32_t)i)) : leave ? seg0 + (uint32_t)o : via);
-  }
-  pr_sync();
-  // ---- B: block exits, in place (lane = block, wave + 4 * j = offset in the segment)
-#pragma unroll
-  for (int k = BLK / SEG - 2; k >= 0; --k) {
-#pragma unroll 4
-    for (int j = 0; j < SEG / 4; ++j) {
-      const uint32_t p = lane * BLK + (uint32_t)k * SEG + wave + 4u * (uint32_t)j;
-      const uint32_t q = E[G::eix(p)];
-      const bool hop = !(q & PR_STOP) && q < (lane + 1) * (uint32_t)BLK && rbase + q < slen;
-      const uint32_t v = E[G::eix(hop ? q : p)];
-      E[G::eix(p)] = (uint16_t)(hop ? v : q);
-    }
-    pr_sync();
-  }
-}
-
-// C (wave 0): the chain from region index e0 (a stream position). Returns block `lane`'s entry
-// (PR_NONE if the chain skips it); kind 0: the chain leaves the region / stream at stream
-// offset `at`; kind 1: stop at region index `at`.
-template <int REG>
-__device__ inline uint32_t pc_chain(const uint16_t* E, uint32_t e0, uint32_t rbase, uint32_t slen,
-                                    uint32_t& kind, uint32_t& at) {
-  using G = PC<REG>;
-  constexpr int BLK = G::BLK;
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t xv[64];  // block k's exits for entry offsets lane < 64
-#pragma unroll
-  for (int k = 0; k < 64; ++k) xv[k] = E[G::eix((uint32_t)k * BLK + lane)];
-  uint32_t e = e0, bent = PR_NONE;
-  kind = 2;
-  at = 0;
-  if (rbase + e >= slen) {
-    kind = 0;
-    at = rbase + e;
-  }
-#pragma unroll
-  for (int k = 0; k < 64; ++k) {
-    if (kind == 2 && e < (uint32_t)(k + 1) * BLK) {  // e is in block k
-      bent = lane == (uint32_t)k ? e : bent;
-      const uint32_t off = e - (uint32_t)k * BLK;
-      const uint32_t q = off < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)xv[k], (int)off) : rfl(E[G::eix(e)]);
-      if (q & PR_STOP) {
-        kind = 1;
-        at = q & 0x7FFFu;
-      } else {
-        e = q;
-        if (rbase + e >= slen || e >= (uint32_t)REG) {
-          kind = 0;
-          at = rbase + e;
-        }
-      }
-    }
-  }
-  return bent;
-}
-
-// D (wave 0, lane u = block u): calls put(p) for the true headers of the block in order.
-template <int REG, class F>
-__device__ inline void pc_walk(const uint32_t* region, uint32_t bent, uint32_t stop_at, uint32_t rbase,
-                               uint32_t slen, uint32_t w, uint32_t vb, F&& put) {
-  if (bent == PR_NONE) return;
-  const uint32_t b1e = ((threadIdx.x & 63) + 1) * (uint32_t)PC<REG>::BLK;
-  uint32_t p = bent;
-  while (true) {
-    put(p);
-    if (p == stop_at) break;
-    p = pr_next(region, p, w, vb);
-    if (p >= b1e || rbase + p >= slen) break;
-  }
-}
-
-// ------------------------------------------------------------------------------ parallel index pass
-//
-// run_index_par: the index pass of a dense stream with the parallel chain walk, PR_REG bytes per
-// region; the listed headers go through ix_batch (wave 0, 64 per batch): the same parse, checks
-// and records as run_index. A stop ends the region's listing at that header; the walk resumes
-// after it. Streams it does not take (bit widths > 8, more than PR_POSCAP headers in a region)
-// return PR_BAIL and are walked by run_index.
-constexpr int PR_REG = 16384;
-constexpr int PR_POSCAP = 8192;
-constexpr int PR_CHUNKS = (PR_REG + 64) / 16;
-constexpr int PR_PF = (PR_CHUNKS + WG - 1) / WG;
-constexpr int32_t PR_BAIL = 0x7FFF0000;
-
-struct ParIndexSmem {
-  uint32_t region[(PR_REG + 64) / 4];
-  uint16_t E[PC<PR_REG>::ESZ];
-  uint16_t pos[PR_POSCAP];
-  uint32_t ctl[8];
-};
-
-// Whole workgroup (WG threads). Returns the stream's status in every thread, or PR_BAIL.
-__device__ inline int32_t run_index_par(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                        const Stream& s, RunCkpt* __restrict__ ck,
-                                        uint2* __restrict__ runs, uint32_t* __restrict__ nruns,
-                                        ParIndexSmem& sm, uint64_t* stamps = nullptr) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // diagnostics (PQG_DEBUG bit 5): s_memtime cycles in fetch + exits, chain + listing, batches
-  uint64_t t_ab = 0, t_chain = 0, t_list = 0, t0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
-  auto stamp = [&](uint64_t& acc) {
-    if (stamps) {
-      const uint64_t t1 = __builtin_amdgcn_s_memtime();
-      acc += t1 - t0;
-      t0 = t1;
-    }
-  };
-  if (s.err) return s.err;
-  const uint32_t n = s.n;
-  if (n == 0) return 0;
-  const uint32_t w = (uint32_t)s.w;
-  if (s.kind == LK_BIT_PACKED) {  // one header-less run (levels.rs:203-209)
-    if ((uint64_t)n * (uint64_t)w > (uint64_t)s.slen * 8ull) return ST_EOF;
-    if (w > 32) return ST_PANIC;
-    return 0;
-  }
-  if (w == 0 || w > 8) return PR_BAIL;
-  const uint64_t S = s.S;
-  const uint32_t slen = s.slen;
-  const uint64_t G = S & ~15ull;
-  const uint32_t off0 = (uint32_t)(S - G);
-  const uint32_t vb = (w + 7u) >> 3;
-  const uint32_t nregions = (off0 + slen + PR_REG - 1) / PR_REG;
-  uint4 pf[PR_PF];
-  auto fetch = [&](uint32_t r) {
-    const uint64_t A0 = G + (uint64_t)r * PR_REG;
-    const bool fast = A0 + PR_REG + 64 <= blob_len;
-#pragma unroll
-    for (int k = 0; k < PR_PF; ++k) {
-      const uint32_t c = tid + WG * (uint32_t)k;
-      if (c < (uint32_t)PR_CHUNKS)
-        pf[k] = fast ? *reinterpret_cast<const uint4*>(blob + A0 + (uint64_t)c * 16)
-                     : gload_u128_tail(blob, blob_len, A0 + (uint64_t)c * 16);
-    }
-  };
-  uint32_t cur_r = 0xFFFFFFFFu, pf_r = 0xFFFFFFFFu;
-  uint32_t cur = 0;
-  IxCarry cy{0u, 0u, 0u};  // meaningful in wave 0
-  while (true) {
-    if (cur >= slen) return ST_EOF;  // the reference stalls at the end of the data (A.4)
-    const uint32_t r = (off0 + cur) / PR_REG;
-    const uint32_t rbase = r * PR_REG - off0;  // stream offset of region byte 0 (mod 2^32)
-    if (r != cur_r) {
-      if (r != pf_r) fetch(r);
-#pragma unroll
-      for (int k = 0; k < PR_PF; ++k) {
-        const uint32_t c = tid + WG * (uint32_t)k;
-        if (c < (uint32_t)PR_CHUNKS) reinterpret_cast<uint4*>(sm.region)[c] = pf[k];
-      }
-      cur_r = r;
-      pf_r = 0xFFFFFFFFu;
-      if (r + 1 < nregions) {
-        fetch(r + 1);
-        pf_r = r + 1;
-      }
-      pr_sync();
-      pc_exits<PR_REG>(sm.region, sm.E, r, rbase, off0, slen, w, vb);
-    }
-    stamp(t_ab);
-    // ---- chain, listing and batches: wave 0
-    if (wave == 0) {
-      uint32_t kind, at;
-      const uint32_t bent = pc_chain<PR_REG>(sm.E, cur - rbase, rbase, slen, kind, at);
-      const uint32_t stop_at = kind == 1 ? at : 0xFFFFFFFFu;
-      uint32_t c = 0;
-      pc_walk<PR_REG>(sm.region, bent, stop_at, rbase, slen, w, vb, [&](uint32_t) { ++c; });
-      uint32_t incl = c;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += y;
-      }
-      const uint32_t H = rfl(__shfl(incl, 63, 64));
-      int32_t st = PR_BAIL;
-      uint32_t done = 1, nxt = at;
-      stamp(t_chain);
-      if (H <= (uint32_t)PR_POSCAP) {
-        uint32_t base = incl - c;
-        pc_walk<PR_REG>(sm.region, bent, stop_at, rbase, slen, w, vb,
-                        [&](uint32_t p) { sm.pos[base++] = (uint16_t)p; });
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-        st = 0;
-        done = 0;
-        for (uint32_t b = 0; b < H; b += 64) {
-          const uint32_t k = H - b < 64u ? H - b : 64u;
-          const uint32_t posv = lane < k ? rbase + sm.pos[b + lane] : 0u;
-          st = ix_batch(sm.region, rbase, posv, k, slen, n, w, ck, runs, nruns, cy);
-          if (st || cy.produced >= n) {
-            done = 1;
-            break;
-          }
-        }
-        if (!done && kind == 1) {  // resume after the stop header
-          uint32_t nx, cnt, inf, flg;
-          run_parse(sm.region, at, rbase + at, slen, (int)w, nx, cnt, inf, flg);
-          nxt = rfl(nx);
-        }
-      }
-      if (lane == 0) {
-        sm.ctl[2] = done;
-        sm.ctl[3] = (uint32_t)st;
-        sm.ctl[4] = nxt;
-      }
-      stamp(t_list);
-    }
-    pr_sync();
-    if (sm.ctl[2]) {
-      if (stamps && tid == 0)
-        *reinterpret_cast<uint4*>(stamps) = make_uint4((uint32_t)t_ab, (uint32_t)t_chain, (uint32_t)t_list, 0u);
-      return (int32_t)sm.ctl[3];
-    }
-    cur = sm.ctl[4];
-    pr_sync();  // ctl reuse
-  }
-}
-
-// ------------------------------------------------------------------------------ expand pass
-
-struct ExpandSmem {
-  uint32_t stage[EX_WORDS];
-  uint32_t start[EX_RCAP + 2];
-  uint32_t info[EX_RCAP + 1];
-  uint32_t fix[RUN_TILE / 8];  // output chunks left to the general path
-  uint32_t ctl[4];
-  uint64_t red[4];
-};
-
-// Expand outputs [lo, hi) of stream s (page-relative indices) from checkpoint c, with the
-// 256 threads of the workgroup. Uniform control flow; stream already validated by run_index.
-template <class Emit>
-__device__ inline void run_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                  const Stream& s, RunCkpt c, uint32_t next_pos,
-                                  const uint2* __restrict__ recs, uint32_t nrec, uint32_t lo,
-                                  uint32_t hi, ExpandSmem& sm, Emit& emit) {
-  const int tid = threadIdx.x;
-  const int w = s.w;
-  const uint64_t S = s.S;
-  const uint32_t slen = s.slen;
-  const uint64_t wmask = (w >= 32) ? 0xFFFFFFFFull : ((1ull << w) - 1ull);
-  // ---- stage the tile's stream bytes
-  uint32_t q0;
-  if (s.kind == LK_BIT_PACKED) {
-    q0 = (uint32_t)(((uint64_t)lo * (uint64_t)w) >> 3);
-    c.pos = 0;
-    c.first = 0;
-  } else {
-    q0 = c.pos;
-  }
-  const uint64_t A0 = (S + q0) & ~15ull;
-  const uint32_t first_eff = s.kind == LK_BIT_PACKED ? lo : (c.first < lo ? c.first : lo);
-  const uint64_t need_end = S + (uint64_t)q0 + 64 + ((uint64_t)(hi - first_eff) * (uint64_t)w + 7) / 8 +
-                            (s.kind == LK_BIT_PACKED ? 0 : 2 * (uint64_t)(hi - lo));
-  const uint64_t S_end = S + slen + 16;
-  // the tile's runs end in the run whose header is the next tile's checkpoint
-  const uint64_t next_end = S + (uint64_t)next_pos + 32 + ((uint64_t)RUN_TILE * (uint64_t)w + 7) / 8;
-  uint64_t A1 = need_end < S_end ? need_end : S_end;
-  if (A1 > next_end) A1 = next_end;
-  if (A1 > A0 + EX_STAGE) A1 = A0 + EX_STAGE;
-  const uint32_t nchunks = (uint32_t)((A1 - A0 + 15) / 16);
-  const bool have_recs = s.kind != LK_BIT_PACKED && nrec <= RUN_CAPT;
-  {
-    // all loads in flight together: the tile's bytes and its run records
-    constexpr int PER = (EX_STAGE / 16 + WG - 1) / WG;
-    uint4 v[PER];
-    const bool fast = A0 + (uint64_t)nchunks * 16 <= blob_len;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t cidx = (uint32_t)tid + (uint32_t)(k * WG);
-      if (cidx < nchunks) {
-        const uint64_t a = A0 + (uint64_t)cidx * 16;
-        v[k] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
-      }
-    }
-    uint2 rr = make_uint2(0, 0);
-    if (have_recs && (uint32_t)tid < nrec) rr = recs[tid];
-    uint2 rr2 = make_uint2(0, 0);
-    if (have_recs && (uint32_t)tid + WG < nrec) rr2 = recs[tid + WG];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t cidx = (uint32_t)tid + (uint32_t)(k * WG);
-      if (cidx < nchunks) reinterpret_cast<uint4*>(sm.stage)[cidx] = v[k];
-    }
-    if (have_recs) {
-      if ((uint32_t)tid < nrec) {
-        sm.start[tid] = rr.x;
-        sm.info[tid] = rr.y;
-      }
-      if ((uint32_t)tid + WG < nrec) {
-        sm.start[tid + WG] = rr2.x;
-        sm.info[tid + WG] = rr2.y;
-      }
-      if (tid == 0) {
-        sm.start[nrec] = hi;
-        sm.start[nrec + 1] = hi;
-        sm.ctl[0] = nrec;
-      }
-    }
-  }
-  if (tid < 16) sm.stage[nchunks * 4 + tid] = 0;
-  const uint64_t staged = (uint64_t)nchunks * 16;  // bytes [A0, A0 + staged) valid
-  __syncthreads();
-
-  uint32_t cur = c.pos, produced = c.first, seg_lo = lo;
-  bool first_batch = true;
-  while (seg_lo < hi) {
-    // ---- runs covering [seg_lo, seg_hi) into the LDS run list: the index pass's records, or
-    // a re-walk from the checkpoint when the tile has more runs than it keeps (wave 0, uniform)
-    if (!(have_recs && first_batch) && tid < 64) {
-      uint32_t nr = 0;
-      if (s.kind == LK_BIT_PACKED) {
-        if (tid == 0) {
-          sm.start[0] = 0;
-          sm.info[0] = 0;
-          sm.start[1] = hi;
-        }
-        nr = 1;
-        produced = hi;
-      } else {
-        while (produced < hi && nr < (uint32_t)EX_RCAP) {
-          if (cur >= slen) break;  // cannot happen on a stream run_index accepted
-          uint32_t nxt, cnt, inf, flg;
-          const uint64_t ri = S + cur - A0;
-          if (S + cur >= A0 && ri + 24 <= staged)
-            run_parse(sm.stage, (uint32_t)ri, cur, slen, w, nxt, cnt, inf, flg);
-          else
-            run_parse_global(blob, blob_len, S, cur, slen, w, nxt, cnt, inf, flg);
-          if (cnt) {
-            const uint32_t left = s.n - produced;
-            const uint32_t need = cnt < left ? cnt : left;
-            if (produced + need > seg_lo) {
-              if (tid == 0) {
-                sm.start[nr] = produced;
-                sm.info[nr] = (flg & RF_BP) ? inf : (R_RLE | inf);
-              }
-              ++nr;
-            }
-            produced += need;
-          }
-          cur = nxt;
-        }
-        if (tid == 0) sm.start[nr] = produced;
-      }
-      if (tid == 0) {
-        sm.ctl[0] = nr;
-        sm.start[nr + 1] = sm.start[nr];
-      }
-    }
-    if (tid == 0) sm.ctl[1] = 0;
-    __syncthreads();
-    const uint32_t nr = sm.ctl[0];
-    if (nr == 0) break;  // defensive: nothing left to expand
-    const uint32_t seg_hi = sm.start[nr] < hi ? sm.start[nr] : hi;
-    if (seg_hi <= seg_lo) break;
-    // ---- expand: lane chunks of 8 outputs, two coalesced halves per tile. Chunks inside one
-    // or two runs (nearly all) take a branch-free path: per output, pick run a or a+1, one LDS
-    // window read, shift and mask. Chunks over three or more runs, or whose payload is not
-    // staged, go to a list handled after the barrier by the general path.
-    const uint32_t sb32 = (uint32_t)(A0 - S);  // stream offset of staged byte 0 (mod 2^32)
-    const uint32_t wm = (uint32_t)wmask;
-    const uint32_t stg = (uint32_t)staged;
-#pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-      const uint32_t g = lo + (uint32_t)half * (RUN_TILE / 2) + (uint32_t)tid * 8u;
-      if (g + 8 <= seg_lo || g >= seg_hi) continue;
-      const uint32_t o0 = g < seg_lo ? seg_lo : g;
-      uint32_t a = 0;
-#pragma unroll
-      for (uint32_t step = EX_RCAP / 2; step; step >>= 1)
-        if (a + step < nr && sm.start[a + step] <= o0) a += step;
-      const uint32_t stA = sm.start[a], infA = sm.info[a];
-      const uint32_t stB = sm.start[a + 1];
-      const uint32_t infB = sm.info[a + 1 < nr ? a + 1 : a];
-      const uint32_t stC = sm.start[a + 2 <= nr ? a + 2 : nr];
-      const uint32_t end = g + 8 < seg_hi ? g + 8 : seg_hi;
-      bool fixup = end > stC;  // three or more runs
-      uint32_t v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t oj = g + (uint32_t)j;
-        const bool inB = oj >= stB;
-        const uint32_t inf = inB ? infB : infA;
-        const uint32_t d = oj - (inB ? stB : stA);
-        const uint32_t rel = inf - sb32;
-        const uint32_t bit = rel * 8u + d * (uint32_t)w;
-        const bool rle = (inf & R_RLE) != 0;
-        const bool ok = rle || (d < (1u << 20) && rel < stg && (bit >> 3) + 12u <= stg);
-        const uint32_t byte = ok && !rle ? bit >> 3 : 0u;
-        uint32_t val;
-        if (w <= 24) val = (lload_u32(sm.stage, byte) >> (bit & 7)) & wm;
-        else val = (uint32_t)(lload_u64(sm.stage, byte) >> (bit & 7)) & wm;
-        val = rle ? (inf & 0x7FFFFFFFu) : val;
-        const bool in = oj >= seg_lo && oj < seg_hi;
-        fixup |= in && !ok;
-        v[j] = in ? val : 0u;
-      }
-      if (fixup) {
-        const uint32_t slot = atomicAdd(&sm.ctl[1], 1u);
-        sm.fix[slot] = g;
-        continue;
-      }
-      uint32_t mask = 0xFFu;
-      if (g < seg_lo || g + 8 > seg_hi) {
-        mask = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (g + j >= seg_lo && g + j < seg_hi) mask |= 1u << j;
-      }
-      emit(s.out + g, v, mask);
-    }
-    __syncthreads();
-    // ---- general path for the listed chunks (one lane each)
-    const uint32_t nfix = sm.ctl[1];
-    for (uint32_t f = tid; f < nfix; f += WG) {
-      const uint32_t g = sm.fix[f];
-      const uint32_t o0 = g < seg_lo ? seg_lo : g;
-      uint32_t r = 0;
-#pragma unroll
-      for (uint32_t step = EX_RCAP / 2; step; step >>= 1)
-        if (r + step < nr && sm.start[r + step] <= o0) r += step;
-      uint32_t st = sm.start[r], nst = sm.start[r + 1], inf = sm.info[r];
-      uint32_t v[8];
-      uint32_t mask = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t oj = g + (uint32_t)j;
-        v[j] = 0;
-        if (oj < seg_lo || oj >= seg_hi) continue;
-        while (oj >= nst && r + 1 < nr) {
-          ++r;
-          st = nst;
-          nst = sm.start[r + 1];
-          inf = sm.info[r];
-        }
-        uint32_t val = inf & 0x7FFFFFFFu;
-        if (!(inf & R_RLE)) {
-          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(oj - st) * (uint64_t)w;
-          const uint64_t abs = S + (bit >> 3);
-          const uint64_t ri = abs - A0;
-          const uint64_t x = (abs >= A0 && ri + 12 <= staged) ? lload_u64(sm.stage, (uint32_t)ri)
-                                                              : gload_u64(blob, blob_len, abs);
-          val = (uint32_t)((x >> (bit & 7)) & wmask);
-        }
-        v[j] = val;
-        mask |= 1u << j;
-      }
-      emit(s.out + g, v, mask);
-    }
-    seg_lo = seg_hi;
-    first_batch = false;
-    __syncthreads();
-  }
-}
-
-// Common front of the expand kernels: tile -> page, stream and output range.
-// Expand tiles per workgroup: the per-tile setup (page lookup, stream, checkpoint) is scalar
-// work that a larger grain amortises.
-constexpr uint32_t EX_TPW = 4;
-
-__device__ inline bool expand_setup(const uint8_t* blob, PageWork* pages, const uint32_t* tile_page,
-                                    const RunTables& rt, ColumnParams cp, int sel, uint32_t t,
-                                    int& p, Stream& s, uint32_t& lo, uint32_t& hi, RunCkpt& c,
-                                    uint32_t& next_pos, const uint2*& recs, uint32_t& nrec) {
-  p = (int)tile_page[t];
-  const PageWork& pw = pages[p];
-  if (pw.status != 0) return false;
-  if (!get_stream(blob, pw, sel, cp, s) || s.err) return false;
-  const uint32_t k = t - pw.ltile0;
-  lo = k * RUN_TILE;
-  if (lo >= s.n) return false;
-  hi = lo + RUN_TILE < s.n ? lo + RUN_TILE : s.n;
-  if (s.kind == LK_BIT_PACKED) {
-    c = RunCkpt{0, 0};
-    next_pos = s.slen;
-    nrec = 1;
-    recs = nullptr;
-  } else {
-    recs = rt.runs + (uint64_t)t * RUN_CAPT;
-    c = rt.ck[t];
-    next_pos = hi < s.n ? rt.ck[t + 1].pos : s.slen;
-    nrec = rt.nruns[t];
-  }
-  return true;
 }
 
 }  // namespace pqg

@@ -345,7 +345,7 @@ struct TxDictTraits {
   static constexpr int V = ES == 8 ? 2 : ES == 4 ? 4 : ES == 12 ? 4 : 16;
 };
 
-template <int ES, int MODE = 0>
+template <int ES>
 struct TxDict {
   static constexpr int V = TxDictTraits<ES>::V;
   static constexpr int PG = ES == 8 ? 4 : 2;
@@ -369,9 +369,7 @@ struct TxDict {
           const bool ok = want && idx < ndict;
           err |= (want && !ok) ? ST_PANIC : 0;
           T t = 0;
-          if (MODE == 1) {
-            t = idx;
-          } else if (ok) {
+          if (ok) {
             if (aligned) {
               t = reinterpret_cast<const T*>(dict)[idx];
             } else {
@@ -427,9 +425,7 @@ struct TxDict {
     }
     uint8_t* d = out + (uint64_t)o * ES;
     const uint8_t* p = dict + (uint64_t)idx * ES;
-    if (MODE == 1) {
-      *reinterpret_cast<uint32_t*>(d) = idx;
-    } else if ((ES == 4 || ES == 8) && aligned) {
+    if ((ES == 4 || ES == 8) && aligned) {
       if constexpr (ES == 8) *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(p);
       else *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(p);
     } else {

@@ -25,8 +25,8 @@ hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnPa
 hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
                                 RunTables, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                             const uint32_t*, RunTables, int16_t*, ChunkResult*, hipStream_t,
-                             hipEvent_t*);
+                             const uint32_t*, RunTables, LevelTables, int16_t*, ChunkResult*,
+                             hipStream_t, hipEvent_t*);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
@@ -37,7 +37,8 @@ hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, 
 hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
                                  ChunkResult*, hipStream_t);
 hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
-                               const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t);
+                               const uint32_t*, RunTables, LevelTables, uint8_t*, ChunkResult*,
+                               hipStream_t);
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
@@ -63,7 +64,7 @@ struct Slot {
   PageWork* h_pages = nullptr;  // pinned staging
   ChunkResult* d_res = nullptr;
   ChunkResult* h_res = nullptr;  // pinned
-  hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the levels / values kernel
+  hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the def-level path / values kernel
   bool kl = false, kv = false;  // events 6-7 / 8-9 recorded by the last decode
   bool used = false;
   // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix;
@@ -82,6 +83,20 @@ struct Slot {
   size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
+  uint32_t* lvwb[3] = {}; // level path (def, rep, RLE booleans): per-page window bases
+  size_t lvwbcap[3] = {};
+  uint2* lvtab[3] = {};   // window tables
+  size_t lvtabcap[3] = {};
+  uint2* lvwin[3] = {};   // per-window entries
+  size_t lvwincap[3] = {};
+  LevelTables lt(int k) const {
+    LevelTables t{};
+    t.wbase = lvwb[k];
+    t.tab = lvtab[k];
+    t.win = lvwin[k];
+    t.wcap = (uint32_t)lvwincap[k];
+    return t;
+  }
 };
 
 struct pqg_ctx {
@@ -154,6 +169,12 @@ static int log2_ceil(uint64_t x) {  // bit_util.rs:91-104
   return r;
 }
 
+// Entries a level-path window table keeps per window (device/pqg_levels.hip lv_ent).
+static uint32_t lv_ent(uint32_t w) {
+  return w == 1 ? 64u : w == 2 ? 128u : w <= 4 ? 256u : w <= 8 ? 512u : 1024u;
+}
+static const uint64_t LV_WIN = 1024;
+
 static int value_size(int t, int tl) {
   switch (t) {
     case PQG_BOOLEAN: return 1;
@@ -220,6 +241,11 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dt.inc);
     hipFree(sl.dt.flag);
     hipFree(sl.dt.nfall);
+    for (int k = 0; k < 3; ++k) {
+      hipFree(sl.lvwb[k]);
+      hipFree(sl.lvtab[k]);
+      hipFree(sl.lvwin[k]);
+    }
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   delete ctx;
@@ -363,6 +389,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   uint64_t level_out = 0, max_page_bytes = 0, max_page_vals = 0;
   uint32_t total_tiles = 0;
   bool enc_present[16] = {};
+  uint64_t nwin = 0;           // level-path windows, upper bound (a stream is part of its page)
   for (uint32_t i = 0; i < npages; ++i) {
     PageWork& w = ctx->h_pages[i];
     memset(&w, 0, sizeof(w));
@@ -387,6 +414,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       if (w.encoding >= 0 && w.encoding < 16) enc_present[w.encoding] = true;
       if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
       if (w.num_values > max_page_vals) max_page_vals = w.num_values;
+      nwin += (w.nbytes + LV_WIN - 1) / LV_WIN;
     }
     if (vst && (int)i == bad) w.status = vst;
     if (vst && (int)i > bad) w.status = -1;  // never reached by the reference
@@ -420,8 +448,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
 #endif
   cp.debug = dbg_env;
   cp.dbgbuf = nullptr;
-  if (dbg_env & 48) {
-    const size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
+  if (dbg_env & 112) {
+    size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
+    if (need < (size_t)npages * 64) need = (size_t)npages * 64;
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
@@ -518,25 +547,46 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
-  // page-pass flags: with the page pass every stream starts "none left over"; without it the
-  // tiled passes take every page
-  const bool pagepass = (cp.debug & PQG_DBG_PAGEPASS) != 0;
-  // level streams: fused page pass first, for every page (PQG_DBG_FUSED) or the dense ones (PQG_DBG_AUTO)
-  const bool fused = (cp.debug & (PQG_DBG_FUSED | PQG_DBG_AUTO)) != 0;
+  // Level path buffers (normalized streams) per stream kind, grown on demand.
+  const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
+  const bool need_lv[3] = {want_def, want_rep, rle_bool};
+  auto grow = [&](void** p, size_t* cap, size_t need, size_t elem, const char* what) -> int {
+    if (need <= *cap) return PQG_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t c = need + need / 8 + 1024;
+    HIPCHK(hipMalloc(p, c * elem), what);
+    *cap = c;
+    return PQG_OK;
+  };
+  for (int k = 0; k < 3; ++k) {
+    if (!need_lv[k]) continue;
+    int st;
+    if ((st = grow((void**)&sl.lvwb[k], &sl.lvwbcap[k], (size_t)npages + 1, 4, "hipMalloc level windows"))) return st;
+    if ((st = grow((void**)&sl.lvwin[k], &sl.lvwincap[k], nwin + 1, sizeof(uint2), "hipMalloc level windows"))) return st;
+    const size_t ent = lv_ent(k == 2 ? 1u : (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width));
+    if ((st = grow((void**)&sl.lvtab[k], &sl.lvtabcap[k], (nwin + 1) * ent, sizeof(uint2), "hipMalloc level tables"))) return st;
+  }
+  // Hybrid-stream flags: the level path (def, rep, RLE booleans) sets every page's flag and counts
+  // the streams it hands back; dictionary indices always take the general decoder.
   for (int k = 0; k < 3; ++k) {
     if (!sl.rt[k].nfall) continue;
-    const bool pm = pagepass || (k < 2 && fused);
-    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, pm ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
-    if (!pm && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+    const bool lvpath = k < 2 || rle_bool;
+    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, lvpath ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
+    if (!lvpath && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
   }
-  if (np && want_def)
+  if (np && want_def) {
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
-                             out->def_levels, ctx->d_res, s, ctx->timing ? &sl.ev[6] : nullptr),
+                             sl.lt(0), out->def_levels, ctx->d_res, s,
+                             ctx->timing ? &sl.ev[6] : nullptr),
            "def levels");
-  if (np && want_def) sl.kl = nt > 0 || pagepass || fused;
+    sl.kl = ctx->timing;
+  }
   if (np && want_rep)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
-                             out->rep_levels, ctx->d_res, s, nullptr), "rep levels");
+                             sl.lt(1), out->rep_levels, ctx->d_res, s, nullptr),
+           "rep levels");
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
   HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
@@ -570,10 +620,10 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       ctx->values_kernel = PQG_PLAIN;
       if (t == PQG_BOOLEAN)
         HIPCHK(pqg_launch_plain_bool(blob, ctx->d_pages, np, max_page_vals, vo, ctx->d_res, s), "plain bool");
-      else if (es > 0)
-      {
+      else if (es > 0) {
         if (ctx->timing) hipEventRecord(sl.ev[8], s);
-        HIPCHK(pqg_launch_plain_copy(blob, blob_len, ctx->d_pages, np, es, PQG_PLAIN, max_page_bytes, vo, ctx->d_res, s), "plain");
+        HIPCHK(pqg_launch_plain_copy(blob, blob_len, ctx->d_pages, np, es, PQG_PLAIN, max_page_bytes, vo,
+                                     ctx->d_res, s), "plain");
         if (ctx->timing) hipEventRecord(sl.ev[9], s);
         sl.kv = true;
       }
@@ -619,8 +669,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
     if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
       ctx->values_kernel = PQG_RLE;
-      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2], vo,
-                                 ctx->d_res, s), "rle bool");
+      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2],
+                                 sl.lt(2), vo, ctx->d_res, s), "rle bool");
     }
   }
   if (ctx->timing) hipEventRecord(ctx->ev[4], s);
@@ -687,6 +737,12 @@ int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
 
 // Diagnostics: average per-wave phase cycles of the last decode's wave expand kernel
 // (PQG_DEBUG bit 4). out[0..2] = desc, expand, tail cycles; out[3] = waves.
+// Diagnostics: raw copy of the debug buffer (PQG_DIAG builds; u64 words).
+int pqg_debug_read(pqg_ctx* ctx, uint64_t* out, size_t n) {
+  if (!ctx || !ctx->dbgbuf || !out || n * 8 > ctx->dbg_cap) return PQG_ERR_INVALID;
+  return hipMemcpy(out, ctx->dbgbuf, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
 int pqg_debug_stamps(pqg_ctx* ctx, double* out4) {
   if (!ctx || !ctx->dbgbuf || !out4) return PQG_ERR_INVALID;
   std::vector<uint32_t> h((size_t)ctx->dbg_n * 4);

@@ -113,8 +113,8 @@ struct RunTables {
   uint32_t* nruns;  // [tiles]
   QDesc* desc;      // [tiles * 4]
   uint32_t* qcount; // [tiles * 4] per quarter-tile counts (def levels == max_def; byte totals)
-  uint32_t* pflag;  // [pages] 1: stream decoded by the page pass (k_rlepage_*)
-  uint32_t* nfall;  // streams the page pass left to the tiled path (0: its kernels exit at once)
+  uint32_t* pflag;  // [pages] PF_PAGE: stream decoded by the level path (pqg_levels.hip)
+  uint32_t* nfall;  // streams the level path left to the tiled path (0: its kernels exit at once)
 };
 
 // DELTA_BINARY_PACKED index-pass outputs (device/pqg_delta.hip). Tiles of DELTA_TILE values
@@ -148,17 +148,17 @@ struct DeltaTables {
   uint32_t* nfall;    // pages k_delta_page left to the tiled path (0: its tile kernels exit at once)
 };
 
-// ColumnParams::debug bit: decode RLE/bit-packed streams with the page pass (pqg_rlepage.hpp)
-// instead of the tiled index + expand passes (PQG_DEBUG=16384). Off by default: on the benchmark
-// pages the tiled passes are as fast (dictionary) or faster (levels).
-constexpr int32_t PQG_DBG_PAGEPASS = 0x4000;
-constexpr int32_t PQG_DBG_SERIAL_INDEX = 0x8000;  // one-wave index walker for every stream
-constexpr int32_t PQG_DBG_FUSED = 0x10000;        // level streams: fused page pass for every page
-// Level streams, optional (PQG_DEBUG=131072): the fused page pass takes only the pages whose
-// first headers are dense (< 24 levels per header) and leaves the rest to the tiled passes. Off by
-// default: measured slower than either pure mode when the pages split between the two.
-constexpr int32_t PQG_DBG_AUTO = 0x20000;
-// RunTables::pflag values: stream decoded by the page pass / handed back by the parallel index walker
+// Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
+struct LevelTables {
+  uint32_t* wbase;  // [pages + 1] first window of each page's stream (k_lv_plan)
+  uint2* tab;       // [windows * entries] per window and entry offset: (exit offset, outputs)
+  uint2* win;       // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
+  uint32_t wcap;    // windows the per-window arrays hold
+  uint32_t pad;
+};
+
+// RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) / handed back by it
+// to the general hybrid decoder (pqg_runs.hpp)
 constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u;
 
 struct ColumnParams {
