@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
                                                   int bailed_only = 0) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
-  if (bailed_only ? rt.pflag[p] != PF_BAIL : (*rt.nfall == 0 || rt.pflag[p] == PF_PAGE)) return;
+  if (bailed_only ? rt.pflag[p] != PF_BAIL : (*rt.nfall == 0 || pf_level_path(rt.pflag[p]))) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   Stream s;
@@ -195,7 +195,7 @@ struct LevelsMaker {
   __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
   const uint32_t* pflag;
   __device__ void done(const QDesc& d, uint32_t t, TxLevels& em) {
-    if (!count || (!d.qhi && pflag[d.page] == PF_PAGE)) return;  // the page pass wrote these counts
+    if (!count || (!d.qhi && pf_level_path(pflag[d.page]))) return;  // the level path wrote these counts
     const uint32_t nn = wave_sum_u32(em.nonnull);
     if ((threadIdx.x & 63) == 0) qcount[4 * t + (threadIdx.x >> 6)] = nn;
   }
@@ -209,7 +209,10 @@ struct LevelsMaker {
     if (*rt.nfall == 0) return;                                                                   \
     LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount,     \
                    rt.pflag};                                                                     \
-    if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);     \
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {                                   \
+      tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);                                      \
+      __syncthreads(); /* sm is refilled by the next tile */                                      \
+    }                                                                                             \
   }
 PQG_TEXPAND_LEVELS(k_texpand_levels, __attribute__((amdgpu_waves_per_eu(8, 8))))
 
@@ -273,7 +276,7 @@ __global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint3
   const int p = blockIdx.x;
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pflag[p] == PF_PAGE) return;
+  if (pf_level_path(pflag[p])) return;
   const uint32_t q0 = pw.ltile0 * 4u, nq = pw.ntiles * 4u;
   uint64_t s = 0;
   for (uint32_t i = threadIdx.x; i < nq; i += WG) s += qcount[q0 + i];
@@ -480,7 +483,9 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   if (ntiles) {
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
-    hipLaunchKernelGGL(k_texpand_levels, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, cp, sel, out);
+    // persistent grid: most calls leave no stream to this pass, and its workgroups exit at once
+    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles < 4096u ? ntiles : 4096u), dim3(WG), 0, s, blob, blob_len,
+                       ntiles, rt, cp, sel, out);
     if (sel == SS_DEF)
       hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, 0);
   }

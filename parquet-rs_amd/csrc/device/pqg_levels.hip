@@ -1,53 +1,73 @@
 // pqg_levels.hip — level streams (def / rep levels) and RLE boolean values: the
 // RLE/bit-packing hybrid (RleDecoder::reload / get_batch, rle.rs:352-434, 490-508;
-// LevelDecoder::get, levels.rs:249-271), decoded window-parallel.
+// LevelDecoder::get, levels.rs:249-271), decoded on the GPU without a per-output serial loop.
 //
 // Run headers sit at data-dependent offsets: where a header starts depends on every header
-// before it. Instead of walking that chain once per page, every 1 KiB window of every stream is
-// solved independently for ALL the places the chain could enter it:
+// before it. Two ways to find them, chosen per page by the page itself:
 //
-//   k_lv_plan    windows per page stream (exclusive scan), eligibility of each stream.
-//   k_lv_win     one wave per window: every byte position of the window is parsed as if a header
+//   k_lv_plan    windows (1 KiB of stream) per page (exclusive scan), eligibility of each stream.
+//   k_lv_walk    one wave per page walks the header chain: a scalar hop loop follows up to 64
+//                headers in an LDS-staged 4 KiB region (one LDS read and a few scalar ops per
+//                one-byte header), then the 64 lanes parse those headers together, check them,
+//                prefix-sum their output counts and write run records (first output, RLE value or
+//                payload offset) plus, per window, the index of its first run. Sparse streams
+//                (bit-packed runs of tens of bytes: random levels) finish here in a few hundred
+//                microseconds for the whole chunk. A page whose 64-header batches span less than
+//                1 KiB is dense (short RLE runs) and goes to the window path instead.
+//   window path, for the dense pages (k_lv_plan2 compacts their windows):
+//     k_lv_win   one wave per window: every byte position of the window is parsed as if a header
 //                started there (next header offset, output count), then pointer jumping (ten
 //                rounds of J[i] = J[J[i]], C[i] += C[J[i]]) gives, for every position, where its
 //                chain leaves the window and how many outputs it produces on the way. The
 //                answers for the positions a chain can enter at (the first 64 * w bytes: a
 //                header plus at most 63 bit-packed groups) go to a table.
-//   k_lv_stitch  one wave per page: follows the window tables from offset 0 (one lookup per
+//     k_lv_stitch one wave per page: follows the window tables from offset 0 (one lookup per
 //                window) to each window's true entry and first output.
-//   k_lv_emit    one wave per window: pointer jumping again, now marking the positions
-//                reachable from the true entry (the window's true headers); they are parsed in
-//                parallel, a wave scan places their runs, and the window's outputs are written:
-//                int16 levels (column/reader.rs:162-163) or one byte per boolean, 16-byte
-//                stores (element stores for the groups shared with a neighbouring window). Def
-//                streams add their count of outputs == max_def (the non-null count read_batch
-//                uses, column/reader.rs:212-226) to the page.
+//     k_lv_emit  one wave per window: pointer jumping again, now marking the positions reachable
+//                from the true entry (the window's true headers), which are parsed in parallel
+//                and placed by a wave scan into the window's run list.
+//   k_lv_emit_walk  one wave per window of the walked pages: loads the window's run records.
+//
+// Both emits then write the window's outputs from its run list: int16 levels
+// (column/reader.rs:162-163) or one byte per boolean, 16-byte stores (element stores for the
+// groups shared with a neighbouring window); one-bit streams one 32-output word per lane. Def
+// streams add their count of outputs == max_def (the non-null count read_batch uses,
+// column/reader.rs:212-226) to the page.
 //
 // Streams off the common path (a header form the fast parse does not take, a stream that ends
-// before its outputs, truncated payload, an RLE value wider than sw, an entry past the table)
-// go to the general decoder (pqg_runs.hpp / pqg_texpand.hpp), which reproduces every reference
-// error. Work is proportional to stream bytes, not to the number of headers, and no page waits
-// on a serial walk longer than one table lookup per 1 KiB.
+// before its outputs, truncated payload, an RLE value wider than the bit width) go to the
+// general decoder (pqg_runs.hpp / pqg_texpand.hpp), which reproduces every reference error.
 #include "pqg_runs.hpp"
 
 namespace pqg {
 
 constexpr uint32_t LV_WIN = 1024;                  // stream bytes per window (one wave)
 constexpr uint32_t LV_PPL = LV_WIN / WAVE;         // positions per lane (16)
-constexpr uint32_t LV_STG = LV_WIN + 48;           // staged bytes (+ alignment slack, read-ahead)
+constexpr uint32_t LV_STG = LV_WIN + 48;           // window path: staged bytes (+ alignment, read-ahead)
 constexpr uint32_t LV_STG_CH = LV_STG / 16;        // 16-byte chunks (67)
 constexpr uint32_t LV_RCAP = LV_WIN;               // runs per window
 constexpr uint32_t LV_ROUNDS = 10;                 // 2^10 = LV_WIN: chains of any length
 constexpr uint32_t LV_SERIAL = 64;                 // k_lv_emit: windows with at most this many
                                                    // true headers are walked by one lane
-constexpr uint32_t LV_BM = 16384;                  // one-bit outputs per bitmap chunk
 constexpr uint32_t LV_NONE = 0xFFFFFFFFu;          // window not on the true chain
 // jump-table values >= LV_WIN are terminal: the chain leaves the window at W0 + value, or
 constexpr uint32_t LV_J_FAR = 0xFFFDu;             //   leaves it beyond W0 + 0xFFFC,
 constexpr uint32_t LV_J_END = 0xFFFEu;             //   reaches the end of the stream,
 constexpr uint32_t LV_J_DEAD = 0xFFFFu;            //   meets a header the fast parse refuses
 
-// Bit widths the window path takes: levels up to 16 bits (RLE values of <= 2 bytes).
+// page walker (k_lv_walk) and the emit of walked pages (k_lv_emit_walk)
+constexpr uint32_t LW_REG = 4096 - 16;             // stream bytes whose headers one region holds
+                                                   // (+ alignment: its first 4 KiB stay in VGPRs)
+constexpr uint32_t LW_CH = 5;                      // 16-byte loads per lane per region
+constexpr uint32_t LW_STG = LW_CH * 16 * WAVE;     // staged bytes (region + alignment + read-ahead)
+constexpr uint32_t LW_SPAN = 1024;                 // 64 headers within fewer bytes: a dense page
+constexpr uint32_t LW_RPW = 256;                   // runs per window k_lv_emit_walk takes (the span
+                                                   // rule keeps walked windows at <= 192)
+constexpr uint32_t LW_REC = 64;                    // run records per window (+ 2 windows per page)
+constexpr uint32_t LE_STG = LV_WIN + 64 * 16 + 64; // k_lv_emit_walk: staged bytes (runs of w <= 16
+                                                   // whose header is in the window)
+
+// Bit widths the level path takes: levels up to 16 bits (RLE values of <= 2 bytes).
 __device__ inline bool lv_width_ok(uint32_t w) { return w >= 1 && w <= 16; }
 
 // Entry offsets a window table keeps: a chain enters a window at most one hop past its start,
@@ -55,6 +75,8 @@ __device__ inline bool lv_width_ok(uint32_t w) { return w >= 1 && w <= 16; }
 __device__ __host__ inline uint32_t lv_ent(uint32_t w) {
   return w == 1 ? 64u : w == 2 ? 128u : w <= 4 ? 256u : w <= 8 ? 512u : 1024u;
 }
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 // Wave-private LDS of the window kernels. Lane l owns positions j * 64 + l (j < 16), so the
 // wave's accesses to its own entries are consecutive (conflict-free).
@@ -67,10 +89,7 @@ struct LvWave {
       uint32_t rinfo[LV_RCAP];
     } runs;
   };
-  union {
-    uint8_t R[LV_WIN];           // k_lv_emit: 1 = position reachable from the true entry
-    uint32_t bm[LV_BM / 32];     // k_lv_emit, one-bit outputs: a chunk of them as a bitmap
-  };
+  uint8_t R[LV_WIN];        // k_lv_emit: 1 = position reachable from the true entry
 };
 
 struct LvSmem {
@@ -88,54 +107,27 @@ __device__ inline uint32_t wave_incl_scan_u32(uint32_t x) {
   return x;
 }
 
+// Inclusive scan of output counts (32-bit DPP while every count is below 2^25, else 64-bit).
+__device__ inline uint64_t wave_incl_scan_cnt(uint32_t c) {
+  if (!__ballot(c >= (1u << 25))) return wave_incl_scan_u32(c);
+  uint64_t ic = c;
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t b = __shfl_up(ic, d, 64);
+    if (lane >= (uint32_t)d) ic += b;
+  }
+  return ic;
+}
+
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS accesses have completed
   __builtin_amdgcn_wave_barrier();
 }
 
-// Header at stream position p (stage byte index rel), general form: varints of <= 4 bytes,
-// <= 2 value bytes. False for anything else, including a header or RLE value that runs past
-// the stream end.
-__device__ inline bool lv_parse(const uint32_t* st, uint32_t rel, uint32_t p, uint32_t slen,
-                                uint32_t w, uint32_t vb, uint32_t& nxt, uint32_t& cnt,
-                                uint32_t& val, bool& bp) {
-  if (p >= slen) return false;
-  const uint64_t x = lload_u64(st, rel);
-  const uint32_t lo = (uint32_t)x;
-  uint32_t h, hl;
-  if (!(lo & 0x80u)) {
-    h = lo & 0x7Fu;
-    hl = 1;
-  } else {
-    const uint32_t t = ~lo & 0x80808080u;
-    if (!t) return false;  // varint longer than 4 bytes: not the writer's form
-    hl = ((uint32_t)__builtin_ctz(t) >> 3) + 1u;
-    const uint32_t y = lo & 0x7F7F7F7Fu;
-    h = (y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u) | ((y >> 3) & 0xFE00000u);
-    if (hl < 4) h &= (1u << (7 * hl)) - 1u;
-  }
-  if (hl > slen - p) return false;
-  if (h & 1u) {
-    bp = true;
-    const uint32_t g = h >> 1;
-    cnt = g * 8u;
-    val = p + hl;
-    const uint64_t nx = (uint64_t)p + hl + (uint64_t)g * w;
-    nxt = nx > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nx;
-  } else {
-    bp = false;
-    cnt = h >> 1;
-    if (vb > slen - p - hl) return false;
-    const uint32_t v = (uint32_t)(x >> (8 * hl));
-    val = vb == 1 ? (v & 0xFFu) : (v & 0xFFFFu);
-    nxt = p + hl + vb;
-  }
-  return true;
-}
-
-// Header at stream position p for the window kernels: branch-free for varints of 1-4 bytes
-// (run lengths < 2^27; every header the reference writer emits, rle.rs:167-178), reading a
-// third dword only for an RLE value past the first 4 bytes. Longer varints, and headers
+// Header at stream position p (stage byte index rel): branch-free for varints of 1-4 bytes (run
+// lengths < 2^27; every header the reference writer emits, rle.rs:167-178), reading a third
+// dword only for an RLE value past the first 4 bytes. Longer varints, and headers or RLE values
 // running past the stream end, return false (dead): a true chain that meets one goes to the
 // general decoder.
 __device__ inline bool lv_parse4(const uint32_t* st, uint32_t rel, uint32_t p, uint32_t slen,
@@ -168,6 +160,15 @@ __device__ inline bool lv_parse4(const uint32_t* st, uint32_t rel, uint32_t p, u
   return !(c012 & c3) && p < slen && len <= slen - p;
 }
 
+// What the reader consumes of a run must be decodable: the bit-packed payload of its first
+// min(c, n - acc) outputs inside the stream, an RLE value that fits the bit width.
+__device__ inline bool lv_run_ok(bool bp, uint32_t v, uint32_t c, uint64_t acc, uint32_t n, uint32_t slen,
+                                 uint32_t w) {
+  if (!c || acc >= n) return true;
+  return bp ? (uint64_t)v * 8ull + (uint64_t)min((uint64_t)c, (uint64_t)n - acc) * w <= (uint64_t)slen * 8ull
+            : (v >> w) == 0;
+}
+
 // A window's stream: the page stream `sel`, its window k (stage origin, bytes).
 struct LvWin {
   Stream s;
@@ -175,16 +176,17 @@ struct LvWin {
   uint32_t k;      // window of the page
   uint32_t W0;     // stream offset of the window
   uint32_t sb;     // stage byte of stream offset W0
+  uint32_t cap;    // staged bytes
 };
 
-// Stage stream bytes [W0, W0 + LV_WIN + 32) (16-byte aligned loads, guarded at the blob end).
-__device__ inline void lv_stage(const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x,
-                                uint32_t* stage, uint32_t& sb) {
+// Stage nch 16-byte chunks from stream offset W0 (aligned down; guarded at the blob end).
+__device__ inline void lv_stage(const uint8_t* __restrict__ blob, uint64_t blob_len, LvWin& x,
+                                uint32_t* stage, uint32_t nch) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t A = (x.s.S + x.W0) & ~15ull;
-  sb = (uint32_t)(x.s.S + x.W0 - A);
-#pragma unroll
-  for (uint32_t c = lane; c < LV_STG_CH; c += WAVE) {
+  x.sb = (uint32_t)(x.s.S + x.W0 - A);
+  x.cap = nch * 16u;
+  for (uint32_t c = lane; c < nch; c += WAVE) {
     const uint64_t a = A + (uint64_t)c * 16u;
     const uint4 v = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
     reinterpret_cast<uint4*>(stage)[c] = v;
@@ -192,7 +194,8 @@ __device__ inline void lv_stage(const uint8_t* __restrict__ blob, uint64_t blob_
   wave_lds_sync();
 }
 
-// Page and window of global window index g (wbase: exclusive scan of windows per page).
+// Page and window of global window index g (wbase: exclusive scan of windows per page; pages
+// without windows share their offset with the next page, which this finds).
 __device__ inline uint32_t lv_page_of(const uint32_t* __restrict__ wbase, uint32_t npages, uint32_t g) {
   uint32_t lo = 0, hi = npages;  // last page with wbase[p] <= g
   while (hi - lo > 1) {
@@ -210,8 +213,8 @@ __device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int se
 }
 
 // Hand page p to the general decoder (once).
-__device__ inline void lv_bail(RunTables& rt, uint32_t p) {
-  if (atomicCAS(&rt.pflag[p], PF_PAGE, PF_BAIL) == PF_PAGE) atomicAdd(rt.nfall, 1u);
+__device__ inline void lv_bail(RunTables& rt, uint32_t p, uint32_t from) {
+  if (atomicCAS(&rt.pflag[p], from, PF_BAIL) == from) atomicAdd(rt.nfall, 1u);
 }
 
 // Own positions' first hop (window-relative next offset, terminal codes >= LV_WIN) and output
@@ -241,34 +244,16 @@ __device__ inline void lv_first_hops(const uint32_t* stage, uint32_t sb, uint32_
   }
 }
 
-// ------------------------------------------------------------------------------ k_lv_plan
-// One workgroup: per page the stream's windows (exclusive scan into wbase), and the page flag:
-// PF_PAGE (level path) or PF_BAIL (general decoder). Def streams start their count at 0.
-__global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
-                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+// Exclusive scan of per-page window counts over one workgroup (pages in order).
+template <class F>
+__device__ inline void lv_scan_windows(int npages, uint32_t* wbase, F nwin_of) {
   __shared__ uint32_t wsum[WG / 64];
   __shared__ uint32_t carry_s;
   if (threadIdx.x == 0) carry_s = 0;
   __syncthreads();
   for (int base = 0; base < npages; base += WG) {
     const int p = base + (int)threadIdx.x;
-    uint32_t nw = 0;
-    if (p < npages) {
-      const PageWork& pw = pages[p];
-      Stream s;
-      uint32_t flag = 0;
-      if (get_stream(blob, pw, sel, cp, s)) {
-        if (lv_stream(blob, pw, sel, cp, s) && (s.n == 0 || s.slen > 0)) {
-          flag = PF_PAGE;
-          nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
-          if (sel == SS_DEF) pages[p].nonnull = 0;
-        } else {
-          flag = PF_BAIL;
-          atomicAdd(rt.nfall, 1u);
-        }
-      }
-      rt.pflag[p] = flag;
-    }
+    const uint32_t nw = p < npages ? nwin_of(p) : 0u;
     uint32_t incl = nw;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -279,31 +264,229 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
     __syncthreads();
     uint32_t pre = carry_s;
     for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
-    if (p < npages) lt.wbase[p] = pre + incl - nw;
+    if (p < npages) wbase[p] = pre + incl - nw;
     __syncthreads();
     if (threadIdx.x == WG - 1) carry_s = pre + incl;
     __syncthreads();
   }
-  if (threadIdx.x == 0) lt.wbase[npages] = carry_s;
+  if (threadIdx.x == 0) wbase[npages] = carry_s;
+}
+
+// ------------------------------------------------------------------------------ k_lv_plan
+// One workgroup: per page the stream's windows (exclusive scan into wbase), and the page flag:
+// PF_PAGE (level path) or PF_BAIL (general decoder). Def streams start their count at 0.
+__global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
+                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  lv_scan_windows(npages, lt.wbase, [&](int p) -> uint32_t {
+    const PageWork& pw = pages[p];
+    Stream s;
+    uint32_t flag = 0, nw = 0;
+    if (get_stream(blob, pw, sel, cp, s)) {
+      if (lv_stream(blob, pw, sel, cp, s) && (s.n == 0 || s.slen > 0)) {
+        flag = PF_PAGE;
+        nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
+        if (sel == SS_DEF) pages[p].nonnull = 0;
+      } else {
+        flag = PF_BAIL;
+        atomicAdd(rt.nfall, 1u);
+      }
+    }
+    rt.pflag[p] = flag;
+    return nw;
+  });
+}
+
+// One workgroup: windows of the pages the walker left to the window path (wbase2).
+__global__ void __launch_bounds__(WG) k_lv_plan2(int npages, RunTables rt, LevelTables lt) {
+  lv_scan_windows(npages, lt.wbase2, [&](int p) -> uint32_t {
+    return rt.pflag[p] == PF_PAGE ? lt.wbase[p + 1] - lt.wbase[p] : 0u;
+  });
+}
+
+// ------------------------------------------------------------------------------ k_lv_walk
+// One wave per page. Status: walked (PF_WALK; run records and per-window first runs written),
+// dense (PF_PAGE stays: window path), or handed to the general decoder (PF_BAIL).
+__global__ void __launch_bounds__(WG) k_lv_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                const PageWork* __restrict__ pages, int npages,
+                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  __shared__ uint32_t stg[WG / WAVE][LW_STG / 4];
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  const uint32_t p = blockIdx.x * (WG / WAVE) + wid;
+  if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
+  Stream s;
+  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
+  uint32_t* st = stg[wid];
+  const uint32_t n = s.n, slen = s.slen, w = (uint32_t)s.w, vb = (w + 7u) >> 3;
+  const uint32_t k0 = lt.wbase[p], nwin = lt.wbase[p + 1] - k0;
+  uint32_t* wf = lt.wfirst + k0 + p;                           // nwin + 1 entries
+  uint2* rec = lt.rec + (uint64_t)LW_REC * (k0 + 2ull * p);     // cap entries
+  const uint32_t cap = LW_REC * (nwin + 2u);
+  uint32_t cur = 0, nr = 0, nextw = 0, loaded = 0xFFFFFFFFu, sb = 0;
+  uint64_t acc = 0;
+  int status = 0;  // 0 walked, 1 dense, 2 general decoder
+  uint4 pf[LW_CH];
+  // the region's first 4 KiB also in registers: staged dword d is in rg[(d >> 8) * 4 + (d & 3)] of
+  // lane (d >> 2) & 63, which the hop loop reads with a uniform register index and v_readlane
+  // (a few cycles, where an LDS round trip costs a few hundred)
+  u32x16 rg;
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 6): per page s_memtime cycles in region installs, hop loops,
+  // batches, and the headers walked
+  const bool stamps = (cp.debug & 64) && cp.dbgbuf;
+  uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, t_reg = 0, t_hop = 0, t_bat = 0, nhops = 0;
+#define LW_STAMP(acc)                                      \
+  if (stamps) {                                            \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();      \
+    acc += t1 - t0;                                        \
+    t0 = t1;                                               \
+  }
+#else
+#define LW_STAMP(acc)
+#endif
+  auto fetch = [&](uint32_t r) {  // region r's bytes into registers
+    const uint64_t A = (s.S + (uint64_t)r * LW_REG) & ~15ull;
+#pragma unroll
+    for (uint32_t j = 0; j < LW_CH; ++j) {
+      const uint64_t a = A + (uint64_t)(j * WAVE + lane) * 16u;
+      pf[j] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+    }
+  };
+  const uint32_t nreg = (slen + LW_REG - 1) / LW_REG;
+  fetch(0);
+  uint32_t fetched = 0;
+  while (acc < n) {
+    if (cur >= slen) {  // the stream ends before n outputs
+      status = 2;
+      break;
+    }
+    const uint32_t r = cur / LW_REG;
+    if (r != loaded) {
+      if (r != fetched) fetch(r);
+#pragma unroll
+      for (uint32_t j = 0; j < LW_CH; ++j) reinterpret_cast<uint4*>(st)[j * WAVE + lane] = pf[j];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        rg[4 * j] = pf[j].x;
+        rg[4 * j + 1] = pf[j].y;
+        rg[4 * j + 2] = pf[j].z;
+        rg[4 * j + 3] = pf[j].w;
+      }
+      sb = (uint32_t)(s.S + (uint64_t)r * LW_REG - ((s.S + (uint64_t)r * LW_REG) & ~15ull));
+      loaded = r;
+      wave_lds_sync();
+      if (r + 1 < nreg) {  // the next region's loads fly while this one is walked
+        fetch(r + 1);
+        fetched = r + 1;
+      }
+      LW_STAMP(t_reg);
+    }
+    const uint32_t rb = r * LW_REG;
+    const uint32_t lim = min(rb + LW_REG, slen);
+    // hop loop (wave-uniform): up to 64 headers; one-byte headers take the short path
+    uint32_t k = 0, posv = 0;
+    const uint32_t c0 = cur;
+    uint64_t a2 = acc;
+    while (k < 64u && cur < lim && a2 < n) {
+      const uint32_t rel = cur - rb + sb;  // < LW_REG + 16 = 4096
+      const uint32_t d = rel >> 2;
+      const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)rg[((d >> 8) << 2) | (d & 3u)], (int)((d >> 2) & 63u));
+      const uint32_t b = (dw >> ((rel & 3u) * 8u)) & 0xFFu;
+      uint32_t cnt, nxt;
+      bool dead = false;
+      if (!(b & 0x80u)) {
+        const uint32_t g = b >> 1;
+        cnt = (b & 1u) ? g * 8u : g;
+        nxt = cur + 1u + ((b & 1u) ? g * w : vb);
+      } else {
+        uint32_t v;
+        bool bp;
+        dead = !lv_parse4(st, rel, cur, slen, w, vb, nxt, cnt, v, bp);
+        nxt = rfl(nxt);
+        cnt = rfl(cnt);
+        dead = rfl(dead ? 1u : 0u) != 0;
+      }
+      posv = lane == k ? cur : posv;
+      ++k;
+      if (dead) break;  // the batch's parse refuses it
+      a2 += cnt;
+      cur = nxt;
+    }
+    LW_STAMP(t_hop);
+#ifdef PQG_DIAG
+    nhops += k;
+#endif
+    // batch: lane l parses header l, checks it, places it
+    const bool act = lane < k;
+    uint32_t nx, c = 0, v = 0;
+    bool bp = false, ok = true;
+    if (act) {
+      ok = lv_parse4(st, posv - rb + sb, posv, slen, w, vb, nx, c, v, bp);
+      if (!ok) c = 0;
+    }
+    const uint64_t ic = wave_incl_scan_cnt(c);
+    const uint64_t accb = acc + ic - c;
+    if (act && ok) ok = lv_run_ok(bp, v, c, accb, n, slen, w);
+    if (__ballot(act && !ok)) {
+      status = 2;
+      break;
+    }
+    if ((k == 64u && cur - c0 < LW_SPAN) || nr + k + 1u > cap) {
+      status = 1;
+      break;
+    }
+    if (act) rec[nr + lane] = make_uint2(accb < 0xFFFFFFFFull ? (uint32_t)accb : 0xFFFFFFFFu, bp ? v : (R_RLE | v));
+    // windows whose start lies in (previous header, this header] begin with this run
+    const uint32_t whi = act ? posv / LV_WIN + 1u : 0u;
+    uint32_t wlo = (uint32_t)__shfl_up((int)whi, 1, 64);
+    if (lane == 0) wlo = nextw;
+    if (act)
+      for (uint32_t kw = wlo; kw < whi; ++kw) wf[kw] = nr + lane;
+    // wave-uniform state stays scalar: the compiler cannot know a shuffle result is uniform
+    nextw = rfl((uint32_t)__shfl((int)whi, (int)k - 1, 64));
+    nr += k;
+    const uint64_t bt = __shfl(ic, (int)k - 1, 64);
+    acc += ((uint64_t)rfl((uint32_t)(bt >> 32)) << 32) | rfl((uint32_t)bt);
+    LW_STAMP(t_bat);
+  }
+#ifdef PQG_DIAG
+  if (stamps && lane == 0) {
+    uint64_t* d = cp.dbgbuf + 8ull * p;
+    d[0] = t_reg;
+    d[1] = t_hop;
+    d[2] = t_bat;
+    d[3] = nhops;
+    d[4] = (uint64_t)status;
+  }
+#endif
+#undef LW_STAMP
+  if (status == 0) {
+    if (lane == 0) rec[nr] = make_uint2(acc < 0xFFFFFFFFull ? (uint32_t)acc : 0xFFFFFFFFu, 0u);  // sentinel
+    for (uint32_t kw = nextw + lane; kw <= nwin; kw += WAVE) wf[kw] = nr;
+    if (lane == 0) rt.pflag[p] = PF_WALK;
+  } else if (status == 2 && lane == 0) {
+    lv_bail(rt, p, PF_PAGE);
+  }
 }
 
 // ------------------------------------------------------------------------------ k_lv_win
+// Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
 __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                const PageWork* __restrict__ pages, int npages,
                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
   __shared__ LvSmem sm;
-  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
-  const uint32_t total = lt.wbase[npages];
-  for (uint32_t g = blockIdx.x * (WG / WAVE) + wid; g < total; g += gridDim.x * (WG / WAVE)) {
+  const uint32_t total = lt.wbase2[npages];
+  for (uint32_t g2 = blockIdx.x * (WG / WAVE) + wid; g2 < total; g2 += gridDim.x * (WG / WAVE)) {
     LvWin x;
-    x.p = lv_page_of(lt.wbase, (uint32_t)npages, g);
+    x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
     const PageWork& pw = pages[x.p];
     if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, cp, x.s)) continue;
-    x.k = g - lt.wbase[x.p];
+    x.k = g2 - lt.wbase2[x.p];
+    const uint32_t g = lt.wbase[x.p] + x.k;
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
-    lv_stage(blob, blob_len, x, W.stage, x.sb);
+    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
     uint32_t jv[LV_PPL], cv[LV_PPL];
     lv_first_hops(W.stage, x.sb, x.W0, slen, w, vb, jv, cv);
 #pragma unroll
@@ -347,11 +530,11 @@ __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob,
 }
 
 // ------------------------------------------------------------------------------ k_lv_stitch
-// One wave per page: the true entry and first output of every window of the page.
+// One wave per dense page: the true entry and first output of every window of the page.
 __global__ void __launch_bounds__(WG) k_lv_stitch(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
                                                   int npages, ColumnParams cp, int sel, RunTables rt,
                                                   LevelTables lt) {
-  const uint32_t p = blockIdx.x * (WG / WAVE) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  const uint32_t p = blockIdx.x * (WG / WAVE) + rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   const PageWork& pw = pages[p];
   Stream s;
@@ -380,18 +563,17 @@ __global__ void __launch_bounds__(WG) k_lv_stitch(const uint8_t* __restrict__ bl
     if (jt >= LV_J_FAR || t.y == 0xFFFFFFFFu) break;  // far / end / dead, or a saturated count
     e = kk * LV_WIN + jt;
   }
-  if (!ok) lv_bail(rt, p);
+  if (!ok) lv_bail(rt, p, PF_PAGE);
 }
 
-// ------------------------------------------------------------------------------ k_lv_emit
+// ------------------------------------------------------------------------------ output writers
 
 // 64-bit little-endian window of stream bytes at stream offset q: staged or from global memory.
 __device__ inline uint64_t lv_bytes8(const uint32_t* stage, const uint8_t* __restrict__ blob,
-                                     uint64_t blob_len, uint64_t S, uint32_t W0, uint32_t sb,
-                                     uint32_t q) {
-  const uint32_t r = q - W0 + sb;
-  if (q >= W0 && r + 12 <= LV_STG) return lload_u64(stage, r);
-  return gload_u64(blob, blob_len, S + q);
+                                     uint64_t blob_len, const LvWin& x, uint32_t q) {
+  const uint32_t r = q - x.W0 + x.sb;
+  if (q >= x.W0 && r + 12 <= x.cap) return lload_u64(stage, r);
+  return gload_u64(blob, blob_len, x.s.S + q);
 }
 
 __device__ inline uint32_t wave_sum_u32_(uint32_t v) {
@@ -402,41 +584,202 @@ __device__ inline uint32_t wave_sum_u32_(uint32_t v) {
 
 // Outputs [o, e) (page-relative, e - o <= 32) of run `info` starting at output `start`, w = 1:
 // bit j = output o + j.
-__device__ inline uint32_t lv_run_bits1(const LvWave& W, const uint8_t* __restrict__ blob, uint64_t blob_len,
+__device__ inline uint32_t lv_run_bits1(const uint32_t* stage, const uint8_t* __restrict__ blob, uint64_t blob_len,
                                         const LvWin& x, uint32_t start, uint32_t info, uint32_t o, uint32_t e) {
   const uint32_t nb = e - o;
   const uint32_t m = nb >= 32 ? 0xFFFFFFFFu : (1u << nb) - 1u;
   if (info & R_RLE) return (info & 1u) ? m : 0u;
   const uint64_t bit = (uint64_t)info * 8ull + (o - start);
-  return (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x.s.S, x.W0, x.sb, (uint32_t)(bit >> 3)) >> (bit & 7u)) & m;
+  return (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & m;
 }
 
-// OUT = 2: int16 levels; OUT = 1: one byte per boolean.
+// Run list in LDS: runs [0, R), rstart[R] = 0xFFFFFFFF; the window writes page outputs
+// [base, endo) (base = rstart[0]).
+struct LvRuns {
+  const uint32_t* rstart;
+  const uint32_t* rinfo;
+  uint32_t R;
+};
+
+// One-bit outputs. Each step the wave builds 64 consecutive 32-output words (aligned on the
+// global output index), one per lane, from the runs covering them; then the words are
+// redistributed (ds_bpermute) so that every store instruction covers one contiguous 1 KiB:
+// lane l stores outputs [8l, 8l + 8) (int16) or [16l, 16l + 16) (bytes) of each KiB. Chunks
+// shared with a neighbouring window are stored element by element, inside [base, endo) only.
+// Returns this lane's count of 1s.
+template <int OUT>
+__device__ inline uint32_t lv_write1(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+                                     uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
+                                     uint8_t* __restrict__ out) {
+  constexpr uint32_t V = 16u / OUT;        // outputs per 16-byte chunk
+  constexpr uint32_t NQ = 64u * 32u / (V * 64u);  // store instructions per step (4 / 2)
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t go = x.s.out;  // global index of the page's output 0
+  const uint64_t lo = go + base, hi = go + endo;
+  const uint64_t A0 = lo & ~31ull;
+  const uint32_t nwords = (uint32_t)((hi - A0 + 31u) >> 5);
+  uint32_t lgn = 1;
+  while (lgn * 2u <= rl.R) lgn *= 2u;
+  uint32_t cnt = 0;
+#pragma unroll 1
+  for (uint32_t w0 = 0; w0 < nwords; w0 += WAVE) {
+    const uint32_t wd = w0 + lane;
+    const uint64_t ga = A0 + (uint64_t)wd * 32u;
+    uint32_t bits = 0;
+    if (wd < nwords) {
+      const uint32_t pa = (uint32_t)(ga - go);  // page-relative output of bit 0 (may wrap)
+      const uint32_t olo = ga >= lo ? pa : base;
+      const uint32_t ohi = ga + 32u <= hi ? pa + 32u : endo;
+      uint32_t b = 0;  // last run starting at or before olo
+      for (uint32_t sp = lgn; sp; sp >>= 1)
+        if (b + sp < rl.R && rl.rstart[b + sp] <= olo) b += sp;
+      for (uint32_t o = olo; o < ohi; ++b) {
+        const uint32_t nst = rl.rstart[b + 1];
+        const uint32_t e = nst < ohi ? nst : ohi;
+        if (e > o) bits |= lv_run_bits1(stage, blob, blob_len, x, rl.rstart[b], rl.rinfo[b], o, e) << (o - pa);
+        o = e > o ? e : o;
+      }
+      cnt += __builtin_popcount(bits);
+    }
+    const uint64_t gb = A0 + (uint64_t)w0 * 32u;  // global output of this step's bit 0
+#pragma unroll
+    for (uint32_t q = 0; q < NQ; ++q) {
+      const uint32_t per = 32u / V;  // chunks per word
+      const uint32_t wv = (uint32_t)__shfl((int)bits, (int)(q * (WAVE / per) + lane / per), 64);
+      const uint32_t cb = (wv >> (V * (lane % per))) & ((1u << V) - 1u);
+      const uint64_t gc = gb + (uint64_t)(q * WAVE + lane) * V;  // the chunk's first output
+      if (gc >= hi || gc + V <= lo) continue;
+      if (gc >= lo && gc + V <= hi) {
+        uint32_t d[4];
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t)
+          d[t] = OUT == 2 ? (((cb >> (2u * t)) & 3u) * 0x8001u) & 0x10001u
+                          : (((cb >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
+        *reinterpret_cast<uint4*>(out + gc * OUT) = make_uint4(d[0], d[1], d[2], d[3]);
+      } else {
+        for (uint32_t j = 0; j < V; ++j) {
+          const uint64_t gi = gc + j;
+          if (gi >= lo && gi < hi) {
+            if (OUT == 2) reinterpret_cast<int16_t*>(out)[gi] = (int16_t)((cb >> j) & 1u);
+            else out[gi] = (uint8_t)((cb >> j) & 1u);
+          }
+        }
+      }
+    }
+  }
+  return cnt;
+}
+
+// Wider levels: groups of G outputs (one 16-byte store), each from the runs covering it.
+// Returns this lane's count of outputs == maxl.
+template <int OUT>
+__device__ inline uint32_t lv_write_wide(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+                                         uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
+                                         uint32_t maxl, bool count, uint8_t* __restrict__ out) {
+  constexpr uint32_t G = 16u / OUT;  // outputs per 16-byte store
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
+  const uint64_t go = x.s.out;
+  const uint64_t k0 = (go + base) / G, k1 = (go + endo + G - 1) / G;
+  uint32_t lgn = 1;
+  while (lgn * 2u <= rl.R) lgn *= 2u;
+  uint32_t a = 0, cnt = 0;
+#pragma unroll 1
+  for (uint64_t k = k0 + lane; k < k1; k += WAVE) {
+    const uint64_t gl = k * G;
+    const uint32_t olo = (uint32_t)((gl > go + base ? gl : go + base) - go);
+    const uint32_t ohi = (uint32_t)((gl + G < go + endo ? gl + G : go + endo) - go);
+    const uint32_t f0 = (uint32_t)(gl - go);  // page-relative index of field 0 (may wrap)
+    for (uint32_t sp = lgn; sp; sp >>= 1)
+      if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
+    uint32_t f[G];
+#pragma unroll
+    for (uint32_t j = 0; j < G; ++j) f[j] = 0;
+    uint32_t b = a, o = olo;
+    while (o < ohi) {
+      const uint32_t st = rl.rstart[b], nst = rl.rstart[b + 1], inf = rl.rinfo[b];
+      const uint32_t be = nst < ohi ? nst : ohi;
+      for (; o < be; ++o) {
+        uint32_t v;
+        if (inf & R_RLE) {
+          v = inf & 0x7FFFFFFFu;
+        } else {
+          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - st) * w;
+          v = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j)
+          if (o - f0 == j) f[j] = v;
+        if (count) cnt += v == maxl ? 1u : 0u;
+      }
+      ++b;
+    }
+    if (ohi - olo == G) {
+      uint4 v;
+      if (OUT == 2) {
+        v = make_uint4((f[0] & 0xFFFFu) | (f[1] << 16), (f[2] & 0xFFFFu) | (f[3] << 16),
+                       (f[4] & 0xFFFFu) | (f[5] << 16), (f[6] & 0xFFFFu) | (f[7] << 16));
+      } else {
+        uint32_t q[4];
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t)
+          q[t] = (f[4 * t] & 0xFFu) | ((f[4 * t + 1] & 0xFFu) << 8) | ((f[4 * t + 2] & 0xFFu) << 16) |
+                 ((f[4 * t + 3] & 0xFFu) << 24);
+        v = make_uint4(q[0], q[1], q[2], q[3]);
+      }
+      *reinterpret_cast<uint4*>(out + gl * OUT) = v;
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < G; ++j) {
+        const uint32_t oo = f0 + j;
+        if (oo >= olo && oo < ohi) {
+          if (OUT == 2) reinterpret_cast<int16_t*>(out)[gl + j] = (int16_t)f[j];
+          else out[gl + j] = (uint8_t)f[j];
+        }
+      }
+    }
+  }
+  return cnt;
+}
+
+// Outputs of one window from its run list, and the def count.
+template <int OUT>
+__device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+                                uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo, int sel,
+                                const ColumnParams& cp, PageWork* pages, uint8_t* __restrict__ out) {
+  const bool count = sel == SS_DEF;
+  const uint32_t maxl = sel == SS_DEF ? (uint32_t)cp.max_def : (uint32_t)cp.max_rep;
+  uint32_t cnt = x.s.w == 1 ? lv_write1<OUT>(rl, stage, blob, blob_len, x, base, endo, out)
+                            : lv_write_wide<OUT>(rl, stage, blob, blob_len, x, base, endo, maxl, count, out);
+  if (count) {
+    cnt = wave_sum_u32_(cnt);
+    if ((threadIdx.x & 63u) == 0 && cnt) atomicAdd((unsigned long long*)&pages[x.p].nonnull, (unsigned long long)cnt);
+  }
+}
+
+// ------------------------------------------------------------------------------ k_lv_emit
+// Window path: windows g2 of the dense pages.
 template <int OUT>
 __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                 PageWork* pages, int npages, ColumnParams cp, int sel,
                                                 RunTables rt, LevelTables lt, uint8_t* __restrict__ out) {
   __shared__ LvSmem sm;
-  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
-  const uint32_t total = lt.wbase[npages];
-  const bool count = sel == SS_DEF;
-  const uint32_t maxl = sel == SS_DEF ? (uint32_t)cp.max_def : (uint32_t)cp.max_rep;
-  constexpr uint32_t G = 16u / OUT;  // outputs per 16-byte store
-  for (uint32_t g = blockIdx.x * (WG / WAVE) + wid; g < total; g += gridDim.x * (WG / WAVE)) {
+  const uint32_t total = lt.wbase2[npages];
+  for (uint32_t g2 = blockIdx.x * (WG / WAVE) + wid; g2 < total; g2 += gridDim.x * (WG / WAVE)) {
     LvWin x;
-    x.p = lv_page_of(lt.wbase, (uint32_t)npages, g);
+    x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
     const PageWork& pw = pages[x.p];
     if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, cp, x.s)) continue;
-    const uint2 wi = lt.win[g];
+    x.k = g2 - lt.wbase2[x.p];
+    const uint2 wi = lt.win[lt.wbase[x.p] + x.k];
     if (wi.x == LV_NONE) continue;  // no true header in this window
-    x.k = g - lt.wbase[x.p];
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen, n = x.s.n;
-    const uint32_t wm = w >= 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
     const uint32_t e0 = wi.x & 0xFFFFu, nh = wi.x >> 16;  // entry, true headers (saturated)
     const uint32_t base = wi.y;
-    lv_stage(blob, blob_len, x, W.stage, x.sb);
+    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
@@ -454,8 +797,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
           }
           W.runs.rstart[nr] = acc < 0xFFFFFFFFull ? (uint32_t)acc : 0xFFFFFFFFu;
           W.runs.rinfo[nr] = bp ? v : (R_RLE | v);
-          bad |= c && !(bp ? ((uint64_t)v * 8ull + (uint64_t)min((uint64_t)c, n - acc) * w <= (uint64_t)slen * 8ull)
-                           : (v >> w) == 0);
+          bad |= !lv_run_ok(bp, v, c, acc, n, slen, w);
           ++nr;
           acc += c;
           q = nx;
@@ -517,29 +859,14 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
         const uint64_t hb = __ballot(hdr);
         const uint64_t db = __ballot(dead);
         if (!hb && !db) continue;  // no true header in this row
-        // inclusive counts over the lanes: runs by popcount, outputs by a DPP scan (32-bit while
-        // every count is below 2^25, else a 64-bit shuffle scan)
         const uint32_t ir = (uint32_t)__builtin_popcountll(hb & ((2ull << lane) - 1ull));
-        uint64_t ic;
-        if (!__ballot(c >= (1u << 25))) {
-          ic = wave_incl_scan_u32(c);
-        } else {
-          ic = c;
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t b = __shfl_up(ic, d, 64);
-            if (lane >= (uint32_t)d) ic += b;
-          }
-        }
+        const uint64_t ic = wave_incl_scan_cnt(c);
         const uint64_t acc = (uint64_t)base + T + ic - c;
         if (hdr) {
           const uint32_t k = R + ir - 1u;
           W.runs.rstart[k] = acc < 0xFFFFFFFFull ? (uint32_t)acc : 0xFFFFFFFFu;
           W.runs.rinfo[k] = bp ? v : (R_RLE | v);
-          // what the reader consumes must be decodable: payload inside the stream, an RLE
-          // value that fits the bit width
-          bad |= acc < n && c && !(bp ? ((uint64_t)v * 8ull + (uint64_t)min((uint64_t)c, n - acc) * w <= (uint64_t)slen * 8ull)
-                                      : (v >> w) == 0);
+          bad |= !lv_run_ok(bp, v, c, acc, n, slen, w);
         }
         bad |= dead && acc < n;
         R += (uint32_t)__builtin_popcountll(hb);
@@ -548,7 +875,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
       }
     }
     if (__ballot(bad)) {
-      if (lane == 0) lv_bail(rt, x.p);
+      if (lane == 0) lv_bail(rt, x.p, PF_PAGE);
       continue;
     }
     if (lane == 0) W.runs.rstart[R] = 0xFFFFFFFFu;
@@ -556,182 +883,105 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (endo <= base || R == 0) continue;
-#ifdef PQG_DIAG
-    if (cp.debug & 128) continue;  // diagnostics: index work only, no output
-#endif
-    const uint64_t go = x.s.out;  // global index of the page's output 0
-    uint32_t cnt = 0;
-    if (w == 1) {
-      // one-bit outputs: chunks of LV_BM outputs (aligned on global groups of G) go through an
-      // LDS bitmap, filled run by run (lane r: runs r, r + 64, ...), then stored 16 bytes at a time
-      const uint64_t G0 = (go + base) & ~(uint64_t)(G - 1);
-#pragma unroll 1
-      for (uint64_t c0 = G0; c0 < go + endo; c0 += LV_BM) {
-        const uint64_t c1 = c0 + LV_BM < go + endo ? c0 + LV_BM : go + endo;
-        const uint32_t plo = (uint32_t)((c0 > go + base ? c0 : go + base) - go);  // page-relative
-        const uint32_t phi = (uint32_t)(c1 - go);
-        const uint32_t pc0 = (uint32_t)(c0 - go);  // page-relative output of bitmap bit 0 (may wrap)
-#pragma unroll
-        for (uint32_t t = 0; t < LV_BM / 32 / WAVE; ++t) W.bm[t * WAVE + lane] = 0;
-        wave_lds_sync();
-        for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
-          const uint32_t r = r0 + lane;
-          uint32_t st = 0, inf = 0, o = 0, e = 0;
-          if (r < R) {
-            st = W.runs.rstart[r];
-            inf = W.runs.rinfo[r];
-            const uint32_t en = W.runs.rstart[r + 1];
-            o = st > plo ? st : plo;
-            e = en < phi ? en : phi;
-          }
-          const bool lng = e > o && e - o > 1024u;  // long runs: the whole wave, below
-          if (!lng) {
-            while (o < e) {  // one bitmap word at a time
-              const uint32_t b = o - pc0;
-              const uint32_t we = (b | 31u) + 1u + pc0;  // page output after this word
-              const uint32_t oe = we < e ? we : e;
-              const uint32_t bits = lv_run_bits1(W, blob, blob_len, x, st, inf, o, oe);
-              if (bits) atomicOr(&W.bm[b >> 5], bits << (b & 31u));
-              o = oe;
-            }
-          }
-          for (uint64_t lb = __ballot(lng); lb; lb &= lb - 1) {
-            const int L = __builtin_ctzll(lb);
-            const uint32_t lst = (uint32_t)__shfl((int)st, L, 64), linf = (uint32_t)__shfl((int)inf, L, 64);
-            const uint32_t lo_ = (uint32_t)__shfl((int)o, L, 64), le = (uint32_t)__shfl((int)e, L, 64);
-            const uint32_t b0 = (lo_ - pc0) >> 5, b1 = (le - pc0 + 31u) >> 5;
-            for (uint32_t wd = b0 + lane; wd < b1; wd += WAVE) {
-              const uint32_t wo0 = pc0 + wd * 32u;
-              const uint32_t wo = wo0 > lo_ && wd == b0 ? lo_ : (wd == b0 ? lo_ : wo0);
-              const uint32_t we = wo0 + 32u < le ? wo0 + 32u : le;
-              const uint32_t bits = lv_run_bits1(W, blob, blob_len, x, lst, linf, wo, we);
-              if (bits) atomicOr(&W.bm[wd], bits << ((wo - pc0) & 31u));
-            }
-          }
-        }
-        wave_lds_sync();
-        const uint32_t ngr = (uint32_t)((c1 - c0 + G - 1) / G);
-        for (uint32_t k = lane; k < ngr; k += WAVE) {
-          const uint64_t gl = c0 + (uint64_t)k * G;
-          const uint32_t bits = (W.bm[(k * G) >> 5] >> ((k * G) & 31u)) & ((1u << G) - 1u);
-          if (count) cnt += __builtin_popcount(bits);
-          if (gl >= go + base && gl + G <= go + endo) {
-            uint4 v;
-            if (OUT == 2) {
-              uint32_t q[4];
-#pragma unroll
-              for (uint32_t t = 0; t < 4; ++t) q[t] = ((bits >> (2 * t)) & 1u) | (((bits >> (2 * t + 1)) & 1u) << 16);
-              v = make_uint4(q[0], q[1], q[2], q[3]);
-            } else {
-              uint32_t q[4];
-#pragma unroll
-              for (uint32_t t = 0; t < 4; ++t) {
-                const uint32_t y = bits >> (4 * t);
-                q[t] = (y & 1u) | (((y >> 1) & 1u) << 8) | (((y >> 2) & 1u) << 16) | (((y >> 3) & 1u) << 24);
-              }
-              v = make_uint4(q[0], q[1], q[2], q[3]);
-            }
-            *reinterpret_cast<uint4*>(out + gl * OUT) = v;
-          } else {  // a group shared with a neighbouring window: only this window's outputs
-#pragma unroll
-            for (uint32_t j = 0; j < G; ++j) {
-              const uint64_t gi = gl + j;
-              if (gi >= go + base && gi < go + endo) {
-                if (OUT == 2) reinterpret_cast<int16_t*>(out)[gi] = (int16_t)((bits >> j) & 1u);
-                else out[gi] = (uint8_t)((bits >> j) & 1u);
-              }
-            }
-          }
-        }
-        wave_lds_sync();
-      }
-    } else {
-      // wider levels: groups of G outputs, each from the runs covering it
-      const uint64_t k0 = (go + base) / G, k1 = (go + endo + G - 1) / G;
-      uint32_t lgn = 1;
-      while (lgn * 2 <= R) lgn *= 2;
-      uint32_t a = 0;
-#pragma unroll 1
-      for (uint64_t k = k0 + lane; k < k1; k += WAVE) {
-        const uint64_t gl = k * G;
-        const uint32_t olo = (uint32_t)((gl > go + base ? gl : go + base) - go);
-        const uint32_t ohi = (uint32_t)((gl + G < go + endo ? gl + G : go + endo) - go);
-        const uint32_t f0 = (uint32_t)(gl - go);  // page-relative index of field 0 (may wrap)
-        for (uint32_t st = lgn; st; st >>= 1)
-          if (a + st < R && W.runs.rstart[a + st] <= olo) a += st;
-        uint32_t f[G];
-#pragma unroll
-        for (uint32_t j = 0; j < G; ++j) f[j] = 0;
-        uint32_t b = a, o = olo;
-        while (o < ohi) {
-          const uint32_t st = W.runs.rstart[b], nst = W.runs.rstart[b + 1], inf = W.runs.rinfo[b];
-          const uint32_t be = nst < ohi ? nst : ohi;
-          for (; o < be; ++o) {
-            uint32_t v;
-            if (inf & R_RLE) {
-              v = inf & 0x7FFFFFFFu;
-            } else {
-              const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - st) * w;
-              v = (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x.s.S, x.W0, x.sb, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < G; ++j)
-              if (o - f0 == j) f[j] = v;
-            if (count) cnt += v == maxl ? 1u : 0u;
-          }
-          ++b;
-        }
-        if (ohi - olo == G) {
-          uint4 v;
-          if (OUT == 2) {
-            v = make_uint4((f[0] & 0xFFFFu) | (f[1] << 16), (f[2] & 0xFFFFu) | (f[3] << 16),
-                           (f[4] & 0xFFFFu) | (f[5] << 16), (f[6] & 0xFFFFu) | (f[7] << 16));
-          } else {
-            uint32_t q[4];
-#pragma unroll
-            for (uint32_t t = 0; t < 4; ++t)
-              q[t] = (f[4 * t] & 0xFFu) | ((f[4 * t + 1] & 0xFFu) << 8) | ((f[4 * t + 2] & 0xFFu) << 16) |
-                     ((f[4 * t + 3] & 0xFFu) << 24);
-            v = make_uint4(q[0], q[1], q[2], q[3]);
-          }
-          *reinterpret_cast<uint4*>(out + gl * OUT) = v;
-        } else {
-#pragma unroll
-          for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t oo = f0 + j;
-            if (oo >= olo && oo < ohi) {
-              if (OUT == 2) reinterpret_cast<int16_t*>(out)[gl + j] = (int16_t)f[j];
-              else out[gl + j] = (uint8_t)f[j];
-            }
-          }
-        }
-      }
+    lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel, cp,
+                  pages, out);
+    wave_lds_sync();  // the run list and stage are refilled by the next window
+  }
+}
+
+// ------------------------------------------------------------------------------ k_lv_emit_walk
+// Windows of the walked pages: each wave takes a contiguous range of windows (one page lookup,
+// then the page advances with the window), loads each window's run records and writes its
+// outputs.
+struct LeWave {
+  uint32_t stage[LE_STG / 4];
+  uint32_t rstart[LW_RPW + 1];
+  uint32_t rinfo[LW_RPW];
+};
+
+template <int OUT>
+__global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, int npages, ColumnParams cp, int sel,
+                                                     RunTables rt, LevelTables lt, uint8_t* __restrict__ out) {
+  __shared__ LeWave sm[WG / WAVE];
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  LeWave& E = sm[wid];
+  const uint32_t total = lt.wbase[npages];
+  const uint32_t nwv = gridDim.x * (WG / WAVE), gw = blockIdx.x * (WG / WAVE) + wid;
+  const uint32_t per = (total + nwv - 1u) / nwv;
+  const uint32_t g0 = gw * per, g1 = min(total, g0 + per);
+  if (g0 >= g1) return;
+  uint32_t p = lv_page_of(lt.wbase, (uint32_t)npages, g0);
+  uint32_t wb = lt.wbase[p], pend = lt.wbase[p + 1];
+  LvWin x;
+  x.p = p;
+  bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
+  for (uint32_t g = g0; g < g1; ++g) {
+    while (g >= pend) {  // next page (pages without windows are passed over)
+      ++p;
+      wb = pend;
+      pend = lt.wbase[p + 1];
+      x.p = p;
+      walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
     }
-    if (count) {
-      cnt = wave_sum_u32_(cnt);
-      if (lane == 0 && cnt) atomicAdd((unsigned long long*)&pages[x.p].nonnull, (unsigned long long)cnt);
+    if (!walked) {
+      g = pend - 1u;
+      continue;
     }
+    x.k = g - wb;
+    const uint32_t* wf = lt.wfirst + wb + p;
+    const uint32_t fr = wf[x.k], fe = wf[x.k + 1];
+    if (fr == fe) continue;  // no header starts in this window
+    const uint32_t R = fe - fr;
+    if (R > LW_RPW) {  // more runs than the run list holds (not from the walker's span rule)
+      if (lane == 0) lv_bail(rt, p, PF_WALK);
+      continue;
+    }
+    const uint2* rc = lt.rec + (uint64_t)LW_REC * (wb + 2ull * p) + fr;
+    const uint32_t endn = rc[R].x;  // first output of the next window's first run (or the total)
+    for (uint32_t i = lane; i <= R; i += WAVE) {
+      const uint2 r = rc[i];
+      E.rstart[i] = i < R ? r.x : 0xFFFFFFFFu;
+      E.rinfo[i] = r.y;
+    }
+    x.W0 = x.k * LV_WIN;
+    const uint32_t w = (uint32_t)x.s.w;
+    uint32_t nch = (LV_WIN + 16u + 64u * w + 16u) / 16u + 1u;
+    if (nch > LE_STG / 16) nch = LE_STG / 16;
+    lv_stage(blob, blob_len, x, E.stage, nch);  // ends with a wave LDS sync (run list too)
+    const uint32_t base = E.rstart[0];
+    const uint32_t endo = endn < x.s.n ? endn : x.s.n;
+    if (endo > base) lv_write<OUT>(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp,
+                                   pages, out);
+    wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
 
 extern "C" {
 
-// Level path of stream `sel` (def / rep levels: int16 out; RLE booleans: bytes out): plan,
-// window tables, stitch, emit (+ def counts). 2048 workgroups (4 windows each) sweep the
-// windows of every page.
+// Level path of stream `sel` (def / rep levels: int16 out; RLE booleans: bytes out): plan, page
+// walk, window path for the dense pages, emits (+ def counts).
 hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                          ColumnParams cp, int sel, RunTables rt, LevelTables lt, void* out, hipStream_t s) {
   if (npages <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_walk, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
+                     lt);
+  hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   const uint32_t wgrid = 256u * 8u;
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_stitch, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
-  if (sel == SS_BOOL)
+  if (sel == SS_BOOL) {
     hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt,
                        (uint8_t*)out);
-  else
+    hipLaunchKernelGGL(k_lv_emit_walk<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
+                       lt, (uint8_t*)out);
+  } else {
     hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt,
                        (uint8_t*)out);
+    hipLaunchKernelGGL(k_lv_emit_walk<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
+                       lt, (uint8_t*)out);
+  }
   return hipGetLastError();
 }
 

@@ -716,7 +716,7 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   const PageWork& pw = pages[p];
   d.page = p;
   if (pw.status != 0) return d;
-  if (rt.pflag && rt.pflag[p] == PF_PAGE) return d;  // decoded by the page pass
+  if (rt.pflag && pf_level_path(rt.pflag[p])) return d;  // decoded by the level path
   if (sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0)) return d;
   Stream s;
   if (!get_stream(blob, pw, sel, cp, s) || s.err) return d;

@@ -83,18 +83,18 @@ struct Slot {
   size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
-  uint32_t* lvwb[3] = {}; // level path (def, rep, RLE booleans): per-page window bases
-  size_t lvwbcap[3] = {};
-  uint2* lvtab[3] = {};   // window tables
-  size_t lvtabcap[3] = {};
-  uint2* lvwin[3] = {};   // per-window entries
-  size_t lvwincap[3] = {};
+  // level path (def, rep, RLE booleans): buffers of LevelTables (pqg_internal.hpp), grown on demand
+  static constexpr int LV_BUFS = 6;  // wbase, wbase2, wfirst, rec, tab, win
+  void* lvbuf[3][LV_BUFS] = {};
+  size_t lvcap[3][LV_BUFS] = {};
   LevelTables lt(int k) const {
     LevelTables t{};
-    t.wbase = lvwb[k];
-    t.tab = lvtab[k];
-    t.win = lvwin[k];
-    t.wcap = (uint32_t)lvwincap[k];
+    t.wbase = (uint32_t*)lvbuf[k][0];
+    t.wbase2 = (uint32_t*)lvbuf[k][1];
+    t.wfirst = (uint32_t*)lvbuf[k][2];
+    t.rec = (uint2*)lvbuf[k][3];
+    t.tab = (uint2*)lvbuf[k][4];
+    t.win = (uint2*)lvbuf[k][5];
     return t;
   }
 };
@@ -242,9 +242,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dt.flag);
     hipFree(sl.dt.nfall);
     for (int k = 0; k < 3; ++k) {
-      hipFree(sl.lvwb[k]);
-      hipFree(sl.lvtab[k]);
-      hipFree(sl.lvwin[k]);
+      for (void* b : sl.lvbuf[k]) hipFree(b);
     }
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
@@ -448,7 +446,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
 #endif
   cp.debug = dbg_env;
   cp.dbgbuf = nullptr;
-  if (dbg_env & 112) {
+  if (dbg_env & (16 | 32 | 64)) {
     size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
     if (need < (size_t)npages * 64) need = (size_t)npages * 64;
     if (need > ctx->dbg_cap) {
@@ -563,10 +561,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   for (int k = 0; k < 3; ++k) {
     if (!need_lv[k]) continue;
     int st;
-    if ((st = grow((void**)&sl.lvwb[k], &sl.lvwbcap[k], (size_t)npages + 1, 4, "hipMalloc level windows"))) return st;
-    if ((st = grow((void**)&sl.lvwin[k], &sl.lvwincap[k], nwin + 1, sizeof(uint2), "hipMalloc level windows"))) return st;
     const size_t ent = lv_ent(k == 2 ? 1u : (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width));
-    if ((st = grow((void**)&sl.lvtab[k], &sl.lvtabcap[k], (nwin + 1) * ent, sizeof(uint2), "hipMalloc level tables"))) return st;
+    const size_t need[Slot::LV_BUFS] = {(size_t)npages + 1, (size_t)npages + 1, nwin + npages + 1,
+                                        64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1};
+    const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2)};
+    for (int b = 0; b < Slot::LV_BUFS; ++b)
+      if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
   }
   // Hybrid-stream flags: the level path (def, rep, RLE booleans) sets every page's flag and counts
   // the streams it hands back; dictionary indices always take the general decoder.

@@ -149,17 +149,21 @@ struct DeltaTables {
 };
 
 // Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
+// Windows are 1 KiB of a page's stream; run records of walked pages are 64 per window + 128.
 struct LevelTables {
-  uint32_t* wbase;  // [pages + 1] first window of each page's stream (k_lv_plan)
-  uint2* tab;       // [windows * entries] per window and entry offset: (exit offset, outputs)
-  uint2* win;       // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
-  uint32_t wcap;    // windows the per-window arrays hold
-  uint32_t pad;
+  uint32_t* wbase;   // [pages + 1] first window of each page's stream (k_lv_plan)
+  uint32_t* wbase2;  // [pages + 1] the same over the pages the walker left to the window path
+  uint32_t* wfirst;  // [windows + pages] walked pages: first run of each window, then the run count
+  uint2* rec;        // [64 * (windows + 2 * pages)] walked pages' runs: (first output, info)
+  uint2* tab;        // [windows * entries] per window and entry offset: (exit offset, outputs)
+  uint2* win;        // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
 };
 
-// RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) / handed back by it
-// to the general hybrid decoder (pqg_runs.hpp)
-constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u;
+// RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window
+// kernels (PF_PAGE) or after its page walker (PF_WALK) — or handed back by it to the general
+// hybrid decoder (pqg_runs.hpp, PF_BAIL)
+constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u, PF_WALK = 3u;
+__host__ __device__ inline bool pf_level_path(uint32_t f) { return f == PF_PAGE || f == PF_WALK; }
 
 struct ColumnParams {
   int32_t physical_type;
