@@ -56,9 +56,8 @@ constexpr uint32_t LV_J_END = 0xFFFEu;             //   reaches the end of the s
 constexpr uint32_t LV_J_DEAD = 0xFFFFu;            //   meets a header the fast parse refuses
 
 // page walker (k_lv_walk) and the emit of walked pages (k_lv_emit_walk)
-constexpr uint32_t LW_REG = 4096 - 16;             // stream bytes whose headers one region holds
-                                                   // (+ alignment: its first 4 KiB stay in VGPRs)
-constexpr uint32_t LW_CH = 5;                      // 16-byte loads per lane per region
+constexpr uint32_t LW_REG = 3072 - 128;            // stream bytes whose headers one region holds
+constexpr uint32_t LW_CH = 3;                      // 16-byte loads per lane per region
 constexpr uint32_t LW_STG = LW_CH * 16 * WAVE;     // staged bytes (region + alignment + read-ahead)
 constexpr uint32_t LW_SPAN = 1024;                 // 64 headers within fewer bytes: a dense page
 constexpr uint32_t LW_RPW = 256;                   // runs per window k_lv_emit_walk takes (the span
@@ -75,8 +74,6 @@ __device__ inline bool lv_width_ok(uint32_t w) { return w >= 1 && w <= 16; }
 __device__ __host__ inline uint32_t lv_ent(uint32_t w) {
   return w == 1 ? 64u : w == 2 ? 128u : w <= 4 ? 256u : w <= 8 ? 512u : 1024u;
 }
-
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 // Wave-private LDS of the window kernels. Lane l owns positions j * 64 + l (j < 16), so the
 // wave's accesses to its own entries are consecutive (conflict-free).
@@ -294,6 +291,11 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
     rt.pflag[p] = flag;
     return nw;
   });
+  lv_scan_windows(npages, lt.sbase, [&](int p) -> uint32_t {
+    Stream s;
+    if (!lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
+    return ((s.slen + LV_WIN - 1) / LV_WIN + LW_SEGW - 1) / LW_SEGW;
+  });
 }
 
 // One workgroup: windows of the pages the walker left to the window path (wbase2).
@@ -303,36 +305,226 @@ __global__ void __launch_bounds__(WG) k_lv_plan2(int npages, RunTables rt, Level
   });
 }
 
-// ------------------------------------------------------------------------------ k_lv_walk
-// One wave per page. Status: walked (PF_WALK; run records and per-window first runs written),
-// dense (PF_PAGE stays: window path), or handed to the general decoder (PF_BAIL).
-__global__ void __launch_bounds__(WG) k_lv_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                const PageWork* __restrict__ pages, int npages,
-                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
-  __shared__ uint32_t stg[WG / WAVE][LW_STG / 4];
+// ------------------------------------------------------------------------------ sparse streams
+// A page stream is cut into segments of LW_SEGW windows, each walked by its own wave: the
+// chain of a sparse stream enters segment j somewhere in its first window, and chains entering
+// a window at different offsets meet within a few headers. k_lv_bound finds, for segment j's
+// first window, where every chain entering it leaves it; when they all leave at one offset
+// (X_j), the true chain passes there whatever its entry. Segment j's walk starts at X_j and stops
+// when it lands exactly on X_m, a later segment's start (one it jumps over was not on the true
+// chain, and it walks on to the next); the page scan follows the walks from offset 0 and places
+// their runs. A dense stream hands the page to the window path.
+
+// LvSeg::status
+constexpr uint32_t LS_LANDED = 1;    // reached X_next
+constexpr uint32_t LS_END = 2;       // reached the end of the stream
+constexpr uint32_t LS_DEAD = 3;      // met a header the fast parse refuses (not recorded)
+constexpr uint32_t LS_TRUNC = 4;     // last recorded run: bit-packed payload past the stream end
+constexpr uint32_t LS_BADVAL = 5;    // last recorded run: RLE value wider than the bit width
+constexpr uint32_t LS_DENSE = 6;     // 64 headers within fewer than LW_SPAN bytes, or too many runs
+constexpr uint32_t LS_NOSTART = 7;   // the first window has no exit to start from
+constexpr uint32_t LV_BX_NONE = 0xFFFFFFFFu, LV_BX_AMBIG = 0xFFFFFFFEu;
+
+// Pointer jumping over the staged window x (see k_lv_win): jv/cv for the lane's positions.
+__device__ inline void lv_jump(LvWave& W, const LvWin& x, uint32_t (&jv)[LV_PPL], uint32_t (&cv)[LV_PPL]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3;
+  lv_first_hops(W.stage, x.sb, x.W0, x.s.slen, w, vb, jv, cv);
+#pragma unroll
+  for (uint32_t j = 0; j < LV_PPL; ++j) W.JC[j * WAVE + lane] = make_uint2(jv[j], cv[j]);
+  wave_lds_sync();
+  // after round r, jv[j] is 2^(r+1) hops on (or terminal) and cv[j] the outputs along the way
+  // (saturating); the high half of jv counts the headers passed (also saturating). Stops once
+  // every chain has left the window.
+#pragma unroll 1
+  for (uint32_t r = 0; r < LV_ROUNDS; ++r) {
+    bool live = false;
+#pragma unroll
+    for (uint32_t j = 0; j < LV_PPL; ++j) live |= (jv[j] & 0xFFFFu) < LV_WIN;
+    if (!__any(live)) break;
+    uint2 nx[LV_PPL];
+#pragma unroll
+    for (uint32_t j = 0; j < LV_PPL; ++j) {
+      const uint32_t t = jv[j] & 0xFFFFu;
+      nx[j] = t < LV_WIN ? W.JC[t] : make_uint2(t, 0u);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < LV_PPL; ++j) {
+      const uint32_t s2 = cv[j] + nx[j].y;
+      cv[j] = s2 < cv[j] ? 0xFFFFFFFFu : s2;
+      const uint32_t hs = (jv[j] >> 16) + (nx[j].x >> 16);
+      jv[j] = (nx[j].x & 0xFFFFu) | ((hs < 0xFFFFu ? hs : 0xFFFFu) << 16);
+      W.JC[j * WAVE + lane] = make_uint2(jv[j], cv[j]);
+    }
+    wave_lds_sync();
+  }
+}
+
+// Segment s of the level streams: page, segment of the page; false unless the page is still
+// on the level path's sparse candidates.
+__device__ inline bool lv_seg_of(const uint8_t* blob, const PageWork* pages, uint32_t npages, const ColumnParams& cp,
+                                 int sel, const RunTables& rt, const LevelTables& lt, uint32_t s, uint32_t& p,
+                                 uint32_t& j, Stream& st) {
+  p = lv_page_of(lt.sbase, npages, s);
+  j = s - lt.sbase[p];
+  return rt.pflag[p] == PF_PAGE && lv_stream(blob, pages[p], sel, cp, st);
+}
+
+// ------------------------------------------------------------------------------ k_lv_bound
+// One wave per segment j >= 1: the common exit of its first window's chains (bexit).
+__global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                 const PageWork* __restrict__ pages, int npages, ColumnParams cp,
+                                                 int sel, RunTables rt, LevelTables lt) {
+  __shared__ LvSmem sm;
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  const uint32_t p = blockIdx.x * (WG / WAVE) + wid;
-  if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
+  LvWave& W = sm.wv[wid];
+  const uint32_t total = lt.sbase[npages];
+  for (uint32_t s = blockIdx.x * (WG / WAVE) + wid; s < total; s += gridDim.x * (WG / WAVE)) {
+    LvWin x;
+    uint32_t j;
+    if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, s, x.p, j, x.s) || j == 0) continue;
+    x.k = j * LW_SEGW;
+    x.W0 = x.k * LV_WIN;
+    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
+    uint32_t jv[LV_PPL], cv[LV_PPL];
+    lv_jump(W, x, jv, cv);
+    // Where the chains entering at offsets [0, ent) leave the window, among the exits one hop of
+    // the writer's form can reach (a <= 2-byte header and <= 64 groups: rle.rs:48-50); then,
+    // through the next window's table, where they leave that one (chains keep meeting: two
+    // windows leave fewer apart). The exit most of them share is taken — chains entering on
+    // payload bytes that do not meet the true chain mostly jump far away. The walk of the
+    // segment before verifies the choice by landing on it exactly.
+    const uint32_t w = (uint32_t)x.s.w;
+    const uint32_t ent = lv_ent(w);
+    const uint32_t hop = 8u + 64u * w;
+    uint32_t ex[LV_PPL];
+#pragma unroll
+    for (uint32_t q = 0; q < LV_PPL; ++q) {
+      const uint32_t t = jv[q] & 0xFFFFu;
+      ex[q] = (q * WAVE + lane < ent && t < LV_WIN + hop) ? t : 0xFFFFFFFFu;
+    }
+    uint32_t near = LV_WIN + hop;
+    if (x.W0 + LV_WIN < x.s.slen) {
+      wave_lds_sync();
+      LvWin x2 = x;
+      x2.W0 = x.W0 + LV_WIN;
+      lv_stage(blob, blob_len, x2, W.stage, LV_STG_CH);
+      lv_jump(W, x2, jv, cv);
+#pragma unroll
+      for (uint32_t q = 0; q < LV_PPL; ++q) {
+        if (ex[q] == 0xFFFFFFFFu) continue;
+        const uint32_t o = ex[q] - LV_WIN;
+        if (o >= LV_WIN) continue;  // enters past the second window: keep its first exit
+        const uint32_t t = W.JC[o].x & 0xFFFFu;
+        ex[q] = t < LV_WIN + hop ? LV_WIN + t : 0xFFFFFFFFu;
+      }
+      near = 2u * LV_WIN + hop;
+    }
+    uint32_t best = 0xFFFFFFFFu, bestn = 0;
+#pragma unroll 1
+    for (uint32_t q = 0; q < LV_PPL && q * WAVE < ent; ++q) {
+      const uint32_t mine = ex[q] < near ? ex[q] : 0xFFFFFFFFu;
+      uint32_t cnt = 0;
+#pragma unroll 1
+      for (uint32_t q2 = 0; q2 < LV_PPL && q2 * WAVE < ent; ++q2) {
+        const uint32_t other = ex[q2] < near ? ex[q2] : 0xFFFFFFFEu;
+#pragma unroll 8
+        for (uint32_t l = 0; l < WAVE; ++l) cnt += (uint32_t)__builtin_amdgcn_readlane((int)other, (int)l) == mine;
+      }
+      if (mine != 0xFFFFFFFFu && (cnt > bestn || (cnt == bestn && mine < best))) {
+        best = mine;
+        bestn = cnt;
+      }
+    }
+    // wave arg-max: most chains, then the lowest exit
+    const uint32_t top = wave_max_u32(bestn);
+    const uint32_t pick = wave_min_u32(bestn == top ? best : 0xFFFFFFFFu);
+    if (lane == 0) lt.bexit[s] = top == 0 ? LV_BX_NONE : x.W0 + pick;
+    wave_lds_sync();  // the stage and jump table are refilled by the next segment
+  }
+}
+
+// Follows one-byte headers through the hop-length table: while addr < alim and k < 64, the
+// table byte at LDS address addr is the hop (0: not a one-byte header, stop); lane k of posv
+// records addr. Ten scalar instructions and one LDS byte read per header: the walk is bound by
+// the CU's scalar issue rate, shared by every wave walking on it.
+__device__ inline void lv_hops(uint32_t& addr, uint32_t alim, uint32_t& k, uint32_t& posv) {
+  uint32_t len, vt;
+  asm volatile(
+      "1:\n\t"
+      "s_cmp_ge_u32 %[addr], %[alim]\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_cmp_eq_u32 %[k], 64\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "v_mov_b32 %[vt], %[addr]\n\t"
+      "ds_read_u8 %[vt], %[vt]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %[len], %[vt]\n\t"
+      "s_cmp_eq_u32 %[len], 0\n\t"
+      "s_cbranch_scc1 2f\n\t"
+      "s_mov_b32 m0, %[k]\n\t"
+      "v_writelane_b32 %[posv], %[addr], m0\n\t"
+      "s_add_u32 %[addr], %[addr], %[len]\n\t"
+      "s_add_u32 %[k], %[k], 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : [addr] "+s"(addr), [k] "+s"(k), [posv] "+v"(posv), [len] "=&s"(len), [vt] "=&v"(vt)
+      : [alim] "s"(alim)
+      : "scc", "m0", "memory");
+}
+
+// ------------------------------------------------------------------------------ k_lv_segwalk
+// One wave per segment: walks the chain from X_j (segment 0: offset 0) to X_m, the next segment
+// start with a common exit. A scalar hop loop follows up to 64 headers in an LDS-staged region
+// (header bytes read from VGPRs: one v_readlane per one-byte header), then the 64 lanes parse
+// those headers together, check them and record their runs (output offset within the segment,
+// RLE value or payload offset) and header offsets.
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6, 8))) k_lv_segwalk(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   const PageWork* __restrict__ pages, int npages,
+                                                   ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  __shared__ uint32_t stg[WG / WAVE][LW_STG / 4];
+  __shared__ uint4 lent_s[WG / WAVE][LW_STG / 16];  // per staged byte: hop length if a one-byte header
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  // LDS address of this wave's hop-length table
+  const uint32_t lb = rfl((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint4*)lent_s[wid]);
+  const uint32_t total = lt.sbase[npages];
+  for (uint32_t sidx = blockIdx.x * (WG / WAVE) + wid; sidx < total; sidx += gridDim.x * (WG / WAVE)) {
+  uint32_t p, j;
   Stream s;
-  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
+  if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, sidx, p, j, s)) continue;
+  LvSeg& sg = lt.seg[sidx];
+  const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
+  const uint32_t start = j == 0 ? 0u : lt.bexit[sidx];
+  if (start >= LV_BX_AMBIG) {
+    if (lane == 0) sg.status = LS_NOSTART;
+    continue;
+  }
+  // the next segment start the walk must land on (a start it jumps over was not on the true
+  // chain: the walk goes on to the following one, and the segment is left off the page's chain)
+  uint32_t stop = 0xFFFFFFFFu, m = j;
+  auto next_stop = [&]() {
+    stop = 0xFFFFFFFFu;
+    for (++m; m < nseg; ++m) {
+      const uint32_t b = lt.bexit[s0 + m];
+      if (b < LV_BX_AMBIG) {
+        stop = b;
+        break;
+      }
+    }
+  };
+  next_stop();
   uint32_t* st = stg[wid];
-  const uint32_t n = s.n, slen = s.slen, w = (uint32_t)s.w, vb = (w + 7u) >> 3;
-  const uint32_t k0 = lt.wbase[p], nwin = lt.wbase[p + 1] - k0;
-  uint32_t* wf = lt.wfirst + k0 + p;                           // nwin + 1 entries
-  uint2* rec = lt.rec + (uint64_t)LW_REC * (k0 + 2ull * p);     // cap entries
-  const uint32_t cap = LW_REC * (nwin + 2u);
-  uint32_t cur = 0, nr = 0, nextw = 0, loaded = 0xFFFFFFFFu, sb = 0;
+  const uint32_t slen = s.slen, w = (uint32_t)s.w, vb = (w + 7u) >> 3;
+  uint2* rec = lt.srec + (uint64_t)sidx * LW_SCAP;
+  uint32_t* pos = lt.spos + (uint64_t)sidx * LW_SCAP;
+  uint32_t cur = start, nr = 0, loaded = 0xFFFFFFFFu, sb = 0, lastpos = 0xFFFFFFFFu, status = 0, tv = 0, tc = 0;
   uint64_t acc = 0;
-  int status = 0;  // 0 walked, 1 dense, 2 general decoder
   uint4 pf[LW_CH];
-  // the region's first 4 KiB also in registers: staged dword d is in rg[(d >> 8) * 4 + (d & 3)] of
-  // lane (d >> 2) & 63, which the hop loop reads with a uniform register index and v_readlane
-  // (a few cycles, where an LDS round trip costs a few hundred)
-  u32x16 rg;
 #ifdef PQG_DIAG
-  // diagnostics (PQG_DEBUG bit 6): per page s_memtime cycles in region installs, hop loops,
+  // diagnostics (PQG_DEBUG bit 7): per segment s_memtime cycles in region installs, hop loops,
   // batches, and the headers walked
-  const bool stamps = (cp.debug & 64) && cp.dbgbuf;
+  const bool stamps = (cp.debug & 128) && cp.dbgbuf;
   uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, t_reg = 0, t_hop = 0, t_bat = 0, nhops = 0;
 #define LW_STAMP(acc)                                      \
   if (stamps) {                                            \
@@ -346,30 +538,49 @@ __global__ void __launch_bounds__(WG) k_lv_walk(const uint8_t* __restrict__ blob
   auto fetch = [&](uint32_t r) {  // region r's bytes into registers
     const uint64_t A = (s.S + (uint64_t)r * LW_REG) & ~15ull;
 #pragma unroll
-    for (uint32_t j = 0; j < LW_CH; ++j) {
-      const uint64_t a = A + (uint64_t)(j * WAVE + lane) * 16u;
-      pf[j] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+    for (uint32_t q = 0; q < LW_CH; ++q) {
+      const uint64_t a = A + (uint64_t)(q * WAVE + lane) * 16u;
+      pf[q] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
     }
   };
   const uint32_t nreg = (slen + LW_REG - 1) / LW_REG;
-  fetch(0);
-  uint32_t fetched = 0;
-  while (acc < n) {
-    if (cur >= slen) {  // the stream ends before n outputs
-      status = 2;
+  uint32_t fetched = cur / LW_REG;
+  fetch(fetched);
+  while (true) {
+    if (cur == stop) {
+      status = LS_LANDED;
+      break;
+    }
+    if (cur > stop) {
+      next_stop();
+      continue;
+    }
+    if (cur >= slen) {
+      status = LS_END;
       break;
     }
     const uint32_t r = cur / LW_REG;
     if (r != loaded) {
       if (r != fetched) fetch(r);
 #pragma unroll
-      for (uint32_t j = 0; j < LW_CH; ++j) reinterpret_cast<uint4*>(st)[j * WAVE + lane] = pf[j];
+      for (uint32_t q = 0; q < LW_CH; ++q) {
+        reinterpret_cast<uint4*>(st)[q * WAVE + lane] = pf[q];
+        // hop lengths of one-byte headers, 0 for any other first byte (and hops over 255 bytes):
+        // the hop loop then costs one LDS byte read per header
+        uint32_t lw[4];
+        const uint32_t src[4] = {pf[q].x, pf[q].y, pf[q].z, pf[q].w};
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        rg[4 * j] = pf[j].x;
-        rg[4 * j + 1] = pf[j].y;
-        rg[4 * j + 2] = pf[j].z;
-        rg[4 * j + 3] = pf[j].w;
+        for (uint32_t t = 0; t < 4; ++t) {
+          uint32_t o = 0;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t b = (src[t] >> (8u * i)) & 0xFFu;
+            const uint32_t len = 1u + ((b & 1u) ? (b >> 1) * w : vb);
+            o |= ((b & 0x80u) || len > 255u ? 0u : len) << (8u * i);
+          }
+          lw[t] = o;
+        }
+        lent_s[wid][q * WAVE + lane] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
       }
       sb = (uint32_t)(s.S + (uint64_t)r * LW_REG - ((s.S + (uint64_t)r * LW_REG) & ~15ull));
       loaded = r;
@@ -380,91 +591,223 @@ __global__ void __launch_bounds__(WG) k_lv_walk(const uint8_t* __restrict__ blob
       }
       LW_STAMP(t_reg);
     }
-    const uint32_t rb = r * LW_REG;
-    const uint32_t lim = min(rb + LW_REG, slen);
-    // hop loop (wave-uniform): up to 64 headers; one-byte headers take the short path
+    const uint32_t rb = rfl(r * LW_REG);
+    const uint32_t lim = rfl(min(min(rb + LW_REG, slen), stop));
+    // hop loop (wave-uniform): up to 64 headers. One-byte headers take lv_hops (scalar loop
+    // over the hop-length table, positions as LDS addresses of their table entries); any other
+    // header the general parse.
     uint32_t k = 0, posv = 0;
     const uint32_t c0 = cur;
-    uint64_t a2 = acc;
-    while (k < 64u && cur < lim && a2 < n) {
-      const uint32_t rel = cur - rb + sb;  // < LW_REG + 16 = 4096
-      const uint32_t d = rel >> 2;
-      const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)rg[((d >> 8) << 2) | (d & 3u)], (int)((d >> 2) & 63u));
-      const uint32_t b = (dw >> ((rel & 3u) * 8u)) & 0xFFu;
-      uint32_t cnt, nxt;
-      bool dead = false;
-      if (!(b & 0x80u)) {
-        const uint32_t g = b >> 1;
-        cnt = (b & 1u) ? g * 8u : g;
-        nxt = cur + 1u + ((b & 1u) ? g * w : vb);
-      } else {
-        uint32_t v;
-        bool bp;
-        dead = !lv_parse4(st, rel, cur, slen, w, vb, nxt, cnt, v, bp);
-        nxt = rfl(nxt);
-        cnt = rfl(cnt);
-        dead = rfl(dead ? 1u : 0u) != 0;
+    const uint32_t ab = rfl(lb - rb + sb);  // LDS address of stream offset 0's entry (mod 2^32)
+    uint32_t addr = ab + cur;
+    const uint32_t alim = ab + lim;
+    bool dead = false;
+    while (true) {
+      lv_hops(addr, alim, k, posv);
+      if (addr >= alim || k == 64u) break;
+      const uint32_t q = addr - ab;  // stream offset of a header whose hop is not in the table
+      uint32_t nxt, v, cnt;
+      bool bp;
+      const bool ok = lv_parse4(st, q - rb + sb, q, slen, w, vb, nxt, cnt, v, bp);
+      if (!rfl(ok ? 1u : 0u)) {
+        dead = true;
+        break;
       }
-      posv = lane == k ? cur : posv;
+      posv = lane == k ? addr : posv;
       ++k;
-      if (dead) break;  // the batch's parse refuses it
-      a2 += cnt;
-      cur = nxt;
+      addr += rfl(nxt) - q;
     }
+    cur = addr - ab;
+    posv -= ab;
     LW_STAMP(t_hop);
 #ifdef PQG_DIAG
     nhops += k;
 #endif
-    // batch: lane l parses header l, checks it, places it
-    const bool act = lane < k;
-    uint32_t nx, c = 0, v = 0;
-    bool bp = false, ok = true;
-    if (act) {
-      ok = lv_parse4(st, posv - rb + sb, posv, slen, w, vb, nx, c, v, bp);
-      if (!ok) c = 0;
+    if (k) {
+      // batch: lane l parses header l, checks it and records its run
+      const bool act = lane < k;
+      uint32_t nx, c = 0, v = 0;
+      bool bp = false, okp = true;
+      if (act) okp = lv_parse4(st, posv - rb + sb, posv, slen, w, vb, nx, c, v, bp);
+      const uint64_t ic = wave_incl_scan_cnt(act ? c : 0u);
+      const uint64_t accb = acc + ic - (act ? c : 0u);
+      if ((k == 64u && cur - c0 < LW_SPAN) || nr + k > LW_SCAP) {
+        status = LS_DENSE;
+        break;
+      }
+      // the first run whose payload runs past the stream end, or whose RLE value does not fit
+      const bool trunc = act && c && bp && (uint64_t)v * 8ull + (uint64_t)c * w > (uint64_t)slen * 8ull;
+      const bool badv = act && !bp && (!okp || (c && (v >> w) != 0));  // (or its value past the end)
+      const uint64_t bb = __ballot(trunc || badv);
+      const uint32_t kk = bb ? (uint32_t)__builtin_ctzll(bb) + 1u : k;  // runs kept
+      if (lane < kk) {
+        rec[nr + lane] = make_uint2(accb < 0xFFFFFFFFull ? (uint32_t)accb : 0xFFFFFFFFu, bp ? v : (R_RLE | v));
+        pos[nr + lane] = posv;
+      }
+      lastpos = rfl((uint32_t)__shfl((int)posv, (int)kk - 1, 64));
+      nr += kk;
+      const uint64_t bt = __shfl(ic, (int)kk - 1, 64);
+      acc += ((uint64_t)rfl((uint32_t)(bt >> 32)) << 32) | rfl((uint32_t)bt);  // through run kk - 1
+      if (bb) {
+        const uint32_t L = kk - 1u;
+        status = rfl((uint32_t)__shfl((int)(trunc ? LS_TRUNC : LS_BADVAL), (int)L, 64));
+        tv = rfl((uint32_t)__shfl((int)v, (int)L, 64));
+        tc = rfl((uint32_t)__shfl((int)c, (int)L, 64));
+        break;
+      }
     }
-    const uint64_t ic = wave_incl_scan_cnt(c);
-    const uint64_t accb = acc + ic - c;
-    if (act && ok) ok = lv_run_ok(bp, v, c, accb, n, slen, w);
-    if (__ballot(act && !ok)) {
-      status = 2;
-      break;
-    }
-    if ((k == 64u && cur - c0 < LW_SPAN) || nr + k + 1u > cap) {
-      status = 1;
-      break;
-    }
-    if (act) rec[nr + lane] = make_uint2(accb < 0xFFFFFFFFull ? (uint32_t)accb : 0xFFFFFFFFu, bp ? v : (R_RLE | v));
-    // windows whose start lies in (previous header, this header] begin with this run
-    const uint32_t whi = act ? posv / LV_WIN + 1u : 0u;
-    uint32_t wlo = (uint32_t)__shfl_up((int)whi, 1, 64);
-    if (lane == 0) wlo = nextw;
-    if (act)
-      for (uint32_t kw = wlo; kw < whi; ++kw) wf[kw] = nr + lane;
-    // wave-uniform state stays scalar: the compiler cannot know a shuffle result is uniform
-    nextw = rfl((uint32_t)__shfl((int)whi, (int)k - 1, 64));
-    nr += k;
-    const uint64_t bt = __shfl(ic, (int)k - 1, 64);
-    acc += ((uint64_t)rfl((uint32_t)(bt >> 32)) << 32) | rfl((uint32_t)bt);
     LW_STAMP(t_bat);
+    if (dead) {
+      status = LS_DEAD;
+      break;
+    }
   }
 #ifdef PQG_DIAG
   if (stamps && lane == 0) {
-    uint64_t* d = cp.dbgbuf + 8ull * p;
+    uint64_t* d = cp.dbgbuf + 4ull * sidx;
     d[0] = t_reg;
     d[1] = t_hop;
     d[2] = t_bat;
     d[3] = nhops;
-    d[4] = (uint64_t)status;
   }
 #endif
 #undef LW_STAMP
-  if (status == 0) {
-    if (lane == 0) rec[nr] = make_uint2(acc < 0xFFFFFFFFull ? (uint32_t)acc : 0xFFFFFFFFu, 0u);  // sentinel
-    for (uint32_t kw = nextw + lane; kw <= nwin; kw += WAVE) wf[kw] = nr;
-    if (lane == 0) rt.pflag[p] = PF_WALK;
-  } else if (status == 2 && lane == 0) {
-    lv_bail(rt, p, PF_PAGE);
+  if (lane == 0) {
+    sg.out = acc;
+    sg.runs = nr;
+    sg.status = status;
+    sg.next = m;
+    sg.lastpos = lastpos;
+    sg.tv = tv;
+    sg.tc = tc;
+  }
+  wave_lds_sync();  // the stage is refilled by the next segment
+  }
+}
+
+// ------------------------------------------------------------------------------ k_lv_segscan
+// One lane per page: follows the segment walks from offset 0, places them (first run, first
+// output), finds the run holding output n - 1, and decides the page: walked (PF_WALK), window
+// path (PF_PAGE stays) or general decoder (PF_BAIL).
+__global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
+                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  const uint32_t p = blockIdx.x * WG + threadIdx.x;
+  if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
+  Stream s;
+  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
+  const uint32_t n = s.n, w = (uint32_t)s.w;
+  const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
+  if (n == 0 || nseg == 0) {  // nothing to read: no windows, no runs
+    lt.wfirst[lt.wbase[p] + p] = 0;
+    rt.pflag[p] = PF_WALK;
+    return;
+  }
+  const uint32_t cap = LW_REC * (lt.wbase[p + 1] - lt.wbase[p] + 2u);
+  uint64_t acc = 0;
+  uint32_t runs = 0, prevpos = 0xFFFFFFFFu, j = 0, verdict = 0;  // 0 walked, 1 window path, 2 general
+  while (true) {
+    LvSeg& sg = lt.seg[s0 + j];
+    if (sg.status == LS_NOSTART) {
+      verdict = 1;
+      break;
+    }
+    sg.base_out = acc;
+    sg.base_run = runs;
+    sg.prevpos = prevpos;
+    if (acc + sg.out >= n) {
+      // the run holding output n - 1: the last one starting before it
+      const uint2* rec = lt.srec + (uint64_t)(s0 + j) * LW_SCAP;
+      uint32_t lo = 0, hi = sg.runs;  // runs [0, sg.runs) start at acc + rec[i].x (ascending)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (acc + rec[mid].x < n) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t keep = lo + 1;
+      if (keep == sg.runs && (sg.status == LS_TRUNC || sg.status == LS_BADVAL)) {
+        const uint64_t before = acc + rec[lo].x;
+        const uint64_t need = sg.status == LS_TRUNC ? (uint64_t)sg.tv * 8ull + min((uint64_t)sg.tc, n - before) * w : 0;
+        if (sg.status == LS_BADVAL || need > (uint64_t)s.slen * 8ull) {
+          verdict = 2;
+          break;
+        }
+      }
+      if (runs + keep + 1u > cap) {
+        verdict = 1;
+        break;
+      }
+      sg.keep = keep;
+      sg.flags = 3;
+      break;
+    }
+    acc += sg.out;
+    runs += sg.runs;
+    sg.keep = sg.runs;
+    sg.flags = 1;
+    if (sg.runs) prevpos = sg.lastpos;
+    if (sg.status == LS_LANDED) {
+      j = sg.next;
+      continue;
+    }
+    verdict = sg.status == LS_DENSE ? 1 : 2;  // else: the stream ends or breaks before n
+    break;
+  }
+#ifdef PQG_DIAG
+  if ((cp.debug & 64) && cp.dbgbuf) {  // diagnostics: the page's verdict and the segment deciding it
+    uint64_t* d = cp.dbgbuf + 8ull * p;
+    const LvSeg& sg = lt.seg[s0 + j];
+    d[0] = verdict;
+    d[1] = j;
+    d[2] = sg.status;
+    d[3] = sg.runs;
+    d[4] = sg.out;
+    d[5] = nseg;
+    d[6] = sg.lastpos;
+    d[7] = j + 1 < nseg ? lt.bexit[s0 + j + 1] : 0;
+  }
+#endif
+  if (verdict == 0) {
+    rt.pflag[p] = PF_WALK;
+  } else {
+    for (uint32_t q = 0; q < nseg; ++q) lt.seg[s0 + q].flags = 0;
+    if (verdict == 2) lv_bail(rt, p, PF_PAGE);
+  }
+}
+
+// ------------------------------------------------------------------------------ k_lv_compact
+// One wave per segment on a walked page's chain: its runs to the page's run list (first outputs
+// made page-relative), the first run of every window whose start lies before one of its headers,
+// and after the page's last run a sentinel and the windows past it.
+__global__ void __launch_bounds__(WG) k_lv_compact(int npages, RunTables rt, LevelTables lt) {
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  const uint32_t total = lt.sbase[npages];
+  for (uint32_t sidx = blockIdx.x * (WG / WAVE) + wid; sidx < total; sidx += gridDim.x * (WG / WAVE)) {
+  const uint32_t p = lv_page_of(lt.sbase, (uint32_t)npages, sidx);
+  if (rt.pflag[p] != PF_WALK) continue;
+  const LvSeg& sg = lt.seg[sidx];
+  if (!(sg.flags & 1u)) continue;
+  const uint32_t k0 = lt.wbase[p], nwin = lt.wbase[p + 1] - k0;
+  uint32_t* wf = lt.wfirst + k0 + p;
+  uint2* rec = lt.rec + (uint64_t)LW_REC * (k0 + 2ull * p);
+  const uint2* sr = lt.srec + (uint64_t)sidx * LW_SCAP;
+  const uint32_t* sp = lt.spos + (uint64_t)sidx * LW_SCAP;
+  const uint32_t K = sg.keep, br = sg.base_run;
+  const uint64_t bo = sg.base_out;
+  for (uint32_t i = lane; i < K; i += WAVE) {
+    const uint2 r = sr[i];
+    const uint64_t o = bo + r.x;
+    rec[br + i] = make_uint2(o < 0xFFFFFFFFull ? (uint32_t)o : 0xFFFFFFFFu, r.y);
+    const uint32_t q = sp[i];
+    const uint32_t prev = i ? sp[i - 1] : sg.prevpos;
+    const uint32_t wlo = prev == 0xFFFFFFFFu ? 0u : prev / LV_WIN + 1u;
+    for (uint32_t kw = wlo; kw <= q / LV_WIN; ++kw) wf[kw] = br + i;
+  }
+  if (sg.flags & 2u) {
+    const uint64_t o = bo + (K < sg.runs ? (uint64_t)sr[K].x : sg.out);
+    if (lane == 0) rec[br + K] = make_uint2(o < 0xFFFFFFFFull ? (uint32_t)o : 0xFFFFFFFFu, 0u);  // sentinel
+    const uint32_t wlo = K ? sp[K - 1] / LV_WIN + 1u : (sg.prevpos == 0xFFFFFFFFu ? 0u : sg.prevpos / LV_WIN + 1u);
+    for (uint32_t kw = wlo + lane; kw <= nwin; kw += WAVE) wf[kw] = br + K;
+  }
   }
 }
 
@@ -485,39 +828,10 @@ __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob,
     x.k = g2 - lt.wbase2[x.p];
     const uint32_t g = lt.wbase[x.p] + x.k;
     x.W0 = x.k * LV_WIN;
-    const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
+    const uint32_t w = (uint32_t)x.s.w;
     lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
     uint32_t jv[LV_PPL], cv[LV_PPL];
-    lv_first_hops(W.stage, x.sb, x.W0, slen, w, vb, jv, cv);
-#pragma unroll
-    for (uint32_t j = 0; j < LV_PPL; ++j) W.JC[j * WAVE + lane] = make_uint2(jv[j], cv[j]);
-    wave_lds_sync();
-    // pointer jumping: after round r, jv[j] is 2^(r+1) hops on (or terminal) and cv[j] the
-    // outputs along the way (saturating); the high half of jv counts the headers passed (also
-    // saturating). Stops once every chain has left the window.
-#pragma unroll 1
-    for (uint32_t r = 0; r < LV_ROUNDS; ++r) {
-      bool live = false;
-#pragma unroll
-      for (uint32_t j = 0; j < LV_PPL; ++j) live |= (jv[j] & 0xFFFFu) < LV_WIN;
-      if (!__any(live)) break;
-      uint2 nx[LV_PPL];
-#pragma unroll
-      for (uint32_t j = 0; j < LV_PPL; ++j) {
-        const uint32_t t = jv[j] & 0xFFFFu;
-        nx[j] = t < LV_WIN ? W.JC[t] : make_uint2(t, 0u);
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (uint32_t j = 0; j < LV_PPL; ++j) {
-        const uint32_t s2 = cv[j] + nx[j].y;
-        cv[j] = s2 < cv[j] ? 0xFFFFFFFFu : s2;
-        const uint32_t hs = (jv[j] >> 16) + (nx[j].x >> 16);
-        jv[j] = (nx[j].x & 0xFFFFu) | ((hs < 0xFFFFu ? hs : 0xFFFFu) << 16);
-        W.JC[j * WAVE + lane] = make_uint2(jv[j], cv[j]);
-      }
-      wave_lds_sync();
-    }
+    lv_jump(W, x, jv, cv);
     // table of the entry offsets: (exit offset from W0 or terminal code | headers << 16, outputs)
     const uint32_t ent = lv_ent(w);
     uint2* tab = lt.tab + (uint64_t)g * ent;
@@ -965,10 +1279,12 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
                          ColumnParams cp, int sel, RunTables rt, LevelTables lt, void* out, hipStream_t s) {
   if (npages <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_walk, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
-                     lt);
-  hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   const uint32_t wgrid = 256u * 8u;
+  hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segscan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
+  hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_stitch, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   if (sel == SS_BOOL) {

@@ -84,7 +84,7 @@ struct Slot {
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
   // level path (def, rep, RLE booleans): buffers of LevelTables (pqg_internal.hpp), grown on demand
-  static constexpr int LV_BUFS = 6;  // wbase, wbase2, wfirst, rec, tab, win
+  static constexpr int LV_BUFS = 11;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos
   void* lvbuf[3][LV_BUFS] = {};
   size_t lvcap[3][LV_BUFS] = {};
   LevelTables lt(int k) const {
@@ -95,6 +95,11 @@ struct Slot {
     t.rec = (uint2*)lvbuf[k][3];
     t.tab = (uint2*)lvbuf[k][4];
     t.win = (uint2*)lvbuf[k][5];
+    t.sbase = (uint32_t*)lvbuf[k][6];
+    t.bexit = (uint32_t*)lvbuf[k][7];
+    t.seg = (LvSeg*)lvbuf[k][8];
+    t.srec = (uint2*)lvbuf[k][9];
+    t.spos = (uint32_t*)lvbuf[k][10];
     return t;
   }
 };
@@ -446,9 +451,10 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
 #endif
   cp.debug = dbg_env;
   cp.dbgbuf = nullptr;
-  if (dbg_env & (16 | 32 | 64)) {
+  if (dbg_env & (16 | 32 | 64 | 128)) {
     size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
     if (need < (size_t)npages * 64) need = (size_t)npages * 64;
+    if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + npages + 1) * 32;  // per level-stream segment
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
@@ -562,9 +568,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (!need_lv[k]) continue;
     int st;
     const size_t ent = lv_ent(k == 2 ? 1u : (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width));
+    const size_t nseg = nwin / LW_SEGW + npages + 1;  // segments, upper bound
     const size_t need[Slot::LV_BUFS] = {(size_t)npages + 1, (size_t)npages + 1, nwin + npages + 1,
-                                        64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1};
-    const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2)};
+                                        64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1,
+                                        (size_t)npages + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP};
+    const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2),
+                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4};
     for (int b = 0; b < Slot::LV_BUFS; ++b)
       if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
   }

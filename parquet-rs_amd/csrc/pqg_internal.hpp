@@ -149,9 +149,32 @@ struct DeltaTables {
 };
 
 // Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
+// One segment (LW_SEGW windows of 1 KiB) of a sparse level stream, walked by its own wave
+// (pqg_levels.hip); it records at most LW_SCAP runs (room for a walk through two segments).
+constexpr uint32_t LW_SEGW = 16;
+constexpr uint32_t LW_SCAP = 64 * (2 * LW_SEGW + 2);
+struct LvSeg {
+  uint64_t out;       // outputs of the runs the segment's walk recorded
+  uint64_t base_out;  // (page scan) outputs before the segment
+  uint32_t runs;      // runs recorded
+  uint32_t status;    // how the walk ended (LS_* in pqg_levels.hip)
+  uint32_t next;      // LS_LANDED: the segment whose start the walk reached
+  uint32_t lastpos;   // stream offset of the last recorded header
+  uint32_t base_run;  // (page scan) runs before the segment
+  uint32_t keep;      // (page scan) runs the page keeps (the last segment stops at the n-th output)
+  uint32_t prevpos;   // (page scan) last header before the segment's first one (~0u: none)
+  uint32_t flags;     // (page scan) 1: on the page's chain, 2: its last segment
+  uint32_t tv, tc;    // a truncated last run: payload offset and output count
+};
+
 // Windows are 1 KiB of a page's stream; run records of walked pages are 64 per window + 128.
 struct LevelTables {
   uint32_t* wbase;   // [pages + 1] first window of each page's stream (k_lv_plan)
+  uint32_t* sbase;   // [pages + 1] first segment of each page's stream (k_lv_plan)
+  uint32_t* bexit;   // [segments] where every chain entering a segment's first window leaves it
+  LvSeg* seg;        // [segments]
+  uint2* srec;       // [segments * LW_SCAP] runs recorded by each segment walk: (outputs before, info)
+  uint32_t* spos;    // [segments * LW_SCAP] their header offsets
   uint32_t* wbase2;  // [pages + 1] the same over the pages the walker left to the window path
   uint32_t* wfirst;  // [windows + pages] walked pages: first run of each window, then the run count
   uint2* rec;        // [64 * (windows + 2 * pages)] walked pages' runs: (first output, info)
