@@ -435,7 +435,8 @@ __global__ void k_finalize(PageWork* pages, ChunkResult* res) {
 extern "C" {
 
 hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                         ColumnParams cp, int sel, RunTables rt, LevelTables lt, void* out, hipStream_t s);
+                         ColumnParams cp, int sel, int dict_page, int es, RunTables rt, LevelTables lt, void* out,
+                         ChunkResult* res, hipStream_t s);
 
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                               int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
@@ -476,7 +477,7 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
                              ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
   const int sel = which ? SS_REP : SS_DEF;
   if (kev) (void)hipEventRecord(kev[0], s);
-  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, rt, lt, out, s);
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, -1, 0, rt, lt, out, res, s);
   if (kev) (void)hipEventRecord(kev[1], s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel, -1, rt, res, 1);
@@ -484,7 +485,7 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
     hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                        ntiles, rt, cp, sel, -1);
     // persistent grid: most calls leave no stream to this pass, and its workgroups exit at once
-    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles < 4096u ? ntiles : 4096u), dim3(WG), 0, s, blob, blob_len,
+    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles < 1024u ? ntiles : 1024u), dim3(WG), 0, s, blob, blob_len,
                        ntiles, rt, cp, sel, out);
     if (sel == SS_DEF)
       hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, 0);
@@ -498,18 +499,30 @@ hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es
   return hipGetLastError();
 }
 
+// RLE_DICTIONARY values. 4- and 8-byte values take the hybrid-stream path (pqg_levels.hip: segment
+// walks, then a gather per output); its pages the general decoder takes back (dense or malformed
+// streams, indices wider than 16 bits), and other value sizes, take the index pass and tiled
+// expand.
 hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                            uint32_t ntiles, ColumnParams cp, int dict_page, int es,
-                           const uint32_t* tile_page, RunTables rt, uint8_t* out, ChunkResult* res,
-                           hipStream_t s, hipEvent_t* kev) {
+                           const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
+                           ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
+  const bool lvpath = es == 4 || es == 8;
+  if (kev) (void)hipEventRecord(kev[0], s);
+  if (lvpath) {
+    const hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, es, rt, lt, out, res, s);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
-                     dict_page, rt, res);
-  if (!ntiles) return hipGetLastError();
+                     dict_page, rt, res, lvpath ? 1 : 0);
+  if (!ntiles) {
+    if (kev) (void)hipEventRecord(kev[1], s);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
                      ntiles, rt, cp, (int)SS_DICT, dict_page);
   const dim3 g = tx_grid(ntiles);
-  if (kev) (void)hipEventRecord(kev[0], s);
   switch (es) {
     case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
     case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
@@ -547,7 +560,7 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
                                int npages, uint32_t ntiles, ColumnParams cp,
                                const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
                                ChunkResult* res, hipStream_t s) {
-  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_BOOL, rt, lt, out, s);
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_BOOL, -1, 0, rt, lt, out, res, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
                      -1, rt, res, 1);

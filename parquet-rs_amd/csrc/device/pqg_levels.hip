@@ -203,10 +203,13 @@ __device__ inline uint32_t lv_page_of(const uint32_t* __restrict__ wbase, uint32
   return lo;
 }
 
+// Streams this path takes. Dictionary indices only up to 4 bits: wider index streams are runs
+// of ~64 * w bytes, too far apart for the segment starts' chains to meet within two windows, and
+// the general decoder's streaming index pass serves them better.
 __device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int sel, const ColumnParams& cp,
                                  Stream& s) {
   return get_stream(blob, pw, sel, cp, s) && pw.status == 0 && !s.err && s.kind == LK_RLE &&
-         lv_width_ok((uint32_t)s.w);
+         lv_width_ok((uint32_t)s.w) && (sel != SS_DICT || s.w <= 4);
 }
 
 // Hand page p to the general decoder (once).
@@ -273,13 +276,16 @@ __device__ inline void lv_scan_windows(int npages, uint32_t* wbase, F nwin_of) {
 // One workgroup: per page the stream's windows (exclusive scan into wbase), and the page flag:
 // PF_PAGE (level path) or PF_BAIL (general decoder). Def streams start their count at 0.
 __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
-                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+                                                ColumnParams cp, int sel, int dict_page, RunTables rt,
+                                                LevelTables lt) {
+  // dictionary indices without a usable dictionary: the general decoder reports it
+  const bool nodict = sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0);
   lv_scan_windows(npages, lt.wbase, [&](int p) -> uint32_t {
     const PageWork& pw = pages[p];
     Stream s;
     uint32_t flag = 0, nw = 0;
     if (get_stream(blob, pw, sel, cp, s)) {
-      if (lv_stream(blob, pw, sel, cp, s) && (s.n == 0 || s.slen > 0)) {
+      if (!nodict && lv_stream(blob, pw, sel, cp, s) && (s.n == 0 || s.slen > 0)) {
         flag = PF_PAGE;
         nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
         if (sel == SS_DEF) pages[p].nonnull = 0;
@@ -293,8 +299,9 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
   });
   lv_scan_windows(npages, lt.sbase, [&](int p) -> uint32_t {
     Stream s;
-    if (!lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
-    return ((s.slen + LV_WIN - 1) / LV_WIN + LW_SEGW - 1) / LW_SEGW;
+    if (nodict || !lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
+    const uint32_t sw = lw_segw((uint32_t)s.w);
+    return ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
   });
 }
 
@@ -306,7 +313,7 @@ __global__ void __launch_bounds__(WG) k_lv_plan2(int npages, RunTables rt, Level
 }
 
 // ------------------------------------------------------------------------------ sparse streams
-// A page stream is cut into segments of LW_SEGW windows, each walked by its own wave: the
+// A page stream is cut into segments of lw_segw(w) windows, each walked by its own wave: the
 // chain of a sparse stream enters segment j somewhere in its first window, and chains entering
 // a window at different offsets meet within a few headers. k_lv_bound finds, for segment j's
 // first window, where every chain entering it leaves it; when they all leave at one offset
@@ -372,106 +379,110 @@ __device__ inline bool lv_seg_of(const uint8_t* blob, const PageWork* pages, uin
 }
 
 // ------------------------------------------------------------------------------ k_lv_bound
-// One wave per segment j >= 1: the common exit of its first window's chains (bexit).
+// One wave per segment j >= 1: a start for its walk (bexit). The chains entering the segment's
+// first window at offsets [0, ent) are walked by their own lanes over two windows (chains keep
+// meeting; capped at LB_HOPS headers: a dense stream is the window path's anyway); among the
+// exits one hop of the writer's form can reach past them (a <= 2-byte header and <= 64 groups:
+// rle.rs:48-50), the one most chains share is taken — chains entering on payload bytes that do
+// not meet the true chain mostly jump far away. The walk of the segment before verifies the
+// choice by landing on it exactly.
+constexpr uint32_t LB_SPAN = 2 * LV_WIN;         // bytes walked from the segment start
+constexpr uint32_t LB_STG = LB_SPAN + 64;        // staged bytes
+constexpr uint32_t LB_HOPS = 128;                // headers per chain at most
+constexpr uint32_t LB_BINS = 8 + 64 * 16;        // exits one writer-form hop can reach past the span
+
 __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                  const PageWork* __restrict__ pages, int npages, ColumnParams cp,
                                                  int sel, RunTables rt, LevelTables lt) {
-  __shared__ LvSmem sm;
+  __shared__ uint32_t stg[WG / WAVE][LB_STG / 4];
+  __shared__ uint32_t hist_s[WG / WAVE][LB_BINS];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  LvWave& W = sm.wv[wid];
+  uint32_t* st = stg[wid];
+  uint32_t* hist = hist_s[wid];
   const uint32_t total = lt.sbase[npages];
   for (uint32_t s = blockIdx.x * (WG / WAVE) + wid; s < total; s += gridDim.x * (WG / WAVE)) {
     LvWin x;
     uint32_t j;
     if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, s, x.p, j, x.s) || j == 0) continue;
-    x.k = j * LW_SEGW;
+    x.k = j * lw_segw((uint32_t)x.s.w);
     x.W0 = x.k * LV_WIN;
-    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
-    uint32_t jv[LV_PPL], cv[LV_PPL];
-    lv_jump(W, x, jv, cv);
-    // Where the chains entering at offsets [0, ent) leave the window, among the exits one hop of
-    // the writer's form can reach (a <= 2-byte header and <= 64 groups: rle.rs:48-50); then,
-    // through the next window's table, where they leave that one (chains keep meeting: two
-    // windows leave fewer apart). The exit most of them share is taken — chains entering on
-    // payload bytes that do not meet the true chain mostly jump far away. The walk of the
-    // segment before verifies the choice by landing on it exactly.
-    const uint32_t w = (uint32_t)x.s.w;
+    lv_stage(blob, blob_len, x, st, LB_STG / 16);
+    const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
     const uint32_t ent = lv_ent(w);
-    const uint32_t hop = 8u + 64u * w;
+    const uint32_t span = min(LB_SPAN, slen - x.W0);  // walked bytes (the stream may end first)
+    const uint32_t near = span + 8u + 64u * w;
     uint32_t ex[LV_PPL];
 #pragma unroll
     for (uint32_t q = 0; q < LV_PPL; ++q) {
-      const uint32_t t = jv[q] & 0xFFFFu;
-      ex[q] = (q * WAVE + lane < ent && t < LV_WIN + hop) ? t : 0xFFFFFFFFu;
+      ex[q] = 0xFFFFFFFFu;
+      if (q * WAVE >= ent) continue;
+      uint32_t o = q * WAVE + lane;
+      bool ok = o < ent;
+      for (uint32_t h = 0; h < LB_HOPS && __any(ok && o < span); ++h) {
+        if (ok && o < span) {
+          uint32_t nx, c, v;
+          bool bp;
+          ok = lv_parse4(st, o + x.sb, x.W0 + o, slen, w, vb, nx, c, v, bp);
+          const uint32_t o2 = nx - x.W0;
+          // a hop out of the first window must be one of the writer's form as well
+          if (o < LV_WIN && o2 >= LV_WIN + 8u + 64u * w) ok = false;
+          o = o2;
+        }
+      }
+      if (ok && o >= span && o < near) ex[q] = o;
     }
-    uint32_t near = LV_WIN + hop;
-    if (x.W0 + LV_WIN < x.s.slen) {
-      wave_lds_sync();
-      LvWin x2 = x;
-      x2.W0 = x.W0 + LV_WIN;
-      lv_stage(blob, blob_len, x2, W.stage, LV_STG_CH);
-      lv_jump(W, x2, jv, cv);
+    // histogram of the exits (LDS), then its arg-max: most chains, then the lowest exit
+    const uint32_t nb = near - span;
+    for (uint32_t i = lane; i < nb; i += WAVE) hist[i] = 0;
+    wave_lds_sync();
 #pragma unroll
-      for (uint32_t q = 0; q < LV_PPL; ++q) {
-        if (ex[q] == 0xFFFFFFFFu) continue;
-        const uint32_t o = ex[q] - LV_WIN;
-        if (o >= LV_WIN) continue;  // enters past the second window: keep its first exit
-        const uint32_t t = W.JC[o].x & 0xFFFFu;
-        ex[q] = t < LV_WIN + hop ? LV_WIN + t : 0xFFFFFFFFu;
-      }
-      near = 2u * LV_WIN + hop;
-    }
+    for (uint32_t q = 0; q < LV_PPL; ++q)
+      if (ex[q] != 0xFFFFFFFFu) atomicAdd(&hist[ex[q] - span], 1u);
+    wave_lds_sync();
     uint32_t best = 0xFFFFFFFFu, bestn = 0;
-#pragma unroll 1
-    for (uint32_t q = 0; q < LV_PPL && q * WAVE < ent; ++q) {
-      const uint32_t mine = ex[q] < near ? ex[q] : 0xFFFFFFFFu;
-      uint32_t cnt = 0;
-#pragma unroll 1
-      for (uint32_t q2 = 0; q2 < LV_PPL && q2 * WAVE < ent; ++q2) {
-        const uint32_t other = ex[q2] < near ? ex[q2] : 0xFFFFFFFEu;
-#pragma unroll 8
-        for (uint32_t l = 0; l < WAVE; ++l) cnt += (uint32_t)__builtin_amdgcn_readlane((int)other, (int)l) == mine;
-      }
-      if (mine != 0xFFFFFFFFu && (cnt > bestn || (cnt == bestn && mine < best))) {
-        best = mine;
-        bestn = cnt;
+    for (uint32_t i = lane; i < nb; i += WAVE) {
+      const uint32_t c = hist[i];
+      if (c > bestn) {
+        bestn = c;
+        best = span + i;
       }
     }
-    // wave arg-max: most chains, then the lowest exit
     const uint32_t top = wave_max_u32(bestn);
     const uint32_t pick = wave_min_u32(bestn == top ? best : 0xFFFFFFFFu);
     if (lane == 0) lt.bexit[s] = top == 0 ? LV_BX_NONE : x.W0 + pick;
-    wave_lds_sync();  // the stage and jump table are refilled by the next segment
+    wave_lds_sync();  // the stage is refilled by the next segment
   }
 }
 
 // Follows one-byte headers through the hop-length table: while addr < alim and k < 64, the
-// table byte at LDS address addr is the hop (0: not a one-byte header, stop); lane k of posv
-// records addr. Ten scalar instructions and one LDS byte read per header: the walk is bound by
+// u16 at LDS address addr is the step to the next header's entry (0: not a one-byte header,
+// stop, with lane k of posv already holding addr — harmless, the caller overwrites or ignores
+// lanes >= k); lane k of posv records addr. Ten scalar instructions and one LDS byte read per header: the walk is bound by
 // the CU's scalar issue rate, shared by every wave walking on it.
 __device__ inline void lv_hops(uint32_t& addr, uint32_t alim, uint32_t& k, uint32_t& posv) {
-  uint32_t len, vt;
+  uint32_t len, vt, va;
+  const uint32_t vlane = threadIdx.x & 63u;
   asm volatile(
       "1:\n\t"
       "s_cmp_ge_u32 %[addr], %[alim]\n\t"
       "s_cbranch_scc1 2f\n\t"
       "s_cmp_eq_u32 %[k], 64\n\t"
       "s_cbranch_scc1 2f\n\t"
-      "v_mov_b32 %[vt], %[addr]\n\t"
-      "ds_read_u8 %[vt], %[vt]\n\t"
+      "v_mov_b32 %[va], %[addr]\n\t"
+      "ds_read_u16 %[vt], %[va]\n\t"
+      "v_cmp_eq_u32 vcc, %[k], %[vlane]\n\t"
+      "v_cndmask_b32 %[posv], %[posv], %[va], vcc\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_readfirstlane_b32 %[len], %[vt]\n\t"
       "s_cmp_eq_u32 %[len], 0\n\t"
       "s_cbranch_scc1 2f\n\t"
-      "s_mov_b32 m0, %[k]\n\t"
-      "v_writelane_b32 %[posv], %[addr], m0\n\t"
       "s_add_u32 %[addr], %[addr], %[len]\n\t"
       "s_add_u32 %[k], %[k], 1\n\t"
       "s_branch 1b\n"
       "2:"
-      : [addr] "+s"(addr), [k] "+s"(k), [posv] "+v"(posv), [len] "=&s"(len), [vt] "=&v"(vt)
-      : [alim] "s"(alim)
-      : "scc", "m0", "memory");
+      : [addr] "+s"(addr), [k] "+s"(k), [posv] "+v"(posv), [len] "=&s"(len), [vt] "=&v"(vt), [va] "=&v"(va)
+      : [alim] "s"(alim), [vlane] "v"(vlane)
+      : "scc", "vcc", "memory");
 }
 
 // ------------------------------------------------------------------------------ k_lv_segwalk
@@ -480,11 +491,11 @@ __device__ inline void lv_hops(uint32_t& addr, uint32_t alim, uint32_t& k, uint3
 // (header bytes read from VGPRs: one v_readlane per one-byte header), then the 64 lanes parse
 // those headers together, check them and record their runs (output offset within the segment,
 // RLE value or payload offset) and header offsets.
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6, 8))) k_lv_segwalk(const uint8_t* __restrict__ blob, uint64_t blob_len,
+__global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                    const PageWork* __restrict__ pages, int npages,
                                                    ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
   __shared__ uint32_t stg[WG / WAVE][LW_STG / 4];
-  __shared__ uint4 lent_s[WG / WAVE][LW_STG / 16];  // per staged byte: hop length if a one-byte header
+  __shared__ uint4 lent_s[WG / WAVE][LW_STG / 8];  // per staged byte (u16): 2 * hop length of a one-byte header
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   // LDS address of this wave's hop-length table
   const uint32_t lb = rfl((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint4*)lent_s[wid]);
@@ -565,22 +576,19 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6, 8)))
 #pragma unroll
       for (uint32_t q = 0; q < LW_CH; ++q) {
         reinterpret_cast<uint4*>(st)[q * WAVE + lane] = pf[q];
-        // hop lengths of one-byte headers, 0 for any other first byte (and hops over 255 bytes):
-        // the hop loop then costs one LDS byte read per header
-        uint32_t lw[4];
+        // twice the hop lengths of one-byte headers (byte offsets of the u16 table), 0 for any
+        // other first byte: the hop loop then costs one LDS read per header
+        uint32_t lw[8];
         const uint32_t src[4] = {pf[q].x, pf[q].y, pf[q].z, pf[q].w};
 #pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) {
-          uint32_t o = 0;
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t b = (src[t] >> (8u * i)) & 0xFFu;
-            const uint32_t len = 1u + ((b & 1u) ? (b >> 1) * w : vb);
-            o |= ((b & 0x80u) || len > 255u ? 0u : len) << (8u * i);
-          }
-          lw[t] = o;
+        for (uint32_t t = 0; t < 8; ++t) {
+          const uint32_t b0 = (src[t >> 1] >> (16u * (t & 1u))) & 0xFFu, b1 = (src[t >> 1] >> (16u * (t & 1u) + 8u)) & 0xFFu;
+          const uint32_t l0 = (b0 & 0x80u) ? 0u : 2u + ((b0 & 1u) ? (b0 >> 1) * w : vb) * 2u;
+          const uint32_t l1 = (b1 & 0x80u) ? 0u : 2u + ((b1 & 1u) ? (b1 >> 1) * w : vb) * 2u;
+          lw[t] = l0 | (l1 << 16);
         }
-        lent_s[wid][q * WAVE + lane] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        lent_s[wid][2 * (q * WAVE + lane)] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        lent_s[wid][2 * (q * WAVE + lane) + 1] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
       }
       sb = (uint32_t)(s.S + (uint64_t)r * LW_REG - ((s.S + (uint64_t)r * LW_REG) & ~15ull));
       loaded = r;
@@ -598,14 +606,14 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6, 8)))
     // header the general parse.
     uint32_t k = 0, posv = 0;
     const uint32_t c0 = cur;
-    const uint32_t ab = rfl(lb - rb + sb);  // LDS address of stream offset 0's entry (mod 2^32)
-    uint32_t addr = ab + cur;
-    const uint32_t alim = ab + lim;
+    const uint32_t ab = rfl(lb + 2u * (sb - rb));  // LDS address of stream offset 0's entry (mod 2^32)
+    uint32_t addr = ab + 2u * cur;
+    const uint32_t alim = ab + 2u * lim;
     bool dead = false;
     while (true) {
       lv_hops(addr, alim, k, posv);
       if (addr >= alim || k == 64u) break;
-      const uint32_t q = addr - ab;  // stream offset of a header whose hop is not in the table
+      const uint32_t q = (addr - ab) >> 1;  // stream offset of a header whose hop is not in the table
       uint32_t nxt, v, cnt;
       bool bp;
       const bool ok = lv_parse4(st, q - rb + sb, q, slen, w, vb, nxt, cnt, v, bp);
@@ -615,10 +623,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(6, 8)))
       }
       posv = lane == k ? addr : posv;
       ++k;
-      addr += rfl(nxt) - q;
+      addr += 2u * (rfl(nxt) - q);
     }
-    cur = addr - ab;
-    posv -= ab;
+    cur = (addr - ab) >> 1;
+    posv = (posv - ab) >> 1;
     LW_STAMP(t_hop);
 #ifdef PQG_DIAG
     nhops += k;
@@ -766,6 +774,7 @@ __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ b
     d[7] = j + 1 < nseg ? lt.bexit[s0 + j + 1] : 0;
   }
 #endif
+  if (verdict == 1 && sel == SS_DICT) verdict = 2;  // no window path for dictionary indices
   if (verdict == 0) {
     rt.pflag[p] = PF_WALK;
   } else {
@@ -1071,6 +1080,109 @@ __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const u
   }
 }
 
+// RLE_DICTIONARY values (get_batch_with_dict, rle.rs:437-487): each output's index, from its
+// run, gathers its value from the PLAIN dictionary page; groups of 16 / ES outputs, one 16-byte
+// store each (element stores for the groups shared with a neighbouring window). Returns nonzero
+// when an index is out of the dictionary (the reference panics).
+template <int ES>
+__device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+                                         uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
+                                         const uint8_t* __restrict__ dict, uint32_t ndict, bool aligned,
+                                         uint8_t* __restrict__ out) {
+  using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
+  constexpr uint32_t V = 16u / ES;  // outputs per 16-byte store
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
+  const uint64_t go = x.s.out;
+  const uint64_t lo = go + base, hi = go + endo;
+  const uint64_t k0 = lo / V, k1 = (hi + V - 1) / V;
+  uint32_t lgn = 1;
+  while (lgn * 2u <= rl.R) lgn *= 2u;
+  uint32_t a = 0, bad = 0;
+#pragma unroll 1
+  for (uint64_t k = k0 + lane; k < k1; k += WAVE) {
+    const uint64_t gl = k * V;
+    const uint32_t olo = (uint32_t)((gl > lo ? gl : lo) - go);
+    const uint32_t ohi = (uint32_t)((gl + V < hi ? gl + V : hi) - go);
+    const uint32_t f0 = (uint32_t)(gl - go);  // page-relative index of field 0 (may wrap)
+    for (uint32_t sp = lgn; sp; sp >>= 1)
+      if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
+    T f[V];
+#pragma unroll
+    for (uint32_t j = 0; j < V; ++j) f[j] = 0;
+    uint32_t b = a;
+#pragma unroll
+    for (uint32_t j = 0; j < V; ++j) {
+      const uint32_t o = f0 + j;
+      if (o < olo || o >= ohi) continue;
+      while (rl.rstart[b + 1] <= o) ++b;
+      const uint32_t inf = rl.rinfo[b];
+      uint32_t idx;
+      if (inf & R_RLE) {
+        idx = inf & 0x7FFFFFFFu;
+      } else {
+        const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[b]) * w;
+        idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+      }
+      if (idx >= ndict) {
+        bad = 1;
+        continue;
+      }
+      if (aligned) {
+        f[j] = reinterpret_cast<const T*>(dict)[idx];
+      } else {
+        const uint8_t* pv = dict + (uint64_t)idx * ES;
+        T t = 0;
+#pragma unroll
+        for (int q = 0; q < ES; ++q) t |= (T)pv[q] << (8 * q);
+        f[j] = t;
+      }
+    }
+    if (ohi - olo == V) {
+      uint4 v;
+      if constexpr (ES == 8)
+        v = make_uint4((uint32_t)f[0], (uint32_t)(f[0] >> 32), (uint32_t)f[1], (uint32_t)(f[1] >> 32));
+      else
+        v = make_uint4(f[0], f[1], f[2], f[3]);
+      *reinterpret_cast<uint4*>(out + gl * ES) = v;
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < V; ++j) {
+        const uint32_t o = f0 + j;
+        if (o >= olo && o < ohi) reinterpret_cast<T*>(out)[gl + j] = f[j];
+      }
+    }
+  }
+  return bad;
+}
+
+// What the walked-page emit writes: levels / booleans, or dictionary values.
+template <int OUT>
+struct LvLevelOut {
+  uint8_t* out;
+  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+                             const LvWin& x, uint32_t base, uint32_t endo, int sel, const ColumnParams& cp,
+                             PageWork* pages) const {
+    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, cp, pages, out);
+  }
+};
+
+template <int ES>
+struct LvDictOut {
+  int dict_page;  // the chunk's PLAIN dictionary page (k_lv_plan checked it)
+  uint8_t* out;
+  ChunkResult* res;
+  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+                             const LvWin& x, uint32_t base, uint32_t endo, int, const ColumnParams&,
+                             PageWork* pages) const {
+    const PageWork& dp = pages[dict_page];
+    const bool aligned = (dp.base % ES) == 0;
+    const uint32_t bad = lv_write_dict<ES>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base,
+                                           dp.num_values, aligned, out);
+    if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, res, (int)x.p, ST_PANIC);
+  }
+};
+
 // ------------------------------------------------------------------------------ k_lv_emit
 // Window path: windows g2 of the dense pages.
 template <int OUT>
@@ -1213,10 +1325,10 @@ struct LeWave {
   uint32_t rinfo[LW_RPW];
 };
 
-template <int OUT>
+template <class Writer>
 __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                      PageWork* pages, int npages, ColumnParams cp, int sel,
-                                                     RunTables rt, LevelTables lt, uint8_t* __restrict__ out) {
+                                                     RunTables rt, LevelTables lt, Writer wr) {
   __shared__ LeWave sm[WG / WAVE];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LeWave& E = sm[wid];
@@ -1265,38 +1377,47 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     lv_stage(blob, blob_len, x, E.stage, nch);  // ends with a wave LDS sync (run list too)
     const uint32_t base = E.rstart[0];
     const uint32_t endo = endn < x.s.n ? endn : x.s.n;
-    if (endo > base) lv_write<OUT>(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp,
-                                   pages, out);
+    if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp, pages);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
 
 extern "C" {
 
-// Level path of stream `sel` (def / rep levels: int16 out; RLE booleans: bytes out): plan, page
-// walk, window path for the dense pages, emits (+ def counts).
+// Hybrid-stream path of stream `sel`: plan, segment starts and walks, page scan, run compaction,
+// window path for the dense pages, emits. Def / rep levels: int16 out (+ def counts); RLE
+// booleans: bytes out; dictionary indices (SS_DICT, es 4 or 8): dictionary values out.
 hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                         ColumnParams cp, int sel, RunTables rt, LevelTables lt, void* out, hipStream_t s) {
+                         ColumnParams cp, int sel, int dict_page, int es, RunTables rt, LevelTables lt, void* out,
+                         ChunkResult* res, hipStream_t s) {
   if (npages <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
   const uint32_t wgrid = 256u * 8u;
   hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segscan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
+  uint8_t* o = (uint8_t*)out;
+  if (sel == SS_DICT) {  // (dense dictionary streams went to the general decoder)
+    if (es == 8)
+      hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut<8>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
+                         cp, sel, rt, lt, LvDictOut<8>{dict_page, o, res});
+    else
+      hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut<4>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
+                         cp, sel, rt, lt, LvDictOut<4>{dict_page, o, res});
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_stitch, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   if (sel == SS_BOOL) {
-    hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt,
-                       (uint8_t*)out);
-    hipLaunchKernelGGL(k_lv_emit_walk<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
-                       lt, (uint8_t*)out);
+    hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
+    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
+                       sel, rt, lt, LvLevelOut<1>{o});
   } else {
-    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt,
-                       (uint8_t*)out);
-    hipLaunchKernelGGL(k_lv_emit_walk<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt,
-                       lt, (uint8_t*)out);
+    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
+    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
+                       sel, rt, lt, LvLevelOut<2>{o});
   }
   return hipGetLastError();
 }

@@ -30,7 +30,7 @@ hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t,
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                           int, const uint32_t*, RunTables, uint8_t*, ChunkResult*, hipStream_t,
+                           int, const uint32_t*, RunTables, LevelTables, uint8_t*, ChunkResult*, hipStream_t,
                            hipEvent_t*);
 hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
                                  uint8_t*, ChunkResult*, hipStream_t);
@@ -553,7 +553,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
   // Level path buffers (normalized streams) per stream kind, grown on demand.
   const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
-  const bool need_lv[3] = {want_def, want_rep, rle_bool};
+  // 4- / 8-byte dictionary values: their index streams take the same path (pqg_launch_dict)
+  const bool dict_lv = enc_present[PQG_RLE_DICTIONARY] && !is_ba && out->values && (es == 4 || es == 8);
+  const bool need_lv[3] = {want_def, want_rep, rle_bool || dict_lv};
   auto grow = [&](void** p, size_t* cap, size_t need, size_t elem, const char* what) -> int {
     if (need <= *cap) return PQG_OK;
     hipFree(*p);
@@ -581,7 +583,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   // the streams it hands back; dictionary indices always take the general decoder.
   for (int k = 0; k < 3; ++k) {
     if (!sl.rt[k].nfall) continue;
-    const bool lvpath = k < 2 || rle_bool;
+    const bool lvpath = k < 2 || rle_bool || dict_lv;
     HIPCHK(hipMemsetAsync(sl.rt[k].nfall, lvpath ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
     if (!lvpath && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
   }
@@ -640,8 +642,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (enc_present[PQG_RLE_DICTIONARY]) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
       HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
-                             sl.rt[2], vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "dict");
-      sl.kv = nt > 0;
+                             sl.rt[2], sl.lt(2), vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "dict");
+      sl.kv = ctx->timing;
     }
     if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;

@@ -149,10 +149,12 @@ struct DeltaTables {
 };
 
 // Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
-// One segment (LW_SEGW windows of 1 KiB) of a sparse level stream, walked by its own wave
+// One segment (lw_segw(w) windows of 1 KiB: ~16 KiB of one-bit levels, more for wider
+// streams, whose runs are longer) of a sparse hybrid stream, walked by its own wave
 // (pqg_levels.hip); it records at most LW_SCAP runs (room for a walk through two segments).
 constexpr uint32_t LW_SEGW = 16;
 constexpr uint32_t LW_SCAP = 64 * (2 * LW_SEGW + 2);
+__host__ __device__ inline uint32_t lw_segw(uint32_t w) { return w <= 4 ? LW_SEGW : w <= 8 ? 4 * LW_SEGW : 16 * LW_SEGW; }
 struct LvSeg {
   uint64_t out;       // outputs of the runs the segment's walk recorded
   uint64_t base_out;  // (page scan) outputs before the segment
