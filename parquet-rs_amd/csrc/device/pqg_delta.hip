@@ -594,8 +594,9 @@ __global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__
 // then parses each block's header on its own lane (the checks of k_delta_index); every thread
 // unpacks 16 deltas of one mini-block (hoisted parameters, 32-bit bit offsets, one funnel shift
 // per delta), the workgroup scans, adds the carry and stores through an LDS transpose (quarters
-// of 1024 values). The next tile's bytes are loaded into registers while the current tile is
-// expanded. Anything else (an error the reference reports, a header or payload outside the
+// of 1024 values). The next tile's bytes are loaded into registers
+// while the current tile is expanded, as many as the current tile spanned plus a margin (a tile
+// that needs more reloads the full window). Anything else (an error the reference reports, a header or payload outside the
 // staged window, more than 8 mini-blocks, mini-blocks of a size not a multiple of 16, blocks
 // not dividing 4096) marks the page DP_FALLBACK for the tiled path, which reports errors exactly.
 constexpr int DPG_STAGE = 12288;
@@ -613,7 +614,7 @@ struct DeltaPageSmem {
   uint32_t mboff[DPG_NB][8];
   uint32_t mbw[DPG_NB][8];
   uint64_t wsum[WG / 64];
-  uint32_t ctl[4];  // 0: fallback, 1: header of the next tile's first block
+  uint32_t ctl[4];  // 0: fallback, 1: header of the next tile's first block, 2: window too short
 };
 
 template <int ES>
@@ -678,22 +679,27 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
   }
   uint4 pv[DPG_CH];
   uint64_t SB = (S + q) & ~15ull;  // stage base of the current tile (absolute)
-  auto issue = [&](uint64_t base) {
+  uint32_t win = DPG_STAGE;        // bytes staged for the current tile
+  auto issue = [&](uint64_t base, uint32_t nbytes) {
     const bool fast = base + DPG_STAGE <= blob_len;
 #pragma unroll
     for (int c = 0; c < DPG_CH; ++c) {
-      const uint64_t a = base + (uint64_t)(tid + c * WG) * 16;
-      pv[c] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+      const uint32_t off = (uint32_t)(tid + c * WG) * 16u;
+      const uint64_t a = base + off;
+      pv[c] = off >= nbytes ? make_uint4(0u, 0u, 0u, 0u)
+              : fast        ? *reinterpret_cast<const uint4*>(blob + a)
+                            : gload_u128_tail(blob, blob_len, a);
     }
   };
   const uint32_t ntl = (need + DPG_T - 1) / DPG_T;
-  if (ntl) issue(SB);
+  if (ntl) issue(SB, win);
   uint32_t hdr = q;        // header of the current tile's first block (stream offset)
   uint64_t carry = first;  // value before the tile's first delta
   for (uint32_t k = 0; k < ntl; ++k) {
     const uint32_t D0 = k * DPG_T;
     const uint32_t D1 = D0 + DPG_T < need ? D0 + DPG_T : need;
     const uint32_t nb = (D1 - D0 + vpb - 1) / vpb;  // blocks of the tile
+  restage:
     // ---- install the staged bytes
 #pragma unroll
     for (int c = 0; c < DPG_CH; ++c) sm.stq[tid + c * WG] = pv[c];
@@ -705,10 +711,15 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
       const uint32_t lane = (uint32_t)tid;
       uint32_t hp = hdr, posv = 0;
       bool fb = false;
+      bool shortwin = false;
       for (uint32_t j = 0; j < nb; ++j) {
         const uint32_t rel = hp - sb;
         if (hp >= slen || rel + 24u > (uint32_t)DPG_STAGE) {
           fb = true;
+          break;
+        }
+        if (rel + 24u > win) {  // past the bytes staged for this tile: stage the full window
+          shortwin = true;
           break;
         }
         posv = lane == j ? hp : posv;
@@ -727,7 +738,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
         hp = nx > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nx;
       }
       bool lfb = false;
-      if (!fb && lane < nb) {
+      if (!fb && !shortwin && lane < nb) {
         const uint32_t pos = posv, rel = pos - sb, b = D0 / vpb + lane;
         const uint64_t lo8 = lload_u64(sm.stage, rel), hi8 = lload_u64(sm.stage, rel + 8);
         const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
@@ -739,6 +750,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
         const uint64_t zz = (y & 0x000000000FFFFFFFull) | ((y & 0x0FFFFFFF00000000ull) >> 4);
         if ((uint64_t)pos + vl + nmb32 > slen) lfb = true;
         const uint32_t payload = pos + vl + nmb32;
+        if (rel + 24u > win) shortwin = true;
         const uint32_t left = need - b * vpb;
         const uint32_t inblk = left < vpb ? left : vpb;
         const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
@@ -758,12 +770,21 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
         sm.mind[lane] = (uint64_t)unzigzag(zz);
       }
       fb = fb || __ballot(lfb) != 0;
+      // the tile's payload must be staged too (its last block's end is the next tile's header)
+      if (!fb && (hp - sb > win || __ballot(shortwin))) shortwin = true;
       if (lane == 0) {
         sm.ctl[0] = fb ? 1u : 0u;
         sm.ctl[1] = hp;
+        sm.ctl[2] = shortwin ? 1u : 0u;
       }
     }
     __syncthreads();
+    if (sm.ctl[2] && !sm.ctl[0] && win < (uint32_t)DPG_STAGE) {  // stage the full window and redo
+      win = DPG_STAGE;
+      issue(SB, win);
+      __syncthreads();  // every read of the stage is done before the reinstall
+      goto restage;
+    }
     if (sm.ctl[0]) {  // leave the page to the tiled path
       if (tid == 0) {
         dt.page[p] = info;
@@ -771,11 +792,13 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
       }
       return;
     }
+    const uint32_t span = sm.ctl[1] - hdr;  // this tile's bytes: the next tile likely needs as many
     hdr = sm.ctl[1];
     const uint64_t SBn = (S + hdr) & ~15ull;
-    if (k + 1 < ntl) issue(SBn);
+    const uint32_t winn = min((uint32_t)DPG_STAGE, (span + span / 8u + 256u + 15u) & ~15u);
+    if (k + 1 < ntl) issue(SBn, winn);
     // ---- 16 deltas of one mini-block per thread
-    const uint32_t lim = DPG_STAGE * 8u;
+    const uint32_t lim = win * 8u;  // staged bits
     const uint32_t r0 = (uint32_t)tid * DPT;  // tile-relative first delta
     uint64_t x[DPT];
     uint64_t s = 0;
@@ -880,6 +903,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
       __syncthreads();
     }
     SB = SBn;
+    win = winn;
   }
   if (tid == 0) {
     info.first = first;
