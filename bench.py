@@ -40,7 +40,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="levels", choices=["levels", "dict", "delta"])
+    ap.add_argument("--config", default="levels", choices=["levels", "dict", "delta", "alltypes"])
     ap.add_argument("--n", type=float, default=1e9, help="levels/values per GPU")
     ap.add_argument("--p-null", type=float, default=0.5)
     ap.add_argument("--page-values", type=int, default=1 << 20)
@@ -54,6 +54,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--threads", type=int, default=16, help="host threads (box CPU share: 16)")
     ap.add_argument("--seed", type=int, default=0x5EED0000)
+    ap.add_argument("--rowgroups", type=int, default=11,
+                    help="alltypes: row groups per GPU (11 x 2^23 rows ~ 8 GiB decoded: 1/8 of config 5)")
+    ap.add_argument("--rg-rows", type=int, default=1 << 23, help="alltypes: rows per row group")
+    ap.add_argument("--at-p-null", type=float, default=0.05, help="alltypes: null fraction per column")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
     return ap.parse_args(argv)
@@ -353,6 +357,227 @@ def dry_run(args, world, rank, dist):
               flush=True)
 
 
+class AlltypesWorkload:
+    """Config 5 (one GPU's share): `rowgroups` row groups of the alltypes_plain schema, written by
+    the reference writer's defaults (tools/gen pqg_gen_alltypes), pages of all row groups in one
+    pinned host buffer and one device buffer; one pqg_decode_chunk per column chunk."""
+
+    def __init__(self, pqgpu, args, rank):
+        import torch
+        import pqgtools
+        self.rows, self.R, self.p_null = args.rg_rows, args.rowgroups, args.at_p_null
+        self.seed = shard_seed(args.seed + 5, 0)
+        self.row0 = rank * self.R * self.rows  # this rank's row groups
+        self.cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+        t0 = time.time()
+        rgs = [pqgtools.alltypes_row_group(self.rows, self.row0 + g * self.rows, self.p_null, self.seed,
+                                           args.threads) for g in range(self.R)]
+        self.gen_s = time.time() - t0
+        self.base = []
+        off = 0
+        for blob, pages, info in rgs:
+            self.base.append(off)
+            off += (info.blob_len + 255) & ~255
+        self.blob_len = off
+        self.h_blob = torch.empty(off + 64, dtype=torch.uint8).pin_memory()
+        hb = self.h_blob.numpy()
+        self.info, self.chunks = [], []
+        for g, (blob, pages, info) in enumerate(rgs):
+            hb[self.base[g]:self.base[g] + info.blob_len] = blob[:info.blob_len]
+            self.info.append(info)
+            per = []
+            for j in range(len(self.cols)):
+                lo, hi = info.chunk_first[j], info.chunk_first[j + 1]
+                arr = (pqgpu.Page * (hi - lo))(*[pages[i] for i in range(lo, hi)])
+                per.append(arr)
+            self.chunks.append(per)
+        del rgs
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.d_blob = torch.empty(off + 64, dtype=torch.uint8, device=dev)
+        self.d_blob.copy_(self.h_blob)
+        # outputs: two sets (the PCIe pipeline decodes row group g + 1 while g drains)
+        self.vcap = [max(i.value_bytes[j] for i in self.info) + 64 for j in range(len(self.cols))]
+        self.ncap = [self.rows + 1] * len(self.cols)  # BYTE_ARRAY offsets: num_levels + 1 (pqgpu.h)
+        self.out = []
+        for _ in range(2):
+            o = []
+            for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+                d_def = torch.empty(self.rows + 64, dtype=torch.int16, device=dev)
+                d_val = torch.empty(self.vcap[j], dtype=torch.uint8, device=dev)
+                d_off = torch.empty(self.ncap[j] + 8, dtype=torch.int64, device=dev) if pt == 6 else None
+                st = pqgpu.Output(d_def.data_ptr(), None, d_val.data_ptr(), self.vcap[j],
+                                  d_off.data_ptr() if d_off is not None else None,
+                                  self.ncap[j] if d_off is not None else 0, 0, 0, 0)
+                o.append((d_def, d_val, d_off, st))
+            self.out.append(o)
+        self.levels = self.R * self.rows * len(self.cols)  # cells: one level per row and column
+        self.in_bytes = sum(i.blob_len for i in self.info)
+        es = {0: 1, 1: 4, 2: 8, 3: 12, 4: 4, 5: 8}
+        self.out_bytes = 0
+        for i in self.info:
+            for j, (_, pt) in enumerate(pqgtools.ALLTYPES):
+                self.out_bytes += 2 * self.rows + i.value_bytes[j] + (8 * (i.num_values[j] + 1) if pt == 6 else 0)
+
+    def decode_rg(self, ctx, g, stream, oset=0):
+        for j, col in enumerate(self.cols):
+            ctx.decode_async(col, self.d_blob.data_ptr() + self.base[g], self.info[g].blob_len,
+                             self.chunks[g][j], self.out[oset][j][3], stream)
+
+
+def alltypes_check(ctx, w, stream):
+    """Decode row group 0 and compare every column (levels, values, BYTE_ARRAY offsets) with the
+    generator's own cells (pqg_truth_alltypes)."""
+    import pqgtools
+    w.decode_rg(ctx, 0, stream)
+    st, bad = ctx.sync()
+    assert st == 0, (st, bad, ctx.error_message())
+    for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+        nv, nb = w.info[0].num_values[j], w.info[0].value_bytes[j]
+        lv, vals, offs = pqgtools.alltypes_truth(w.row0, w.rows, j, w.p_null, w.seed, nb)
+        d_def, d_val, d_off, _ = w.out[0][j]
+        assert np.array_equal(d_def[:w.rows].cpu().numpy(), lv), f"{name}: def levels differ"
+        assert np.array_equal(d_val[:nb].cpu().numpy(), vals), f"{name}: values differ"
+        if offs is not None:
+            assert np.array_equal(d_off[:nv + 1].cpu().numpy(), offs), f"{name}: offsets differ"
+    return {"row_groups_checked": 1, "columns": len(pqgtools.ALLTYPES), "status": st}
+
+
+def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
+    import torch
+    import pqgpu
+    for _ in range(warmup):
+        for g in range(w.R):
+            w.decode_rg(ctx, g, stream)
+    ctx.sync()
+    pqgpu.lib().pqg_reset_timings(ctx.h)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for g in range(w.R):
+            w.decode_rg(ctx, g, stream)
+    st, bad = ctx.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    assert st == 0, (st, bad, ctx.error_message())
+    return (t1 - t0) / steps
+
+
+def alltypes_pcie(ctx, w, stream):
+    """Host-to-host rate: pinned page bytes of row group g + 1 go up (H2D stream) while row group g
+    decodes; its decoded columns come back (D2H stream) into two alternating pinned buffers."""
+    import torch
+    s_dec = torch.cuda.ExternalStream(stream)
+    s_up, s_dn = torch.cuda.Stream(), torch.cuda.Stream()
+    h_out = []
+    for k in range(2):
+        h_out.append([(torch.empty(d.numel(), dtype=d.dtype).pin_memory(),
+                       torch.empty(v.numel(), dtype=v.dtype).pin_memory(),
+                       torch.empty(o.numel(), dtype=o.dtype).pin_memory() if o is not None else None)
+                      for d, v, o, _ in w.out[k]])
+    up = [torch.cuda.Event() for _ in range(w.R)]
+    dec = [torch.cuda.Event() for _ in range(w.R)]
+    free = [torch.cuda.Event() for _ in range(2)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s_up):  # every row group's upload, in order, on its own stream
+        for g in range(w.R):
+            lo, hi = w.base[g], w.base[g] + w.info[g].blob_len
+            w.d_blob[lo:hi].copy_(w.h_blob[lo:hi], non_blocking=True)
+            up[g].record(s_up)
+    for g in range(w.R):
+        s_dec.wait_event(up[g])
+        if g >= 2:
+            s_dec.wait_event(free[g % 2])
+        w.decode_rg(ctx, g, stream, g % 2)
+        dec[g].record(s_dec)
+        with torch.cuda.stream(s_dn):
+            s_dn.wait_event(dec[g])
+            for (d, v, o, _), (hd, hv, ho) in zip(w.out[g % 2], h_out[g % 2]):
+                hd.copy_(d, non_blocking=True)
+                hv.copy_(v, non_blocking=True)
+                if o is not None:
+                    ho.copy_(o, non_blocking=True)
+            free[g % 2].record(s_dn)
+    st, bad = ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert st == 0, (st, bad)
+    return {"values_per_s": w.levels / dt, "ms": dt * 1e3, "pcie_bytes": w.in_bytes + w.out_bytes,
+            "note": "pinned H2D of row group g+1 overlapped with the decode of g and the D2H of its "
+                    "decoded columns (three streams), one pass over all row groups"}
+
+
+def alltypes_cpu_baseline(w, threads):
+    """The C restatement of read_batch(1024) (oracle, kind "port") over row group 0's 11 column
+    chunks: one reader per chunk, at 1 thread and at `threads` threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    import pqgtools
+    from concurrent.futures import ThreadPoolExecutor
+    hb = w.h_blob.numpy()
+    specs = []
+    for j, (_, pt) in enumerate(pqgtools.ALLTYPES):
+        ps = [pyoracle.PageSpec(p.page_type, hb[w.base[0] + p.offset:w.base[0] + p.offset + p.nbytes].tobytes(),
+                                p.num_values, p.encoding, p.def_encoding, p.rep_encoding)
+              for p in w.chunks[0][j]]
+        specs.append((pt, ps))
+
+    def run(t):
+        rr = pyoracle.read_column(t[0], t[1], max_def=1, batch_size=1024)
+        assert rr["status"] == 0, rr["message"]
+        return w.rows
+
+    res = {}
+    for th in (1, threads):
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(th) as ex:
+            n = sum(ex.map(run, specs))
+        res[th] = (n / (time.perf_counter() - t0), time.perf_counter() - t0)
+    return {"value": res[threads][0], "unit": "values/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"row group 0 ({w.rows} rows x 11 columns), read_batch(1024), one reader per column "
+                      f"chunk, {res[threads][1]:.1f}s wall",
+            "by_threads": {f"{th}t_b1024": round(v[0], 1) for th, v in res.items()}}
+
+
+def main_alltypes(args, world, rank, dist, ctx, stream):
+    import pqgpu
+    w = AlltypesWorkload(pqgpu, args, rank)
+    checked = alltypes_check(ctx, w, stream)
+    per_step = alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist)
+    per_step = max_over_ranks(per_step, dist, device="cuda")
+    step_bytes = w.in_bytes + w.out_bytes
+    achieved = step_bytes / per_step / 1e9
+    result = {
+        "metric": METRIC, "value": w.levels * world / per_step, "unit": "values/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int16 levels + native values (i32/i64/f32/f64/int96/bool bytes/byte arrays)",
+        "data": "synthetic alltypes_plain-schema row groups from the reference writer's defaults (SplitMix64 seeded)",
+        "gbps": step_bytes / per_step / 1e9 * world,
+        "config": {"workload": "configs[4]: alltypes_plain schema, one GPU's 1/8 share, row groups of "
+                               f"{w.rows} rows", "row_groups_per_gpu": w.R, "rows_per_gpu": w.R * w.rows,
+                   "cells_per_gpu": w.levels, "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes,
+                   "out_bytes_per_gpu": w.out_bytes, "chunk_decodes_per_step": w.R * len(w.cols),
+                   "gen_seconds": round(w.gen_s, 1),
+                   "parallelism": f"row-group partitions x{world}, no collective"},
+        "roofline": {"bound": "hbm", "kernel": "whole step (every chunk decode)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": step_bytes, "avg_ms": per_step * 1e3,
+                     "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
+        "value_check": checked,
+    }
+    if rank == 0 and args.pcie and world == 1:
+        result["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)
+    if rank == 0 and args.cpu_baseline and world == 1:
+        result["cpu_baseline"] = alltypes_cpu_baseline(w, min(args.threads, os.cpu_count() or 1))
+    return result
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -387,6 +612,14 @@ def main(argv=None):
     stream = torch.cuda.current_stream().cuda_stream
 
     kind = args.config
+    if kind == "alltypes":
+        result = main_alltypes(args, world, rank, dist, ctx, stream)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        ctx.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     w = Workload(pqgpu, args, rank, kind, p_null=args.p_null if kind == "levels" else None)
     checked = check_values(ctx, w, stream)
     per_step, tm = time_steps(pqgpu, ctx, w, stream, args.steps, args.warmup, dist)

@@ -508,7 +508,10 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
                            const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
                            ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
   hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
-  const bool lvpath = es == 4 || es == 8;
+  bool lvpath = es == 4 || es == 8;
+#ifdef PQG_DIAG
+  if (cp.debug & 256) lvpath = false;
+#endif
   if (kev) (void)hipEventRecord(kev[0], s);
   if (lvpath) {
     const hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, es, rt, lt, out, res, s);

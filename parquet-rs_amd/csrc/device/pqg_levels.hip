@@ -711,6 +711,7 @@ __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ b
     return;
   }
   const uint32_t cap = LW_REC * (lt.wbase[p + 1] - lt.wbase[p] + 2u);
+  for (uint32_t q = 0; q < nseg; ++q) lt.seg[s0 + q].flags = 0;  // (the tables outlive a decode)
   uint64_t acc = 0;
   uint32_t runs = 0, prevpos = 0xFFFFFFFFu, j = 0, verdict = 0;  // 0 walked, 1 window path, 2 general
   while (true) {

@@ -554,7 +554,10 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   // Level path buffers (normalized streams) per stream kind, grown on demand.
   const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
   // 4- / 8-byte dictionary values: their index streams take the same path (pqg_launch_dict)
-  const bool dict_lv = enc_present[PQG_RLE_DICTIONARY] && !is_ba && out->values && (es == 4 || es == 8);
+  bool dict_lv = enc_present[PQG_RLE_DICTIONARY] && !is_ba && out->values && (es == 4 || es == 8);
+#ifdef PQG_DIAG
+  if (cp.debug & 256) dict_lv = false;  // diagnostics: dictionary indices through the general decoder
+#endif
   const bool need_lv[3] = {want_def, want_rep, rle_bool || dict_lv};
   auto grow = [&](void** p, size_t* cap, size_t need, size_t elem, const char* what) -> int {
     if (need <= *cap) return PQG_OK;

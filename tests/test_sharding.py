@@ -88,3 +88,114 @@ def test_bench_refuses_debug_env():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "PQG_DEBUG" in r.stderr
+
+
+# ---- shards decode independently: the concatenation of per-rank decodes is the whole decode
+
+
+def _rg_decode_oracle(rg_index, rows):
+    """Oracle decode of alltypes row group `rg_index` (columns id and date_string_col)."""
+    import pyoracle
+    import pqgtools
+    blob, pages, info = pqgtools.alltypes_row_group(rows, rg_index * rows, 0.1, 77, threads=2)
+    out = []
+    for j in (0, 8):
+        specs = [pyoracle.PageSpec(p.page_type, blob[p.offset:p.offset + p.nbytes].tobytes(), p.num_values,
+                                   p.encoding, p.def_encoding, p.rep_encoding)
+                 for p in (pages[i] for i in range(info.chunk_first[j], info.chunk_first[j + 1]))]
+        r = pyoracle.read_column(pqgtools.ALLTYPES[j][1], specs, max_def=1)
+        assert r["status"] == 0, r["message"]
+        out.append((r["def"].tobytes(), r["values"].tobytes() if j == 0 else r["bytes"]))
+    return info.blob_len, out
+
+
+def _shard_worker(rank, world, port, q, nrg, rows):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gen"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sizes = [rows * (1 + (i % 3)) for i in range(nrg)]  # uneven byte sizes
+        mine = sharding.row_groups_for_rank(sizes, world, rank)
+        dec = {g: _rg_decode_oracle(g, rows)[1] for g in mine}
+        allp = [None] * world
+        dist.all_gather_object(allp, dec)
+        q.put((rank, allp))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_gloo_world2_shards_concatenate_to_whole():
+    world, nrg, rows = 2, 5, 20_000
+    port = 31500 + os.getpid() % 2000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, nrg, rows)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(world)]
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    _, allp = res[0]
+    merged = {}
+    for part in allp:
+        assert not (set(part) & set(merged))  # every row group decoded by exactly one rank
+        merged.update(part)
+    assert sorted(merged) == list(range(nrg))
+    for g in range(nrg):  # the unsharded decode, row group by row group in file order
+        assert merged[g] == _rg_decode_oracle(g, rows)[1], g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["levels", "dict"])
+def test_gpu_page_shards_concatenate_to_whole(kind):
+    """Configs 2-3 shard a chunk's pages across GPUs (the dictionary page goes to
+    every shard). Decoding 4 contiguous page ranges in sequence gives the whole chunk's decode."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import pqgpu
+    import pqgtools
+    L = pqgtools.lib()
+    info = pqgtools.WorkloadInfo()
+    n, pv = 3_000_000, 1 << 18
+    if kind == "levels":
+        gen = lambda b, cap, pg, pc: L.pqg_gen_levels_plain(n, 0.3, pv, 99, 8, b, cap, pg, pc, C.byref(info))
+        col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
+    else:
+        gen = lambda b, cap, pg, pc: L.pqg_gen_dict_int64(n, 4096, pv, 99, 8, b, cap, pg, pc, C.byref(info))
+        col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
+    assert gen(None, 0, None, 0) == 0
+    host = np.zeros(info.blob_len + 64, np.uint8)
+    pages = (pqgpu.Page * info.npages)()
+    assert gen(host.ctypes.data_as(C.c_void_p), info.blob_len, pages, info.npages) == 0
+    d_blob = torch.from_numpy(host).cuda()
+    es = 4 if kind == "levels" else 8
+    ctx = pqgpu.Context(0)
+
+    def decode(idx):
+        sel = (pqgpu.Page * len(idx))(*[pages[i] for i in idx])
+        nlev = sum(pages[i].num_values for i in idx if pages[i].page_type == pqgpu.PAGE_DATA)
+        d_def = torch.empty(nlev + 8, dtype=torch.int16, device="cuda")
+        d_val = torch.empty(nlev * es + 64, dtype=torch.uint8, device="cuda")
+        out = pqgpu.Output(d_def.data_ptr() if col.max_def else None, None, d_val.data_ptr(), nlev * es, None, 0, 0, 0, 0)
+        ctx.decode_async(col, d_blob.data_ptr(), info.blob_len, sel, out, torch.cuda.current_stream().cuda_stream)
+        st, bad = ctx.sync()
+        assert st == 0, (st, bad, ctx.error_message())
+        return (d_def[:out.num_levels].cpu().numpy().tobytes() if col.max_def else b"",
+                d_val[:out.num_values * es].cpu().numpy().tobytes())
+
+    try:
+        first = 1 if kind == "dict" else 0
+        data = list(range(first, info.npages))
+        whole = decode(list(range(info.npages)))
+        parts = [decode(list(range(first)) + data[r * len(data) // 4:(r + 1) * len(data) // 4]) for r in range(4)]
+    finally:
+        ctx.close()
+    assert b"".join(p[0] for p in parts) == whole[0]
+    assert b"".join(p[1] for p in parts) == whole[1]

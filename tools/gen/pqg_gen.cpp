@@ -15,8 +15,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdio.h>
+
 #include <algorithm>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "pqg_gen.h"
@@ -485,6 +488,293 @@ uint64_t pqg_truth_delta_int64(uint64_t n, int delta_bits, uint32_t page_values,
   delta_page_values(n, delta_bits, page_values, seed, page, v);
   memcpy(values, v.data(), v.size() * 8);
   return v.size();
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ config 5
+// One row group of the alltypes_plain schema (data/alltypes_plain.parquet: 11 OPTIONAL
+// columns, max_def 1), written the way ColumnWriterImpl does with the default properties
+// (file/properties.rs:56-65: v1 pages, 1 MiB data pages, dictionary on with a 1 MiB limit,
+// batches of 1024 levels, no compression):
+//   - after each 1024-level mini-batch (column/writer.rs:230-245, 345-364) a data page is cut
+//     once the PLAIN encoder's estimate reaches 1 MiB (:406-410); while the dictionary encoder
+//     holds the values that estimate stays 0, so a dictionary chunk buffers one data page;
+//   - once the dictionary's PLAIN size reaches 1 MiB (:395-402) the dictionary page and the
+//     buffered data page are written and the rest of the chunk is PLAIN (:412-420, 543-556);
+//   - at the end the dictionary page (if still in use) then the last data page;
+//   - BOOLEAN has no dictionary support (:744-756);
+//   - data page v1: [i32 length][RLE def levels][values] (:441-480); dictionary data pages
+//     PLAIN_DICTIONARY with [bit width][RLE hybrid] indices (encoding.rs:338-355, bit width
+//     :324-334), the dictionary page PLAIN_DICTIONARY with the PLAIN uniques.
+// Cell contents are counter-based (seed, column, row): the row-group generator and the truth
+// function below agree without sharing state.
+namespace {
+
+constexpr int AT_NCOL = 11;
+const int at_ptype[AT_NCOL] = {PQG_INT32, PQG_BOOLEAN, PQG_INT32, PQG_INT32, PQG_INT32, PQG_INT64,
+                               PQG_FLOAT, PQG_DOUBLE, PQG_BYTE_ARRAY, PQG_BYTE_ARRAY, PQG_INT96};
+constexpr uint64_t AT_PAGE = 1 << 20;  // data page size limit (properties.rs:56)
+constexpr uint64_t AT_DICT = 1 << 20;  // dictionary page size limit (properties.rs:61)
+constexpr uint64_t AT_BATCH = 1024;    // write batch size (properties.rs:57)
+
+inline uint64_t at_hash(uint64_t seed, uint32_t col, uint64_t row, uint32_t k) {
+  uint64_t s = seed ^ ((uint64_t)col * 0x9E3779B97F4A7C15ULL) ^ (row * 0xD1B54A32D192ED03ULL) ^
+               ((uint64_t)k * 0xC2B2AE3D27D4EB4FULL);
+  return splitmix64(s);
+}
+
+// Cell (col, row): null, or the value's PLAIN bytes (BYTE_ARRAY: the bytes alone).
+struct AtCell {
+  bool null;
+  uint32_t len;
+  uint8_t v[16];
+};
+
+void at_cell(uint64_t seed, double p_null, uint32_t col, uint64_t row, AtCell& c) {
+  const uint64_t thresh = (uint64_t)(p_null * 9007199254740992.0);
+  c.null = (at_hash(seed, col, row, 0) >> 11) < thresh;
+  const uint64_t h = at_hash(seed, col, row, 1);
+  const uint32_t k = (uint32_t)((h >> 32) * 10 >> 32);  // 0..9, as the fixture's small columns
+  switch (col) {
+    case 0: {  // id: the row number
+      const int32_t x = (int32_t)row;
+      memcpy(c.v, &x, 4);
+      c.len = 4;
+      break;
+    }
+    case 1:  // bool_col: alternating
+      c.v[0] = (row & 1) == 0;
+      c.len = 1;
+      break;
+    case 2:
+    case 3:
+    case 4: {  // tinyint / smallint / int
+      const int32_t x = (int32_t)k;
+      memcpy(c.v, &x, 4);
+      c.len = 4;
+      break;
+    }
+    case 5: {  // bigint
+      const int64_t x = (int64_t)k * 10;
+      memcpy(c.v, &x, 8);
+      c.len = 8;
+      break;
+    }
+    case 6: {  // float
+      const float x = (float)k * 1.1f;
+      memcpy(c.v, &x, 4);
+      c.len = 4;
+      break;
+    }
+    case 7: {  // double
+      const double x = (double)k * 10.1;
+      memcpy(c.v, &x, 8);
+      c.len = 8;
+      break;
+    }
+    case 8: {  // date_string_col "MM/DD/YY" over two years
+      const uint32_t d = (uint32_t)(h % 730);
+      const uint32_t y = 9 + d / 365, doy = d % 365;
+      const uint32_t mo = doy / 31 + 1, dd = doy % 31 + 1;
+      char b[16];
+      snprintf(b, sizeof(b), "%02u/%02u/%02u", mo, dd, y);
+      memcpy(c.v, b, 8);
+      c.len = 8;
+      break;
+    }
+    case 9:  // string_col: one digit
+      c.v[0] = (uint8_t)('0' + k);
+      c.len = 1;
+      break;
+    default: {  // timestamp_col INT96: nanoseconds of the day, then the Julian day
+      const uint64_t ns = h % 86400000000000ULL;
+      const uint32_t jd = 2454833u + (uint32_t)(at_hash(seed, col, row, 2) % 730);
+      memcpy(c.v, &ns, 8);
+      memcpy(c.v + 8, &jd, 4);
+      c.len = 12;
+      break;
+    }
+  }
+}
+
+// One column chunk of the row group: its pages (offsets relative to the chunk start, each
+// payload 64-byte aligned).
+struct AtChunk {
+  std::vector<uint8_t> buf;
+  std::vector<pqg_page> pages;
+  uint64_t values = 0, value_bytes = 0;
+};
+
+struct AtKey {
+  uint8_t v[16];
+  uint32_t len;
+  bool operator==(const AtKey& o) const { return len == o.len && memcmp(v, o.v, len) == 0; }
+};
+struct AtKeyHash {
+  size_t operator()(const AtKey& k) const {
+    uint64_t s = k.len;
+    for (uint32_t i = 0; i < k.len; ++i) s = s * 131 + k.v[i];
+    return (size_t)splitmix64(s);
+  }
+};
+
+void at_write_chunk(uint64_t rows, uint64_t row0, double p_null, uint64_t seed, uint32_t col, AtChunk& ch) {
+  const int pt = at_ptype[col];
+  bool dict = pt != PQG_BOOLEAN;
+  std::unordered_map<AtKey, uint32_t, AtKeyHash> map;
+  std::vector<uint8_t> uniq;   // PLAIN dictionary page payload
+  uint32_t nuniq = 0;
+  uint64_t dict_size = 0;      // DictEncoder::dict_encoded_size
+  std::vector<uint32_t> idx;   // buffered indices (dictionary data page)
+  std::vector<uint8_t> plain;  // PLAIN values of the pending page
+  uint64_t nbool = 0;          // PLAIN booleans of the pending page (bit-packed into plain)
+  std::vector<int16_t> lv;     // def levels of the pending page
+  auto put_page = [&](const uint8_t* p, uint64_t n, uint32_t nv, int type, int enc) {
+    const uint64_t off = align64(ch.buf.size());
+    ch.buf.resize(off + n);
+    memcpy(ch.buf.data() + off, p, n);
+    ch.pages.push_back(pqg_page{off, (uint32_t)n, nv, type, enc, PQG_RLE, PQG_RLE, 0, 0});
+  };
+  auto data_page = [&](bool dict_page) {
+    if (lv.empty()) return;
+    std::vector<uint8_t> b(8 + rle_bound(1, lv.size()) + plain.size() + rle_bound(32, idx.size()) + 16);
+    const uint64_t ll = pqg_encode_levels_v1(lv.data(), lv.size(), 1, b.data(), b.size());
+    uint64_t vl;
+    if (dict_page) {
+      const int bw = nuniq == 0 ? 0 : nuniq == 1 ? 1 : log2_ceil(nuniq);
+      vl = pqg_encode_dict_indices(idx.data(), idx.size(), bw, b.data() + ll, b.size() - ll);
+    } else {
+      memcpy(b.data() + ll, plain.data(), plain.size());
+      vl = plain.size();
+    }
+    put_page(b.data(), ll + vl, (uint32_t)lv.size(), PQG_PAGE_DATA, dict_page ? PQG_PLAIN_DICTIONARY : PQG_PLAIN);
+    lv.clear();
+    idx.clear();
+    plain.clear();
+    nbool = 0;
+  };
+  auto dict_out = [&]() {
+    put_page(uniq.data(), uniq.size(), nuniq, PQG_PAGE_DICTIONARY, PQG_PLAIN_DICTIONARY);
+    data_page(true);
+    dict = false;
+  };
+  AtCell c;
+  for (uint64_t b0 = 0; b0 < rows; b0 += AT_BATCH) {
+    const uint64_t b1 = std::min(rows, b0 + AT_BATCH);
+    for (uint64_t r = b0; r < b1; ++r) {
+      at_cell(seed, p_null, col, row0 + r, c);
+      lv.push_back(c.null ? 0 : 1);
+      if (c.null) continue;
+      ch.values++;
+      ch.value_bytes += c.len;
+      if (dict) {
+        AtKey key;
+        memcpy(key.v, c.v, c.len);
+        key.len = c.len;
+        auto it = map.find(key);
+        uint32_t id;
+        if (it == map.end()) {
+          id = nuniq++;
+          map.emplace(key, id);
+          if (pt == PQG_BYTE_ARRAY) {
+            const uint32_t l = c.len;
+            uniq.insert(uniq.end(), (const uint8_t*)&l, (const uint8_t*)&l + 4);
+          }
+          uniq.insert(uniq.end(), c.v, c.v + c.len);
+          dict_size += pt == PQG_BYTE_ARRAY ? 4 + c.len : c.len;
+        } else {
+          id = it->second;
+        }
+        idx.push_back(id);
+      } else if (pt == PQG_BOOLEAN) {
+        if ((nbool & 7) == 0) plain.push_back(0);
+        plain.back() |= (uint8_t)(c.v[0] << (nbool & 7));
+        ++nbool;
+      } else {
+        if (pt == PQG_BYTE_ARRAY) {
+          const uint32_t l = c.len;
+          plain.insert(plain.end(), (const uint8_t*)&l, (const uint8_t*)&l + 4);
+        }
+        plain.insert(plain.end(), c.v, c.v + c.len);
+      }
+    }
+    // write_mini_batch's tail: page cut on the PLAIN estimate, then the dictionary fallback
+    if (!dict && plain.size() >= AT_PAGE) data_page(false);
+    if (dict && dict_size >= AT_DICT) dict_out();
+  }
+  if (dict) dict_out();
+  else data_page(false);
+}
+
+struct AtGen {
+  std::vector<AtChunk> ch;
+  pqg_alltypes_info info;
+};
+
+}  // namespace
+
+extern "C" {
+
+void* pqg_gen_alltypes(uint64_t rows, uint64_t row0, double p_null, uint64_t seed, int threads,
+                       pqg_alltypes_info* info) {
+  if (!info) return nullptr;
+  AtGen* g = new AtGen();
+  g->ch.resize(AT_NCOL);
+  parallel_pages(AT_NCOL, threads, [&](uint32_t j) { at_write_chunk(rows, row0, p_null, seed, j, g->ch[j]); });
+  pqg_alltypes_info& in = g->info;
+  memset(&in, 0, sizeof(in));
+  uint64_t off = 0;
+  uint32_t np = 0;
+  for (int j = 0; j < AT_NCOL; ++j) {
+    in.chunk_first[j] = np;
+    in.chunk_offset[j] = off;
+    np += (uint32_t)g->ch[j].pages.size();
+    off = align64(off + g->ch[j].buf.size());
+    in.num_values[j] = g->ch[j].values;
+    in.value_bytes[j] = g->ch[j].value_bytes;
+  }
+  in.chunk_first[AT_NCOL] = np;
+  in.chunk_offset[AT_NCOL] = off;
+  in.npages = np;
+  in.blob_len = off;
+  in.rows = rows;
+  *info = in;
+  return g;
+}
+
+int pqg_alltypes_copy(void* h, uint8_t* blob, uint64_t cap, pqg_page* pages, uint32_t pages_cap) {
+  const AtGen* g = (const AtGen*)h;
+  if (!g || cap < g->info.blob_len || pages_cap < g->info.npages) return PQG_ERR_CAPACITY;
+  for (int j = 0; j < AT_NCOL; ++j) {
+    const AtChunk& c = g->ch[j];
+    memcpy(blob + g->info.chunk_offset[j], c.buf.data(), c.buf.size());
+    for (size_t i = 0; i < c.pages.size(); ++i) {
+      pqg_page p = c.pages[i];
+      p.offset += g->info.chunk_offset[j];
+      pages[g->info.chunk_first[j] + i] = p;
+    }
+  }
+  return PQG_OK;
+}
+
+void pqg_alltypes_free(void* h) { delete (AtGen*)h; }
+
+uint64_t pqg_truth_alltypes(uint64_t row0, uint64_t rows, int col, double p_null, uint64_t seed,
+                            int16_t* levels, uint8_t* values, int64_t* offsets) {
+  AtCell c;
+  uint64_t nv = 0, nb = 0;
+  if (offsets) offsets[0] = 0;
+  for (uint64_t r = 0; r < rows; ++r) {
+    at_cell(seed, p_null, (uint32_t)col, row0 + r, c);
+    if (levels) levels[r] = c.null ? 0 : 1;
+    if (c.null) continue;
+    if (values) memcpy(values + nb, c.v, c.len);
+    nb += c.len;
+    ++nv;
+    if (offsets) offsets[nv] = (int64_t)nb;
+  }
+  return nv;
 }
 
 }  // extern "C"

@@ -52,6 +52,31 @@ int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int bl
                         uint64_t blob_cap, pqg_page *pages, uint32_t pages_cap,
                         pqg_workload_info *info);
 
+/* Config 5: one row group (`rows` rows from global row `row0`) of the alltypes_plain schema (11
+ * OPTIONAL columns: id INT32, bool_col BOOLEAN, tinyint/smallint/int INT32, bigint INT64, float,
+ * double, date_string / string BYTE_ARRAY, timestamp INT96), written with the reference writer's
+ * defaults (see pqg_gen.cpp). pqg_gen_alltypes builds it in host memory (one thread per column)
+ * and returns a handle; pqg_alltypes_copy lays the 11 column chunks out in `blob` (64-byte
+ * aligned pages; chunk j's pages are [chunk_first[j], chunk_first[j + 1])). */
+typedef struct {
+  uint64_t blob_len;
+  uint64_t rows;
+  uint32_t npages;
+  uint32_t chunk_first[12];
+  uint64_t chunk_offset[12];
+  uint64_t num_values[11];   /* non-null values per column */
+  uint64_t value_bytes[11];  /* decoded value bytes (BYTE_ARRAY: the concatenated bytes) */
+} pqg_alltypes_info;
+void *pqg_gen_alltypes(uint64_t rows, uint64_t row0, double p_null, uint64_t seed, int threads,
+                       pqg_alltypes_info *info);
+int pqg_alltypes_copy(void *handle, uint8_t *blob, uint64_t cap, pqg_page *pages, uint32_t pages_cap);
+void pqg_alltypes_free(void *handle);
+/* Raw content of column `col` over rows [row0, row0 + rows): levels (0/1), the non-null values'
+ * bytes (PLAIN form; BYTE_ARRAY: the bytes alone, with int64 offsets[values + 1]). Returns the
+ * non-null count. Any output pointer may be NULL. */
+uint64_t pqg_truth_alltypes(uint64_t row0, uint64_t rows, int col, double p_null, uint64_t seed,
+                            int16_t *levels, uint8_t *values, int64_t *offsets);
+
 /* Raw content of one generated page (same seeds as the generators): */
 /* config 2: levels (0/1) of page `page` and its non-null INT32 values; returns the count. */
 uint64_t pqg_truth_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,

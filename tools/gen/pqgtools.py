@@ -10,12 +10,24 @@ LIB_PATH = os.path.join(_HERE, "libpqgtools.so")
 
 EXPORTS = ["pqg_encode_rle", "pqg_encode_levels_v1", "pqg_encode_delta", "pqg_encode_dict_indices",
            "pqg_gen_levels_plain", "pqg_gen_dict_int64", "pqg_gen_delta_int64",
-           "pqg_truth_levels_plain", "pqg_truth_dict_int64", "pqg_truth_delta_int64"]
+           "pqg_truth_levels_plain", "pqg_truth_dict_int64", "pqg_truth_delta_int64",
+           "pqg_gen_alltypes", "pqg_alltypes_copy", "pqg_alltypes_free", "pqg_truth_alltypes"]
+
+# alltypes_plain schema (data/alltypes_plain.parquet): 11 OPTIONAL leaves, physical types
+ALLTYPES = [("id", 1), ("bool_col", 0), ("tinyint_col", 1), ("smallint_col", 1), ("int_col", 1),
+            ("bigint_col", 2), ("float_col", 4), ("double_col", 5), ("date_string_col", 6),
+            ("string_col", 6), ("timestamp_col", 3)]
 
 
 class WorkloadInfo(C.Structure):
     _fields_ = [("blob_len", C.c_uint64), ("npages", C.c_uint32), ("total_levels", C.c_uint64),
                 ("total_values", C.c_uint64)]
+
+
+class AlltypesInfo(C.Structure):
+    _fields_ = [("blob_len", C.c_uint64), ("rows", C.c_uint64), ("npages", C.c_uint32),
+                ("chunk_first", C.c_uint32 * 12), ("chunk_offset", C.c_uint64 * 12),
+                ("num_values", C.c_uint64 * 11), ("value_bytes", C.c_uint64 * 11)]
 
 
 _lib = None
@@ -54,5 +66,46 @@ def lib():
         L.pqg_encode_delta.argtypes = [i32, vp, u64, i32, i32, vp, u64]
         L.pqg_encode_dict_indices.restype = u64
         L.pqg_encode_dict_indices.argtypes = [vp, u64, i32, vp, u64]
+        L.pqg_gen_alltypes.restype = vp
+        L.pqg_gen_alltypes.argtypes = [u64, u64, C.c_double, u64, i32, C.POINTER(AlltypesInfo)]
+        L.pqg_alltypes_copy.argtypes = [vp, vp, u64, C.POINTER(Page), u32]
+        L.pqg_alltypes_free.argtypes = [vp]
+        L.pqg_truth_alltypes.restype = u64
+        L.pqg_truth_alltypes.argtypes = [u64, u64, i32, C.c_double, u64, vp, vp, vp]
         _lib = L
     return _lib
+
+
+def alltypes_row_group(rows, row0, p_null, seed, threads=16, out=None):
+    """One alltypes row group: (host bytes as numpy uint8, pqgpu.Page array, AlltypesInfo).
+    `out`, if given, is a uint8 array (e.g. pinned) the pages are laid out into."""
+    import numpy as np
+    import pqgpu
+    L = lib()
+    info = AlltypesInfo()
+    h = L.pqg_gen_alltypes(rows, row0, p_null, seed, threads, C.byref(info))
+    if not h:
+        raise RuntimeError("pqg_gen_alltypes failed")
+    try:
+        blob = np.zeros(info.blob_len + 64, np.uint8) if out is None else out
+        assert blob.nbytes >= info.blob_len
+        pages = (pqgpu.Page * info.npages)()
+        st = L.pqg_alltypes_copy(h, blob.ctypes.data, blob.nbytes, pages, info.npages)
+        assert st == 0, st
+    finally:
+        L.pqg_alltypes_free(h)
+    return blob, pages, info
+
+
+def alltypes_truth(row0, rows, col, p_null, seed, value_bytes):
+    """Raw content of one alltypes column over rows [row0, row0 + rows): (levels, values bytes,
+    offsets or None)."""
+    import numpy as np
+    L = lib()
+    lv = np.zeros(rows, np.int16)
+    vals = np.zeros(max(value_bytes, 1), np.uint8)
+    ba = ALLTYPES[col][1] == 6
+    offs = np.zeros(rows + 1, np.int64) if ba else None
+    nv = L.pqg_truth_alltypes(row0, rows, col, p_null, seed, lv.ctypes.data, vals.ctypes.data,
+                              offs.ctypes.data if ba else None)
+    return lv, vals[:value_bytes], (offs[:nv + 1] if ba else None)
