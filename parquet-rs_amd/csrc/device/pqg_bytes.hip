@@ -319,40 +319,94 @@ __global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, int npages, 
 }
 
 // Gathers value slices into the output and writes their offsets (all encodings but
-// DELTA_BYTE_ARRAY). One workgroup per page, 256 values per pass.
+// DELTA_BYTE_ARRAY), tiled so a page of millions of values (a dictionary column's single data
+// page) spreads over the chip: tiles of BA_T values, grid (tile, page).
+//   k_ba_tsum   per tile: the tile-relative offset of each value (into `offsets`) and the
+//               tile's byte total;
+//   k_ba_tscan  per page: the tiles' start offsets (page byte_out + exclusive scan);
+//   k_ba_copy   per tile: final offsets and the bytes.
+constexpr uint32_t BA_VPT = 16;            // values per thread
+constexpr uint32_t BA_T = BA_VPT * WG;     // values per tile
+
+__device__ inline bool ba_page_ok(const PageWork& pw, const ChunkResult* res, uint64_t cap) {
+  return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) &&
+         pw.encoding != E_DELTA_BYTE_ARRAY && res->total_bytes <= cap;
+}
+
+__global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const uint32_t* __restrict__ vlen, uint64_t cap,
+                                                uint32_t maxt, uint64_t* __restrict__ tsum,
+                                                int64_t* __restrict__ offsets, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const uint32_t t = blockIdx.x, p = blockIdx.y;
+  const PageWork pw = pages[p];
+  if (!ba_page_ok(pw, res, cap)) return;
+  const uint64_t n = pw.nonnull, vo = pw.value_out;
+  const uint64_t i0 = (uint64_t)t * BA_T + (uint64_t)threadIdx.x * BA_VPT;
+  if ((uint64_t)t * BA_T >= n) return;
+  uint32_t l[BA_VPT];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    l[k] = i0 + k < n ? vlen[vo + i0 + k] : 0u;
+    s += l[k];
+  }
+  uint64_t tot;
+  uint64_t pre = block_exscan(sm, s, tot);
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    if (i0 + k < n) offsets[vo + i0 + k] = (int64_t)pre;
+    pre += l[k];
+  }
+  if (threadIdx.x == 0) tsum[(uint64_t)p * maxt + t] = tot;
+}
+
+__global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, uint64_t cap, uint32_t maxt,
+                                                 uint64_t* __restrict__ tsum, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  const uint32_t p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (!ba_page_ok(pw, res, cap)) return;
+  const uint32_t nt = (uint32_t)((pw.nonnull + BA_T - 1) / BA_T);
+  uint64_t carry = pw.byte_out;
+  for (uint32_t b = 0; b < nt; b += WG) {
+    const uint32_t t = b + threadIdx.x;
+    const uint64_t x = t < nt ? tsum[(uint64_t)p * maxt + t] : 0;
+    uint64_t tot;
+    const uint64_t pre = block_exscan(sm, x, tot);
+    __syncthreads();  // every read of this pass's sums is done before the starts overwrite them
+    if (t < nt) tsum[(uint64_t)p * maxt + t] = carry + pre;
+    carry += tot;
+  }
+}
+
 __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
                                                 const uint64_t* __restrict__ vsrc,
-                                                const uint32_t* __restrict__ vlen, uint64_t cap,
-                                                int64_t* __restrict__ offsets,
+                                                const uint32_t* __restrict__ vlen, uint64_t cap, uint32_t maxt,
+                                                const uint64_t* __restrict__ tsum, int64_t* __restrict__ offsets,
                                                 uint8_t* __restrict__ out, ChunkResult* res) {
-  __shared__ DeltaSmem sm;
-  const int p = blockIdx.x;
+  const uint32_t t = blockIdx.x, p = blockIdx.y;
   const PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding == E_DELTA_BYTE_ARRAY) return;
-  if (res->total_bytes > cap) return;
+  if (!ba_page_ok(pw, res, cap)) return;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
-  uint64_t carry = pw.byte_out;
-  for (uint64_t b = 0; b < n; b += WG) {
-    const uint64_t i = b + threadIdx.x;
-    const uint32_t l = i < n ? vlen[vo + i] : 0;
-    uint64_t tot;
-    const uint64_t pre = block_exscan(sm, l, tot);
-    if (i < n) {
-      const uint64_t d = carry + pre;
-      offsets[vo + i] = (int64_t)d;
-      const uint8_t* s = blob + vsrc[vo + i];
-      uint8_t* o = out + d;
-      uint32_t k = 0;
-      for (; k + 8 <= l; k += 8) {
-        uint64_t x;
-        __builtin_memcpy(&x, s + k, 8);
-        __builtin_memcpy(o + k, &x, 8);
-      }
-      for (; k < l; ++k) o[k] = s[k];
+  if ((uint64_t)t * BA_T >= n) return;
+  const uint64_t base = tsum[(uint64_t)p * maxt + t];
+  // lanes take consecutive values: neighbouring lanes write neighbouring bytes
+#pragma unroll 1
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+    if (i >= n) break;
+    const uint64_t d = base + (uint64_t)offsets[vo + i];
+    offsets[vo + i] = (int64_t)d;
+    const uint32_t l = vlen[vo + i];
+    const uint8_t* sp = blob + vsrc[vo + i];
+    uint8_t* o = out + d;
+    uint32_t q = 0;
+    for (; q + 8 <= l; q += 8) {
+      uint64_t x;
+      __builtin_memcpy(&x, sp + q, 8);
+      __builtin_memcpy(o + q, &x, 8);
     }
-    carry += tot;
+    for (; q < l; ++q) o[q] = sp[q];
   }
 }
 
@@ -419,13 +473,18 @@ extern "C" hipError_t pqg_launch_badict_expand(const uint8_t* blob, uint64_t blo
 extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                                        int npages, int type_length, bool has_dba, uint64_t* vsrc,
                                        uint32_t* vlen, uint32_t* vpre, uint64_t cap,
-                                       int64_t* offsets, uint8_t* out, ChunkResult* res,
-                                       hipStream_t s) {
+                                       int64_t* offsets, uint8_t* out, uint64_t max_page_vals,
+                                       uint64_t* tsum, ChunkResult* res, hipStream_t s) {
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, type_length,
                      vsrc, vlen, vpre, res);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);
-  hipLaunchKernelGGL(k_ba_copy, dim3(npages), dim3(WG), 0, s, blob, pages, vsrc, vlen, cap,
-                     offsets, out, res);
+  const uint32_t maxt = (uint32_t)((max_page_vals + BA_T - 1) / BA_T);
+  if (maxt) {
+    hipLaunchKernelGGL(k_ba_tsum, dim3(maxt, npages), dim3(WG), 0, s, pages, vlen, cap, maxt, tsum, offsets, res);
+    hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, cap, maxt, tsum, res);
+    hipLaunchKernelGGL(k_ba_copy, dim3(maxt, npages), dim3(WG), 0, s, blob, pages, vsrc, vlen, cap, maxt, tsum,
+                       offsets, out, res);
+  }
   if (has_dba)
     hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, vsrc, vlen, vpre,
                        cap, offsets, out, res);

@@ -48,7 +48,8 @@ hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint
 hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
                                    uint32_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, bool, uint64_t*, uint32_t*,
-                            uint32_t*, uint64_t, int64_t*, uint8_t*, ChunkResult*, hipStream_t);
+                            uint32_t*, uint64_t, int64_t*, uint8_t*, uint64_t, uint64_t*, ChunkResult*,
+                            hipStream_t);
 hipError_t pqg_launch_badict_expand(const uint8_t*, uint64_t, PageWork*, uint32_t, RunTables, int,
                                     uint64_t*, uint32_t*, uint64_t*, uint32_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_tile_desc(const uint8_t*, PageWork*, uint32_t, const uint32_t*, RunTables,
@@ -72,6 +73,8 @@ struct Slot {
   uint64_t* vsrc = nullptr;
   uint32_t* vlen = nullptr;
   uint32_t* vpre = nullptr;
+  uint64_t* tsum = nullptr;  // BYTE_ARRAY copy: per page and tile of 4096 values, bytes then start
+  size_t tsumcap = 0;
   size_t vcap = 0;
   uint64_t* dsrc = nullptr;
   uint32_t* dlen = nullptr;
@@ -228,6 +231,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.vsrc);
     hipFree(sl.vlen);
     hipFree(sl.vpre);
+    hipFree(sl.tsum);
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
     hipFree(sl.tile_page);
@@ -489,6 +493,14 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       HIPCHK(hipMalloc(&sl.vpre, need * 4), "hipMalloc vpre");
       sl.vcap = need;
     }
+    const size_t tneed = (size_t)np * ((max_page_vals + 4095) / 4096) + 1;
+    if (tneed > sl.tsumcap) {
+      hipFree(sl.tsum);
+      sl.tsum = nullptr;
+      sl.tsumcap = 0;
+      HIPCHK(hipMalloc(&sl.tsum, tneed * 8), "hipMalloc byte-array tiles");
+      sl.tsumcap = tneed;
+    }
     size_t dn = dict_page >= 0 && pages[dict_page].num_values ? pages[dict_page].num_values : 1;
     if (dn > sl.dcap) {
       hipFree(sl.dsrc);
@@ -626,8 +638,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       HIPCHK(pqg_launch_page_counts(ctx->d_pages, np, sl.rt[2], 1, s), "dictionary byte counts");
     }
     HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, tl, enc_present[PQG_DELTA_BYTE_ARRAY],
-                            sl.vsrc, sl.vlen, sl.vpre, out->values_capacity, out->offsets, vo,
-                            ctx->d_res, s),
+                            sl.vsrc, sl.vlen, sl.vpre, out->values_capacity, out->offsets, vo, max_page_vals,
+                            sl.tsum, ctx->d_res, s),
            "byte arrays");
   } else if (np && vo) {
     if (enc_present[PQG_PLAIN]) {
