@@ -146,6 +146,13 @@ int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
 /* Wait for the last decode and report its status. On error *first_bad_page names the
  * lowest page index that failed (the page the reference would fail on first). */
 int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
+/* Record assembly on the device (the layout TypedTripletIter builds per batch,
+ * record/triplet.rs:300-318, over a whole decoded chunk): spaced[i] = the value of level i when
+ * def_levels[i] == max_def (values = the decode's dense fixed-width values, value_size 1 / 4 / 8
+ * / 12 bytes), zero bytes otherwise. All pointers are device memory; enqueued on `stream`
+ * (NULL: the ctx's stream) after the decode that produced them. */
+int pqg_space_values(pqg_ctx *ctx, const int16_t *def_levels, uint64_t num_levels, int16_t max_def,
+                     const void *values, int value_size, void *spaced, void *stream);
 /* Averages over all decodes since pqg_reset_timings (timing must be enabled). */
 int pqg_get_timings(pqg_ctx *ctx, pqg_timings *t);
 int pqg_reset_timings(pqg_ctx *ctx);
@@ -186,6 +193,23 @@ void pqg_column_reader_close(pqg_column_reader *cr);
 int pqg_column_reader_read_batch(pqg_column_reader *cr, size_t batch_size, int16_t *def,
                                  int16_t *rep, void *values, uint64_t values_bytes_cap,
                                  uint32_t *lengths, size_t *values_read, size_t *levels_read);
+
+/* Record assembly's leaf iterator: TypedTripletIter (record/triplet.rs:168-330) over a column
+ * reader. read_next (triplet.rs:270-294) advances one (definition level, repetition level,
+ * value) triplet, refilling `batch_size` levels at a time through read_batch and spacing the
+ * values onto the levels whose def == max_def (:300-318); *has_next = 0 when none is left.
+ * def/rep levels of a column without them read as its max level (:246-262). value copies the
+ * current value (BYTE_ARRAY/FLBA: its bytes; *len set) and returns PQG_ERR_PANIC on a null
+ * slot, where the reference asserts (:236-243). The reader must outlive the iterator. */
+typedef struct pqg_triplet_iter pqg_triplet_iter;
+int pqg_triplet_iter_open(pqg_column_reader *cr, size_t batch_size, pqg_triplet_iter **out);
+void pqg_triplet_iter_close(pqg_triplet_iter *it);
+int pqg_triplet_iter_read_next(pqg_triplet_iter *it, int *has_next);
+int pqg_triplet_iter_has_next(pqg_triplet_iter *it);
+int16_t pqg_triplet_iter_def_level(pqg_triplet_iter *it);
+int16_t pqg_triplet_iter_rep_level(pqg_triplet_iter *it);
+int pqg_triplet_iter_is_null(pqg_triplet_iter *it);
+int pqg_triplet_iter_value(pqg_triplet_iter *it, void *out, size_t cap, size_t *len);
 
 #ifdef __cplusplus
 }

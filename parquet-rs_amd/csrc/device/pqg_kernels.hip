@@ -582,4 +582,110 @@ hipError_t pqg_launch_finalize(PageWork* pages, ChunkResult* res, hipStream_t s)
 
 }  // extern "C"
 
+// ------------------------------------------------------------------------------ spacing
+// Record assembly on the device: the layout TypedTripletIter builds batch by batch
+// (record/triplet.rs:300-318), over a whole decoded chunk. Slot i of `spaced` receives dense
+// value k(i) = the number of levels before i with def == max_def when def[i] == max_def, zero
+// bytes otherwise. Tiles of SP_T levels: counts, one exclusive scan, scatter.
+constexpr uint32_t SP_VPT = 16;
+constexpr uint32_t SP_T = SP_VPT * WG;
+
+__global__ void __launch_bounds__(WG) k_space_count(const int16_t* __restrict__ def, uint64_t n, int16_t max_def,
+                                                    uint64_t* __restrict__ tcount) {
+  __shared__ uint64_t red[WG / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SP_T + (uint64_t)threadIdx.x * SP_VPT;
+  uint64_t c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SP_VPT; ++k) c += (i0 + k < n && def[i0 + k] == max_def) ? 1u : 0u;
+  const uint64_t t = block_sum_u64(c, red);
+  if (threadIdx.x == 0) tcount[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(WG) k_space_scan(uint64_t* __restrict__ tcount, uint32_t ntiles) {
+  __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint64_t carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < ntiles; b += WG) {
+    const uint32_t t = b + threadIdx.x;
+    const uint64_t x = t < ntiles ? tcount[t] : 0;
+    uint64_t incl = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d, 64);
+      if ((threadIdx.x & 63) >= (unsigned)d) incl += y;
+    }
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint64_t pre = carry_s;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
+    if (t < ntiles) tcount[t] = pre + incl - x;
+    __syncthreads();
+    if (threadIdx.x == WG - 1) carry_s = pre + incl;
+    __syncthreads();
+  }
+}
+
+template <int ES>
+__global__ void __launch_bounds__(WG) k_space_scatter(const int16_t* __restrict__ def, uint64_t n, int16_t max_def,
+                                                      const uint8_t* __restrict__ values,
+                                                      const uint64_t* __restrict__ tbase,
+                                                      uint8_t* __restrict__ spaced) {
+  __shared__ uint64_t wsum[WG / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SP_T + (uint64_t)threadIdx.x * SP_VPT;
+  uint32_t m = 0;  // max_def flags of this thread's levels
+#pragma unroll
+  for (uint32_t k = 0; k < SP_VPT; ++k) m |= (i0 + k < n && def[i0 + k] == max_def ? 1u : 0u) << k;
+  const uint64_t c = (uint64_t)__builtin_popcount(m);
+  uint64_t incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if ((threadIdx.x & 63) >= (unsigned)d) incl += y;
+  }
+  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  uint64_t k = tbase[blockIdx.x] + incl - c;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) k += wsum[w];
+#pragma unroll
+  for (uint32_t q = 0; q < SP_VPT; ++q) {
+    const uint64_t i = i0 + q;
+    if (i >= n) break;
+    uint8_t* o = spaced + i * ES;
+    if ((m >> q) & 1u) {
+      const uint8_t* v = values + k * ES;
+      if constexpr (ES == 1) *o = *v;
+      else if constexpr (ES == 4) *reinterpret_cast<uint32_t*>(o) = *reinterpret_cast<const uint32_t*>(v);
+      else if constexpr (ES == 8) *reinterpret_cast<uint64_t*>(o) = *reinterpret_cast<const uint64_t*>(v);
+      else
+        for (int b = 0; b < ES; b += 4) *reinterpret_cast<uint32_t*>(o + b) = *reinterpret_cast<const uint32_t*>(v + b);
+      ++k;
+    } else {
+      for (int b = 0; b < ES; ++b) o[b] = 0;
+    }
+  }
+}
+
+extern "C" {
+
+hipError_t pqg_launch_space(const int16_t* def, uint64_t n, int16_t max_def, const void* values, int es,
+                            uint64_t* tiles, void* spaced, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nt = (uint32_t)((n + SP_T - 1) / SP_T);
+  hipLaunchKernelGGL(k_space_count, dim3(nt), dim3(WG), 0, s, def, n, max_def, tiles);
+  hipLaunchKernelGGL(k_space_scan, dim3(1), dim3(WG), 0, s, tiles, nt);
+  const uint8_t* v = (const uint8_t*)values;
+  uint8_t* o = (uint8_t*)spaced;
+  switch (es) {
+    case 1: hipLaunchKernelGGL(k_space_scatter<1>, dim3(nt), dim3(WG), 0, s, def, n, max_def, v, tiles, o); break;
+    case 4: hipLaunchKernelGGL(k_space_scatter<4>, dim3(nt), dim3(WG), 0, s, def, n, max_def, v, tiles, o); break;
+    case 8: hipLaunchKernelGGL(k_space_scatter<8>, dim3(nt), dim3(WG), 0, s, def, n, max_def, v, tiles, o); break;
+    case 12: hipLaunchKernelGGL(k_space_scatter<12>, dim3(nt), dim3(WG), 0, s, def, n, max_def, v, tiles, o); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // extern "C"
+
 }  // namespace pqg

@@ -42,6 +42,7 @@ hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
+hipError_t pqg_launch_space(const int16_t*, uint64_t, int16_t, const void*, int, uint64_t*, void*, hipStream_t);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
                                   DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t,
                                   hipEvent_t*);
@@ -128,6 +129,8 @@ struct pqg_ctx {
   int host_status = 0;
   int host_bad_page = -1;
   uint32_t values_kernel = 0;
+  uint64_t* sp_tiles = nullptr;  // pqg_space_values: per tile of levels, max_def count then base
+  size_t sp_cap = 0;
   pqg_output* out = nullptr;
   uint64_t total_levels = 0;
   std::string msg;
@@ -255,6 +258,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     }
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
+  hipFree(ctx->sp_tiles);
   delete ctx;
   return PQG_OK;
 }
@@ -706,6 +710,26 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   sl.used = true;
   ctx->pending = true;
   return PQG_OK;
+}
+
+// Device-side record assembly of a decoded chunk (pqg_launch_space, device/pqg_kernels.hip).
+int pqg_space_values(pqg_ctx* ctx, const int16_t* def_levels, uint64_t num_levels, int16_t max_def,
+                     const void* values, int value_size, void* spaced, void* stream) {
+  if (!ctx || (num_levels && (!def_levels || !spaced || (!values && max_def >= 0))) ||
+      (value_size != 1 && value_size != 4 && value_size != 8 && value_size != 12))
+    return PQG_ERR_INVALID;
+  if (num_levels == 0) return PQG_OK;
+  const size_t nt = (size_t)((num_levels + 4095) / 4096);
+  if (nt > ctx->sp_cap) {
+    hipFree(ctx->sp_tiles);
+    ctx->sp_tiles = nullptr;
+    ctx->sp_cap = 0;
+    if (hipMalloc(&ctx->sp_tiles, nt * 8) != hipSuccess) return set_err(ctx, PQG_ERR_HIP, "hipMalloc spacing tiles");
+    ctx->sp_cap = nt;
+  }
+  const hipError_t e = pqg_launch_space(def_levels, num_levels, max_def, values, value_size, ctx->sp_tiles, spaced,
+                                        stream ? (hipStream_t)stream : ctx->stream);
+  return e == hipSuccess ? PQG_OK : set_err(ctx, PQG_ERR_HIP, "spacing launch: %s", hipGetErrorString(e));
 }
 
 int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {

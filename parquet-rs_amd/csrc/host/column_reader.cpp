@@ -313,3 +313,127 @@ int pqg_column_reader_read_batch(pqg_column_reader* cr, size_t batch_size, int16
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- triplets
+// TypedTripletIter (record/triplet.rs:168-330) over a column reader: `batch_size` levels at a
+// time through read_batch, values spaced onto the level slots whose def == max_def. The
+// reference moves the dense values into place with swaps (triplet.rs:300-318); here slot i
+// reads dense value k(i) = the count of max_def levels before it, the same triplets.
+struct pqg_triplet_iter {
+  pqg_column_reader* cr = nullptr;
+  size_t batch = 0;
+  std::vector<int16_t> def, rep;
+  std::vector<uint8_t> vals;      // dense values of the batch (fixed width or BYTE_ARRAY bytes)
+  std::vector<uint32_t> lens;     // BYTE_ARRAY lengths
+  std::vector<uint64_t> slot;     // per triplet: dense value index, ~0 for a null slot
+  std::vector<uint64_t> boff;     // BYTE_ARRAY: byte offset of each dense value
+  size_t cur = 0, left = 0;
+  bool has_next = false;
+};
+
+extern "C" {
+
+int pqg_triplet_iter_open(pqg_column_reader* cr, size_t batch_size, pqg_triplet_iter** out) {
+  if (!cr || !out || batch_size == 0) return PQG_ERR_INVALID;
+  auto it = std::make_unique<pqg_triplet_iter>();
+  it->cr = cr;
+  it->batch = batch_size;
+  if (cr->col.max_def > 0) it->def.resize(batch_size);
+  if (cr->col.max_rep > 0) it->rep.resize(batch_size);
+  it->slot.resize(batch_size);
+  if (cr->is_ba) {
+    it->lens.resize(batch_size);
+    it->boff.resize(batch_size + 1);
+  } else {
+    it->vals.resize(batch_size * (size_t)cr->es + 16);
+  }
+  *out = it.release();
+  return PQG_OK;
+}
+
+void pqg_triplet_iter_close(pqg_triplet_iter* it) { delete it; }
+
+int pqg_triplet_iter_read_next(pqg_triplet_iter* it, int* has_next) {
+  if (!it || !has_next) return PQG_ERR_INVALID;
+  *has_next = 0;
+  it->cur += 1;
+  if (it->cur < it->left) {
+    *has_next = it->has_next = true;
+    return PQG_OK;
+  }
+  pqg_column_reader* cr = it->cr;
+  size_t vr = 0, lr = 0;
+  int st;
+  if (cr->is_ba) {
+    // the batch's bytes: at most the chunk's remaining bytes
+    const uint64_t cap = (uint64_t)cr->offsets[cr->total_values] - (uint64_t)cr->offsets[cr->V] + 1;
+    if (it->vals.size() < cap) it->vals.resize(cap);
+    st = pqg_column_reader_read_batch(cr, it->batch, it->def.empty() ? nullptr : it->def.data(),
+                                      it->rep.empty() ? nullptr : it->rep.data(), it->vals.data(),
+                                      it->vals.size(), it->lens.data(), &vr, &lr);
+  } else {
+    st = pqg_column_reader_read_batch(cr, it->batch, it->def.empty() ? nullptr : it->def.data(),
+                                      it->rep.empty() ? nullptr : it->rep.data(), it->vals.data(),
+                                      it->vals.size(), nullptr, &vr, &lr);
+  }
+  if (st != PQG_OK) return st;
+  if (vr == 0 && lr == 0) {  // no more values or levels
+    it->has_next = false;
+    return PQG_OK;
+  }
+  if (cr->is_ba) {
+    it->boff[0] = 0;
+    for (size_t k = 0; k < vr; ++k) it->boff[k + 1] = it->boff[k] + it->lens[k];
+  }
+  if (lr == 0 || vr == lr) {  // required column, or every level holds a value
+    for (size_t i = 0; i < vr; ++i) it->slot[i] = i;
+    it->left = vr;
+  } else if (vr < lr) {       // spacing (triplet.rs:300-318)
+    size_t k = 0;
+    for (size_t i = 0; i < lr; ++i) it->slot[i] = it->def[i] == cr->col.max_def ? k++ : ~0ull;
+    it->left = lr;
+  } else {
+    cr->err = "Spacing of values/levels is wrong, values_read: " + std::to_string(vr) +
+              ", levels_read: " + std::to_string(lr);
+    return PQG_ERR_GENERAL;
+  }
+  it->cur = 0;
+  *has_next = it->has_next = true;
+  return PQG_OK;
+}
+
+int pqg_triplet_iter_has_next(pqg_triplet_iter* it) { return it && it->has_next ? 1 : 0; }
+
+int16_t pqg_triplet_iter_def_level(pqg_triplet_iter* it) {
+  return it->def.empty() ? it->cr->col.max_def : it->def[it->cur];
+}
+
+int16_t pqg_triplet_iter_rep_level(pqg_triplet_iter* it) {
+  return it->rep.empty() ? it->cr->col.max_rep : it->rep[it->cur];
+}
+
+int pqg_triplet_iter_is_null(pqg_triplet_iter* it) {
+  return pqg_triplet_iter_def_level(it) < it->cr->col.max_def ? 1 : 0;
+}
+
+int pqg_triplet_iter_value(pqg_triplet_iter* it, void* out, size_t cap, size_t* len) {
+  if (!it || !it->has_next || !len) return PQG_ERR_INVALID;
+  // "Cannot extract value, max definition level: ..., current level: ..." (triplet.rs:236-243)
+  if (pqg_triplet_iter_def_level(it) != it->cr->col.max_def) return PQG_ERR_PANIC;
+  const uint64_t k = it->slot[it->cur];
+  const uint8_t* src;
+  size_t n;
+  if (it->cr->is_ba) {
+    src = it->vals.data() + it->boff[k];
+    n = it->lens[k];
+  } else {
+    n = (size_t)it->cr->es;
+    src = it->vals.data() + k * n;
+  }
+  *len = n;
+  if (n > cap) return PQG_ERR_CAPACITY;
+  if (out && n) memcpy(out, src, n);
+  return PQG_OK;
+}
+
+}  // extern "C"

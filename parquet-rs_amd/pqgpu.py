@@ -63,7 +63,10 @@ EXPORTS = [
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
     "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
-    "pqg_column_reader_read_batch",
+    "pqg_column_reader_read_batch", "pqg_triplet_iter_open", "pqg_triplet_iter_close",
+    "pqg_triplet_iter_read_next", "pqg_triplet_iter_has_next", "pqg_triplet_iter_def_level",
+    "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
+    "pqg_space_values",
 ]
 
 _lib = None
@@ -108,6 +111,16 @@ def lib():
         L.pqg_column_reader_close.restype = None
         L.pqg_column_reader_read_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, u64, vp,
                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        L.pqg_triplet_iter_open.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
+        L.pqg_triplet_iter_close.argtypes = [vp]
+        L.pqg_triplet_iter_read_next.argtypes = [vp, C.POINTER(C.c_int)]
+        for f in ("has_next", "is_null"):
+            getattr(L, "pqg_triplet_iter_" + f).argtypes = [vp]
+        for f in ("def_level", "rep_level"):
+            getattr(L, "pqg_triplet_iter_" + f).argtypes = [vp]
+            getattr(L, "pqg_triplet_iter_" + f).restype = C.c_int16
+        L.pqg_triplet_iter_value.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.pqg_space_values.argtypes = [vp, vp, u64, C.c_int16, vp, i32, vp, vp]
         _lib = L
     return _lib
 
@@ -373,3 +386,66 @@ class ColumnReader:
             values = raw.reshape(-1, 12) if t == INT96 else raw.view(NP_DTYPE[t])
         return (values, d[:nl] if d is not None else None, r[:nl] if r is not None else None,
                 nv, nl)
+
+
+class TripletIter:
+    """TypedTripletIter (record/triplet.rs:168-330) over a ColumnReader: read_next() advances one
+    (definition level, repetition level, value) triplet; values are spaced onto the levels whose
+    def == max_def. current_value() raises (the reference asserts) on a null slot."""
+
+    def __init__(self, reader, batch_size=1024):
+        self.reader = reader  # kept alive: the iterator reads through it
+        self.col = reader.col
+        h = C.c_void_p()
+        st = lib().pqg_triplet_iter_open(reader.h, batch_size, C.byref(h))
+        if st:
+            raise PqgError(st, "pqg_triplet_iter_open failed")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pqg_triplet_iter_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def read_next(self):
+        hn = C.c_int(0)
+        st = lib().pqg_triplet_iter_read_next(self.h, C.byref(hn))
+        if st:
+            raise PqgError(st, self.reader.fr.error())
+        return bool(hn.value)
+
+    def has_next(self):
+        return bool(lib().pqg_triplet_iter_has_next(self.h))
+
+    def current_def_level(self):
+        return int(lib().pqg_triplet_iter_def_level(self.h))
+
+    def current_rep_level(self):
+        return int(lib().pqg_triplet_iter_rep_level(self.h))
+
+    def is_null(self):
+        return bool(lib().pqg_triplet_iter_is_null(self.h))
+
+    def current_value(self):
+        """bytes for BYTE_ARRAY/FLBA, else the value in the reference's numpy layout."""
+        n = C.c_size_t(0)
+        buf = np.zeros(16, np.uint8)
+        st = lib().pqg_triplet_iter_value(self.h, buf.ctypes.data, buf.nbytes, C.byref(n))
+        if st == CAPACITY:
+            buf = np.zeros(n.value, np.uint8)
+            st = lib().pqg_triplet_iter_value(self.h, buf.ctypes.data, buf.nbytes, C.byref(n))
+        if st:
+            raise PqgError(st, "current_value on a triplet below the max definition level")
+        raw = buf[: n.value]
+        t = self.col.physical_type
+        if t in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY):
+            return raw.tobytes()
+        if t == INT96:
+            return raw.copy()
+        return raw.view(NP_DTYPE[t])[0]

@@ -94,3 +94,38 @@ def test_gpu_malformed_dictionary_file(ctx):
             read_all(cr, 7)
         except pqgpu.PqgError as e:
             assert 1 <= e.status <= 7
+
+
+@pytest.mark.parametrize("fname,path,values,defs,reps", TRIPLET_KATS)
+@pytest.mark.parametrize("batch", [1, 2, 3, 5, 7, 10, 128, 256])
+def test_gpu_triplet_iter_kats(ctx, fname, path, values, defs, reps, batch):
+    """TypedTripletIter over the GPU-decoded chunk (record/triplet.rs:270-318, tests :442-456):
+    the triplet sequence is the KAT's levels, values sit on the max_def slots, and reading a
+    value on a null slot is refused as the reference asserts."""
+    import pqgpu
+    fr = pqgpu.FileReader(os.path.join(DATA, fname))
+    j = _col_index(fname, path)
+    c = MANIFEST[fname]["columns"][j]
+    cr = fr.column_reader(0, j, ctx)
+    it = pqgpu.TripletIter(cr, batch)
+    got_d, got_r, got_v = [], [], []
+    while it.read_next():
+        d, r = it.current_def_level(), it.current_rep_level()
+        got_d.append(d)
+        got_r.append(r)
+        if d == c["max_def"]:
+            v = it.current_value()
+            got_v.append(v if isinstance(v, bytes) else int(v))
+        else:
+            assert it.is_null()
+            with pytest.raises(pqgpu.PqgError):
+                it.current_value()
+    assert not it.has_next()
+    if c["max_def"] > 0:
+        assert got_d == list(defs)
+    if c["max_rep"] > 0:
+        assert got_r == list(reps)
+    if values:
+        assert got_v == [v if isinstance(v, bytes) else int(v) for v in values]
+    it.close()
+    cr.close()

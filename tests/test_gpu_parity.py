@@ -301,3 +301,32 @@ def test_large_chunk_properties(oracle, ctx):
     assert got["status"] == 0, got["message"]
     np.testing.assert_array_equal(got["def"], np.concatenate(exp_def))
     np.testing.assert_array_equal(got["values"], np.concatenate(exp_val))
+
+
+@pytest.mark.parametrize("ptype,dtype", [(None, np.int32), ("int64", np.int64), ("int96", None), ("bool", None)])
+def test_space_values_matches_levels(oracle, ctx, ptype, dtype):
+    """pqg_space_values: the decoded dense values spread onto the def == max_def level slots,
+    zeros elsewhere (record/triplet.rs:300-318 over a whole chunk)."""
+    import torch
+
+    import pqgpu
+    rng = np.random.default_rng(7)
+    n = 300_000
+    t = {None: oracle.INT32, "int64": oracle.INT64, "int96": oracle.INT96, "bool": oracle.BOOLEAN}[ptype]
+    es = {oracle.INT32: 4, oracle.INT64: 8, oracle.INT96: 12, oracle.BOOLEAN: 1}[t]
+    d = (rng.random(n) > 0.3).astype(np.int16)
+    nn = int(d.sum())
+    raw = rng.integers(0, 256, size=nn * es, dtype=np.uint8)
+    if t == oracle.BOOLEAN:
+        raw = (raw & 1).astype(np.uint8)
+    dev = torch.device("cuda")
+    d_def = torch.from_numpy(d).to(dev)
+    d_val = torch.from_numpy(raw).to(dev)
+    d_sp = torch.full((n * es + 16,), 0x5A, dtype=torch.uint8, device=dev)
+    st = pqgpu.lib().pqg_space_values(ctx.h, d_def.data_ptr(), n, 1, d_val.data_ptr(), es, d_sp.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    got = d_sp[: n * es].cpu().numpy().reshape(n, es)
+    want = np.zeros((n, es), np.uint8)
+    want[d == 1] = raw.reshape(nn, es)
+    np.testing.assert_array_equal(got, want)
