@@ -68,13 +68,19 @@ __device__ inline int64_t v1_level_stream(const uint8_t* page, uint32_t nbytes, 
   return -1;  // LevelDecoder::v1 panics on other encodings (levels.rs:170)
 }
 
-__global__ void k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                          PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                          uint32_t* __restrict__ tile_page, ChunkResult* res) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per page: the lanes fill the page's tile -> page entries (a dictionary column's
+// single data page has thousands), lane 0 the rest.
+__global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                PageWork* __restrict__ pages, int npages, ColumnParams cp,
+                                                uint32_t* __restrict__ tile_page, ChunkResult* res) {
+  const int p = blockIdx.x;
   if (p >= npages) return;
+  {
+    const uint32_t t0 = pages[p].ltile0, nt = pages[p].ntiles;
+    for (uint32_t k = threadIdx.x; k < nt; k += 64) tile_page[t0 + k] = (uint32_t)p;
+  }
+  if (threadIdx.x != 0) return;
   PageWork pw = pages[p];
-  for (uint32_t k = 0; k < pw.ntiles; ++k) tile_page[pw.ltile0 + k] = (uint32_t)p;
   const int32_t host_status = pw.status;  // set by the host for pages the reference rejects
   pw.rep_kind = pw.def_kind = LK_NONE;
   pw.rep_off = pw.rep_bytes = pw.def_off = pw.def_bytes = 0;
@@ -441,8 +447,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                               int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
                               hipStream_t s) {
-  hipLaunchKernelGGL(k_prepare, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, blob_len,
-                     pages, npages, cp, tile_page, res);
+  hipLaunchKernelGGL(k_prepare, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, npages, cp, tile_page, res);
   return hipGetLastError();
 }
 

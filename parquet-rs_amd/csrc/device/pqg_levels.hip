@@ -21,8 +21,9 @@
 //                chain leaves the window and how many outputs it produces on the way. The
 //                answers for the positions a chain can enter at (the first 64 * w bytes: a
 //                header plus at most 63 bit-packed groups) go to a table.
-//     k_lv_stitch one wave per page: follows the window tables from offset 0 (one lookup per
-//                window) to each window's true entry and first output.
+//     k_lv_stitch one workgroup per page: follows the window tables from offset 0 (one lookup per
+//                window, the tables streamed through LDS) to each window's true entry and first
+//                output.
 //     k_lv_emit  one wave per window: pointer jumping again, now marking the positions reachable
 //                from the true entry (the window's true headers), which are parsed in parallel
 //                and placed by a wave scan into the window's run list.
@@ -203,13 +204,13 @@ __device__ inline uint32_t lv_page_of(const uint32_t* __restrict__ wbase, uint32
   return lo;
 }
 
-// Streams this path takes. Dictionary indices only up to 4 bits: wider index streams are runs
-// of ~64 * w bytes, too far apart for the segment starts' chains to meet within two windows, and
-// the general decoder's streaming index pass serves them better.
+// Streams this path takes (wide streams: k_lv_bound's wide mode finds their segment starts).
+// Dictionary indices up to cp.dict_maxw bits: wider indices into 4- / 8-byte values (a large
+// dictionary, its gathers served from L2) expand faster through the general decoder's tiles.
 __device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int sel, const ColumnParams& cp,
                                  Stream& s) {
   return get_stream(blob, pw, sel, cp, s) && pw.status == 0 && !s.err && s.kind == LK_RLE &&
-         lv_width_ok((uint32_t)s.w) && (sel != SS_DICT || s.w <= 4);
+         lv_width_ok((uint32_t)s.w) && (sel != SS_DICT || (uint32_t)s.w <= cp.dict_maxw);
 }
 
 // Hand page p to the general decoder (once).
@@ -386,10 +387,18 @@ __device__ inline bool lv_seg_of(const uint8_t* blob, const PageWork* pages, uin
 // rle.rs:48-50), the one most chains share is taken — chains entering on payload bytes that do
 // not meet the true chain mostly jump far away. The walk of the segment before verifies the
 // choice by landing on it exactly.
+// Wide streams (w > 4: dictionary indices, mostly bit-packed runs of 1 + 63w bytes) give chains
+// entering at different offsets little chance to meet: there every hop of a chain must be of the
+// writer's form (a one-byte header of <= 63 groups, or an RLE value that fits w bits) and the
+// chains are walked over LB_SPANW bytes (~8 headers at w = 16), so that a chain entering on
+// payload bytes rarely survives (~1/4 per hop) and the true chain's exit is the one left.
 constexpr uint32_t LB_SPAN = 2 * LV_WIN;         // bytes walked from the segment start
-constexpr uint32_t LB_STG = LB_SPAN + 64;        // staged bytes
+constexpr uint32_t LB_SPANW = 8 * LV_WIN;        // the same for wide streams
+constexpr uint32_t LB_STG = LB_SPANW + 64;       // staged bytes
 constexpr uint32_t LB_HOPS = 128;                // headers per chain at most
 constexpr uint32_t LB_BINS = 8 + 64 * 16;        // exits one writer-form hop can reach past the span
+constexpr uint32_t LB_PER = 7;                   // wide streams: full bit-packed runs in a row that
+                                                 // place the true chain
 
 __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                  const PageWork* __restrict__ pages, int npages, ColumnParams cp,
@@ -406,11 +415,35 @@ __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blo
     if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, s, x.p, j, x.s) || j == 0) continue;
     x.k = j * lw_segw((uint32_t)x.s.w);
     x.W0 = x.k * LV_WIN;
-    lv_stage(blob, blob_len, x, st, LB_STG / 16);
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
+    const bool wide = w > 4;
+    const uint32_t span = min(wide ? LB_SPANW : LB_SPAN, slen - x.W0);  // walked bytes (the stream may end first)
+    lv_stage(blob, blob_len, x, st, (span + 64u) / 16u);
     const uint32_t ent = lv_ent(w);
-    const uint32_t span = min(LB_SPAN, slen - x.W0);  // walked bytes (the stream may end first)
     const uint32_t near = span + 8u + 64u * w;
+    if (wide) {
+      // the writer's full bit-packed runs (header 0x7F, then 63 groups: P bytes apart): an offset
+      // of the first period whose next LB_PER headers all are is on the true chain (a chain of
+      // payload bytes matching LB_PER times has odds 2^-8 each)
+      const uint32_t P = 1u + 63u * w;
+      uint32_t hit = 0xFFFFFFFFu;
+      if ((LB_PER - 1u) * P + P + 1u <= span) {
+        for (uint32_t q0 = 0; q0 < P && hit == 0xFFFFFFFFu; q0 += WAVE) {
+          const uint32_t o = q0 + lane;
+          bool all = o < P;
+          for (uint32_t h = 0; h < LB_PER && all; ++h) {
+            const uint32_t r = o + h * P + x.sb;
+            all = ((st[r >> 2] >> (8u * (r & 3u))) & 0xFFu) == 0x7Fu;
+          }
+          hit = wave_min_u32(all ? o : 0xFFFFFFFFu);
+        }
+      }
+      if (hit != 0xFFFFFFFFu) {
+        if (lane == 0) lt.bexit[s] = x.W0 + hit;
+        wave_lds_sync();  // the stage is refilled by the next segment
+        continue;
+      }
+    }
     uint32_t ex[LV_PPL];
 #pragma unroll
     for (uint32_t q = 0; q < LV_PPL; ++q) {
@@ -426,6 +459,7 @@ __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blo
           const uint32_t o2 = nx - x.W0;
           // a hop out of the first window must be one of the writer's form as well
           if (o < LV_WIN && o2 >= LV_WIN + 8u + 64u * w) ok = false;
+          if (wide && (bp ? c > 504u : (v >> w) != 0u)) ok = false;
           o = o2;
         }
       }
@@ -527,6 +561,7 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
   next_stop();
   uint32_t* st = stg[wid];
   const uint32_t slen = s.slen, w = (uint32_t)s.w, vb = (w + 7u) >> 3;
+  const bool ffw = w >= 4;  // fast-forward over full bit-packed runs (>= 253 bytes each)
   uint2* rec = lt.srec + (uint64_t)sidx * LW_SCAP;
   uint32_t* pos = lt.spos + (uint64_t)sidx * LW_SCAP;
   uint32_t cur = start, nr = 0, loaded = 0xFFFFFFFFu, sb = 0, lastpos = 0xFFFFFFFFu, status = 0, tv = 0, tc = 0;
@@ -570,8 +605,27 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
       status = LS_END;
       break;
     }
+    uint32_t k = 0, posv = 0;
+    const uint32_t c0 = cur;
+    bool dead = false;
+    if (ffw) {
+      // wide streams: the writer's full bit-packed runs (header 0x7F, P bytes each) in one step —
+      // lane l reads the header byte P * l past cur; the matching prefix is the chain's next
+      // headers (each 0x7F header puts the next one exactly P bytes on)
+      const uint32_t P = 1u + 63u * w;
+      const uint32_t lim = min(slen, stop);
+      const uint32_t q = cur + lane * P;
+      const bool hit = q < lim && blob[s.S + q] == 0x7Fu;
+      const uint64_t m = __ballot(hit);
+      const uint32_t run = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u;
+      if (run >= 2u) {
+        k = run;
+        posv = q;
+        cur = rfl(cur + run * P);
+      }
+    }
     const uint32_t r = cur / LW_REG;
-    if (r != loaded) {
+    if (k == 0 && r != loaded) {
       if (r != fetched) fetch(r);
 #pragma unroll
       for (uint32_t q = 0; q < LW_CH; ++q) {
@@ -600,33 +654,33 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
       LW_STAMP(t_reg);
     }
     const uint32_t rb = rfl(r * LW_REG);
-    const uint32_t lim = rfl(min(min(rb + LW_REG, slen), stop));
-    // hop loop (wave-uniform): up to 64 headers. One-byte headers take lv_hops (scalar loop
-    // over the hop-length table, positions as LDS addresses of their table entries); any other
-    // header the general parse.
-    uint32_t k = 0, posv = 0;
-    const uint32_t c0 = cur;
-    const uint32_t ab = rfl(lb + 2u * (sb - rb));  // LDS address of stream offset 0's entry (mod 2^32)
-    uint32_t addr = ab + 2u * cur;
-    const uint32_t alim = ab + 2u * lim;
-    bool dead = false;
-    while (true) {
-      lv_hops(addr, alim, k, posv);
-      if (addr >= alim || k == 64u) break;
-      const uint32_t q = (addr - ab) >> 1;  // stream offset of a header whose hop is not in the table
-      uint32_t nxt, v, cnt;
-      bool bp;
-      const bool ok = lv_parse4(st, q - rb + sb, q, slen, w, vb, nxt, cnt, v, bp);
-      if (!rfl(ok ? 1u : 0u)) {
-        dead = true;
-        break;
+    const bool ffb = k != 0;  // this batch came from the fast-forward
+    if (!ffb) {
+      const uint32_t lim = rfl(min(min(rb + LW_REG, slen), stop));
+      // hop loop (wave-uniform): up to 64 headers. One-byte headers take lv_hops (scalar loop
+      // over the hop-length table, positions as LDS addresses of their table entries); any other
+      // header the general parse.
+      const uint32_t ab = rfl(lb + 2u * (sb - rb));  // LDS address of stream offset 0's entry (mod 2^32)
+      uint32_t addr = ab + 2u * cur;
+      const uint32_t alim = ab + 2u * lim;
+      while (true) {
+        lv_hops(addr, alim, k, posv);
+        if (addr >= alim || k == 64u) break;
+        const uint32_t q = (addr - ab) >> 1;  // stream offset of a header whose hop is not in the table
+        uint32_t nxt, v, cnt;
+        bool bp;
+        const bool ok = lv_parse4(st, q - rb + sb, q, slen, w, vb, nxt, cnt, v, bp);
+        if (!rfl(ok ? 1u : 0u)) {
+          dead = true;
+          break;
+        }
+        posv = lane == k ? addr : posv;
+        ++k;
+        addr += 2u * (rfl(nxt) - q);
       }
-      posv = lane == k ? addr : posv;
-      ++k;
-      addr += 2u * (rfl(nxt) - q);
+      cur = (addr - ab) >> 1;
+      posv = (posv - ab) >> 1;
     }
-    cur = (addr - ab) >> 1;
-    posv = (posv - ab) >> 1;
     LW_STAMP(t_hop);
 #ifdef PQG_DIAG
     nhops += k;
@@ -636,7 +690,15 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
       const bool act = lane < k;
       uint32_t nx, c = 0, v = 0;
       bool bp = false, okp = true;
-      if (act) okp = lv_parse4(st, posv - rb + sb, posv, slen, w, vb, nx, c, v, bp);
+      if (act) {
+        if (ffb) {  // a full bit-packed run
+          c = 504u;
+          v = posv + 1u;
+          bp = true;
+        } else {
+          okp = lv_parse4(st, posv - rb + sb, posv, slen, w, vb, nx, c, v, bp);
+        }
+      }
       const uint64_t ic = wave_incl_scan_cnt(act ? c : 0u);
       const uint64_t accb = acc + ic - (act ? c : 0u);
       if ((k == 64u && cur - c0 < LW_SPAN) || nr + k > LW_SCAP) {
@@ -854,40 +916,73 @@ __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob,
 }
 
 // ------------------------------------------------------------------------------ k_lv_stitch
-// One wave per dense page: the true entry and first output of every window of the page.
+// One workgroup per dense page: the true entry and first output of every window of the page.
+// One lane follows the window tables from offset 0 (one lookup per window); the tables come
+// through LDS in chunks of STC_ENT entries, the next chunk loaded by the other waves while the
+// walker is on the current one, so a step costs an LDS read instead of a global round trip.
+constexpr uint32_t STC_ENT = 4096;  // table entries per LDS buffer (>= 4 windows of any width)
+
 __global__ void __launch_bounds__(WG) k_lv_stitch(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
                                                   int npages, ColumnParams cp, int sel, RunTables rt,
                                                   LevelTables lt) {
-  const uint32_t p = blockIdx.x * (WG / WAVE) + rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  __shared__ uint2 buf[2][STC_ENT];
+  __shared__ uint32_t stop_s;
+  const uint32_t p = blockIdx.x, tid = threadIdx.x;
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   const PageWork& pw = pages[p];
   Stream s;
   if (!lv_stream(blob, pw, sel, cp, s)) return;
   const uint32_t k0 = lt.wbase[p], nw = lt.wbase[p + 1] - k0;
-  for (uint32_t k = lane; k < nw; k += WAVE) lt.win[k0 + k] = make_uint2(LV_NONE, 0u);
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the NONE marks land before the walk's writes
-  __builtin_amdgcn_wave_barrier();
-  if (lane != 0 || nw == 0) return;
-  const uint32_t ent = lv_ent((uint32_t)s.w), n = s.n;
-  uint32_t e = 0;
+  for (uint32_t k = tid; k < nw; k += WG) lt.win[k0 + k] = make_uint2(LV_NONE, 0u);
+  if (nw == 0) return;
+  const uint32_t ent = lv_ent((uint32_t)s.w), n = s.n, slen = s.slen;
+  const uint32_t CH = STC_ENT / ent, nch = (nw + CH - 1) / CH;
+  const uint2* tab = lt.tab + (uint64_t)k0 * ent;
+  auto load = [&](uint32_t c, uint2* b, uint32_t t0, uint32_t stride) {
+    const uint32_t cnt = min(CH, nw - c * CH) * ent;
+    const uint2* src = tab + (uint64_t)c * CH * ent;
+    for (uint32_t i = t0; i < cnt; i += stride) b[i] = src[i];
+  };
+  if (tid == 0) stop_s = 0;
+  load(0, buf[0], tid, WG);
+  __syncthreads();  // (also orders the NONE marks before the walker's writes)
+  uint32_t cur = 0, e = 0, ok = 0;  // walker (thread 0): next window on the chain, its entry
   uint64_t acc = 0;
-  bool ok = false;
-  while (true) {
-    if (e >= s.slen) break;  // the stream ends before n outputs
-    const uint32_t kk = e / LV_WIN, idx = e - kk * LV_WIN;
-    if (kk >= nw || idx >= ent) break;  // an entry past the table (foreign long runs)
-    const uint2 t = lt.tab[(uint64_t)(k0 + kk) * ent + idx];
-    lt.win[k0 + kk] = make_uint2(idx | (t.x & 0xFFFF0000u), (uint32_t)acc);  // entry | headers << 16
-    acc += t.y;
-    if (acc >= n) {
-      ok = true;
-      break;
+  for (uint32_t c = 0; c < nch; ++c) {
+    if (tid >= WAVE) {
+      if (c + 1 < nch) load(c + 1, buf[(c + 1) & 1], tid - WAVE, WG - WAVE);
+    } else if (tid == 0 && !stop_s) {
+      const uint2* b = buf[c & 1];
+      const uint32_t lo = c * CH, hi = min(nw, lo + CH);
+      uint32_t stop = 0;
+      while (cur < hi) {
+        const uint2 t = b[(cur - lo) * ent + e];
+        lt.win[k0 + cur] = make_uint2(e | (t.x & 0xFFFF0000u), (uint32_t)acc);  // entry | headers << 16
+        acc += t.y;
+        if (acc >= n) {
+          ok = 1;
+          stop = 1;
+          break;
+        }
+        const uint32_t jt = t.x & 0xFFFFu;
+        if (jt >= LV_J_FAR || t.y == 0xFFFFFFFFu) {  // far / end / dead, or a saturated count
+          stop = 1;
+          break;
+        }
+        const uint32_t q = cur * LV_WIN + jt;
+        cur = q / LV_WIN;
+        e = q - cur * LV_WIN;
+        if (q >= slen || cur >= nw || e >= ent) {  // the stream ends before n outputs, or an entry
+          stop = 1;                                // past the table (foreign long runs)
+          break;
+        }
+      }
+      if (stop) stop_s = 1;
     }
-    const uint32_t jt = t.x & 0xFFFFu;
-    if (jt >= LV_J_FAR || t.y == 0xFFFFFFFFu) break;  // far / end / dead, or a saturated count
-    e = kk * LV_WIN + jt;
+    __syncthreads();
+    if (stop_s) break;
   }
-  if (!ok) lv_bail(rt, p, PF_PAGE);
+  if (tid == 0 && !ok) lv_bail(rt, p, PF_PAGE);
 }
 
 // ------------------------------------------------------------------------------ output writers
@@ -1099,58 +1194,81 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
   const uint64_t k0 = lo / V, k1 = (hi + V - 1) / V;
   uint32_t lgn = 1;
   while (lgn * 2u <= rl.R) lgn *= 2u;
+  // U groups per lane per step: their indices first, then every gather, then the stores (the
+  // gathers of a step are in flight together)
+  constexpr uint32_t U = ES == 8 ? 8 : 4;
   uint32_t a = 0, bad = 0;
 #pragma unroll 1
-  for (uint64_t k = k0 + lane; k < k1; k += WAVE) {
-    const uint64_t gl = k * V;
-    const uint32_t olo = (uint32_t)((gl > lo ? gl : lo) - go);
-    const uint32_t ohi = (uint32_t)((gl + V < hi ? gl + V : hi) - go);
-    const uint32_t f0 = (uint32_t)(gl - go);  // page-relative index of field 0 (may wrap)
-    for (uint32_t sp = lgn; sp; sp >>= 1)
-      if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
-    T f[V];
+  for (uint64_t kb = k0 + lane; kb < k1; kb += (uint64_t)WAVE * U) {
+    uint32_t id[U][V], msk[U];
+    bool full[U];
 #pragma unroll
-    for (uint32_t j = 0; j < V; ++j) f[j] = 0;
-    uint32_t b = a;
-#pragma unroll
-    for (uint32_t j = 0; j < V; ++j) {
-      const uint32_t o = f0 + j;
-      if (o < olo || o >= ohi) continue;
-      while (rl.rstart[b + 1] <= o) ++b;
-      const uint32_t inf = rl.rinfo[b];
-      uint32_t idx;
-      if (inf & R_RLE) {
-        idx = inf & 0x7FFFFFFFu;
-      } else {
-        const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[b]) * w;
-        idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
-      }
-      if (idx >= ndict) {
-        bad = 1;
-        continue;
-      }
-      if (aligned) {
-        f[j] = reinterpret_cast<const T*>(dict)[idx];
-      } else {
-        const uint8_t* pv = dict + (uint64_t)idx * ES;
-        T t = 0;
-#pragma unroll
-        for (int q = 0; q < ES; ++q) t |= (T)pv[q] << (8 * q);
-        f[j] = t;
-      }
-    }
-    if (ohi - olo == V) {
-      uint4 v;
-      if constexpr (ES == 8)
-        v = make_uint4((uint32_t)f[0], (uint32_t)(f[0] >> 32), (uint32_t)f[1], (uint32_t)(f[1] >> 32));
-      else
-        v = make_uint4(f[0], f[1], f[2], f[3]);
-      *reinterpret_cast<uint4*>(out + gl * ES) = v;
-    } else {
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t k = kb + (uint64_t)u * WAVE;
+      msk[u] = 0;
+      full[u] = false;
+      if (k >= k1) continue;
+      const uint64_t gl = k * V;
+      const uint32_t olo = (uint32_t)((gl > lo ? gl : lo) - go);
+      const uint32_t ohi = (uint32_t)((gl + V < hi ? gl + V : hi) - go);
+      const uint32_t f0 = (uint32_t)(gl - go);  // page-relative index of field 0 (may wrap)
+      full[u] = ohi - olo == V;
+      for (uint32_t sp = lgn; sp; sp >>= 1)
+        if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
+      uint32_t b = a;
 #pragma unroll
       for (uint32_t j = 0; j < V; ++j) {
+        id[u][j] = 0;
         const uint32_t o = f0 + j;
-        if (o >= olo && o < ohi) reinterpret_cast<T*>(out)[gl + j] = f[j];
+        if (o < olo || o >= ohi) continue;
+        while (rl.rstart[b + 1] <= o) ++b;
+        const uint32_t inf = rl.rinfo[b];
+        uint32_t idx;
+        if (inf & R_RLE) {
+          idx = inf & 0x7FFFFFFFu;
+        } else {
+          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[b]) * w;
+          idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+        }
+        if (idx >= ndict) {
+          bad = 1;
+        } else {
+          id[u][j] = idx;
+          msk[u] |= 1u << j;
+        }
+      }
+    }
+    T f[U][V];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u)
+#pragma unroll
+      for (uint32_t j = 0; j < V; ++j) {
+        T t = 0;
+        if ((msk[u] >> j) & 1u) {
+          if (aligned) {
+            t = reinterpret_cast<const T*>(dict)[id[u][j]];
+          } else {
+            const uint8_t* pv = dict + (uint64_t)id[u][j] * ES;
+#pragma unroll
+            for (int q = 0; q < ES; ++q) t |= (T)pv[q] << (8 * q);
+          }
+        }
+        f[u][j] = t;
+      }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t gl = (kb + (uint64_t)u * WAVE) * V;
+      if (full[u]) {
+        uint4 v;
+        if constexpr (ES == 8)
+          v = make_uint4((uint32_t)f[u][0], (uint32_t)(f[u][0] >> 32), (uint32_t)f[u][1], (uint32_t)(f[u][1] >> 32));
+        else
+          v = make_uint4(f[u][0], f[u][1], f[u][2], f[u][3]);
+        *reinterpret_cast<uint4*>(out + gl * ES) = v;
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < V; ++j)
+          if ((msk[u] >> j) & 1u) reinterpret_cast<T*>(out)[gl + j] = f[u][j];
       }
     }
   }
@@ -1181,6 +1299,75 @@ struct LvDictOut {
     const uint32_t bad = lv_write_dict<ES>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base,
                                            dp.num_values, aligned, out);
     if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, res, (int)x.p, ST_PANIC);
+  }
+};
+
+// BYTE_ARRAY / FLBA dictionary indices (decoding.rs:256-315 over the entries k_ba_dict_prep
+// decoded): per output the entry's source address and length (the byte-array scan and copy,
+// pqg_bytes.hip, take it from there), and the page's byte total.
+struct LvBaDictOut {
+  int dict_page;
+  const uint64_t* dsrc;
+  const uint32_t* dlen;
+  uint64_t* vsrc;
+  uint32_t* vlen;
+  ChunkResult* res;
+  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+                             const LvWin& x, uint32_t base, uint32_t endo, int, const ColumnParams&,
+                             PageWork* pages) const {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t ndict = pages[dict_page].num_values;
+    const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
+    const uint64_t go = x.s.out;
+    uint32_t lgn = 1;
+    while (lgn * 2u <= rl.R) lgn *= 2u;
+    uint32_t b = 0, bad = 0;
+    uint64_t bytes = 0;
+    const uint32_t o0 = base + lane;
+    for (uint32_t sp = lgn; sp; sp >>= 1)
+      if (b + sp < rl.R && rl.rstart[b + sp] <= o0) b += sp;
+    constexpr uint32_t U = 4;  // outputs per lane per step: indices, then the gathers together
+#pragma unroll 1
+    for (uint32_t ob = o0; ob < endo; ob += U * WAVE) {
+      uint32_t id[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t o = ob + u * WAVE;
+        id[u] = 0xFFFFFFFFu;
+        if (o >= endo) continue;
+        while (rl.rstart[b + 1] <= o) ++b;
+        const uint32_t inf = rl.rinfo[b];
+        uint32_t idx;
+        if (inf & R_RLE) {
+          idx = inf & 0x7FFFFFFFu;
+        } else {
+          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[b]) * w;
+          idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+        }
+        if (idx >= ndict) bad = 1;  // dict[idx] out of bounds: the reference panics
+        else id[u] = idx;
+      }
+      uint64_t sv[U];
+      uint32_t lv[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u)
+        if (id[u] != 0xFFFFFFFFu) {
+          sv[u] = dsrc[id[u]];
+          lv[u] = dlen[id[u]];
+        }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u)
+        if (id[u] != 0xFFFFFFFFu) {
+          const uint64_t g = go + ob + u * WAVE;
+          vsrc[g] = sv[u];
+          vlen[g] = lv[u];
+          bytes += lv[u];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off, 64);
+    if (lane == 0 && bytes) atomicAdd((unsigned long long*)&pages[x.p].nbytes_out, (unsigned long long)bytes);
+    if (__ballot(bad) && lane == 0) report(pages, res, (int)x.p, ST_PANIC);
   }
 };
 
@@ -1383,7 +1570,32 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   }
 }
 
+// Plan, segment starts and walks, page scan, run compaction: every page of stream `sel` ends
+// walked (PF_WALK, its run list built), dense (PF_PAGE) or handed back (PF_BAIL).
+static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ColumnParams cp,
+                     int sel, int dict_page, RunTables rt, LevelTables lt, uint32_t wgrid, hipStream_t s) {
+  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
+  hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segscan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
+}
+
 extern "C" {
+
+// BYTE_ARRAY / FLBA dictionary indices on the hybrid-stream path (walked pages only: dense or
+// malformed streams go back to the general decoder): per value its entry's address and length.
+hipError_t pqg_launch_lv_badict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                ColumnParams cp, int dict_page, RunTables rt, LevelTables lt, const uint64_t* dsrc,
+                                const uint32_t* dlen, uint64_t* vsrc, uint32_t* vlen, ChunkResult* res,
+                                hipStream_t s) {
+  if (npages <= 0) return hipSuccess;
+  const uint32_t wgrid = 256u * 8u;
+  lv_front(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, rt, lt, wgrid, s);
+  hipLaunchKernelGGL(k_lv_emit_walk<LvBaDictOut>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
+                     (int)SS_DICT, rt, lt, LvBaDictOut{dict_page, dsrc, dlen, vsrc, vlen, res});
+  return hipGetLastError();
+}
 
 // Hybrid-stream path of stream `sel`: plan, segment starts and walks, page scan, run compaction,
 // window path for the dense pages, emits. Def / rep levels: int16 out (+ def counts); RLE
@@ -1392,12 +1604,8 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
                          ColumnParams cp, int sel, int dict_page, int es, RunTables rt, LevelTables lt, void* out,
                          ChunkResult* res, hipStream_t s) {
   if (npages <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
   const uint32_t wgrid = 256u * 8u;
-  hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segscan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
+  lv_front(blob, blob_len, pages, npages, cp, sel, dict_page, rt, lt, wgrid, s);
   uint8_t* o = (uint8_t*)out;
   if (sel == SS_DICT) {  // (dense dictionary streams went to the general decoder)
     if (es == 8)
@@ -1410,7 +1618,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
   }
   hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_stitch, dim3((npages + 3) / 4), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_stitch, dim3(npages), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   if (sel == SS_BOOL) {
     hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
     hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,

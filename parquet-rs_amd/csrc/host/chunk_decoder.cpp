@@ -56,6 +56,9 @@ hipError_t pqg_launch_badict_expand(const uint8_t*, uint64_t, PageWork*, uint32_
 hipError_t pqg_launch_tile_desc(const uint8_t*, PageWork*, uint32_t, const uint32_t*, RunTables,
                                 ColumnParams, int, int, hipStream_t);
 hipError_t pqg_launch_page_counts(PageWork*, int, RunTables, int, hipStream_t);
+hipError_t pqg_launch_lv_badict(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, RunTables,
+                                LevelTables, const uint64_t*, const uint32_t*, uint64_t*, uint32_t*,
+                                ChunkResult*, hipStream_t);
 }
 
 // Two staging slots so consecutive async decodes never overwrite pinned memory that an
@@ -450,6 +453,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
   cp.want_def = want_def;
   cp.want_rep = want_rep;
+  // byte-array entries (address + length per value) take every index width; 4- / 8-byte values
+  // up to 8 bits (wider: a large dictionary, gathered faster by the tiled expand)
+  cp.dict_maxw = (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) ? 16u : 8u;
   // Diagnostic kernel modes exist only in a PQG_DIAG build (make DIAG=1); the shipped library
   // never reads the environment and always runs the production path.
 #ifdef PQG_DIAG
@@ -571,9 +577,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
   // 4- / 8-byte dictionary values: their index streams take the same path (pqg_launch_dict)
   bool dict_lv = enc_present[PQG_RLE_DICTIONARY] && !is_ba && out->values && (es == 4 || es == 8);
+  // byte-array dictionary indices: entry addresses and lengths from the same path
+  bool badict_lv = enc_present[PQG_RLE_DICTIONARY] && is_ba && out->values;
 #ifdef PQG_DIAG
-  if (cp.debug & 256) dict_lv = false;  // diagnostics: dictionary indices through the general decoder
+  if (cp.debug & 256) dict_lv = badict_lv = false;  // diagnostics: dictionary indices through the general decoder
 #endif
+  dict_lv = dict_lv || badict_lv;
   const bool need_lv[3] = {want_def, want_rep, rle_bool || dict_lv};
   auto grow = [&](void** p, size_t* cap, size_t need, size_t elem, const char* what) -> int {
     if (need <= *cap) return PQG_OK;
@@ -631,8 +640,13 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (enc_present[PQG_RLE_DICTIONARY]) {
       HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
                                      ctx->d_res, s), "byte-array dictionary");
-      HIPCHK(hipMemsetAsync(sl.rt[2].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
-      HIPCHK(hipMemsetAsync(sl.rt[2].nfall, 0xFF, sizeof(uint32_t), s), "memset fallback count");
+      if (badict_lv) {  // (nfall 0: the flags the plan sets decide which pages the index pass takes)
+        HIPCHK(pqg_launch_lv_badict(blob, blob_len, ctx->d_pages, np, cp, dict_page, sl.rt[2], sl.lt(2), sl.dsrc,
+                                    sl.dlen, sl.vsrc, sl.vlen, ctx->d_res, s), "dictionary indices");
+      } else {
+        HIPCHK(hipMemsetAsync(sl.rt[2].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+        HIPCHK(hipMemsetAsync(sl.rt[2].nfall, 0xFF, sizeof(uint32_t), s), "memset fallback count");
+      }
       HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
                                   sl.rt[2], ctx->d_res, s), "dictionary index pass");
       HIPCHK(pqg_launch_tile_desc(blob, ctx->d_pages, nt, sl.tile_page, sl.rt[2], cp, 2, dict_page, s),

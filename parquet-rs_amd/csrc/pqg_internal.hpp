@@ -200,7 +200,7 @@ struct ColumnParams {
   int32_t want_def;  // def_levels output provided (read_batch(Some(def)))
   int32_t want_rep;
   int32_t debug;     // diagnostics switches (PQG_DEBUG), 0 in production
-  uint32_t pad;
+  uint32_t dict_maxw;  // widest dictionary index stream the hybrid-stream path takes
   uint64_t* dbgbuf;  // diagnostics: per-wave s_memtime phases (PQG_DEBUG bit 4)
 };
 
