@@ -58,6 +58,8 @@ def parse(argv=None):
                     help="alltypes: row groups per GPU (11 x 2^23 rows ~ 8 GiB decoded: 1/8 of config 5)")
     ap.add_argument("--rg-rows", type=int, default=1 << 23, help="alltypes: rows per row group")
     ap.add_argument("--at-p-null", type=float, default=0.05, help="alltypes: null fraction per column")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="alltypes: HIP streams the row-group decoder spreads the column chunks over")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
     return ap.parse_args(argv)
@@ -222,6 +224,11 @@ def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
         dist.barrier()
     assert st == 0, (st, bad, ctx.error_message())
     return (t1 - t0) / steps, ctx.timings()
+
+
+def torch_device():
+    import torch
+    return torch.cuda.current_device()
 
 
 def cpu_model():
@@ -418,21 +425,22 @@ class AlltypesWorkload:
             for j, (_, pt) in enumerate(pqgtools.ALLTYPES):
                 self.out_bytes += 2 * self.rows + i.value_bytes[j] + (8 * (i.num_values[j] + 1) if pt == 6 else 0)
 
-    def decode_rg(self, ctx, g, stream, oset=0):
-        for j, col in enumerate(self.cols):
-            ctx.decode_async(col, self.d_blob.data_ptr() + self.base[g], self.info[g].blob_len,
-                             self.chunks[g][j], self.out[oset][j][3], stream)
+    def decode_rg(self, rgd, g, stream, oset=0):
+        """pqg_rg_decode of row group g: its 11 column chunks over the decoder's streams."""
+        return rgd.decode_async(self.cols, self.d_blob.data_ptr() + self.base[g], self.info[g].blob_len,
+                                self.chunks[g], [o[3] for o in self.out[oset]], stream)
 
 
 def alltypes_check(ctx, w, stream):
     """Decode row group 0 and compare every column (levels, values, BYTE_ARRAY offsets) with the
     generator's own cells (pqg_truth_alltypes)."""
     import pqgtools
-    w.decode_rg(ctx, 0, stream)
-    st, bad = ctx.sync()
-    assert st == 0, (st, bad, ctx.error_message())
+    oa = w.decode_rg(ctx, 0, stream)
+    st, bcol, bad = ctx.sync()
+    assert st == 0, (st, bcol, bad, ctx.error_message())
     for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
         nv, nb = w.info[0].num_values[j], w.info[0].value_bytes[j]
+        assert oa[j].num_values == nv and oa[j].num_levels == w.rows, (name, oa[j].num_values, nv)
         lv, vals, offs = pqgtools.alltypes_truth(w.row0, w.rows, j, w.p_null, w.seed, nb)
         d_def, d_val, d_off, _ = w.out[0][j]
         assert np.array_equal(d_def[:w.rows].cpu().numpy(), lv), f"{name}: def levels differ"
@@ -449,7 +457,6 @@ def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
         for g in range(w.R):
             w.decode_rg(ctx, g, stream)
     ctx.sync()
-    pqgpu.lib().pqg_reset_timings(ctx.h)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -457,12 +464,12 @@ def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
     for _ in range(steps):
         for g in range(w.R):
             w.decode_rg(ctx, g, stream)
-    st, bad = ctx.sync()
+    st, bcol, bad = ctx.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    assert st == 0, (st, bad, ctx.error_message())
+    assert st == 0, (st, bcol, bad, ctx.error_message())
     return (t1 - t0) / steps
 
 
@@ -502,10 +509,10 @@ def alltypes_pcie(ctx, w, stream):
                 if o is not None:
                     ho.copy_(o, non_blocking=True)
             free[g % 2].record(s_dn)
-    st, bad = ctx.sync()
+    st, bcol, bad = ctx.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    assert st == 0, (st, bad)
+    assert st == 0, (st, bcol, bad)
     return {"values_per_s": w.levels / dt, "ms": dt * 1e3, "pcie_bytes": w.in_bytes + w.out_bytes,
             "note": "pinned H2D of row group g+1 overlapped with the decode of g and the D2H of its "
                     "decoded columns (three streams), one pass over all row groups"}
@@ -544,9 +551,10 @@ def alltypes_cpu_baseline(w, threads):
             "by_threads": {f"{th}t_b1024": round(v[0], 1) for th, v in res.items()}}
 
 
-def main_alltypes(args, world, rank, dist, ctx, stream):
+def main_alltypes(args, world, rank, dist, stream):
     import pqgpu
     w = AlltypesWorkload(pqgpu, args, rank)
+    ctx = pqgpu.RowGroupDecoder(torch_device(), args.streams)
     checked = alltypes_check(ctx, w, stream)
     per_step = alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist)
     per_step = max_over_ranks(per_step, dist, device="cuda")
@@ -563,7 +571,7 @@ def main_alltypes(args, world, rank, dist, ctx, stream):
                                f"{w.rows} rows", "row_groups_per_gpu": w.R, "rows_per_gpu": w.R * w.rows,
                    "cells_per_gpu": w.levels, "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes,
                    "out_bytes_per_gpu": w.out_bytes, "chunk_decodes_per_step": w.R * len(w.cols),
-                   "gen_seconds": round(w.gen_s, 1),
+                   "gen_seconds": round(w.gen_s, 1), "streams": args.streams,
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": "whole step (every chunk decode)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -575,6 +583,7 @@ def main_alltypes(args, world, rank, dist, ctx, stream):
         result["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)
     if rank == 0 and args.cpu_baseline and world == 1:
         result["cpu_baseline"] = alltypes_cpu_baseline(w, min(args.threads, os.cpu_count() or 1))
+    ctx.close()
     return result
 
 
@@ -613,10 +622,10 @@ def main(argv=None):
 
     kind = args.config
     if kind == "alltypes":
-        result = main_alltypes(args, world, rank, dist, ctx, stream)
+        ctx.close()
+        result = main_alltypes(args, world, rank, dist, stream)
         if rank == 0:
             print(json.dumps(result), flush=True)
-        ctx.close()
         if dist is not None:
             dist.destroy_process_group()
         return

@@ -143,8 +143,9 @@ int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
                      uint64_t blob_len, const pqg_page *pages, uint32_t npages,
                      pqg_output *out, void *stream);
 
-/* Wait for the last decode and report its status. On error *first_bad_page names the
- * lowest page index that failed (the page the reference would fail on first). */
+/* Wait for every decode enqueued on the ctx since the last pqg_sync, fill their outputs and
+ * report the status of the first one (in issue order) that failed. On error *first_bad_page
+ * names that decode's lowest failing page (the page the reference would fail on first). */
 int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
 /* Record assembly on the device (the layout TypedTripletIter builds per batch,
  * record/triplet.rs:300-318, over a whole decoded chunk): spaced[i] = the value of level i when
@@ -157,6 +158,24 @@ int pqg_space_values(pqg_ctx *ctx, const int16_t *def_levels, uint64_t num_level
 int pqg_get_timings(pqg_ctx *ctx, pqg_timings *t);
 int pqg_reset_timings(pqg_ctx *ctx);
 const char *pqg_error_message(pqg_ctx *ctx);
+
+/* ---------------------------------------------------------------- row groups
+ * The column chunks of one row group decoded concurrently. The reference reads every column
+ * chunk of a row group through its own page reader and column reader (file/reader.rs:252-260,
+ * 306-330); they share nothing, so pqg_rg_decode forks `stream` onto `nstreams` HIP streams,
+ * decodes column j with a context of its own (scratch reused across row groups) and joins the
+ * streams back into `stream` before returning. pages[j] / npages[j] / outs[j] are column j's
+ * arguments of pqg_decode_chunk, all pages in the one device blob. Asynchronous: pqg_rg_sync
+ * waits and fills every outs[j]; it returns the first failing column's status (lowest index)
+ * and names that column and its page. */
+typedef struct pqg_rg_ctx pqg_rg_ctx;
+int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx **out);
+int pqg_rg_ctx_destroy(pqg_rg_ctx *g);
+int pqg_rg_decode(pqg_rg_ctx *g, uint32_t ncols, const pqg_column *cols, const uint8_t *blob,
+                  uint64_t blob_len, const pqg_page *const *pages, const uint32_t *npages,
+                  pqg_output *outs, void *stream);
+int pqg_rg_sync(pqg_rg_ctx *g, int *bad_column, int *bad_page);
+const char *pqg_rg_error_message(pqg_rg_ctx *g);
 
 /* ---------------------------------------------------------------- host-side reader
  * The parquet::file::reader surface kept on the host (src/file/reader.rs:51-90, 140-530):

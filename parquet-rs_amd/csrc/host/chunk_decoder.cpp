@@ -71,7 +71,16 @@ struct Slot {
   ChunkResult* h_res = nullptr;  // pinned
   hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the def-level path / values kernel
   bool kl = false, kv = false;  // events 6-7 / 8-9 recorded by the last decode
-  bool used = false;
+  bool used = false;     // a decode was enqueued and its timings not yet harvested
+  bool pending = false;  // a decode was enqueued and its results not yet delivered
+  uint64_t seq = 0;      // issue order of that decode
+  // the decode's own result delivery (pqg_sync, or the slot's reuse): its output struct, the
+  // level count read_batch reports, and what the host checks found before the launch
+  pqg_output* out = nullptr;
+  uint64_t total_levels = 0;
+  int host_status = 0;
+  int host_bad_page = -1;
+  std::string host_msg;
   // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix;
   // per dictionary entry source address and length
   uint64_t* vsrc = nullptr;
@@ -122,20 +131,20 @@ struct pqg_ctx {
   hipEvent_t* ev = nullptr;
   hipStream_t stream = nullptr;
   bool timing = false;
-  bool pending = false;
+  uint64_t seq = 0;     // decodes issued
+  // first failure among decodes delivered at a slot's reuse, reported by the next pqg_sync
+  int held_status = 0;
+  int held_page = -1;
+  std::string held_msg;
   double acc_ms[7] = {};
   uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
   uint64_t* dbgbuf = nullptr;  // diagnostics (PQG_DEBUG bit 4)
   size_t dbg_cap = 0;
   uint32_t dbg_n = 0;
   uint64_t acc_n = 0;
-  int host_status = 0;
-  int host_bad_page = -1;
   uint32_t values_kernel = 0;
   uint64_t* sp_tiles = nullptr;  // pqg_space_values: per tile of levels, max_def count then base
   size_t sp_cap = 0;
-  pqg_output* out = nullptr;
-  uint64_t total_levels = 0;
   std::string msg;
 };
 
@@ -164,6 +173,40 @@ static int set_err(pqg_ctx* c, int st, const char* fmt, ...) {
 
 static int hip_fail(pqg_ctx* c, hipError_t e, const char* what) {
   return set_err(c, PQG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+static const char* status_name(int st) {
+  static const char* names[] = {"OK", "General", "NYI", "EOF", "panic", "hang", "capacity", "invalid", "hip"};
+  return st >= 0 && st < 9 ? names[st] : "?";
+}
+
+// Delivers the results of slot sl's finished decode into its output struct; returns its status
+// (the host checks' status when they rejected a page no later than the first failing one)
+// and writes the failing page and a message.
+static int finish_slot(Slot& sl, int* page_out, std::string& msg) {
+  const ChunkResult& r = *sl.h_res;
+  pqg_output* out = sl.out;
+  out->num_levels = sl.total_levels;
+  out->num_values = r.total_values;
+  out->num_bytes = r.total_bytes;
+  int st = 0, page = -1;
+  if (r.first_bad_page != 0x7FFFFFFF) {
+    page = r.first_bad_page;
+    st = r.status;
+  }
+  if (sl.host_status && (page < 0 || sl.host_bad_page <= page)) {
+    page = sl.host_bad_page;
+    st = sl.host_status;
+    msg = sl.host_msg;
+  } else if (st) {
+    char buf[160];
+    snprintf(buf, sizeof(buf), "page %d: %s (reference: %s)", page, status_name(st),
+             st == PQG_ERR_PANIC ? "panics" : st == PQG_ERR_HANG ? "loops forever" : "returns Err");
+    msg = buf;
+  }
+  sl.pending = false;
+  *page_out = page;
+  return st;
 }
 
 #define HIPCHK(expr, what)                      \
@@ -229,7 +272,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
   if (!ctx) return PQG_OK;
   hipSetDevice(ctx->device);
   for (Slot& sl : ctx->slot) {
-    if (sl.used) hipEventSynchronize(sl.ev[5]);
+    if (sl.used || sl.pending) hipEventSynchronize(sl.ev[5]);
     hipFree(sl.d_pages);
     hipHostFree(sl.h_pages);
     hipFree(sl.d_res);
@@ -363,24 +406,35 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       return set_err(ctx, PQG_ERR_INVALID, "BYTE_ARRAY/FLBA output needs offsets[num_levels + 1]");
   }
   HIPCHK(hipSetDevice(ctx->device), "hipSetDevice");
-  ctx->msg.clear();
-  ctx->host_status = 0;
-  ctx->host_bad_page = -1;
-  ctx->out = out;
   ctx->stream = s;
   out->num_levels = out->num_values = out->num_bytes = 0;
 
-  // ---- staging slot: wait until its previous decode has finished, harvest its timings
+  // ---- staging slot: wait until its previous decode has finished, harvest its timings and
+  // deliver its results (a failure is held for the next pqg_sync)
   ctx->cur ^= 1;
   Slot& sl = ctx->slot[ctx->cur];
-  if (sl.used) {
+  if (sl.used || sl.pending) {
     HIPCHK(hipEventSynchronize(sl.ev[5]), "slot wait");
-    if (ctx->timing) {
+    if (sl.used && ctx->timing) {
       harvest_times(ctx->acc_ms, sl.ev, sl.kl, sl.kv);
       ctx->acc_n++;
     }
     sl.used = false;
+    if (sl.pending) {
+      int page;
+      std::string m;
+      const int st = finish_slot(sl, &page, m);
+      if (st && !ctx->held_status) {
+        ctx->held_status = st;
+        ctx->held_page = page;
+        ctx->held_msg = m;
+      }
+    }
   }
+  sl.out = out;
+  sl.host_status = 0;
+  sl.host_bad_page = -1;
+  sl.host_msg.clear();
   if (npages > sl.pages_cap) {
     size_t cap = npages < 1024 ? 1024 : npages;
     hipFree(sl.d_pages);
@@ -434,15 +488,15 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (vst && (int)i > bad) w.status = -1;  // never reached by the reference
   }
   if (vst) {
-    ctx->host_status = vst;
-    ctx->host_bad_page = bad;
-    ctx->msg = why;
+    sl.host_status = vst;
+    sl.host_bad_page = bad;
+    sl.host_msg = why;
   }
   const bool want_def = col->max_def > 0 && out->def_levels;
   const bool want_rep = col->max_rep > 0 && out->rep_levels;
   const uint64_t lev_needed = level_out;
   // read_batch reports levels only for the streams it reads (column/reader.rs:259)
-  ctx->total_levels = (want_def || want_rep) ? lev_needed : 0;
+  sl.total_levels = (want_def || want_rep) ? lev_needed : 0;
 
   ColumnParams cp{};
   cp.physical_type = t;
@@ -480,7 +534,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   }
 
   ChunkResult r0{};
-  r0.total_levels = ctx->total_levels;
+  r0.total_levels = sl.total_levels;
   r0.first_bad_page = 0x7FFFFFFF;
   r0.dict_page = dict_page < 0 ? 0xFFFFFFFFu : (uint32_t)dict_page;
   *ctx->h_res = r0;
@@ -722,7 +776,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(ChunkResult), hipMemcpyDeviceToHost, s), "D2H res");
   HIPCHK(hipEventRecord(ctx->ev[5], s), "event");
   sl.used = true;
-  ctx->pending = true;
+  sl.pending = true;
+  sl.seq = ++ctx->seq;
   return PQG_OK;
 }
 
@@ -749,34 +804,41 @@ int pqg_space_values(pqg_ctx* ctx, const int16_t* def_levels, uint64_t num_level
 int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
   if (!ctx) return PQG_ERR_INVALID;
   if (first_bad_page) *first_bad_page = -1;
-  if (!ctx->pending) return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
-  hipError_t e = hipEventSynchronize(ctx->ev[5]);
-  ctx->pending = false;
-  if (ctx->timing && e == hipSuccess) {
-    const Slot& cs = ctx->slot[ctx->cur];
-    harvest_times(ctx->acc_ms, ctx->ev, cs.kl, cs.kv);
-    ctx->acc_n++;
-    ctx->slot[ctx->cur].used = false;  // harvested
+  Slot* order[2] = {&ctx->slot[ctx->cur ^ 1], &ctx->slot[ctx->cur]};
+  if (order[0]->pending && order[1]->pending && order[0]->seq > order[1]->seq) std::swap(order[0], order[1]);
+  if (!order[0]->pending && !order[1]->pending && !ctx->held_status)
+    return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
+  // every pending decode is delivered, in issue order; the first failure is reported
+  int st = ctx->held_status, page = ctx->held_page;
+  std::string msg = ctx->held_msg;
+  ctx->held_status = 0;
+  ctx->held_page = -1;
+  ctx->held_msg.clear();
+  hipError_t herr = hipSuccess;
+  for (Slot* sl : order) {
+    if (!sl->pending) continue;
+    const hipError_t e = hipEventSynchronize(sl->ev[5]);
+    if (e != hipSuccess) {
+      sl->pending = false;
+      if (herr == hipSuccess) herr = e;
+      continue;
+    }
+    if (sl->used && ctx->timing) {
+      harvest_times(ctx->acc_ms, sl->ev, sl->kl, sl->kv);
+      ctx->acc_n++;
+    }
+    sl->used = false;
+    int pg;
+    std::string m;
+    const int s2 = finish_slot(*sl, &pg, m);
+    if (s2 && !st) {
+      st = s2;
+      page = pg;
+      msg = m;
+    }
   }
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
-  const ChunkResult& r = *ctx->h_res;
-  pqg_output* out = ctx->out;
-  out->num_levels = ctx->total_levels;
-  out->num_values = r.total_values;
-  out->num_bytes = r.total_bytes;
-  int st = 0, page = -1;
-  if (r.first_bad_page != 0x7FFFFFFF) {
-    page = r.first_bad_page;
-    st = r.status;
-  }
-  if (ctx->host_status && (page < 0 || ctx->host_bad_page <= page)) {
-    page = ctx->host_bad_page;
-    st = ctx->host_status;
-  } else if (st) {
-    static const char* names[] = {"OK", "General", "NYI", "EOF", "panic", "hang", "capacity", "invalid", "hip"};
-    set_err(ctx, st, "page %d: %s (reference: %s)", page, st < 9 ? names[st] : "?",
-            st == PQG_ERR_PANIC ? "panics" : st == PQG_ERR_HANG ? "loops forever" : "returns Err");
-  }
+  if (herr != hipSuccess) return hip_fail(ctx, herr, "hipEventSynchronize");
+  ctx->msg = msg;
   if (first_bad_page) *first_bad_page = page;
   return st;
 }

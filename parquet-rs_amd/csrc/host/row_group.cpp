@@ -1,0 +1,152 @@
+// row_group.cpp — pqg_rg_*: the column chunks of one row group decoded concurrently.
+//
+// The reference reads a row group column by column, each column chunk through its own
+// SerializedPageReader / ColumnReader (file/reader.rs:252-260, 306-330): the chunks share
+// nothing. A single chunk of a wide row group (8M rows of a small-dictionary column: one data
+// page) leaves most of the GPU idle while its level and index passes run, so the row group
+// decoder forks the caller's stream onto `nstreams` HIP streams, gives every column chunk its
+// own pqg_ctx (own staging and scratch, reused across row groups), places the chunks on the
+// streams by estimated bytes (longest first onto the least-loaded stream) and joins the streams
+// back into the caller's stream. Results per column are delivered by pqg_rg_sync.
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../../include/pqgpu.h"
+
+struct pqg_rg_ctx {
+  int device = 0;
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> join;
+  hipEvent_t fork = nullptr;
+  std::vector<pqg_ctx*> cols;   // one decode context per column index
+  std::vector<int> issued;      // decodes pending per column
+  std::string msg;
+};
+
+static int rg_fail(pqg_rg_ctx* g, int st, const char* what) {
+  g->msg = what;
+  return st;
+}
+
+extern "C" {
+
+int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx** out) {
+  if (!out || nstreams < 1 || nstreams > 16) return PQG_ERR_INVALID;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return PQG_ERR_HIP;
+  pqg_rg_ctx* g = new pqg_rg_ctx();
+  g->device = device;
+  bool ok = hipEventCreateWithFlags(&g->fork, hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; ok && k < nstreams; ++k) {
+    hipStream_t s;
+    hipEvent_t e;
+    ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) break;
+    g->streams.push_back(s);
+    ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (ok) g->join.push_back(e);
+  }
+  if (!ok) {
+    pqg_rg_ctx_destroy(g);
+    return PQG_ERR_HIP;
+  }
+  *out = g;
+  return PQG_OK;
+}
+
+int pqg_rg_ctx_destroy(pqg_rg_ctx* g) {
+  if (!g) return PQG_OK;
+  hipSetDevice(g->device);
+  for (pqg_ctx* c : g->cols) pqg_ctx_destroy(c);  // waits for its decodes
+  for (hipStream_t s : g->streams) hipStreamDestroy(s);
+  for (hipEvent_t e : g->join) hipEventDestroy(e);
+  if (g->fork) hipEventDestroy(g->fork);
+  delete g;
+  return PQG_OK;
+}
+
+const char* pqg_rg_error_message(pqg_rg_ctx* g) { return g ? g->msg.c_str() : "null ctx"; }
+
+int pqg_rg_decode(pqg_rg_ctx* g, uint32_t ncols, const pqg_column* cols, const uint8_t* blob, uint64_t blob_len,
+                  const pqg_page* const* pages, const uint32_t* npages, pqg_output* outs, void* stream_v) {
+  if (!g || (ncols && (!cols || !pages || !npages || !outs))) return PQG_ERR_INVALID;
+  for (uint32_t j = 0; j < ncols; ++j)
+    if (npages[j] && !pages[j]) return rg_fail(g, PQG_ERR_INVALID, "column without its page array");
+  if (hipSetDevice(g->device) != hipSuccess) return rg_fail(g, PQG_ERR_HIP, "hipSetDevice");
+  g->msg.clear();
+  while (g->cols.size() < ncols) {
+    pqg_ctx* c = nullptr;
+    const int st = pqg_ctx_create(g->device, &c);
+    if (st) return rg_fail(g, st, "pqg_ctx_create");
+    g->cols.push_back(c);
+    g->issued.push_back(0);
+  }
+  hipStream_t caller = (hipStream_t)stream_v;
+  if (hipEventRecord(g->fork, caller) != hipSuccess) return rg_fail(g, PQG_ERR_HIP, "fork event");
+  const size_t K = g->streams.size();
+  for (hipStream_t s : g->streams)
+    if (hipStreamWaitEvent(s, g->fork, 0) != hipSuccess) return rg_fail(g, PQG_ERR_HIP, "fork wait");
+  // bytes each chunk moves (payload in; levels + values out, estimated from the page counts)
+  std::vector<std::pair<double, uint32_t>> work(ncols);
+  for (uint32_t j = 0; j < ncols; ++j) {
+    double b = 0;
+    for (uint32_t i = 0; i < npages[j]; ++i) b += pages[j][i].nbytes + 2.0 * pages[j][i].num_values;
+    work[j] = {b + (double)outs[j].values_capacity, j};
+  }
+  std::sort(work.begin(), work.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  std::vector<double> load(K, 0.0);
+  int first_err = PQG_OK;
+  for (const auto& wj : work) {
+    const uint32_t j = wj.second;
+    const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[k] += wj.first;
+    const int st = pqg_decode_chunk(g->cols[j], &cols[j], blob, blob_len, pages[j], npages[j], &outs[j],
+                                    g->streams[k]);
+    if (st) {
+      if (!first_err) {
+        first_err = st;
+        char buf[320];
+        snprintf(buf, sizeof(buf), "column %u: %s", j, pqg_error_message(g->cols[j]));
+        g->msg = buf;
+      }
+      continue;
+    }
+    g->issued[j]++;
+  }
+  for (size_t k = 0; k < K; ++k) {
+    if (hipEventRecord(g->join[k], g->streams[k]) != hipSuccess ||
+        hipStreamWaitEvent(caller, g->join[k], 0) != hipSuccess)
+      return rg_fail(g, PQG_ERR_HIP, "join");
+  }
+  return first_err;
+}
+
+int pqg_rg_sync(pqg_rg_ctx* g, int* bad_column, int* bad_page) {
+  if (!g) return PQG_ERR_INVALID;
+  if (bad_column) *bad_column = -1;
+  if (bad_page) *bad_page = -1;
+  int first = PQG_OK;
+  for (size_t j = 0; j < g->cols.size(); ++j) {
+    if (!g->issued[j]) continue;
+    g->issued[j] = 0;
+    int page = -1;
+    const int st = pqg_sync(g->cols[j], &page);
+    if (st && !first) {
+      first = st;
+      if (bad_column) *bad_column = (int)j;
+      if (bad_page) *bad_page = page;
+      char buf[320];
+      snprintf(buf, sizeof(buf), "column %zu: %s", j, pqg_error_message(g->cols[j]));
+      g->msg = buf;
+    }
+  }
+  return first;
+}
+
+}  // extern "C"

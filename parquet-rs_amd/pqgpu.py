@@ -66,7 +66,8 @@ EXPORTS = [
     "pqg_column_reader_read_batch", "pqg_triplet_iter_open", "pqg_triplet_iter_close",
     "pqg_triplet_iter_read_next", "pqg_triplet_iter_has_next", "pqg_triplet_iter_def_level",
     "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
-    "pqg_space_values",
+    "pqg_space_values", "pqg_rg_ctx_create", "pqg_rg_ctx_destroy", "pqg_rg_decode", "pqg_rg_sync",
+    "pqg_rg_error_message",
 ]
 
 _lib = None
@@ -121,6 +122,13 @@ def lib():
             getattr(L, "pqg_triplet_iter_" + f).restype = C.c_int16
         L.pqg_triplet_iter_value.argtypes = [vp, vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.pqg_space_values.argtypes = [vp, vp, u64, C.c_int16, vp, i32, vp, vp]
+        L.pqg_rg_ctx_create.argtypes = [i32, i32, C.POINTER(vp)]
+        L.pqg_rg_ctx_destroy.argtypes = [vp]
+        L.pqg_rg_decode.argtypes = [vp, C.c_uint32, C.POINTER(Column), vp, u64, C.POINTER(C.POINTER(Page)),
+                                    C.POINTER(C.c_uint32), C.POINTER(Output), vp]
+        L.pqg_rg_sync.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.pqg_rg_error_message.argtypes = [vp]
+        L.pqg_rg_error_message.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -175,6 +183,56 @@ class Context:
         t = Timings()
         lib().pqg_get_timings(self.h, C.byref(t))
         return t
+
+
+class RowGroupDecoder:
+    """pqg_rg_ctx: the column chunks of a row group decoded concurrently on `nstreams` HIP
+    streams, one decode context per column (pqgpu.h, file/reader.rs:252-260)."""
+
+    def __init__(self, device=0, nstreams=4):
+        self.device = device
+        h = C.c_void_p()
+        st = lib().pqg_rg_ctx_create(device, nstreams, C.byref(h))
+        if st:
+            raise PqgError(st, "pqg_rg_ctx_create failed")
+        self.h = h
+        self._keep = []  # argument arrays of the decodes not yet synced (the library fills oa)
+
+    def close(self):
+        if self.h:
+            lib().pqg_rg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error_message(self):
+        return lib().pqg_rg_error_message(self.h).decode(errors="replace")
+
+    def decode_async(self, columns, blob, blob_len, page_arrays, outs, stream=0):
+        """Enqueue pqg_rg_decode: columns[j] (Column), page_arrays[j] (ctypes Page array) and
+        outs[j] (Output) per column chunk, every page in the device blob at `blob`."""
+        n = len(columns)
+        cols = (Column * n)(*columns)
+        pp = (C.POINTER(Page) * n)(*[C.cast(a, C.POINTER(Page)) for a in page_arrays])
+        npg = (C.c_uint32 * n)(*[len(a) for a in page_arrays])
+        oa = (Output * n)(*outs)
+        st = lib().pqg_rg_decode(self.h, n, cols, C.c_void_p(blob), blob_len, pp, npg, oa, C.c_void_p(stream))
+        self._keep.append((cols, pp, npg, oa, page_arrays))
+        if st:
+            raise PqgError(st, self.error_message())
+        return oa
+
+    def sync(self):
+        """(status, bad column, bad page); the Output array the last decode_async returned
+        holds the counters."""
+        col, page = C.c_int(-1), C.c_int(-1)
+        st = lib().pqg_rg_sync(self.h, C.byref(col), C.byref(page))
+        self._keep = self._keep[-1:]
+        return st, col.value, page.value
 
 
 def make_pages(specs):

@@ -76,3 +76,80 @@ def test_gpu_decodes_alltypes_chunks(oracle, rowgroup, j):
         np.testing.assert_array_equal(got["offsets"], offs)
     else:
         assert got["values"].view(np.uint8).tobytes() == vals.tobytes()
+
+
+def _rg_outputs(torch, info, rows):
+    import pqgpu
+    keep, outs = [], []
+    for j, (_, pt) in enumerate(pqgtools.ALLTYPES):
+        d_def = torch.empty(rows + 64, dtype=torch.int16, device="cuda")
+        d_val = torch.empty(info.value_bytes[j] + 64, dtype=torch.uint8, device="cuda")
+        d_off = torch.empty(rows + 8, dtype=torch.int64, device="cuda") if pt == 6 else None
+        outs.append(pqgpu.Output(d_def.data_ptr(), None, d_val.data_ptr(), info.value_bytes[j] + 64,
+                                 d_off.data_ptr() if d_off is not None else None, rows + 1 if pt == 6 else 0,
+                                 0, 0, 0))
+        keep.append((d_def, d_val, d_off))
+    return keep, outs
+
+
+def _rg_pages(pqgpu, pages, info):
+    return [(pqgpu.Page * (info.chunk_first[j + 1] - info.chunk_first[j]))(
+        *[pages[i] for i in range(info.chunk_first[j], info.chunk_first[j + 1])]) for j in range(11)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nstreams", [1, 4])
+def test_gpu_row_group_decoder(rowgroup, nstreams):
+    """pqg_rg_decode: all 11 column chunks of the row group over `nstreams` streams, twice in a
+    row (the second decode into other outputs) before one pqg_rg_sync; every column matches the
+    generator's cells and its counters are filled."""
+    import pqgpu
+    import torch
+    blob, pages, info = rowgroup
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob[:info.blob_len + 64])).cuda()
+    cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+    parr = _rg_pages(pqgpu, pages, info)
+    rgd = pqgpu.RowGroupDecoder(0, nstreams)
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        sets = [_rg_outputs(torch, info, ROWS) for _ in range(2)]
+        oas = [rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, parr, outs, s) for _, outs in sets]
+        st, bcol, bad = rgd.sync()
+        assert st == 0, (st, bcol, bad, rgd.error_message())
+        torch.cuda.current_stream().synchronize()
+        for (keep, _), oa in zip(sets, oas):
+            for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+                lv, vals, offs = pqgtools.alltypes_truth(ROW0, ROWS, j, P_NULL, SEED, info.value_bytes[j])
+                d_def, d_val, d_off = keep[j]
+                assert oa[j].num_levels == ROWS and oa[j].num_values == info.num_values[j], name
+                np.testing.assert_array_equal(d_def[:ROWS].cpu().numpy(), lv)
+                assert d_val[:info.value_bytes[j]].cpu().numpy().tobytes() == vals.tobytes(), name
+                if offs is not None:
+                    assert oa[j].num_bytes == info.value_bytes[j]
+                    np.testing.assert_array_equal(d_off[:len(offs)].cpu().numpy(), offs)
+    finally:
+        rgd.close()
+
+
+@pytest.mark.gpu
+def test_gpu_row_group_decoder_reports_failing_column(rowgroup):
+    """A column chunk whose data page is cut short fails with EOF-class status; pqg_rg_sync names
+    that column (the lowest failing one) and its page while the other columns still decode."""
+    import pqgpu
+    import torch
+    blob, pages, info = rowgroup
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob[:info.blob_len + 64])).cuda()
+    cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+    parr = _rg_pages(pqgpu, pages, info)
+    # bool_col (column 1): one PLAIN data page; drop most of its value bytes
+    parr[1][0].nbytes = 64
+    rgd = pqgpu.RowGroupDecoder(0, 4)
+    try:
+        keep, outs = _rg_outputs(torch, info, ROWS)
+        rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, parr, outs, torch.cuda.current_stream().cuda_stream)
+        st, bcol, bad = rgd.sync()
+        assert st != 0 and bcol == 1 and bad == 0, (st, bcol, bad)
+        lv, vals, _ = pqgtools.alltypes_truth(ROW0, ROWS, 0, P_NULL, SEED, info.value_bytes[0])
+        assert keep[0][1][:info.value_bytes[0]].cpu().numpy().tobytes() == vals.tobytes()
+    finally:
+        rgd.close()

@@ -27,7 +27,9 @@ def main():
     ctx = pqgpu.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
-    bench.alltypes_check(ctx, w, s)
+    rgd = pqgpu.RowGroupDecoder(torch.cuda.current_device())
+    bench.alltypes_check(rgd, w, s)
+    rgd.close()
     tot = 0.0
     for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
