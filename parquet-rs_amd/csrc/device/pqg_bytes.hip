@@ -23,20 +23,29 @@ namespace pqg {
 
 // Walks n PLAIN BYTE_ARRAY values of the stream blob[S, S+slen) (decoding.rs:206-226):
 // PANIC when fewer than 4 bytes remain for a length (read_num_bytes! assert), EOF when the
-// value bytes run past the stream. Writes absolute source addresses and lengths.
+// value bytes run past the stream. Writes absolute source addresses and lengths. One lane
+// follows the chain over the LDS-staged region and records each value's (offset, length) in
+// LDS; the workgroup then writes them out coalesced (global stores from one lane per value
+// would bound the walk).
+constexpr uint32_t BW_CAP = 2048;  // values recorded per pass
 __device__ int32_t plain_ba_walk(DeltaSmem& sm, const uint8_t* __restrict__ blob, uint64_t blob_len,
                                  uint64_t S, uint32_t slen, uint64_t n, uint64_t* __restrict__ src,
                                  uint32_t* __restrict__ len) {
+  __shared__ uint2 rec[BW_CAP];
   uint64_t i = 0;
   uint32_t pos = 0;
+  uint64_t A0 = ~0ull;
   while (i < n) {
-    const uint64_t A0 = (S + pos) & ~15ull;
-    __syncthreads();
-    delta_load_region(sm, blob, blob_len, A0);
-    __syncthreads();
+    if (A0 == ~0ull || S + pos + 4 - A0 > (uint64_t)DBLK) {  // restage: the next length is past the region
+      A0 = (S + pos) & ~15ull;
+      __syncthreads();
+      delta_load_region(sm, blob, blob_len, A0);
+      __syncthreads();
+    }
     if (threadIdx.x == 0) {
       int32_t e = 0;
-      while (i < n) {
+      uint32_t k = 0;
+      while (i + k < n && k < BW_CAP) {
         const uint64_t rel = S + pos - A0;
         if (rel + 4 > (uint64_t)DBLK) break;
         if ((uint64_t)pos + 4 > slen) {
@@ -49,19 +58,24 @@ __device__ int32_t plain_ba_walk(DeltaSmem& sm, const uint8_t* __restrict__ blob
           e = ST_EOF;
           break;
         }
-        src[i] = S + pos;
-        len[i] = l;
+        rec[k++] = make_uint2(pos, l);
         pos += l;
-        ++i;
       }
       sm.ctl[0] = (uint32_t)e;
       sm.ctl[1] = pos;
-      reinterpret_cast<uint64_t*>(&sm.ctl[2])[0] = i;
+      sm.ctl[2] = k;
     }
     __syncthreads();
     const int32_t e = (int32_t)sm.ctl[0];
+    const uint32_t k = sm.ctl[2];
     pos = sm.ctl[1];
-    i = reinterpret_cast<uint64_t*>(&sm.ctl[2])[0];
+    for (uint32_t t = threadIdx.x; t < k; t += WG) {
+      const uint2 r = rec[t];
+      src[i + t] = S + r.x;
+      len[i + t] = r.y;
+    }
+    i += k;
+    __syncthreads();  // rec is refilled by the next pass
     if (e) return e;
   }
   return 0;

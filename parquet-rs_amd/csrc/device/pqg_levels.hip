@@ -273,6 +273,54 @@ __device__ inline void lv_scan_windows(int npages, uint32_t* wbase, F nwin_of) {
   if (threadIdx.x == 0) wbase[npages] = carry_s;
 }
 
+// ------------------------------------------------------------------------------ k_lv_probe
+// One wave per page of a level stream: walks the chain from offset 0 over the first KiB, held
+// in VGPRs (16 bytes per lane; header bytes read by v_readlane, so a hop costs a few scalar
+// cycles). When its first 64 headers lie within 1 KiB (short RLE runs: the segment walk would
+// stop there as dense, LS_DENSE), the page goes to the window path directly (lt.dense).
+// Dictionary indices have no window path and are not probed.
+__device__ inline uint32_t probe_dw(const uint32_t (&d)[4], uint32_t i) {  // dword i of the KiB (uniform)
+  const int l = (int)(i >> 2);
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d[0], l), b = (uint32_t)__builtin_amdgcn_readlane((int)d[1], l),
+                 c = (uint32_t)__builtin_amdgcn_readlane((int)d[2], l), e = (uint32_t)__builtin_amdgcn_readlane((int)d[3], l);
+  const uint32_t k = i & 3u;
+  return k == 0 ? a : k == 1 ? b : k == 2 ? c : e;
+}
+
+__global__ void __launch_bounds__(WG) k_lv_probe(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                 const PageWork* __restrict__ pages, int npages, ColumnParams cp,
+                                                 int sel, LevelTables lt) {
+  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t p = blockIdx.x * (WG / WAVE) + wid;
+  if (p >= (uint32_t)npages) return;
+  Stream st;
+  uint32_t dense = 0;
+  if (sel != SS_DICT && lv_stream(blob, pages[p], sel, cp, st) && st.n && st.slen >= LW_SPAN + 64u) {
+    // 64 lanes x 16 bytes from the stream start, aligned down (the KiB plus up to 15 bytes before)
+    const uint64_t A = st.S & ~15ull;
+    const uint32_t sb = (uint32_t)(st.S - A);
+    const uint64_t a = A + (uint64_t)lane * 16u;
+    const uint4 v = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t w = (uint32_t)st.w, vb = (w + 7u) >> 3;
+    uint32_t q = 0, k = 0;
+    while (k < 64u && q + 20u < LW_SPAN) {  // header bytes q .. q + 3 (+ alignment) stay in the staged KiB
+      const uint32_t r = q + sb;
+      const uint32_t x = __builtin_amdgcn_alignbit(probe_dw(d, (r >> 2) + 1u), probe_dw(d, r >> 2), (r & 3u) * 8u);
+      const uint32_t c0 = (x >> 7) & 1u, c1 = (x >> 15) & 1u, c2 = (x >> 23) & 1u, c3 = x >> 31;
+      const uint32_t c01 = c0 & c1, c012 = c01 & c2;
+      if (c012 & c3) break;  // a varint the fast parse does not take
+      const uint32_t hl = 1u + c0 + c01 + c012;
+      const uint32_t h = (x & 0x7Fu) | (c0 ? ((x >> 1) & 0x3F80u) : 0u) | (c01 ? ((x >> 2) & 0x1FC000u) : 0u) |
+                         (c012 ? ((x >> 3) & 0xFE00000u) : 0u);
+      q += (h & 1u) ? hl + (h >> 1) * w : hl + vb;
+      ++k;
+    }
+    dense = k == 64u && q < LW_SPAN;
+  }
+  if (lane == 0) lt.dense[p] = dense;
+}
+
 // ------------------------------------------------------------------------------ k_lv_plan
 // One workgroup: per page the stream's windows (exclusive scan into wbase), and the page flag:
 // PF_PAGE (level path) or PF_BAIL (general decoder). Def streams start their count at 0.
@@ -300,7 +348,7 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
   });
   lv_scan_windows(npages, lt.sbase, [&](int p) -> uint32_t {
     Stream s;
-    if (nodict || !lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
+    if (nodict || lt.dense[p] || !lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
     const uint32_t sw = lw_segw((uint32_t)s.w);
     return ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
   });
@@ -416,7 +464,7 @@ __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blo
     x.k = j * lw_segw((uint32_t)x.s.w);
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
-    const bool wide = w > 4;
+    const bool wide = w >= 4;
     const uint32_t span = min(wide ? LB_SPANW : LB_SPAN, slen - x.W0);  // walked bytes (the stream may end first)
     lv_stage(blob, blob_len, x, st, (span + 64u) / 16u);
     const uint32_t ent = lv_ent(w);
@@ -756,61 +804,45 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
 }
 
 // ------------------------------------------------------------------------------ k_lv_segscan
-// One lane per page: follows the segment walks from offset 0, places them (first run, first
+// One workgroup per page: follows the segment walks from offset 0, places them (first run, first
 // output), finds the run holding output n - 1, and decides the page: walked (PF_WALK), window
-// path (PF_PAGE stays) or general decoder (PF_BAIL).
-__global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
-  const uint32_t p = blockIdx.x * WG + threadIdx.x;
-  if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
-  Stream s;
-  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
-  const uint32_t n = s.n, w = (uint32_t)s.w;
-  const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
-  if (n == 0 || nseg == 0) {  // nothing to read: no windows, no runs
-    lt.wfirst[lt.wbase[p] + p] = 0;
-    rt.pflag[p] = PF_WALK;
-    return;
+// path (PF_PAGE stays) or general decoder (PF_BAIL). The common case — every walk landed on the
+// next segment's start — is a workgroup scan of the segments' output and run counts; anything
+// else (a start that was not on the true chain, a walk that ended early) is followed by one lane.
+
+// The last segment J of the chain (outputs acc before it reach n): keep its runs up to the one
+// holding output n - 1. Returns the verdict (0 walked, 1 window path, 2 general decoder).
+__device__ inline uint32_t lv_seg_last(LvSeg& sg, const uint2* rec, uint64_t acc, uint32_t runs, uint32_t n,
+                                       uint32_t w, uint32_t slen, uint32_t cap) {
+  uint32_t lo = 0, hi = sg.runs;  // runs [0, sg.runs) start at acc + rec[i].x (ascending)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (acc + rec[mid].x < n) lo = mid;
+    else hi = mid;
   }
-  const uint32_t cap = LW_REC * (lt.wbase[p + 1] - lt.wbase[p] + 2u);
-  for (uint32_t q = 0; q < nseg; ++q) lt.seg[s0 + q].flags = 0;  // (the tables outlive a decode)
+  const uint32_t keep = lo + 1;
+  if (keep == sg.runs && (sg.status == LS_TRUNC || sg.status == LS_BADVAL)) {
+    const uint64_t before = acc + rec[lo].x;
+    const uint64_t need = sg.status == LS_TRUNC ? (uint64_t)sg.tv * 8ull + min((uint64_t)sg.tc, n - before) * w : 0;
+    if (sg.status == LS_BADVAL || need > (uint64_t)slen * 8ull) return 2;
+  }
+  if (runs + keep + 1u > cap) return 1;
+  sg.keep = keep;
+  sg.flags = 3;
+  return 0;
+}
+
+__device__ inline uint32_t lv_segscan_serial(LvSeg* seg, const uint2* srec, uint32_t nseg, uint32_t n, uint32_t w,
+                                             uint32_t slen, uint32_t cap) {
   uint64_t acc = 0;
-  uint32_t runs = 0, prevpos = 0xFFFFFFFFu, j = 0, verdict = 0;  // 0 walked, 1 window path, 2 general
+  uint32_t runs = 0, prevpos = 0xFFFFFFFFu, j = 0;
   while (true) {
-    LvSeg& sg = lt.seg[s0 + j];
-    if (sg.status == LS_NOSTART) {
-      verdict = 1;
-      break;
-    }
+    LvSeg& sg = seg[j];
+    if (sg.status == LS_NOSTART) return 1;
     sg.base_out = acc;
     sg.base_run = runs;
     sg.prevpos = prevpos;
-    if (acc + sg.out >= n) {
-      // the run holding output n - 1: the last one starting before it
-      const uint2* rec = lt.srec + (uint64_t)(s0 + j) * LW_SCAP;
-      uint32_t lo = 0, hi = sg.runs;  // runs [0, sg.runs) start at acc + rec[i].x (ascending)
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (acc + rec[mid].x < n) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t keep = lo + 1;
-      if (keep == sg.runs && (sg.status == LS_TRUNC || sg.status == LS_BADVAL)) {
-        const uint64_t before = acc + rec[lo].x;
-        const uint64_t need = sg.status == LS_TRUNC ? (uint64_t)sg.tv * 8ull + min((uint64_t)sg.tc, n - before) * w : 0;
-        if (sg.status == LS_BADVAL || need > (uint64_t)s.slen * 8ull) {
-          verdict = 2;
-          break;
-        }
-      }
-      if (runs + keep + 1u > cap) {
-        verdict = 1;
-        break;
-      }
-      sg.keep = keep;
-      sg.flags = 3;
-      break;
-    }
+    if (acc + sg.out >= n) return lv_seg_last(sg, srec + (uint64_t)j * LW_SCAP, acc, runs, n, w, slen, cap);
     acc += sg.out;
     runs += sg.runs;
     sg.keep = sg.runs;
@@ -820,30 +852,138 @@ __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ b
       j = sg.next;
       continue;
     }
-    verdict = sg.status == LS_DENSE ? 1 : 2;  // else: the stream ends or breaks before n
-    break;
+    return sg.status == LS_DENSE ? 1 : 2;  // else: the stream ends or breaks before n
   }
-#ifdef PQG_DIAG
-  if ((cp.debug & 64) && cp.dbgbuf) {  // diagnostics: the page's verdict and the segment deciding it
-    uint64_t* d = cp.dbgbuf + 8ull * p;
-    const LvSeg& sg = lt.seg[s0 + j];
-    d[0] = verdict;
-    d[1] = j;
-    d[2] = sg.status;
-    d[3] = sg.runs;
-    d[4] = sg.out;
-    d[5] = nseg;
-    d[6] = sg.lastpos;
-    d[7] = j + 1 < nseg ? lt.bexit[s0 + j + 1] : 0;
+}
+
+__global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
+                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  __shared__ uint64_t wout[WG / WAVE];
+  __shared__ uint32_t wrun[WG / WAVE], wlast[WG / WAVE], wmin[WG / WAVE];
+  __shared__ uint64_t c_out;
+  __shared__ uint32_t c_run, c_pos, J_s, broken_s, verdict_s;
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+  if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
+  Stream s;
+  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
+  if (lt.dense[p]) return;  // the window path's (k_lv_probe)
+  const uint32_t n = s.n, w = (uint32_t)s.w;
+  const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
+  LvSeg* seg = lt.seg + s0;
+  if (n == 0 || nseg == 0) {  // nothing to read: no windows, no runs
+    if (tid == 0) {
+      lt.wfirst[lt.wbase[p] + p] = 0;
+      rt.pflag[p] = PF_WALK;
+    }
+    return;
   }
-#endif
-  if (verdict == 1 && sel == SS_DICT) verdict = 2;  // no window path for dictionary indices
-  if (verdict == 0) {
-    rt.pflag[p] = PF_WALK;
-  } else {
-    for (uint32_t q = 0; q < nseg; ++q) lt.seg[s0 + q].flags = 0;
-    if (verdict == 2) lv_bail(rt, p, PF_PAGE);
+  const uint32_t cap = LW_REC * (lt.wbase[p + 1] - lt.wbase[p] + 2u);
+  for (uint32_t q = tid; q < nseg; q += WG) seg[q].flags = 0;  // (the tables outlive a decode)
+  if (tid == 0) {
+    c_out = 0;
+    c_run = 0;
+    c_pos = 0xFFFFFFFFu;
+    J_s = 0xFFFFFFFFu;
+    broken_s = 0;
   }
+  __syncthreads();
+  // placement assuming the chain visits every segment in order; J = the first segment whose
+  // outputs reach n; the assumption holds when every segment before J landed on its successor
+  for (uint32_t c = 0; c < nseg; c += WG) {
+    const uint32_t j = c + tid;
+    const bool in = j < nseg;
+    uint64_t o = 0;
+    uint32_t r = 0, st = 0, nx = 0, lp = 0;
+    if (in) {
+      const LvSeg& sg = seg[j];
+      o = sg.out;
+      r = sg.runs;
+      st = sg.status;
+      nx = sg.next;
+      lp = sg.lastpos;
+    }
+    // inclusive scans over the workgroup: outputs, runs, last header of a non-empty segment
+    uint64_t io = o;
+    uint32_t ir = r, il = r ? j : 0xFFFFFFFFu;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t yo = __shfl_up(io, d, 64);
+      const uint32_t yr = __shfl_up(ir, d, 64);
+      const uint32_t yl = __shfl_up(il, d, 64);
+      if (lane >= (uint32_t)d) {
+        io += yo;
+        ir += yr;
+        il = il == 0xFFFFFFFFu ? yl : il;
+      }
+    }
+    if (lane == 63) {
+      wout[wid] = io;
+      wrun[wid] = ir;
+      wlast[wid] = il;
+    }
+    __syncthreads();
+    uint64_t bo = c_out;
+    uint32_t br = c_run, bl = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < wid; ++k) {
+      bo += wout[k];
+      br += wrun[k];
+      if (wlast[k] != 0xFFFFFFFFu) bl = wlast[k];
+    }
+    const uint64_t base_out = bo + io - o;
+    const uint32_t base_run = br + ir - r;
+    // last non-empty segment before j: within the wave (exclusive), earlier waves, earlier chunks
+    uint32_t ex = (uint32_t)__shfl_up((int)il, 1, 64);
+    if (lane == 0) ex = 0xFFFFFFFFu;
+    const uint32_t lastj = ex != 0xFFFFFFFFu ? ex : bl;
+    const uint32_t prevpos = lastj != 0xFFFFFFFFu ? seg[lastj].lastpos : c_pos;
+    const bool hit = in && base_out + o >= n;
+    const uint32_t jm = wave_min_u32(hit ? j : 0xFFFFFFFFu);
+    if (lane == 0) wmin[wid] = jm;
+    __syncthreads();
+    uint32_t J = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < WG / WAVE; ++k) J = min(J, wmin[k]);
+    if (in && j <= J) {
+      LvSeg& sg = seg[j];
+      sg.base_out = base_out;
+      sg.base_run = base_run;
+      sg.prevpos = prevpos;
+      const bool ok = st != LS_NOSTART && (j == J || (st == LS_LANDED && nx == j + 1));
+      if (!ok) atomicOr(&broken_s, 1u);
+      if (j < J) {
+        sg.keep = r;
+        sg.flags = 1;
+      }
+    }
+    (void)lp;
+    __syncthreads();
+    if (tid == WG - 1) {  // carries into the next chunk
+      c_out = bo + io;
+      c_run = br + ir;
+      const uint32_t lj = il != 0xFFFFFFFFu ? il : bl;
+      if (lj != 0xFFFFFFFFu) c_pos = seg[lj].lastpos;
+      J_s = J;
+    }
+    __syncthreads();
+    if (J_s != 0xFFFFFFFFu || broken_s) break;
+  }
+  if (tid == 0) {
+    uint32_t verdict;
+    const uint32_t J = J_s;
+    if (broken_s || J == 0xFFFFFFFFu) {
+      for (uint32_t q = 0; q < nseg; ++q) seg[q].flags = 0;
+      verdict = lv_segscan_serial(seg, lt.srec + (uint64_t)s0 * LW_SCAP, nseg, n, w, s.slen, cap);
+    } else {
+      LvSeg& sg = seg[J];
+      verdict = lv_seg_last(sg, lt.srec + (uint64_t)(s0 + J) * LW_SCAP, sg.base_out, sg.base_run, n, w, s.slen, cap);
+    }
+    if (verdict == 1 && sel == SS_DICT) verdict = 2;  // no window path for dictionary indices
+    verdict_s = verdict;
+    if (verdict == 0) rt.pflag[p] = PF_WALK;
+    else if (verdict == 2) lv_bail(rt, p, PF_PAGE);
+  }
+  __syncthreads();
+  if (verdict_s != 0)
+    for (uint32_t q = tid; q < nseg; q += WG) seg[q].flags = 0;
 }
 
 // ------------------------------------------------------------------------------ k_lv_compact
@@ -916,73 +1056,231 @@ __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob,
 }
 
 // ------------------------------------------------------------------------------ k_lv_stitch
-// One workgroup per dense page: the true entry and first output of every window of the page.
-// One lane follows the window tables from offset 0 (one lookup per window); the tables come
-// through LDS in chunks of STC_ENT entries, the next chunk loaded by the other waves while the
-// walker is on the current one, so a step costs an LDS read instead of a global round trip.
-constexpr uint32_t STC_ENT = 4096;  // table entries per LDS buffer (>= 4 windows of any width)
+// One 1024-thread workgroup per dense page: the true entry and first output of every window of
+// the page, i.e. the chain of window tables followed from offset 0. The tables come through LDS
+// in chunks of SC_ENT entries (the next chunk's loads in flight in registers meanwhile); within
+// a chunk every wave composes the tables of its m windows for all entry offsets at once (one
+// lane per entry: m LDS lookups), one wave then follows the chunk's wave compositions and every
+// wave walks its windows from its true entry, writing them. With at most 128 entry offsets per
+// window (bit widths 1 and 2) those two serial walks read the compositions and tables from
+// VGPRs (v_readlane: a few cycles per step instead of an LDS round trip). A chain that leaves
+// the composable form (a hop past the next window, a terminal code, a saturated count) before n
+// outputs is followed window by window by one lane, as the tables give it.
+constexpr uint32_t SC_ENT = 6144;   // table entries staged per chunk (48 KiB)
+constexpr uint32_t SC_FENT = 2048;  // composition entries (16 KiB)
+constexpr uint32_t SC_WG = 1024;
+constexpr uint32_t SC_NW = SC_WG / WAVE;
+constexpr uint32_t SC_MMAX = 6;     // windows per wave with readlane walks (EPL 1: 96 / 16)
+constexpr uint32_t SC_SPEC = 0x80000000u;  // composition left the composable form
 
-__global__ void __launch_bounds__(WG) k_lv_stitch(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                                  int npages, ColumnParams cp, int sel, RunTables rt,
-                                                  LevelTables lt) {
-  __shared__ uint2 buf[2][STC_ENT];
-  __shared__ uint32_t stop_s;
-  const uint32_t p = blockIdx.x, tid = threadIdx.x;
+__device__ inline bool lv_stitch_serial(const uint2* __restrict__ tab, uint2* win, uint32_t nw, uint32_t ent,
+                                        uint32_t n, uint32_t slen) {
+  uint32_t cur = 0, e = 0;
+  uint64_t acc = 0;
+  while (cur < nw) {
+    const uint2 t = tab[(uint64_t)cur * ent + e];
+    win[cur] = make_uint2(e | (t.x & 0xFFFF0000u), (uint32_t)acc);  // entry | headers << 16
+    acc += t.y;
+    if (acc >= n) return true;
+    const uint32_t jt = t.x & 0xFFFFu;
+    if (jt >= LV_J_FAR || t.y == 0xFFFFFFFFu) return false;  // far / end / dead, or a saturated count
+    const uint32_t q = cur * LV_WIN + jt;
+    cur = q / LV_WIN;
+    e = q - cur * LV_WIN;
+    if (q >= slen || cur >= nw || e >= ent) return false;  // the stream ends before n outputs, or an
+  }                                                         // entry past the table (foreign long runs)
+  return false;
+}
+
+// Lane e of an EPL-VGPR "table" (entry e = j * 64 + lane in VGPR j), e wave-uniform.
+template <uint32_t EPL>
+__device__ inline uint32_t sc_rl(const uint32_t (&v)[EPL], uint32_t e) {
+  if (EPL == 1) return (uint32_t)__builtin_amdgcn_readlane((int)v[0], (int)(e & 63u));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v[0], (int)(e & 63u));
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v[EPL - 1], (int)(e & 63u));
+  return e >= 64u ? b : a;
+}
+
+template <uint32_t EPL>  // entries per lane (ent / 64): 1, 2 (readlane walks) or 0 (any ent, LDS walks)
+__global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
+                                                     int npages, ColumnParams cp, int sel, RunTables rt,
+                                                     LevelTables lt) {
+  __shared__ uint2 tb[SC_ENT];
+  __shared__ uint2 F[SC_FENT];  // per composing wave and entry offset: (exit entry | SC_SPEC, outputs)
+  __shared__ uint32_t went[SC_NW];
+  __shared__ uint64_t wacc[SC_NW];
+  __shared__ uint64_t acc_s;
+  __shared__ uint32_t e_s, ok_s, serial_s, nv_s;
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   const PageWork& pw = pages[p];
   Stream s;
   if (!lv_stream(blob, pw, sel, cp, s)) return;
   const uint32_t k0 = lt.wbase[p], nw = lt.wbase[p + 1] - k0;
-  for (uint32_t k = tid; k < nw; k += WG) lt.win[k0 + k] = make_uint2(LV_NONE, 0u);
+  uint2* win = lt.win + k0;
+  for (uint32_t k = tid; k < nw; k += SC_WG) win[k] = make_uint2(LV_NONE, 0u);
   if (nw == 0) return;
-  const uint32_t ent = lv_ent((uint32_t)s.w), n = s.n, slen = s.slen;
-  const uint32_t CH = STC_ENT / ent, nch = (nw + CH - 1) / CH;
+  const uint32_t ent = EPL ? EPL * WAVE : lv_ent((uint32_t)s.w), n = s.n, slen = s.slen;
+  const uint32_t CW = SC_ENT / ent;                        // windows per chunk
+  const uint32_t amax = min(SC_NW, SC_FENT / ent);         // composing waves at most
+  const uint32_t m = (CW + amax - 1) / amax;               // windows per wave
+  const uint32_t A = (CW + m - 1) / m;                     // composing waves
+  const uint32_t nch = (nw + CW - 1) / CW;
   const uint2* tab = lt.tab + (uint64_t)k0 * ent;
-  auto load = [&](uint32_t c, uint2* b, uint32_t t0, uint32_t stride) {
-    const uint32_t cnt = min(CH, nw - c * CH) * ent;
-    const uint2* src = tab + (uint64_t)c * CH * ent;
-    for (uint32_t i = t0; i < cnt; i += stride) b[i] = src[i];
+  constexpr uint32_t PF = SC_ENT / SC_WG;
+  uint2 pf[PF];
+  auto fetch = [&](uint32_t c) {
+    const uint32_t cnt = min(CW, nw - c * CW) * ent;
+    const uint2* src = tab + (uint64_t)c * CW * ent;
+#pragma unroll
+    for (uint32_t i = 0; i < PF; ++i) {
+      const uint32_t idx = tid + i * SC_WG;
+      pf[i] = idx < cnt ? src[idx] : make_uint2(LV_J_DEAD, 0u);
+    }
   };
-  if (tid == 0) stop_s = 0;
-  load(0, buf[0], tid, WG);
-  __syncthreads();  // (also orders the NONE marks before the walker's writes)
-  uint32_t cur = 0, e = 0, ok = 0;  // walker (thread 0): next window on the chain, its entry
-  uint64_t acc = 0;
+  fetch(0);
+  if (tid == 0) {
+    acc_s = 0;
+    e_s = 0;
+    ok_s = serial_s = 0;
+  }
+  __syncthreads();  // (also orders the NONE marks before the window writes)
   for (uint32_t c = 0; c < nch; ++c) {
-    if (tid >= WAVE) {
-      if (c + 1 < nch) load(c + 1, buf[(c + 1) & 1], tid - WAVE, WG - WAVE);
-    } else if (tid == 0 && !stop_s) {
-      const uint2* b = buf[c & 1];
-      const uint32_t lo = c * CH, hi = min(nw, lo + CH);
-      uint32_t stop = 0;
-      while (cur < hi) {
-        const uint2 t = b[(cur - lo) * ent + e];
-        lt.win[k0 + cur] = make_uint2(e | (t.x & 0xFFFF0000u), (uint32_t)acc);  // entry | headers << 16
-        acc += t.y;
-        if (acc >= n) {
-          ok = 1;
-          stop = 1;
-          break;
+    const uint32_t cnt = min(CW, nw - c * CW), cw0 = c * CW;
+#pragma unroll
+    for (uint32_t i = 0; i < PF; ++i) tb[tid + i * SC_WG] = pf[i];
+    __syncthreads();
+    if (c + 1 < nch) fetch(c + 1);  // in flight while this chunk is composed and walked
+    // compositions: wave v over windows [v * m, v * m + m) of the chunk, every entry offset
+    const uint32_t wlo = wid * m, whi = min(cnt, wlo + m);
+    if (wid < A && wlo < cnt) {
+      for (uint32_t e = lane; e < ent; e += WAVE) {
+        uint32_t ce = e, out = 0, spec = 0;
+        for (uint32_t k = wlo; k < whi; ++k) {
+          const uint2 t = tb[k * ent + ce];
+          const uint32_t o2 = out + t.y;
+          out = o2 < out ? 0xFFFFFFFFu : o2;
+          const uint32_t jt = t.x & 0xFFFFu;
+          const uint32_t kn = cw0 + k + 1u;  // the page window the hop lands in, if composable
+          if (t.y == 0xFFFFFFFFu || jt < LV_WIN || jt >= 2u * LV_WIN || jt - LV_WIN >= ent || kn >= nw ||
+              kn * LV_WIN + (jt - LV_WIN) >= slen) {
+            spec = SC_SPEC;
+            break;
+          }
+          ce = jt - LV_WIN;
         }
-        const uint32_t jt = t.x & 0xFFFFu;
-        if (jt >= LV_J_FAR || t.y == 0xFFFFFFFFu) {  // far / end / dead, or a saturated count
-          stop = 1;
-          break;
-        }
-        const uint32_t q = cur * LV_WIN + jt;
-        cur = q / LV_WIN;
-        e = q - cur * LV_WIN;
-        if (q >= slen || cur >= nw || e >= ent) {  // the stream ends before n outputs, or an entry
-          stop = 1;                                // past the table (foreign long runs)
-          break;
-        }
+        F[wid * ent + e] = make_uint2(ce | spec, out);
       }
-      if (stop) stop_s = 1;
     }
     __syncthreads();
-    if (stop_s) break;
+    // the chunk's chain over the wave compositions
+    if (EPL) {
+      if (wid == 0) {
+        constexpr uint32_t E = EPL ? EPL : 1;
+        uint32_t fx[SC_NW][E], fy[SC_NW][E];
+#pragma unroll
+        for (uint32_t v = 0; v < SC_NW; ++v)
+#pragma unroll
+          for (uint32_t j = 0; j < E; ++j) {
+            const uint2 f = v < A ? F[v * ent + j * WAVE + lane] : make_uint2(0u, 0u);
+            fx[v][j] = f.x;
+            fy[v][j] = f.y;
+          }
+        uint32_t e = rfl(e_s), nv = 0, ok = 0, ser = 0;
+        uint64_t acc = acc_s;
+#pragma unroll
+        for (uint32_t v = 0; v < SC_NW; ++v) {
+          if (v < A && v * m < cnt && !ok && !ser) {
+            if (lane == v) {
+              went[v] = e;
+              wacc[v] = acc;
+            }
+            nv = v + 1;
+            const uint32_t x = sc_rl<E>(fx[v], e), y = sc_rl<E>(fy[v], e);
+            acc += y;
+            if (acc >= n) ok = 1;
+            else if (x & SC_SPEC) ser = 1;  // not composable before n: one lane follows the tables
+            else e = x;
+          }
+        }
+        if (lane == 0) {
+          e_s = e;
+          acc_s = acc;
+          ok_s = ok;
+          serial_s = ser;
+          nv_s = ser ? 0u : nv;
+        }
+      }
+    } else if (tid == 0) {
+      uint32_t e = e_s, nv = 0;
+      uint64_t acc = acc_s;
+      for (uint32_t v = 0; v < A && v * m < cnt; ++v) {
+        went[v] = e;
+        wacc[v] = acc;
+        nv = v + 1;
+        const uint2 f = F[v * ent + e];
+        acc += f.y;
+        if (acc >= n) {
+          ok_s = 1;
+          break;
+        }
+        if (f.x & SC_SPEC) {
+          serial_s = 1;
+          break;
+        }
+        e = f.x;
+      }
+      e_s = e;
+      acc_s = acc;
+      nv_s = serial_s ? 0u : nv;
+    }
+    __syncthreads();
+    // every wave on the chain walks its windows from its true entry
+    if (wid < nv_s) {
+      if (EPL) {
+        constexpr uint32_t E = EPL ? EPL : 1;
+        uint32_t tx[SC_MMAX][E], ty[SC_MMAX][E];
+#pragma unroll
+        for (uint32_t k = 0; k < SC_MMAX; ++k)
+#pragma unroll
+          for (uint32_t j = 0; j < E; ++j) {
+            const uint2 t = wlo + k < whi ? tb[(wlo + k) * ent + j * WAVE + lane] : make_uint2(0u, 0u);
+            tx[k][j] = t.x;
+            ty[k][j] = t.y;
+          }
+        uint32_t e = rfl(went[wid]);
+        uint64_t acc = wacc[wid];
+        bool done = false;
+#pragma unroll
+        for (uint32_t k = 0; k < SC_MMAX; ++k) {
+          if (wlo + k < whi && !done) {
+            const uint32_t x = sc_rl<E>(tx[k], e), y = sc_rl<E>(ty[k], e);
+            if (lane == 0) win[cw0 + wlo + k] = make_uint2(e | (x & 0xFFFF0000u), (uint32_t)acc);
+            acc += y;
+            if (acc >= n) done = true;
+            e = (x & 0xFFFFu) - LV_WIN;
+          }
+        }
+      } else if (lane == 0) {
+        uint32_t e = went[wid];
+        uint64_t acc = wacc[wid];
+        for (uint32_t k = wlo; k < whi; ++k) {
+          const uint2 t = tb[k * ent + e];
+          win[cw0 + k] = make_uint2(e | (t.x & 0xFFFF0000u), (uint32_t)acc);
+          acc += t.y;
+          if (acc >= n) break;
+          e = (t.x & 0xFFFFu) - LV_WIN;
+        }
+      }
+    }
+    __syncthreads();
+    if (ok_s || serial_s) break;
   }
-  if (tid == 0 && !ok) lv_bail(rt, p, PF_PAGE);
+  if (tid == 0) {
+    bool ok = ok_s != 0;
+    if (serial_s) ok = lv_stitch_serial(tab, win, nw, ent, n, slen);
+    if (!ok) lv_bail(rt, p, PF_PAGE);
+  }
 }
 
 // ------------------------------------------------------------------------------ output writers
@@ -1574,10 +1872,12 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
 // walked (PF_WALK, its run list built), dense (PF_PAGE) or handed back (PF_BAIL).
 static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ColumnParams cp,
                      int sel, int dict_page, RunTables rt, LevelTables lt, uint32_t wgrid, hipStream_t s) {
+  hipLaunchKernelGGL(k_lv_probe, dim3((npages + WG / WAVE - 1) / (WG / WAVE)), dim3(WG), 0, s, blob, blob_len, pages,
+                     npages, cp, sel, lt);
   hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
   hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segscan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segscan, dim3(npages), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
 }
 
@@ -1618,7 +1918,14 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
   }
   hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_stitch, dim3(npages), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  // window tables of 64 / 128 entry offsets (bit width 1 / 2) take the readlane walks
+  const int lw = sel == SS_DEF ? cp.def_bit_width : sel == SS_REP ? cp.rep_bit_width : 1;
+  if (lw == 1)
+    hipLaunchKernelGGL(k_lv_stitch<1>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  else if (lw == 2)
+    hipLaunchKernelGGL(k_lv_stitch<2>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  else
+    hipLaunchKernelGGL(k_lv_stitch<0>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
   if (sel == SS_BOOL) {
     hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
     hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,

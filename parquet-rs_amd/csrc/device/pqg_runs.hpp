@@ -272,15 +272,26 @@ struct IxCarry {
   uint32_t carry_j;     // records already written for carry_tile
 };
 
+// full != 0: every header of the batch is the writer's full bit-packed run (one byte 0x7F: 63
+// groups, 504 outputs, payload right after it), read by the walker's fast-forward, not staged.
 __device__ inline int32_t ix_batch(const uint32_t* region, uint32_t rbase, uint32_t posv, uint32_t k,
                                    uint32_t slen, uint32_t n, uint32_t w, RunCkpt* __restrict__ ck,
-                                   uint2* __restrict__ runs, uint32_t* __restrict__ nruns, IxCarry& cy) {
+                                   uint2* __restrict__ runs, uint32_t* __restrict__ nruns, IxCarry& cy,
+                                   bool full = false) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   const uint32_t produced = cy.produced, carry_tile = cy.carry_tile, carry_j = cy.carry_j;
   const bool in0 = lane < k;
   uint32_t nx, cnt = 0, inf = 0, flg = 0;
-  if (in0) run_parse(region, posv - rbase, posv, slen, (int)w, nx, cnt, inf, flg);
+  if (in0) {
+    if (full) {
+      cnt = 504u;
+      inf = posv + 1u;
+      flg = RF_BP;
+    } else {
+      run_parse(region, posv - rbase, posv, slen, (int)w, nx, cnt, inf, flg);
+    }
+  }
   // exclusive scan of counts
   uint64_t incl = cnt;
 #pragma unroll
@@ -395,8 +406,28 @@ __device__ inline int32_t run_index(const uint8_t* __restrict__ blob, uint64_t b
   uint32_t cur = 0;            // next header
   IxCarry cy{0u, 0u, 0u};
   const uint32_t& produced = cy.produced;
+  const uint32_t P = 1u + 63u * w;  // stream bytes of the writer's full bit-packed run
   while (true) {
     if (cur >= slen) return ST_EOF;  // reload() finds no more data: the reference stalls (A.4)
+    if (w > 2u && w <= 32u && slen - cur > P) {
+      // fast-forward (wide indices: unique or high-cardinality values leave no RLE runs): lane l
+      // reads the header byte l runs on; the prefix of full-run headers (0x7F) is the chain's
+      // next headers, recorded in one batch without staging their bytes
+      const uint32_t q = cur + lane * P;
+      const bool hit = q < slen && blob[S + q] == 0x7Fu;
+      const uint64_t m = __ballot(hit);
+      const uint32_t run = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u;
+      if (run >= 2u) {
+        const int32_t e = ix_batch(sm.region, 0u, q, run, slen, n, w, ck, runs, nruns, cy, true);
+        if (e) return e;
+        if (cy.produced >= n) {
+          flush();
+          return 0;
+        }
+        cur = rfl(cur + run * P);
+        continue;
+      }
+    }
     const uint32_t r = (off0 + cur) / IX_REG;
     if (r != cur_r) {
       if (r != pf_r) ix_fetch(blob, blob_len, G + (uint64_t)r * IX_REG, lane, pf);

@@ -100,7 +100,7 @@ struct Slot {
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
   // level path (def, rep, RLE booleans): buffers of LevelTables (pqg_internal.hpp), grown on demand
-  static constexpr int LV_BUFS = 11;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos
+  static constexpr int LV_BUFS = 12;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense
   void* lvbuf[3][LV_BUFS] = {};
   size_t lvcap[3][LV_BUFS] = {};
   LevelTables lt(int k) const {
@@ -116,6 +116,7 @@ struct Slot {
     t.seg = (LvSeg*)lvbuf[k][8];
     t.srec = (uint2*)lvbuf[k][9];
     t.spos = (uint32_t*)lvbuf[k][10];
+    t.dense = (uint32_t*)lvbuf[k][11];
     return t;
   }
 };
@@ -655,9 +656,10 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     const size_t nseg = nwin / LW_SEGW + npages + 1;  // segments, upper bound
     const size_t need[Slot::LV_BUFS] = {(size_t)npages + 1, (size_t)npages + 1, nwin + npages + 1,
                                         64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1,
-                                        (size_t)npages + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP};
+                                        (size_t)npages + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP,
+                                        (size_t)npages + 1};
     const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2),
-                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4};
+                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4};
     for (int b = 0; b < Slot::LV_BUFS; ++b)
       if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
   }

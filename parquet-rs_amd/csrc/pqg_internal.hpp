@@ -182,6 +182,8 @@ struct LevelTables {
   uint2* rec;        // [64 * (windows + 2 * pages)] walked pages' runs: (first output, info)
   uint2* tab;        // [windows * entries] per window and entry offset: (exit offset, outputs)
   uint2* win;        // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
+  uint32_t* dense;   // [pages] 1: the stream's first 64 headers lie within 1 KiB (k_lv_probe): the
+                     // window path takes it without a segment walk
 };
 
 // RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window
