@@ -470,12 +470,14 @@ def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
     t0 = time.perf_counter()
     for _ in range(steps):
         one_pass()
+    th = time.perf_counter()
     st, bcol, bad = ctx.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
     assert st == 0, (st, bcol, bad, ctx.error_message())
+    alltypes_steps.host_ms = (th - t0) / steps * 1e3  # enqueue time per step (host side)
     return (t1 - t0) / steps
 
 
@@ -584,6 +586,7 @@ def main_alltypes(args, world, rank, dist, stream):
                      "bytes_per_launch": step_bytes, "avg_ms": per_step * 1e3,
                      "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
         "value_check": checked,
+        "host_enqueue_ms_per_step": getattr(alltypes_steps, "host_ms", None),
     }
     if rank == 0 and args.pcie and world == 1:
         result["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)

@@ -14,8 +14,9 @@ constexpr int WAVE = 64;
 // workgroup reports first: the page status keeps the first code, the chunk keeps the
 // lowest bad page index.
 __device__ inline void report(PageWork* pages, ChunkResult* res, int page, int32_t code) {
-  atomicCAS(&pages[page].status, 0, code);
-  atomicMin(&res->first_bad_page, page);
+  // the code that sets the page's status is the one the chunk reports for it
+  if (atomicCAS(&pages[page].status, 0, code) == 0)
+    atomicMin((unsigned long long*)&res->bad, ((unsigned long long)(uint32_t)page << 32) | (uint32_t)code);
 }
 
 // Little-endian byte load from global memory, guarded by the blob size.

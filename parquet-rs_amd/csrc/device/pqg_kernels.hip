@@ -10,7 +10,6 @@
 //                    decoding.rs:256-315)
 //   k_plain_copy     PLAIN fixed-width values (decoding.rs:138-186, 228-247)
 //   k_plain_bool     PLAIN booleans (decoding.rs:188-204)
-//   k_finalize       chunk status
 //
 // All work is integer/byte movement bound by HBM: no MFMA. The general RLE/bit-packing hybrid
 // decoder (index pass + grid-wide expand pass) is in pqg_runs.hpp / pqg_texpand.hpp; level
@@ -68,18 +67,10 @@ __device__ inline int64_t v1_level_stream(const uint8_t* page, uint32_t nbytes, 
   return -1;  // LevelDecoder::v1 panics on other encodings (levels.rs:170)
 }
 
-// One wave per page: the lanes fill the page's tile -> page entries (a dictionary column's
-// single data page has thousands), lane 0 the rest.
-__global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                                                uint32_t* __restrict__ tile_page, ChunkResult* res) {
-  const int p = blockIdx.x;
-  if (p >= npages) return;
-  {
-    const uint32_t t0 = pages[p].ltile0, nt = pages[p].ntiles;
-    for (uint32_t k = threadIdx.x; k < nt; k += 64) tile_page[t0 + k] = (uint32_t)p;
-  }
-  if (threadIdx.x != 0) return;
+// Thread 0 of k_prepare: page p's layout (level streams, value section) into pages[p] and out.
+__device__ inline void prepare_page(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* __restrict__ pages,
+                                    int p, const ColumnParams& cp, ChunkResult* res, const PrepInit& ini,
+                                    PageWork& out) {
   PageWork pw = pages[p];
   const int32_t host_status = pw.status;  // set by the host for pages the reference rejects
   pw.rep_kind = pw.def_kind = LK_NONE;
@@ -89,6 +80,7 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
   int32_t err = 0;
   if (host_status) {
     pages[p].nonnull = 0;
+    out = pw;  // (status set: not probed)
     return;
   }
   if (pw.base + pw.nbytes > blob_len || pw.nbytes > 0x7FFFFFF0u) err = ST_INVALID_ARG;
@@ -136,9 +128,54 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
   // k_rle_levels), else the page's level count (column/reader.rs:212-226).
   bool data = pw.page_type == P_DATA || pw.page_type == P_DATA_V2;
   if (data && !(cp.max_def > 0 && cp.want_def)) pw.nonnull = pw.num_values;
+  if (!err && p == ini.dict_page && ini.dict_es > 0) {  // DictDecoder::set_dict (was k_dict_check)
+    if (pw.encoding != E_PLAIN && pw.encoding != E_PLAIN_DICTIONARY) err = ST_NYI;
+    else if ((uint64_t)pw.num_values * (uint64_t)ini.dict_es > pw.nbytes) err = ST_EOF;
+  }
   pw.status = err;
   pages[p] = pw;
-  if (err) atomicMin(&res->first_bad_page, p);
+  out = pw;
+  if (err) atomicMin((unsigned long long*)&res->bad, ((unsigned long long)(uint32_t)p << 32) | (uint32_t)err);
+}
+
+// One wave per page: the lanes fill the page's tile -> page entries (a dictionary column's
+// single data page has thousands), lane 0 the rest.
+__global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                PageWork* __restrict__ pages, int npages, ColumnParams cp,
+                                                uint32_t* __restrict__ tile_page, ChunkResult* res, PrepInit ini) {
+  const int p = blockIdx.x;
+  if (p >= npages) return;
+  {
+    const uint32_t t0 = pages[p].ltile0, nt = pages[p].ntiles;
+    for (uint32_t k = threadIdx.x; k < nt; k += 64) tile_page[t0 + k] = (uint32_t)p;
+  }
+  __shared__ PageWork pw_s;
+  if (threadIdx.x == 0) {
+    prepare_page(blob, blob_len, pages, p, cp, res, ini, pw_s);
+    if (p == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (ini.word[i]) *ini.word[i] = ini.val[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (ini.pzero[i]) ini.pzero[i][p] = 0;
+    if (ini.dense_zero) ini.dense_zero[p] = 0;
+  }
+  __syncthreads();
+  // density probes of the level streams just located (wave-uniform from here)
+  for (int k = 0; k < 2; ++k) {
+    uint32_t* dn = k == 0 ? ini.dense_def : ini.dense_rep;
+    if (!dn) continue;
+    const PageWork& pw = pw_s;
+    const bool data = pw.page_type == P_DATA || pw.page_type == P_DATA_V2;
+    const int kind = k == 0 ? pw.def_kind : pw.rep_kind;
+    const uint32_t slen = k == 0 ? pw.def_bytes : pw.rep_bytes;
+    const uint32_t w = (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width);
+    uint32_t dense = 0;
+    if (data && pw.status == 0 && kind == LK_RLE && w >= 1 && w <= 16 && pw.num_values && slen >= PROBE_SPAN + 64u)
+      dense = lv_probe_dense(blob, blob_len, pw.base + (k == 0 ? pw.def_off : pw.rep_off), w);
+    if (threadIdx.x == 0) dn[p] = dense;
+  }
 }
 
 // ------------------------------------------------------------------------------ hybrid streams
@@ -335,18 +372,6 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages,
 
 // ------------------------------------------------------------------------------ dictionary
 
-// Dictionary page checks (decoding.rs:282-288 + PlainDecoder::get EOF, :145-147).
-__global__ void k_dict_check(PageWork* pages, int dict_page, int es, ChunkResult* res) {
-  if (threadIdx.x != 0 || dict_page < 0) return;
-  PageWork dp = pages[dict_page];
-  if (dp.status) return;
-  if (dp.encoding != E_PLAIN && dp.encoding != E_PLAIN_DICTIONARY) {
-    report(pages, res, dict_page, ST_NYI);
-    return;
-  }
-  if ((uint64_t)dp.num_values * (uint64_t)es > dp.nbytes) report(pages, res, dict_page, ST_EOF);
-}
-
 // ------------------------------------------------------------------------------ PLAIN
 
 // Copies each page's `nonnull * es` value bytes to out + value_out * es. grid.y = page,
@@ -428,14 +453,6 @@ __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ b
   }
 }
 
-// ------------------------------------------------------------------------------ finalize
-
-__global__ void k_finalize(PageWork* pages, ChunkResult* res) {
-  if (threadIdx.x != 0) return;
-  int b = res->first_bad_page;
-  res->status = (b != 0x7FFFFFFF) ? pages[b].status : 0;
-}
-
 // ------------------------------------------------------------------------------ launchers
 
 extern "C" {
@@ -446,8 +463,8 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
 
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                               int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
-                              hipStream_t s) {
-  hipLaunchKernelGGL(k_prepare, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, npages, cp, tile_page, res);
+                              PrepInit ini, hipStream_t s) {
+  hipLaunchKernelGGL(k_prepare, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, npages, cp, tile_page, res, ini);
   return hipGetLastError();
 }
 
@@ -512,7 +529,7 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
                            uint32_t ntiles, ColumnParams cp, int dict_page, int es,
                            const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
                            ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
-  hipLaunchKernelGGL(k_dict_check, dim3(1), dim3(64), 0, s, pages, dict_page, es, res);
+  // (the dictionary page's checks ran in k_prepare)
   bool lvpath = es == 4 || es == 8;
 #ifdef PQG_DIAG
   if (cp.debug & 256) lvpath = false;
@@ -580,10 +597,6 @@ hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork*
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_finalize(PageWork* pages, ChunkResult* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, pages, res);
-  return hipGetLastError();
-}
 
 }  // extern "C"
 

@@ -274,50 +274,18 @@ __device__ inline void lv_scan_windows(int npages, uint32_t* wbase, F nwin_of) {
 }
 
 // ------------------------------------------------------------------------------ k_lv_probe
-// One wave per page of a level stream: walks the chain from offset 0 over the first KiB, held
-// in VGPRs (16 bytes per lane; header bytes read by v_readlane, so a hop costs a few scalar
-// cycles). When its first 64 headers lie within 1 KiB (short RLE runs: the segment walk would
-// stop there as dense, LS_DENSE), the page goes to the window path directly (lt.dense).
-// Dictionary indices have no window path and are not probed.
-__device__ inline uint32_t probe_dw(const uint32_t (&d)[4], uint32_t i) {  // dword i of the KiB (uniform)
-  const int l = (int)(i >> 2);
-  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d[0], l), b = (uint32_t)__builtin_amdgcn_readlane((int)d[1], l),
-                 c = (uint32_t)__builtin_amdgcn_readlane((int)d[2], l), e = (uint32_t)__builtin_amdgcn_readlane((int)d[3], l);
-  const uint32_t k = i & 3u;
-  return k == 0 ? a : k == 1 ? b : k == 2 ? c : e;
-}
-
+// One wave per page of an RLE boolean stream: the density probe (pqg_runs.hpp lv_probe_dense);
+// the def / rep streams are probed by k_prepare, dictionary indices (no window path) never.
 __global__ void __launch_bounds__(WG) k_lv_probe(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                  const PageWork* __restrict__ pages, int npages, ColumnParams cp,
                                                  int sel, LevelTables lt) {
-  const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;  // (uniform: scalar readlane indices)
   const uint32_t p = blockIdx.x * (WG / WAVE) + wid;
   if (p >= (uint32_t)npages) return;
   Stream st;
   uint32_t dense = 0;
-  if (sel != SS_DICT && lv_stream(blob, pages[p], sel, cp, st) && st.n && st.slen >= LW_SPAN + 64u) {
-    // 64 lanes x 16 bytes from the stream start, aligned down (the KiB plus up to 15 bytes before)
-    const uint64_t A = st.S & ~15ull;
-    const uint32_t sb = (uint32_t)(st.S - A);
-    const uint64_t a = A + (uint64_t)lane * 16u;
-    const uint4 v = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t w = (uint32_t)st.w, vb = (w + 7u) >> 3;
-    uint32_t q = 0, k = 0;
-    while (k < 64u && q + 20u < LW_SPAN) {  // header bytes q .. q + 3 (+ alignment) stay in the staged KiB
-      const uint32_t r = q + sb;
-      const uint32_t x = __builtin_amdgcn_alignbit(probe_dw(d, (r >> 2) + 1u), probe_dw(d, r >> 2), (r & 3u) * 8u);
-      const uint32_t c0 = (x >> 7) & 1u, c1 = (x >> 15) & 1u, c2 = (x >> 23) & 1u, c3 = x >> 31;
-      const uint32_t c01 = c0 & c1, c012 = c01 & c2;
-      if (c012 & c3) break;  // a varint the fast parse does not take
-      const uint32_t hl = 1u + c0 + c01 + c012;
-      const uint32_t h = (x & 0x7Fu) | (c0 ? ((x >> 1) & 0x3F80u) : 0u) | (c01 ? ((x >> 2) & 0x1FC000u) : 0u) |
-                         (c012 ? ((x >> 3) & 0xFE00000u) : 0u);
-      q += (h & 1u) ? hl + (h >> 1) * w : hl + vb;
-      ++k;
-    }
-    dense = k == 64u && q < LW_SPAN;
-  }
+  if (lv_stream(blob, pages[p], sel, cp, st) && st.n && st.slen >= LW_SPAN + 64u)
+    dense = lv_probe_dense(blob, blob_len, st.S, rfl((uint32_t)st.w));
   if (lane == 0) lt.dense[p] = dense;
 }
 
@@ -1872,8 +1840,9 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
 // walked (PF_WALK, its run list built), dense (PF_PAGE) or handed back (PF_BAIL).
 static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ColumnParams cp,
                      int sel, int dict_page, RunTables rt, LevelTables lt, uint32_t wgrid, hipStream_t s) {
-  hipLaunchKernelGGL(k_lv_probe, dim3((npages + WG / WAVE - 1) / (WG / WAVE)), dim3(WG), 0, s, blob, blob_len, pages,
-                     npages, cp, sel, lt);
+  if (sel == SS_BOOL)  // (def / rep: k_prepare probed them; dictionary indices: cleared there)
+    hipLaunchKernelGGL(k_lv_probe, dim3((npages + WG / WAVE - 1) / (WG / WAVE)), dim3(WG), 0, s, blob, blob_len,
+                       pages, npages, cp, sel, lt);
   hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
   hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);

@@ -223,6 +223,46 @@ __device__ inline void run_parse_global(const uint8_t* blob, uint64_t blob_len, 
   run_parse(tmp, 0, q, slen, w, nxt, cnt, inf, flg);
 }
 
+// ------------------------------------------------------------------------------ density probe
+// Whole wave: the chain of a level stream from offset 0 over its first KiB, held in VGPRs (16
+// bytes per lane; header bytes read by v_readlane, so a hop costs a few scalar cycles). True when
+// its first 64 headers lie within 1 KiB (short RLE runs: the level path's segment walk would stop
+// there as dense), i.e. the stream belongs to the level path's window kernels (pqg_levels.hip).
+// S, slen, w must be wave-uniform; the caller checks slen >= 1088.
+__device__ inline uint32_t probe_dw(const uint32_t (&d)[4], uint32_t i) {  // dword i of the KiB (uniform)
+  const int l = (int)(i >> 2);
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d[0], l), b = (uint32_t)__builtin_amdgcn_readlane((int)d[1], l),
+                 c = (uint32_t)__builtin_amdgcn_readlane((int)d[2], l), e = (uint32_t)__builtin_amdgcn_readlane((int)d[3], l);
+  const uint32_t k = i & 3u;
+  return k == 0 ? a : k == 1 ? b : k == 2 ? c : e;
+}
+
+constexpr uint32_t PROBE_SPAN = 1024;  // 64 headers within fewer bytes: dense
+
+__device__ inline bool lv_probe_dense(const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t S, uint32_t w) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t A = S & ~15ull;
+  const uint32_t sb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S - A));
+  const uint64_t a = A + (uint64_t)lane * 16u;
+  const uint4 v = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t vb = (w + 7u) >> 3;
+  uint32_t q = 0, k = 0;
+  while (k < 64u && q + 20u < PROBE_SPAN) {  // header bytes q .. q + 3 (+ alignment) stay in the staged KiB
+    const uint32_t r = q + sb;
+    const uint32_t x = __builtin_amdgcn_alignbit(probe_dw(d, (r >> 2) + 1u), probe_dw(d, r >> 2), (r & 3u) * 8u);
+    const uint32_t c0 = (x >> 7) & 1u, c1 = (x >> 15) & 1u, c2 = (x >> 23) & 1u, c3 = x >> 31;
+    const uint32_t c01 = c0 & c1, c012 = c01 & c2;
+    if (c012 & c3) break;  // a varint the fast parse does not take
+    const uint32_t hl = 1u + c0 + c01 + c012;
+    const uint32_t h = (x & 0x7Fu) | (c0 ? ((x >> 1) & 0x3F80u) : 0u) | (c01 ? ((x >> 2) & 0x1FC000u) : 0u) |
+                       (c012 ? ((x >> 3) & 0xFE00000u) : 0u);
+    q += (h & 1u) ? hl + (h >> 1) * w : hl + vb;
+    ++k;
+  }
+  return k == 64u && q < PROBE_SPAN;
+}
+
 // ------------------------------------------------------------------------------ index pass
 
 struct IndexSmem {

@@ -21,7 +21,7 @@ using namespace pqg;
 
 extern "C" {
 hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, uint32_t*,
-                              ChunkResult*, hipStream_t);
+                              ChunkResult*, PrepInit, hipStream_t);
 hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
                                 RunTables, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
@@ -41,7 +41,6 @@ hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_
                                hipStream_t);
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
-hipError_t pqg_launch_finalize(PageWork*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_space(const int16_t*, uint64_t, int16_t, const void*, int, uint64_t*, void*, hipStream_t);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
                                   DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t,
@@ -191,9 +190,9 @@ static int finish_slot(Slot& sl, int* page_out, std::string& msg) {
   out->num_values = r.total_values;
   out->num_bytes = r.total_bytes;
   int st = 0, page = -1;
-  if (r.first_bad_page != 0x7FFFFFFF) {
-    page = r.first_bad_page;
-    st = r.status;
+  if (r.bad != ~0ull) {
+    page = (int)(r.bad >> 32);
+    st = (int)(uint32_t)r.bad;
   }
   if (sl.host_status && (page < 0 || sl.host_bad_page <= page)) {
     page = sl.host_bad_page;
@@ -436,19 +435,22 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   sl.host_status = 0;
   sl.host_bad_page = -1;
   sl.host_msg.clear();
+  // page table and the chunk result go up in one copy: the result sits after the pages
+  const size_t res_off = ((size_t)npages * sizeof(PageWork) + 63) & ~(size_t)63;
   if (npages > sl.pages_cap) {
     size_t cap = npages < 1024 ? 1024 : npages;
     hipFree(sl.d_pages);
     hipHostFree(sl.h_pages);
     sl.d_pages = nullptr;
     sl.h_pages = nullptr;
-    HIPCHK(hipMalloc(&sl.d_pages, cap * sizeof(PageWork)), "hipMalloc pages");
-    HIPCHK(hipHostMalloc(&sl.h_pages, cap * sizeof(PageWork), hipHostMallocDefault), "hipHostMalloc");
+    const size_t bytes = ((cap * sizeof(PageWork) + 63) & ~(size_t)63) + sizeof(ChunkResult);
+    HIPCHK(hipMalloc(&sl.d_pages, bytes), "hipMalloc pages");
+    HIPCHK(hipHostMalloc(&sl.h_pages, bytes, hipHostMallocDefault), "hipHostMalloc");
     sl.pages_cap = cap;
   }
   ctx->d_pages = sl.d_pages;
   ctx->h_pages = sl.h_pages;
-  ctx->d_res = sl.d_res;
+  ctx->d_res = (ChunkResult*)((char*)sl.d_pages + res_off);
   ctx->h_res = sl.h_res;
   ctx->ev = sl.ev;
   sl.kl = sl.kv = false;
@@ -536,11 +538,11 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
 
   ChunkResult r0{};
   r0.total_levels = sl.total_levels;
-  r0.first_bad_page = 0x7FFFFFFF;
+  r0.bad = ~0ull;
   r0.dict_page = dict_page < 0 ? 0xFFFFFFFFu : (uint32_t)dict_page;
-  *ctx->h_res = r0;
-  if (npages) HIPCHK(hipMemcpyAsync(ctx->d_pages, ctx->h_pages, npages * sizeof(PageWork), hipMemcpyHostToDevice, s), "H2D pages");
-  HIPCHK(hipMemcpyAsync(ctx->d_res, ctx->h_res, sizeof(ChunkResult), hipMemcpyHostToDevice, s), "H2D res");
+  *(ChunkResult*)((char*)ctx->h_pages + res_off) = r0;
+  HIPCHK(hipMemcpyAsync(ctx->d_pages, ctx->h_pages, res_off + sizeof(ChunkResult), hipMemcpyHostToDevice, s),
+         "H2D pages");
 
   const bool is_ba = t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY;
   const int es = is_ba ? 0 : value_size(t, col->type_length);
@@ -625,9 +627,6 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (want_rep) HIPCHK(tables(1), "hipMalloc run tables");
   if (hybrid_values && out->values) HIPCHK(tables(2), "hipMalloc run tables");
   const uint32_t nt = total_tiles;
-  if (ctx->timing) hipEventRecord(ctx->ev[0], s);
-  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, s), "prepare");
-  if (ctx->timing) hipEventRecord(ctx->ev[1], s);
   // Level path buffers (normalized streams) per stream kind, grown on demand.
   const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
   // 4- / 8-byte dictionary values: their index streams take the same path (pqg_launch_dict)
@@ -664,13 +663,56 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
   }
   // Hybrid-stream flags: the level path (def, rep, RLE booleans) sets every page's flag and counts
-  // the streams it hands back; dictionary indices always take the general decoder.
+  // the streams it hands back; dictionary indices always take the general decoder. k_prepare
+  // sets them (no memset launches), and runs the fixed-width dictionary page's checks.
+  PrepInit ini{};
+  int nw_ = 0, nz = 0;
   for (int k = 0; k < 3; ++k) {
     if (!sl.rt[k].nfall) continue;
     const bool lvpath = k < 2 || rle_bool || dict_lv;
-    HIPCHK(hipMemsetAsync(sl.rt[k].nfall, lvpath ? 0 : 0xFF, sizeof(uint32_t), s), "memset fallback count");
-    if (!lvpath && np) HIPCHK(hipMemsetAsync(sl.rt[k].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
+    ini.word[nw_] = sl.rt[k].nfall;
+    ini.val[nw_++] = lvpath ? 0u : 0xFFFFFFFFu;
+    if (!lvpath) ini.pzero[nz++] = sl.rt[k].pflag;
   }
+  uint8_t* vo = (uint8_t*)out->values;
+  const bool delta_vals = np && vo && !is_ba && enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64);
+  if (delta_vals) {  // DELTA_BINARY_PACKED tables (tiled fallback path), grown on demand
+    if (nt > sl.dt_tcap || (size_t)np > sl.dt_pcap) {
+      hipFree(sl.dt.page);
+      hipFree(sl.dt.blocks);
+      hipFree(sl.dt.agg);
+      hipFree(sl.dt.inc);
+      hipFree(sl.dt.flag);
+      hipFree(sl.dt.nfall);
+      sl.dt = DeltaTables{};
+      sl.dt_tcap = sl.dt_pcap = 0;
+      const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
+      HIPCHK(hipMalloc(&sl.dt.page, pc * sizeof(DeltaPage)), "hipMalloc delta pages");
+      HIPCHK(hipMalloc(&sl.dt.blocks, tc * DELTA_BCAP * sizeof(DeltaBlock)), "hipMalloc delta blocks");
+      HIPCHK(hipMalloc(&sl.dt.agg, tc * sizeof(uint64_t)), "hipMalloc delta agg");
+      HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
+      HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
+      HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
+      HIPCHK(hipMemsetAsync(sl.dt.flag, 0, tc * sizeof(uint32_t), s), "memset delta flags");
+      sl.dt_tcap = tc;
+      sl.dt_pcap = pc;
+    }
+    ctx->epoch = (ctx->epoch + 1) & 0x3FFFFFFFu;
+    if (ctx->epoch == 0) {  // wrapped: flags from 2^30 decodes ago could match
+      HIPCHK(hipMemsetAsync(sl.dt.flag, 0, sl.dt_tcap * sizeof(uint32_t), s), "memset delta flags");
+      ctx->epoch = 1;
+    }
+    ini.word[nw_] = sl.dt.nfall;
+    ini.val[nw_++] = 0u;
+  }
+  ini.dict_page = dict_page;
+  ini.dict_es = (np && vo && !is_ba && enc_present[PQG_RLE_DICTIONARY]) ? es : 0;
+  ini.dense_def = need_lv[0] ? sl.lt(0).dense : nullptr;
+  ini.dense_rep = need_lv[1] ? sl.lt(1).dense : nullptr;
+  ini.dense_zero = (need_lv[2] && dict_lv) ? sl.lt(2).dense : nullptr;
+  if (ctx->timing) hipEventRecord(ctx->ev[0], s);
+  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, ini, s), "prepare");
+  if (ctx->timing) hipEventRecord(ctx->ev[1], s);
   if (np && want_def) {
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              sl.lt(0), out->def_levels, ctx->d_res, s,
@@ -685,7 +727,6 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
   HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
-  uint8_t* vo = (uint8_t*)out->values;
   ctx->values_kernel = 0;
   if (np && vo && is_ba) {
     ctx->values_kernel = enc_present[PQG_RLE_DICTIONARY] ? PQG_RLE_DICTIONARY
@@ -696,13 +737,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (enc_present[PQG_RLE_DICTIONARY]) {
       HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
                                      ctx->d_res, s), "byte-array dictionary");
-      if (badict_lv) {  // (nfall 0: the flags the plan sets decide which pages the index pass takes)
+      if (badict_lv)  // (nfall 0: the flags the plan sets decide which pages the index pass takes)
         HIPCHK(pqg_launch_lv_badict(blob, blob_len, ctx->d_pages, np, cp, dict_page, sl.rt[2], sl.lt(2), sl.dsrc,
                                     sl.dlen, sl.vsrc, sl.vlen, ctx->d_res, s), "dictionary indices");
-      } else {
-        HIPCHK(hipMemsetAsync(sl.rt[2].pflag, 0, (size_t)np * sizeof(uint32_t), s), "memset page flags");
-        HIPCHK(hipMemsetAsync(sl.rt[2].nfall, 0xFF, sizeof(uint32_t), s), "memset fallback count");
-      }
       HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
                                   sl.rt[2], ctx->d_res, s), "dictionary index pass");
       HIPCHK(pqg_launch_tile_desc(blob, ctx->d_pages, nt, sl.tile_page, sl.rt[2], cp, 2, dict_page, s),
@@ -734,35 +771,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
                              sl.rt[2], sl.lt(2), vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "dict");
       sl.kv = ctx->timing;
     }
-    if (enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) {
+    if (delta_vals) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
-      if (nt > sl.dt_tcap || (size_t)np > sl.dt_pcap) {
-        hipFree(sl.dt.page);
-        hipFree(sl.dt.blocks);
-        hipFree(sl.dt.agg);
-        hipFree(sl.dt.inc);
-        hipFree(sl.dt.flag);
-        hipFree(sl.dt.nfall);
-        sl.dt = DeltaTables{};
-        sl.dt_tcap = sl.dt_pcap = 0;
-        const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
-        HIPCHK(hipMalloc(&sl.dt.page, pc * sizeof(DeltaPage)), "hipMalloc delta pages");
-        HIPCHK(hipMalloc(&sl.dt.blocks, tc * DELTA_BCAP * sizeof(DeltaBlock)), "hipMalloc delta blocks");
-        HIPCHK(hipMalloc(&sl.dt.agg, tc * sizeof(uint64_t)), "hipMalloc delta agg");
-        HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
-        HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
-        HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
-        HIPCHK(hipMemsetAsync(sl.dt.flag, 0, tc * sizeof(uint32_t), s), "memset delta flags");
-        sl.dt_tcap = tc;
-        sl.dt_pcap = pc;
-      }
-      ctx->epoch = (ctx->epoch + 1) & 0x3FFFFFFFu;
-      if (ctx->epoch == 0) {  // wrapped: flags from 2^30 decodes ago could match
-        HIPCHK(hipMemsetAsync(sl.dt.flag, 0, sl.dt_tcap * sizeof(uint32_t), s), "memset delta flags");
-        ctx->epoch = 1;
-      }
       sl.dt.dbg = (cp.debug & 32) ? cp.dbgbuf : nullptr;
-      HIPCHK(hipMemsetAsync(sl.dt.nfall, 0, sizeof(uint32_t), s), "memset delta fallback count");
       HIPCHK(pqg_launch_delta_tiled(blob, blob_len, ctx->d_pages, np, nt, sl.tile_page, sl.dt, ctx->epoch,
                                     es, vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "delta");
       sl.kv = true;
@@ -774,7 +785,6 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
   }
   if (ctx->timing) hipEventRecord(ctx->ev[4], s);
-  HIPCHK(pqg_launch_finalize(ctx->d_pages, ctx->d_res, s), "finalize");
   HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(ChunkResult), hipMemcpyDeviceToHost, s), "D2H res");
   HIPCHK(hipEventRecord(ctx->ev[5], s), "event");
   sl.used = true;

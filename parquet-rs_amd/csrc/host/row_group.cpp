@@ -8,16 +8,71 @@
 // own pqg_ctx (own staging and scratch, reused across row groups), places the chunks on the
 // streams by estimated bytes (longest first onto the least-loaded stream) and joins the streams
 // back into the caller's stream. Results per column are delivered by pqg_rg_sync.
+//
+// Enqueueing a chunk decode costs the host ~3 us per kernel launch (~30 launches): for 8M-row
+// row groups that is as long as the GPU work itself, so every stream has a host worker thread
+// that issues its columns' decodes; the streams' submissions then proceed in parallel.
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/pqgpu.h"
+
+// One host thread per stream: runs the enqueue jobs handed to it, one batch per decode call.
+struct RgWorker {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::function<void()>> jobs;
+  bool busy = false, quit = false;
+  int device = 0;
+
+  void start(int dev) {
+    device = dev;
+    th = std::thread([this] {
+      hipSetDevice(device);
+      std::unique_lock<std::mutex> lk(mu);
+      while (true) {
+        cv.wait(lk, [this] { return quit || busy; });
+        if (quit) return;
+        std::vector<std::function<void()>> todo;
+        todo.swap(jobs);
+        lk.unlock();
+        for (auto& f : todo) f();
+        lk.lock();
+        busy = false;
+        cv.notify_all();
+      }
+    });
+  }
+  void run(std::vector<std::function<void()>>&& j) {
+    std::lock_guard<std::mutex> lk(mu);
+    jobs = std::move(j);
+    busy = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !busy; });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+  }
+};
 
 struct pqg_rg_ctx {
   int device = 0;
@@ -26,6 +81,8 @@ struct pqg_rg_ctx {
   hipEvent_t fork = nullptr;
   std::vector<pqg_ctx*> cols;   // one decode context per column index
   std::vector<int> issued;      // decodes pending per column
+  std::vector<RgWorker*> workers;
+  uint64_t calls = 0;           // decode calls: rotates the stream assignment
   std::string msg;
 };
 
@@ -56,6 +113,10 @@ int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx** out) {
     pqg_rg_ctx_destroy(g);
     return PQG_ERR_HIP;
   }
+  for (int k = 0; k < nstreams; ++k) {
+    g->workers.push_back(new RgWorker());
+    g->workers.back()->start(device);
+  }
   *out = g;
   return PQG_OK;
 }
@@ -63,6 +124,10 @@ int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx** out) {
 int pqg_rg_ctx_destroy(pqg_rg_ctx* g) {
   if (!g) return PQG_OK;
   hipSetDevice(g->device);
+  for (RgWorker* w : g->workers) {
+    w->stop();
+    delete w;
+  }
   for (pqg_ctx* c : g->cols) pqg_ctx_destroy(c);  // waits for its decodes
   for (hipStream_t s : g->streams) hipStreamDestroy(s);
   for (hipEvent_t e : g->join) hipEventDestroy(e);
@@ -100,17 +165,37 @@ int pqg_rg_decode(pqg_rg_ctx* g, uint32_t ncols, const pqg_column* cols, const u
     work[j] = {b + (double)outs[j].values_capacity, j};
   }
   std::sort(work.begin(), work.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  // least-loaded stream first; the streams are rotated per call so that the same column of
+  // consecutive row groups lands on different streams (its decodes can then overlap)
   std::vector<double> load(K, 0.0);
-  int first_err = PQG_OK;
+  std::vector<std::vector<uint32_t>> per(K);
+  const size_t rot = (size_t)((g->calls++ * ncols) % K);
   for (const auto& wj : work) {
-    const uint32_t j = wj.second;
-    const size_t k = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+    size_t best = 0;
+    for (size_t i = 1; i < K; ++i)
+      if (load[(rot + i) % K] < load[(rot + best) % K]) best = i;
+    const size_t k = (rot + best) % K;
     load[k] += wj.first;
-    const int st = pqg_decode_chunk(g->cols[j], &cols[j], blob, blob_len, pages[j], npages[j], &outs[j],
-                                    g->streams[k]);
-    if (st) {
+    per[k].push_back(wj.second);
+  }
+  // every stream's decodes enqueued by its own host thread
+  std::vector<int> st(ncols, PQG_OK);
+  for (size_t k = 0; k < K; ++k) {
+    if (per[k].empty()) continue;
+    std::vector<std::function<void()>> jobs;
+    for (uint32_t j : per[k])
+      jobs.push_back([=, &st] {
+        st[j] = pqg_decode_chunk(g->cols[j], &cols[j], blob, blob_len, pages[j], npages[j], &outs[j], g->streams[k]);
+      });
+    g->workers[k]->run(std::move(jobs));
+  }
+  for (size_t k = 0; k < K; ++k)
+    if (!per[k].empty()) g->workers[k]->wait();
+  int first_err = PQG_OK;
+  for (uint32_t j = 0; j < ncols; ++j) {
+    if (st[j]) {
       if (!first_err) {
-        first_err = st;
+        first_err = st[j];
         char buf[320];
         snprintf(buf, sizeof(buf), "column %u: %s", j, pqg_error_message(g->cols[j]));
         g->msg = buf;

@@ -65,12 +65,27 @@ struct PageWork {
 };
 
 // Chunk-level result, copied to pinned host memory at the end of a decode.
+// Scalar state k_prepare sets before any other kernel of the decode runs (in place of memset
+// launches): counters to a value, per-page flag arrays to 0, and the dictionary page check of
+// fixed-width dictionaries (dict_es: value size, 0 = none; decoding.rs:282-288, :145-147).
+struct PrepInit {
+  uint32_t* word[4];
+  uint32_t val[4];
+  uint32_t* pzero[3];
+  int32_t dict_page;
+  int32_t dict_es;
+  // level-path density probe (LevelTables::dense) of the def / rep streams, run by k_prepare's
+  // wave right after it locates them; dense_zero: a stream kind's array cleared instead
+  uint32_t* dense_def;
+  uint32_t* dense_rep;
+  uint32_t* dense_zero;
+};
+
 struct ChunkResult {
   uint64_t total_levels;
   uint64_t total_values;
   uint64_t total_bytes;
-  int32_t first_bad_page;  // INT32_MAX when clean
-  int32_t status;
+  uint64_t bad;            // lowest failing page and its status: (page << 32) | status; ~0 when clean
   uint32_t dict_page;      // index of the dictionary page or UINT32_MAX
   uint32_t pad;
 };
