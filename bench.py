@@ -315,10 +315,15 @@ def pcie_inclusive(ctx, w, stream, iters=3):
             "note": "pinned H2D of page bytes + decode + D2H of decoded levels/values, best of %d" % iters}
 
 
+LEVEL_PATH = ("k_lv_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
+
+
 def pmc_traffic(kind, kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this config
     (profiles/<round>/<config>/kernels.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 +
-    WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). None when not profiled."""
+    WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). The def-level path is a chain of
+    kernels timed as one (HIP events around pqg_launch_levels): its traffic is their sum (every
+    kernel of the chain runs once per decode). None when not profiled."""
     base = kernel.split("<")[0]
     for rnd in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True):
         path = os.path.join(ROOT, "profiles", rnd, kind, "kernels.json")
@@ -328,8 +333,14 @@ def pmc_traffic(kind, kernel):
             ks = json.load(open(path))["kernels"]
         except (OSError, ValueError, KeyError):
             continue
-        for k, e in ks.items():
-            if k.replace("pqg::", "").split("<")[0] == base and "traffic_bytes" in e:
+        names = {k.replace("pqg::", ""): e for k, e in ks.items() if "traffic_bytes" in e}
+        if kernel == "level path":
+            tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(LEVEL_PATH)]
+            if tot:
+                return sum(tot), os.path.relpath(path, ROOT)
+            continue
+        for k, e in names.items():
+            if k.split("<")[0] == base:
                 return e["traffic_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -652,7 +663,7 @@ def main(argv=None):
         lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
         val_b = 2 * w.values * w.es               # PLAIN values in + out
         # the def-level path (pqg_levels.hip kernels) and the PLAIN copy
-        stages = [("k_lv_emit", tm.levels_kernel_ms, lev_b),
+        stages = [("level path", tm.levels_kernel_ms, lev_b),
                   ("k_plain_copy", tm.values_kernel_ms, val_b)]
     elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
         stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
@@ -688,6 +699,11 @@ def main(argv=None):
                    "mini_blocks": args.mini_blocks if kind == "delta" else None,
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "note": ("HIP events around pqg_launch_levels: the def-level kernel chain (k_lv_plan, "
+                              "k_lv_bound, k_lv_segwalk, k_lv_segscan, k_lv_compact, k_lv_plan2, k_lv_win, "
+                              "k_lv_stitch, k_lv_emit, k_lv_emit_walk + the general decoder's fallback "
+                              "kernels), one launch each per step; traffic = their PMC sum")
+                     if name == "level path" else None,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms,
                      "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},

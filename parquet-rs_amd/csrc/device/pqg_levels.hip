@@ -82,6 +82,7 @@ struct LvWave {
   uint32_t stage[LV_STG / 4];
   union {
     uint2 JC[LV_WIN];       // jump table: (next position | terminal code, outputs on the way)
+    uint16_t J16[LV_WIN];   // k_lv_emit: the positions alone (16-bit: a quarter of the LDS traffic)
     struct {
       uint32_t rstart[LV_RCAP + 1];  // k_lv_emit, after the jumps: run list
       uint32_t rinfo[LV_RCAP];
@@ -1694,7 +1695,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
 #pragma unroll
       for (uint32_t j = 0; j < LV_PPL; ++j) {
         jv[j] &= 0xFFFFu;
-        W.JC[j * WAVE + lane] = make_uint2(jv[j], 0u);
+        W.J16[j * WAVE + lane] = (uint16_t)jv[j];
       }
       reinterpret_cast<uint4*>(W.R)[lane] = make_uint4(0u, 0u, 0u, 0u);
       wave_lds_sync();
@@ -1710,14 +1711,14 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
 #pragma unroll
         for (uint32_t j = 0; j < LV_PPL; ++j) {
           rb |= (uint32_t)W.R[j * WAVE + lane] << j;
-          nj[j] = jv[j] < LV_WIN ? W.JC[jv[j]].x : jv[j];
+          nj[j] = jv[j] < LV_WIN ? (uint32_t)W.J16[jv[j]] : jv[j];
         }
         wave_lds_sync();
 #pragma unroll
         for (uint32_t j = 0; j < LV_PPL; ++j) {
           if (((rb >> j) & 1u) && jv[j] < LV_WIN) W.R[jv[j]] = 1;  // idempotent: no atomics needed
           jv[j] = nj[j];
-          W.JC[j * WAVE + lane].x = jv[j];
+          W.J16[j * WAVE + lane] = (uint16_t)jv[j];
         }
         wave_lds_sync();
       }
