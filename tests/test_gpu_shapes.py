@@ -12,6 +12,8 @@ reference writer's defaults:
 
 Every case compares the HIP path (through the C ABI) with the C oracle bit for bit.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -255,3 +257,27 @@ def test_rejected_call_keeps_pending_decode(oracle, ctx):
     assert st == 0 and bad == -1
     assert out.num_values == len(vals)
     assert d_val[: len(vals) * 4].cpu().numpy().view(np.int32).tolist() == vals.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptype,es", [("INT32", 4), ("INT64", 8), ("INT96", 12), ("DOUBLE", 8)])
+@pytest.mark.parametrize("extra", [[0, 0, 0, 0], [0, 3, 0, 0], [0, 0, 1, 0], [5, 0, 0, 7], [0, -1, 0, 0]])
+def test_plain_values_behind_def_levels(oracle, ctx, ptype, es, extra):
+    """PLAIN values behind def levels go through the speculative copy (value counts implied by
+    each value section, copied beside the level decode) and its fix-up: sections with trailing
+    values or bytes (the reader takes the first non-null count, decoding.rs:138-186) and a short
+    section (EOF on that page) must give the oracle's result."""
+    rng = np.random.default_rng(zlib.crc32(repr((ptype, extra)).encode()))
+    t = getattr(oracle, ptype)
+    pages = []
+    for k, x in enumerate(extra):
+        n = 3000 + 1000 * k
+        defs = (rng.random(n) > 0.3).astype(np.int16)
+        nn = int(defs.sum())
+        vals = rng.integers(0, 256, size=(nn + max(x, 0)) * es, dtype=np.uint8).tobytes()
+        if x < 0:
+            vals = vals[:len(vals) - es]  # one value short: EOF on this page
+        elif k == 2 and x:
+            vals += b"\x01"  # a section that is not a whole number of values
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(defs, 1) + vals, n, oracle.PLAIN))
+    _same(oracle, ctx, t, pages, max_def=1, expect_ok=min(extra) >= 0)
