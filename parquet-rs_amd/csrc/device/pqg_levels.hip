@@ -1545,6 +1545,7 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
 // What the walked-page emit writes: levels / booleans, or dictionary values.
 template <int OUT>
 struct LvLevelOut {
+  static constexpr bool PIPE = true;  // k_lv_emit_walk prefetches the next window (registers to spare)
   uint8_t* out;
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                              const LvWin& x, uint32_t base, uint32_t endo, int sel, const ColumnParams& cp,
@@ -1555,6 +1556,7 @@ struct LvLevelOut {
 
 template <int ES>
 struct LvDictOut {
+  static constexpr bool PIPE = false;  // (its gathers hold the registers the prefetch would take)
   int dict_page;  // the chunk's PLAIN dictionary page (k_lv_plan checked it)
   uint8_t* out;
   ChunkResult* res;
@@ -1573,6 +1575,7 @@ struct LvDictOut {
 // decoded): per output the entry's source address and length (the byte-array scan and copy,
 // pqg_bytes.hip, take it from there), and the page's byte total.
 struct LvBaDictOut {
+  static constexpr bool PIPE = false;
   int dict_page;
   const uint64_t* dsrc;
   const uint32_t* dlen;
@@ -1772,13 +1775,78 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
 
 // ------------------------------------------------------------------------------ k_lv_emit_walk
 // Windows of the walked pages: each wave takes a contiguous range of windows (one page lookup,
-// then the page advances with the window), loads each window's run records and writes its
-// outputs.
+// then the page advances with the window), loads each window's run records and staged payload
+// and writes its outputs. Software-pipelined: while window g's outputs are written, window
+// g + 1's records and payload (same page) are in flight in registers and window g + 2's run
+// bounds are read, so a window's three dependent loads (run bounds, records, payload) overlap
+// the previous window's stores.
+constexpr uint32_t LE_RPL = (LW_RPW + 1 + WAVE - 1) / WAVE;  // record registers per lane (5)
+constexpr uint32_t LE_SPL = (LE_STG / 16 + WAVE - 1) / WAVE;  // stage registers per lane (3)
+
 struct LeWave {
   uint32_t stage[LE_STG / 4];
   uint32_t rstart[LW_RPW + 1];
   uint32_t rinfo[LW_RPW];
+  uint32_t endn;
 };
+
+// One window's loads in flight: its run records [fr, fr + R] and staged payload.
+struct LeLoad {
+  uint2 r[LE_RPL];
+  uint4 st[LE_SPL];
+  uint32_t k, R, nch, sb;
+  bool ok;  // loads issued (a window of the same walked page with runs, R <= LW_RPW)
+};
+
+__device__ inline uint32_t le_nch(uint32_t w) {
+  const uint32_t n = (LV_WIN + 16u + 64u * w + 16u) / 16u + 1u;
+  return n > LE_STG / 16 ? LE_STG / 16 : n;
+}
+
+__device__ inline void le_issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const uint2* rc, uint32_t R,
+                                uint64_t S, uint32_t k, uint32_t w, LeLoad& f) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t j = 0; j < LE_RPL; ++j) {
+    const uint32_t i = lane + j * WAVE;
+    f.r[j] = i <= R ? rc[i] : make_uint2(0u, 0u);
+  }
+  const uint64_t A = (S + (uint64_t)k * LV_WIN) & ~15ull;
+  f.sb = (uint32_t)(S + (uint64_t)k * LV_WIN - A);
+  f.nch = le_nch(w);
+#pragma unroll
+  for (uint32_t c = 0; c < LE_SPL; ++c) {
+    const uint32_t ci = lane + c * WAVE;
+    const uint64_t a = A + (uint64_t)ci * 16u;
+    f.st[c] = ci >= f.nch ? make_uint4(0u, 0u, 0u, 0u)
+              : a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+  }
+  f.k = k;
+  f.R = R;
+  f.ok = true;
+}
+
+__device__ inline void le_install(const LeLoad& f, LeWave& E) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t j = 0; j < LE_RPL; ++j) {
+    const uint32_t i = lane + j * WAVE;
+    if (i < f.R) {
+      E.rstart[i] = f.r[j].x;
+      E.rinfo[i] = f.r[j].y;
+    } else if (i == f.R) {
+      E.rstart[i] = 0xFFFFFFFFu;
+      E.rinfo[i] = f.r[j].y;
+      E.endn = f.r[j].x;  // first output of the next window's first run (or the total)
+    }
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < LE_SPL; ++c) {
+    const uint32_t ci = lane + c * WAVE;
+    if (ci < f.nch) reinterpret_cast<uint4*>(E.stage)[ci] = f.st[c];
+  }
+  wave_lds_sync();
+}
 
 template <class Writer>
 __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -1797,6 +1865,10 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   LvWin x;
   x.p = p;
   bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
+  LeLoad nf;  // the next window's loads, issued while the current one is written
+  nf.ok = false;
+  uint32_t nb0 = 0, nb1 = 0, nbk = 0;  // run bounds (wfirst) of window nbk of the page, read ahead
+  bool nbv = false;
   for (uint32_t g = g0; g < g1; ++g) {
     while (g >= pend) {  // next page (pages without windows are passed over)
       ++p;
@@ -1804,6 +1876,8 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       pend = lt.wbase[p + 1];
       x.p = p;
       walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
+      nf.ok = false;
+      nbv = false;
     }
     if (!walked) {
       g = pend - 1u;
@@ -1811,26 +1885,78 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     }
     x.k = g - wb;
     const uint32_t* wf = lt.wfirst + wb + p;
-    const uint32_t fr = wf[x.k], fe = wf[x.k + 1];
-    if (fr == fe) continue;  // no header starts in this window
-    const uint32_t R = fe - fr;
-    if (R > LW_RPW) {  // more runs than the run list holds (not from the walker's span rule)
-      if (lane == 0) lv_bail(rt, p, PF_WALK);
+    const uint2* recp = lt.rec + (uint64_t)LW_REC * (wb + 2ull * p);
+    const uint32_t w = (uint32_t)x.s.w;
+    if constexpr (!Writer::PIPE) {  // one window at a time: records and payload straight to LDS
+      const uint32_t fr = wf[x.k], fe = wf[x.k + 1];
+      if (fr == fe) continue;
+      const uint32_t R = fe - fr;
+      if (R > LW_RPW) {
+        if (lane == 0) lv_bail(rt, p, PF_WALK);
+        continue;
+      }
+      const uint2* rc = recp + fr;
+      const uint32_t endn = rc[R].x;
+      for (uint32_t i = lane; i <= R; i += WAVE) {
+        const uint2 r = rc[i];
+        E.rstart[i] = i < R ? r.x : 0xFFFFFFFFu;
+        E.rinfo[i] = r.y;
+      }
+      x.W0 = x.k * LV_WIN;
+      lv_stage(blob, blob_len, x, E.stage, le_nch(w));  // ends with a wave LDS sync (run list too)
+      const uint32_t base = E.rstart[0];
+      const uint32_t endo = endn < x.s.n ? endn : x.s.n;
+      if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp, pages);
+      wave_lds_sync();
       continue;
     }
-    const uint2* rc = lt.rec + (uint64_t)LW_REC * (wb + 2ull * p) + fr;
-    const uint32_t endn = rc[R].x;  // first output of the next window's first run (or the total)
-    for (uint32_t i = lane; i <= R; i += WAVE) {
-      const uint2 r = rc[i];
-      E.rstart[i] = i < R ? r.x : 0xFFFFFFFFu;
-      E.rinfo[i] = r.y;
+    bool have = nf.ok && nf.k == x.k;
+    uint32_t R;
+    if (have) {
+      R = nf.R;
+    } else {
+      const uint32_t fr = wf[x.k], fe = wf[x.k + 1];
+      if (fr == fe) continue;  // no header starts in this window
+      R = fe - fr;
+      if (R > LW_RPW) {  // more runs than the run list holds (not from the walker's span rule)
+        if (lane == 0) lv_bail(rt, p, PF_WALK);
+        continue;
+      }
+      le_issue(blob, blob_len, recp + fr, R, x.s.S, x.k, w, nf);
+    }
+    le_install(nf, E);  // (waits for its loads)
+    nf.ok = false;
+    // the next window of this page: issue its loads now (its run bounds were read one window ago)
+    if (Writer::PIPE && g + 1 < g1 && g + 1 < pend) {
+      uint32_t fr2, fe2;
+      if (nbv && nbk == x.k + 1) {
+        fr2 = nb0;
+        fe2 = nb1;
+      } else {
+        fr2 = wf[x.k + 1];
+        fe2 = wf[x.k + 2];
+      }
+      if (fe2 > fr2 && fe2 - fr2 <= LW_RPW) le_issue(blob, blob_len, recp + fr2, fe2 - fr2, x.s.S, x.k + 1, w, nf);
+      nbv = false;
+      if (g + 2 < g1 && g + 2 < pend) {  // and the bounds of the one after
+        nb0 = wf[x.k + 2];
+        nb1 = wf[x.k + 3];
+        nbk = x.k + 2;
+        nbv = true;
+      }
+    } else {
+      nbv = false;
     }
     x.W0 = x.k * LV_WIN;
-    const uint32_t w = (uint32_t)x.s.w;
-    uint32_t nch = (LV_WIN + 16u + 64u * w + 16u) / 16u + 1u;
-    if (nch > LE_STG / 16) nch = LE_STG / 16;
-    lv_stage(blob, blob_len, x, E.stage, nch);  // ends with a wave LDS sync (run list too)
+    x.sb = 0;
+    x.cap = 0;
+    {
+      const uint64_t A = (x.s.S + x.W0) & ~15ull;
+      x.sb = (uint32_t)(x.s.S + x.W0 - A);
+      x.cap = le_nch(w) * 16u;
+    }
     const uint32_t base = E.rstart[0];
+    const uint32_t endn = E.endn;
     const uint32_t endo = endn < x.s.n ? endn : x.s.n;
     if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp, pages);
     wave_lds_sync();  // the run list and stage are refilled by the next window
