@@ -32,6 +32,34 @@ __device__ int32_t plain_ba_walk(DeltaSmem& sm, const uint8_t* __restrict__ blob
                                  uint64_t S, uint32_t slen, uint64_t n, uint64_t* __restrict__ src,
                                  uint32_t* __restrict__ len) {
   __shared__ uint2 rec[BW_CAP];
+  __shared__ uint32_t fixed_s;
+  // Values of one length L (dates, codes, ids): value i then starts at i * (4 + L) + 4. Checked
+  // by the whole workgroup in one pass; the chain is only walked when some length differs.
+  if (n > 1 && slen >= 4) {
+    const uint32_t L = (uint32_t)blob[S] | ((uint32_t)blob[S + 1] << 8) | ((uint32_t)blob[S + 2] << 16) |
+                       ((uint32_t)blob[S + 3] << 24);
+    const uint64_t stride = 4ull + L;
+    if (threadIdx.x == 0) fixed_s = 1;
+    __syncthreads();
+    if (n * stride <= (uint64_t)slen) {
+      for (uint64_t k = threadIdx.x; k < n; k += WG) {
+        const uint64_t a = S + k * stride;
+        const uint32_t l = (uint32_t)blob[a] | ((uint32_t)blob[a + 1] << 8) | ((uint32_t)blob[a + 2] << 16) |
+                           ((uint32_t)blob[a + 3] << 24);
+        if (l != L) fixed_s = 0;
+      }
+    } else if (threadIdx.x == 0) {
+      fixed_s = 0;
+    }
+    __syncthreads();
+    if (fixed_s) {
+      for (uint64_t k = threadIdx.x; k < n; k += WG) {
+        src[k] = S + k * stride + 4;
+        len[k] = L;
+      }
+      return 0;
+    }
+  }
   uint64_t i = 0;
   uint32_t pos = 0;
   uint64_t A0 = ~0ull;

@@ -201,3 +201,29 @@ def test_truncated_dictionary_page_ba(oracle, ctx):
     dpage = oracle.PageSpec(oracle.PAGE_DICTIONARY, dbytes, 2, oracle.PLAIN)
     body = bytes([1]) + oracle.rle_encode(np.array([0, 1], np.uint64), 1)
     _err(oracle, ctx, oracle.BYTE_ARRAY, [dpage, oracle.PageSpec(oracle.PAGE_DATA, body, 2, oracle.RLE_DICTIONARY)])
+
+
+@pytest.mark.parametrize("odd", [None, 0, 2500, 4999])
+def test_plain_byte_array_one_length(oracle, ctx, odd):
+    """Values of one length take the workgroup's fixed-stride check instead of the chain walk;
+    one value of another length (first, middle, last) sends the page back to the walk."""
+    rng = np.random.default_rng(11)
+    vals = rand_strings(rng, 5000, 8, 8)
+    if odd is not None:
+        vals[odd] = vals[odd] + b"x"
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.plain_encode_ba(vals), len(vals), oracle.PLAIN)]
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+
+
+def test_dictionary_byte_array_one_length(oracle, ctx):
+    rng = np.random.default_rng(12)
+    pages = _dict_pages(oracle, rng, oracle.BYTE_ARRAY, rand_strings(rng, 700, 8, 8), [3000, 9000], 0.2)
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+@pytest.mark.parametrize("cut", [1, 4, 9])
+def test_plain_ba_one_length_truncated(oracle, ctx, cut):
+    """Equal lengths but the section cut short: the fixed-stride check fails and the walk reports
+    the reference's error (panic on a cut length, EOF on cut bytes)."""
+    body = oracle.plain_encode_ba([b"abcdefgh"] * 50)[:-cut]
+    _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, body, 50, oracle.PLAIN)])
