@@ -375,30 +375,23 @@ __device__ inline bool ba_page_ok(const PageWork& pw, const ChunkResult* res, ui
          pw.encoding != E_DELTA_BYTE_ARRAY && res->total_bytes <= cap;
 }
 
+// Per page and tile of BA_T values: the tile's byte count (the offsets themselves are written
+// once, by k_ba_copy, from the scanned tile starts).
 __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const uint32_t* __restrict__ vlen, uint64_t cap,
-                                                uint32_t maxt, uint64_t* __restrict__ tsum,
-                                                int64_t* __restrict__ offsets, ChunkResult* res) {
-  __shared__ DeltaSmem sm;
+                                                uint32_t maxt, uint64_t* __restrict__ tsum, ChunkResult* res) {
+  __shared__ uint64_t red[WG / 64];
   const uint32_t t = blockIdx.x, p = blockIdx.y;
   const PageWork pw = pages[p];
   if (!ba_page_ok(pw, res, cap)) return;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
-  const uint64_t i0 = (uint64_t)t * BA_T + (uint64_t)threadIdx.x * BA_VPT;
   if ((uint64_t)t * BA_T >= n) return;
-  uint32_t l[BA_VPT];
   uint64_t s = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    l[k] = i0 + k < n ? vlen[vo + i0 + k] : 0u;
-    s += l[k];
+  for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
+    const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+    s += i < n ? vlen[vo + i] : 0u;
   }
-  uint64_t tot;
-  uint64_t pre = block_exscan(sm, s, tot);
-#pragma unroll
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    if (i0 + k < n) offsets[vo + i0 + k] = (int64_t)pre;
-    pre += l[k];
-  }
+  const uint64_t tot = block_sum_u64(s, red);
   if (threadIdx.x == 0) tsum[(uint64_t)p * maxt + t] = tot;
 }
 
@@ -421,34 +414,55 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, uint64_t cap, 
   }
 }
 
+// Per page and tile: the values' byte offsets (tile start from k_ba_tscan + an in-tile scan of
+// the lengths, kept in LDS) written once to `offsets`, then the bytes: lanes take consecutive
+// values, so neighbouring lanes write neighbouring bytes.
 __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
                                                 const uint64_t* __restrict__ vsrc,
                                                 const uint32_t* __restrict__ vlen, uint64_t cap, uint32_t maxt,
                                                 const uint64_t* __restrict__ tsum, int64_t* __restrict__ offsets,
                                                 uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ DeltaSmem sm;
+  __shared__ uint64_t loff[BA_T];  // tile-relative byte offset of each value
   const uint32_t t = blockIdx.x, p = blockIdx.y;
   const PageWork pw = pages[p];
   if (!ba_page_ok(pw, res, cap)) return;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
   const uint64_t base = tsum[(uint64_t)p * maxt + t];
-  // lanes take consecutive values: neighbouring lanes write neighbouring bytes
+  const uint64_t i0 = (uint64_t)t * BA_T + (uint64_t)threadIdx.x * BA_VPT;
+  uint32_t l[BA_VPT];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    l[k] = i0 + k < n ? vlen[vo + i0 + k] : 0u;
+    s += l[k];
+  }
+  uint64_t tot;
+  uint64_t pre = block_exscan(sm, s, tot);
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    if (i0 + k < n) offsets[vo + i0 + k] = (int64_t)(base + pre);
+    loff[threadIdx.x * BA_VPT + k] = pre;
+    pre += l[k];
+  }
+  __syncthreads();
 #pragma unroll 1
   for (uint32_t k = 0; k < BA_VPT; ++k) {
-    const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+    const uint32_t j = k * WG + threadIdx.x;
+    const uint64_t i = (uint64_t)t * BA_T + j;
     if (i >= n) break;
-    const uint64_t d = base + (uint64_t)offsets[vo + i];
-    offsets[vo + i] = (int64_t)d;
-    const uint32_t l = vlen[vo + i];
+    const uint64_t d = base + loff[j];
+    const uint32_t ln = vlen[vo + i];
     const uint8_t* sp = blob + vsrc[vo + i];
     uint8_t* o = out + d;
     uint32_t q = 0;
-    for (; q + 8 <= l; q += 8) {
+    for (; q + 8 <= ln; q += 8) {
       uint64_t x;
       __builtin_memcpy(&x, sp + q, 8);
       __builtin_memcpy(o + q, &x, 8);
     }
-    for (; q < l; ++q) o[q] = sp[q];
+    for (; q < ln; ++q) o[q] = sp[q];
   }
 }
 
@@ -522,7 +536,7 @@ extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, P
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);
   const uint32_t maxt = (uint32_t)((max_page_vals + BA_T - 1) / BA_T);
   if (maxt) {
-    hipLaunchKernelGGL(k_ba_tsum, dim3(maxt, npages), dim3(WG), 0, s, pages, vlen, cap, maxt, tsum, offsets, res);
+    hipLaunchKernelGGL(k_ba_tsum, dim3(maxt, npages), dim3(WG), 0, s, pages, vlen, cap, maxt, tsum, res);
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, cap, maxt, tsum, res);
     hipLaunchKernelGGL(k_ba_copy, dim3(maxt, npages), dim3(WG), 0, s, blob, pages, vsrc, vlen, cap, maxt, tsum,
                        offsets, out, res);
