@@ -153,3 +153,55 @@ def test_gpu_row_group_decoder_reports_failing_column(rowgroup):
         assert keep[0][1][:info.value_bytes[0]].cpu().numpy().tobytes() == vals.tobytes()
     finally:
         rgd.close()
+
+
+@pytest.mark.gpu
+def test_gpu_row_group_pipeline():
+    """The bench's config-5 loop at small scale: four row groups decoded by one row-group decoder
+    (16 streams), alternating two launch streams and two output sets, so that row group g + 1 is
+    enqueued while g still runs and every column context cycles through both staging slots; each
+    row group's columns are checked against the generator's cells once its decode is known done."""
+    import pqgpu
+    import torch
+    rows, nrg = 70_000, 4
+    rgs = [pqgtools.alltypes_row_group(rows, ROW0 + g * rows, P_NULL, SEED, threads=8) for g in range(nrg)]
+    cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+    blobs = [torch.from_numpy(np.ascontiguousarray(b[:i.blob_len + 64])).cuda() for b, _, i in rgs]
+    parrs = [_rg_pages(pqgpu, p, i) for _, p, i in rgs]
+    vcap = max(max(i.value_bytes) for _, _, i in rgs)
+
+    class Info:  # one output set sized for every row group
+        value_bytes = [vcap] * 11
+    sets = [_rg_outputs(torch, Info, rows) for _ in range(2)]
+    lanes = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    rgd = pqgpu.RowGroupDecoder(0, 16)
+    try:
+        done = [torch.cuda.Event() for _ in range(nrg)]
+        oas = []
+        for g in range(nrg):
+            lane = lanes[g % 2]
+            if g >= 2:  # output set g % 2 is free once row group g - 2 was checked
+                lane.wait_event(done[g - 2])
+            oas.append(rgd.decode_async(cols, blobs[g].data_ptr(), rgs[g][2].blob_len, parrs[g], sets[g % 2][1],
+                                        lane.cuda_stream))
+            done[g].record(lane)
+            if g >= 1:  # check row group g - 1 while g runs
+                _check_rg(torch, rgs, sets, done, oas, g - 1, rows)
+        st, bcol, bad = rgd.sync()
+        assert st == 0, (st, bcol, bad, rgd.error_message())
+        _check_rg(torch, rgs, sets, done, oas, nrg - 1, rows)
+    finally:
+        rgd.close()
+
+
+def _check_rg(torch, rgs, sets, done, oas, g, rows):
+    done[g].synchronize()
+    keep = sets[g % 2][0]
+    info = rgs[g][2]
+    for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+        lv, vals, offs = pqgtools.alltypes_truth(ROW0 + g * rows, rows, j, P_NULL, SEED, info.value_bytes[j])
+        d_def, d_val, d_off = keep[j]
+        np.testing.assert_array_equal(d_def[:rows].cpu().numpy(), lv)
+        assert d_val[:info.value_bytes[j]].cpu().numpy().tobytes() == vals.tobytes(), (g, name)
+        if offs is not None:
+            np.testing.assert_array_equal(d_off[:len(offs)].cpu().numpy(), offs)
