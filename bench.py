@@ -58,7 +58,7 @@ def parse(argv=None):
                     help="alltypes: row groups per GPU (11 x 2^23 rows ~ 8 GiB decoded: 1/8 of config 5)")
     ap.add_argument("--rg-rows", type=int, default=1 << 23, help="alltypes: rows per row group")
     ap.add_argument("--at-p-null", type=float, default=0.05, help="alltypes: null fraction per column")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=16,
                     help="alltypes: HIP streams the row-group decoder spreads the column chunks over")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
