@@ -244,20 +244,58 @@ struct LevelsMaker {
   }
 };
 
-#define PQG_TEXPAND_LEVELS(NAME, ATTR)                                                              \
-  __global__ void ATTR __launch_bounds__(WG) NAME(const uint8_t* __restrict__ blob, uint64_t blob_len, \
-                                                  uint32_t ntiles, RunTables rt, ColumnParams cp,     \
-                                                  int which, int16_t* __restrict__ out) {             \
-    __shared__ TileSmem sm;                                                                       \
-    if (*rt.nfall == 0) return;                                                                   \
-    LevelsMaker mk{out, which == SS_DEF ? cp.max_def : cp.max_rep, which == SS_DEF, rt.qcount,     \
-                   rt.pflag};                                                                     \
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {                                   \
-      tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);                                      \
-      __syncthreads(); /* sm is refilled by the next tile */                                      \
-    }                                                                                             \
+// Level streams the level path handed back (PF_BAIL: malformed input, unusual header forms), one
+// workgroup per page: wave 0 walks the page's header chain (run_index: every reference check,
+// per-tile checkpoints and records), then the workgroup expands the page's tiles one after the
+// other and sums the page's def levels == max_def (its non-null count). One launch in place of
+// index pass + tile descriptors + tile expand + page counts: the level path leaves these streams
+// to it only on unusual input, so the latency of a serial page matters less than three launches
+// on every decode.
+struct LevelsPageMaker {
+  int16_t* out;
+  int16_t maxl;
+  bool count;
+  uint32_t acc;  // this thread's outputs == maxl
+  __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
+  __device__ void done(const QDesc&, uint32_t, TxLevels& em) { acc += em.nonnull; }
+};
+
+__global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                    ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
+                                                    int16_t* __restrict__ out) {
+  __shared__ IndexSmem ism;
+  __shared__ TileSmem sm;
+  __shared__ int32_t st_s;
+  __shared__ uint64_t red[WG / 64];
+  const int p = blockIdx.x;
+  if (rt.pflag[p] != PF_BAIL) return;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  Stream s;
+  if (!get_stream(blob, pw, sel, cp, s)) return;
+  if (threadIdx.x < 64) {
+    const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
+                                 rt.nruns + pw.ltile0, ism);
+    if (threadIdx.x == 0) {
+      st_s = st;
+      if (st) report(pages, res, p, st);
+    }
   }
-PQG_TEXPAND_LEVELS(k_texpand_levels, __attribute__((amdgpu_waves_per_eu(8, 8))))
+  __syncthreads();
+  if (st_s) return;
+  LevelsPageMaker mk{out, sel == SS_DEF ? cp.max_def : cp.max_rep, sel == SS_DEF, 0u};
+  for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
+    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, -1, t, 0, RUN_TILE);
+    __syncthreads();  // (the descriptor is read by every thread of the workgroup)
+    tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);
+    __syncthreads();  // sm is refilled by the next tile
+  }
+  if (sel == SS_DEF) {
+    const uint64_t nn = block_sum_u64(mk.acc, red);
+    if (threadIdx.x == 0) pages[p].nonnull = nn;
+  }
+}
 
 // Tile expand of RLE_DICTIONARY indices with the dictionary gather.
 template <int ES>
@@ -502,16 +540,8 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, -1, 0, rt, lt, out, res, s);
   if (kev) (void)hipEventRecord(kev[1], s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel, -1, rt, res, 1);
-  if (ntiles) {
-    hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
-                       ntiles, rt, cp, sel, -1);
-    // persistent grid: most calls leave no stream to this pass, and its workgroups exit at once
-    hipLaunchKernelGGL(k_texpand_levels, dim3(ntiles < 1024u ? ntiles : 1024u), dim3(WG), 0, s, blob, blob_len,
-                       ntiles, rt, cp, sel, out);
-    if (sel == SS_DEF)
-      hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, 0);
-  }
+  hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp, sel, rt, res,
+                     out);
   return hipGetLastError();
 }
 

@@ -281,3 +281,38 @@ def test_plain_values_behind_def_levels(oracle, ctx, ptype, es, extra):
             vals += b"\x01"  # a section that is not a whole number of values
         pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(defs, 1) + vals, n, oracle.PLAIN))
     _same(oracle, ctx, t, pages, max_def=1, expect_ok=min(extra) >= 0)
+
+
+def _leb_padded(x, nbytes):
+    """x as a non-minimal LEB128 varint of exactly nbytes bytes (the reference's reader accepts
+    them, bit_util.rs get_vlq_int; the level path's fast parse takes up to 4 bytes)."""
+    out = []
+    for i in range(nbytes):
+        b = (x >> (7 * i)) & 0x7F
+        out.append(b | (0x80 if i < nbytes - 1 else 0))
+    return bytes(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [5, 7, 10])
+def test_level_streams_the_level_path_hands_back(oracle, ctx, nbytes):
+    """Def-level streams whose first run header is a 5..10-byte varint: the level path hands the
+    page back and the fallback kernel (index walk + tile expand + non-null count, one workgroup
+    per page) decodes it; the page's non-null count places the PLAIN values of every later page.
+    Pages taken by the level path are mixed in."""
+    rng = np.random.default_rng(nbytes)
+    pages = []
+    for k in range(6):
+        n = 5000 + 731 * k
+        defs = (rng.random(n) > 0.25).astype(np.int16)
+        if k % 2 == 0:  # an RLE run of 300 ones with a padded header, then the writer's encoding
+            defs[:300] = 1
+            rest = oracle.rle_encode(defs[300:].astype(np.uint64), 1)
+            body = _leb_padded(300 << 1, nbytes) + b"\x01" + rest
+            lev = len(body).to_bytes(4, "little") + body
+        else:
+            lev = oracle.level_encode(defs, 1)
+        nn = int(defs.sum())
+        vals = rng.integers(-2 ** 31, 2 ** 31, size=nn, dtype=np.int64).astype(np.int32)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, lev + vals.tobytes(), n, oracle.PLAIN))
+    _same(oracle, ctx, oracle.INT32, pages, max_def=1)
