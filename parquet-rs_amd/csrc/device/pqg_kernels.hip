@@ -331,6 +331,48 @@ struct DictMaker {
   }
 PQG_TEXPAND_DICT(k_texpand_dict, )
 
+// Dictionary index streams the level path handed back, when they are expected to be rare (the
+// dictionary's index width is within the level path's limit): one workgroup per page, index walk
+// then the page's tiles with the gather, as k_lv_fallback does for levels.
+template <int ES>
+__global__ void __launch_bounds__(WG) k_dict_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                      PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                      ColumnParams cp, int dict_page, RunTables rt,
+                                                      uint8_t* __restrict__ out, ChunkResult* res) {
+  __shared__ IndexSmem ism;
+  __shared__ TileSmem sm;
+  __shared__ int32_t st_s;
+  const int p = blockIdx.x;
+  if (rt.pflag[p] != PF_BAIL) return;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  Stream s;
+  if (!get_stream(blob, pw, SS_DICT, cp, s)) return;
+  if (dict_page < 0) {  // "Decoder for dict should have been set"
+    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    return;
+  }
+  if (pages[dict_page].status != 0) return;
+  if (threadIdx.x < 64) {
+    const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
+                                 rt.nruns + pw.ltile0, ism);
+    if (threadIdx.x == 0) {
+      st_s = st;
+      if (st) report(pages, res, p, st);
+    }
+  }
+  __syncthreads();
+  if (st_s) return;
+  const PageWork& dp = pages[dict_page];
+  DictMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0), out, pages, res};
+  for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
+    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, SS_DICT, dict_page, t, 0, RUN_TILE);
+    __syncthreads();
+    tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);
+    __syncthreads();
+  }
+}
+
 // Tile expand of RLE booleans (data page v2 values).
 struct BoolMaker {
   uint8_t* out;
@@ -558,7 +600,7 @@ hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es
 hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                            uint32_t ntiles, ColumnParams cp, int dict_page, int es,
                            const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
-                           ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
+                           ChunkResult* res, hipStream_t s, hipEvent_t* kev, int small_dict) {
   // (the dictionary page's checks ran in k_prepare)
   bool lvpath = es == 4 || es == 8;
 #ifdef PQG_DIAG
@@ -568,6 +610,16 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   if (lvpath) {
     const hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, es, rt, lt, out, res, s);
     if (e != hipSuccess) return e;
+    if (small_dict) {  // the level path takes (nearly) every page: its rare leftovers in one launch
+      if (es == 8)
+        hipLaunchKernelGGL((k_dict_fallback<8>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp,
+                           dict_page, rt, out, res);
+      else
+        hipLaunchKernelGGL((k_dict_fallback<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp,
+                           dict_page, rt, out, res);
+      if (kev) (void)hipEventRecord(kev[1], s);
+      return hipGetLastError();
+    }
   }
   hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
                      dict_page, rt, res, lvpath ? 1 : 0);

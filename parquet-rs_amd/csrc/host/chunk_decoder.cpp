@@ -31,7 +31,7 @@ hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_by
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
                            int, const uint32_t*, RunTables, LevelTables, uint8_t*, ChunkResult*, hipStream_t,
-                           hipEvent_t*);
+                           hipEvent_t*, int);
 hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
                                  uint8_t*, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
@@ -767,8 +767,12 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
     if (enc_present[PQG_RLE_DICTIONARY]) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
+      // a dictionary of at most 2^dict_maxw entries: the writer's index width is within the level
+      // path's limit, so the general decoder only sees the rare pages it hands back
+      const int small_dict = dict_page >= 0 && pages[dict_page].num_values <= (1u << cp.dict_maxw);
       HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
-                             sl.rt[2], sl.lt(2), vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "dict");
+                             sl.rt[2], sl.lt(2), vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr, small_dict),
+             "dict");
       sl.kv = ctx->timing;
     }
     if (delta_vals) {
