@@ -124,17 +124,9 @@ __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Header at stream position p (stage byte index rel): branch-free for varints of 1-4 bytes (run
-// lengths < 2^27; every header the reference writer emits, rle.rs:167-178), reading a third
-// dword only for an RLE value past the first 4 bytes. Longer varints, and headers or RLE values
-// running past the stream end, return false (dead): a true chain that meets one goes to the
-// general decoder.
-__device__ inline bool lv_parse4(const uint32_t* st, uint32_t rel, uint32_t p, uint32_t slen,
-                                 uint32_t w, uint32_t vb, uint32_t& nxt, uint32_t& cnt,
-                                 uint32_t& val, bool& bp) {
-  const uint32_t wi = rel >> 2, sh = (rel & 3u) * 8u;
-  const uint32_t d1 = st[wi + 1];
-  const uint32_t x = __builtin_amdgcn_alignbit(d1, st[wi], sh);  // bytes p .. p+3
+// Header at stream position p from its bytes x (p .. p+3) and y (p+4 .. p+7).
+__device__ inline bool lv_parse_xy(uint32_t x, uint32_t y, uint32_t p, uint32_t slen, uint32_t w, uint32_t vb,
+                                   uint32_t& nxt, uint32_t& cnt, uint32_t& val, bool& bp) {
   const uint32_t c0 = (x >> 7) & 1u, c1 = (x >> 15) & 1u, c2 = (x >> 23) & 1u, c3 = x >> 31;
   const uint32_t c01 = c0 & c1, c012 = c01 & c2;
   const uint32_t hl = 1u + c0 + c01 + c012;
@@ -146,17 +138,30 @@ __device__ inline bool lv_parse4(const uint32_t* st, uint32_t rel, uint32_t p, u
   uint32_t v = 0;
   if (!bp) {
     const uint32_t vm = vb == 1 ? 0xFFu : 0xFFFFu;
-    if (hl + vb <= 4u) {
-      v = (x >> (8u * hl)) & vm;
-    } else {
-      const uint32_t y = __builtin_amdgcn_alignbit(st[wi + 2], d1, sh);  // bytes p+4 .. p+7
-      v = (uint32_t)((((uint64_t)y << 32) | x) >> (8u * hl)) & vm;
-    }
+    v = (uint32_t)((((uint64_t)y << 32) | x) >> (8u * hl)) & vm;
   }
   val = bp ? p + hl : v;
   const uint32_t len = bp ? hl + g * w : hl + vb;  // g < 2^27, w <= 16: < 2^32
   nxt = p + len;
   return !(c012 & c3) && p < slen && len <= slen - p;
+}
+
+// Header at stream position p (stage byte index rel): branch-free for varints of 1-4 bytes (run
+// lengths < 2^27; every header the reference writer emits, rle.rs:167-178), reading a third
+// dword only for an RLE value past the first 4 bytes. Longer varints, and headers or RLE values
+// running past the stream end, return false (dead): a true chain that meets one goes to the
+// general decoder.
+__device__ inline bool lv_parse4(const uint32_t* st, uint32_t rel, uint32_t p, uint32_t slen,
+                                 uint32_t w, uint32_t vb, uint32_t& nxt, uint32_t& cnt,
+                                 uint32_t& val, bool& bp) {
+  const uint32_t wi = rel >> 2, sh = (rel & 3u) * 8u;
+  const uint32_t d1 = st[wi + 1];
+  const uint32_t x = __builtin_amdgcn_alignbit(d1, st[wi], sh);  // bytes p .. p+3
+  // the third dword only for an RLE value past byte 3
+  const bool far = (x & 1u) == 0u && 1u + ((x >> 7) & 1u) + ((x >> 7) & (x >> 15) & 1u) +
+                                         ((x >> 7) & (x >> 15) & (x >> 23) & 1u) + vb > 4u;
+  const uint32_t y = far ? __builtin_amdgcn_alignbit(st[wi + 2], d1, sh) : 0u;
+  return lv_parse_xy(x, y, p, slen, w, vb, nxt, cnt, val, bp);
 }
 
 // What the reader consumes of a run must be decodable: the bit-packed payload of its first
@@ -992,6 +997,67 @@ __global__ void __launch_bounds__(WG) k_lv_compact(int npages, RunTables rt, Lev
   }
 }
 
+// ------------------------------------------------------------------------------ segment tables
+// Dense windows (k_lv_win for w = 1, k_lv_emit): lane l takes the 16 positions [16 l, 16 l + 16)
+// of the staged window (a segment) and parses each as a header; a backward pass over the segment
+// gives, per position, where its chain leaves the segment (window-relative, or a terminal code),
+// the outputs on the way (saturating) and the headers it passes (a 16-bit mask), in
+// W.JC[t * 64 + l] for position 16 l + t. A chain then crosses a window in at most 64 lookups.
+constexpr uint32_t LV_SEG = LV_WIN / WAVE;
+
+__device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV_SEG], uint32_t (&pv)[LV_SEG],
+                                    uint32_t& bpm) {
+  constexpr uint32_t SEG = LV_SEG;
+  const uint32_t lane = threadIdx.x & 63u, i0 = lane * SEG;
+  const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
+  uint32_t a[SEG / 4 + 2];  // segment bytes 0 .. 23, dword-aligned on the segment
+  {
+    const uint32_t d0 = (x.sb >> 2) + i0 / 4u, sh = (x.sb & 3u) * 8u;
+    uint32_t d[SEG / 4 + 3];
+#pragma unroll
+    for (uint32_t k = 0; k < SEG / 4 + 3; ++k) d[k] = W.stage[d0 + k];
+#pragma unroll
+    for (uint32_t k = 0; k < SEG / 4 + 2; ++k) a[k] = __builtin_amdgcn_alignbit(d[k + 1], d[k], sh);
+  }
+  uint32_t pn[SEG];
+  bpm = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < SEG; ++t) {
+    const uint32_t q = x.W0 + i0 + t;
+    const uint32_t xx = t & 3u ? __builtin_amdgcn_alignbit(a[t / 4 + 1], a[t / 4], 8u * (t & 3u)) : a[t / 4];
+    const uint32_t yy = t & 3u ? __builtin_amdgcn_alignbit(a[t / 4 + 2], a[t / 4 + 1], 8u * (t & 3u)) : a[t / 4 + 1];
+    uint32_t nx, c = 0, v = 0;
+    bool bp = false;
+    if (q >= slen) {
+      pn[t] = LV_J_END;
+    } else if (!lv_parse_xy(xx, yy, q, slen, w, vb, nx, c, v, bp)) {
+      pn[t] = LV_J_DEAD;
+      c = 0;
+    } else {
+      const uint32_t dd = nx - x.W0;
+      pn[t] = dd < 0xFFFDu ? dd : LV_J_FAR;
+    }
+    pc[t] = c;
+    pv[t] = v;
+    bpm |= (uint32_t)bp << t;
+  }
+  // backward pass: entry (t * 64 + lane) = (exit | headers mask << 16, outputs)
+#pragma unroll
+  for (int t = SEG - 1; t >= 0; --t) {
+    const uint32_t nt = pn[t];
+    uint32_t ex = nt, m = nt < LV_J_END ? 1u << t : 0u, c = pc[t];  // (END / DEAD: no header)
+    if (nt < i0 + SEG) {                                             // lands in this segment
+      const uint2 r = W.JC[(nt - i0) * WAVE + lane];
+      ex = r.x & 0xFFFFu;
+      m |= r.x >> 16;
+      const uint32_t s2 = c + r.y;
+      c = s2 < c ? 0xFFFFFFFFu : s2;
+    }
+    W.JC[t * WAVE + lane] = make_uint2(ex | (m << 16), c);
+  }
+  wave_lds_sync();
+}
+
 // ------------------------------------------------------------------------------ k_lv_win
 // Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
 __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -1011,11 +1077,29 @@ __global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob,
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w;
     lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
-    uint32_t jv[LV_PPL], cv[LV_PPL];
-    lv_jump(W, x, jv, cv);
     // table of the entry offsets: (exit offset from W0 or terminal code | headers << 16, outputs)
     const uint32_t ent = lv_ent(w);
     uint2* tab = lt.tab + (uint64_t)g * ent;
+    if (w == 1) {  // 64 entry offsets: lane e follows entry e across the segments
+      uint32_t pc[LV_SEG], pv[LV_SEG], bpm;
+      lv_seg_build(W, x, pc, pv, bpm);
+      uint32_t e = lane, hs = 0, c = 0;
+#pragma unroll 1
+      while (__any(e < LV_WIN)) {
+        if (e < LV_WIN) {
+          const uint2 r = W.JC[(e % LV_SEG) * WAVE + e / LV_SEG];
+          hs += (uint32_t)__builtin_popcount(r.x >> 16);
+          const uint32_t s2 = c + r.y;
+          c = s2 < c ? 0xFFFFFFFFu : s2;
+          e = r.x & 0xFFFFu;
+        }
+      }
+      tab[lane] = make_uint2(e | (min(hs, 0xFFFFu) << 16), c);
+      wave_lds_sync();  // the next window's stage and table
+      continue;
+    }
+    uint32_t jv[LV_PPL], cv[LV_PPL];
+    lv_jump(W, x, jv, cv);
 #pragma unroll
     for (uint32_t j = 0; j < LV_PPL; ++j) {
       const uint32_t i = j * WAVE + lane;
@@ -1692,71 +1776,52 @@ __global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob
       R = (uint32_t)__shfl((int)R, 0, 64);
       T = __shfl(T, 0, 64);
     } else {
-      // dense window: pointer jumping marks the positions reachable from the entry
-      uint32_t jv[LV_PPL], cv[LV_PPL];
-      lv_first_hops(W.stage, x.sb, x.W0, slen, w, vb, jv, cv);
-#pragma unroll
-      for (uint32_t j = 0; j < LV_PPL; ++j) {
-        jv[j] &= 0xFFFFu;
-        W.J16[j * WAVE + lane] = (uint16_t)jv[j];
-      }
-      reinterpret_cast<uint4*>(W.R)[lane] = make_uint4(0u, 0u, 0u, 0u);
-      wave_lds_sync();
-      if (lane == 0) W.R[e0] = 1;
-      wave_lds_sync();
+      // dense window: lane l takes the 16 positions [16 l, 16 l + 16) (a segment). Every
+      // position is parsed as a header; a backward pass over the segment gives, per position,
+      // where its chain leaves the segment, the outputs on the way and the headers it passes
+      // (a mask); then one walk from the entry, one table lookup per segment, finds the true
+      // headers of every segment and the output each segment starts at.
+      constexpr uint32_t SEG = LV_SEG;
+      uint32_t pc[SEG], pv[SEG], bpm;
+      lv_seg_build(W, x, pc, pv, bpm);
+      // the walk from the entry (wave-uniform): segment s's true headers and first output
+      const uint64_t lim = (uint64_t)n - base;
+      uint32_t e = e0, mym = 0;
+      uint64_t acc = 0, myacc = 0;
 #pragma unroll 1
-      for (uint32_t r = 0; r < LV_ROUNDS; ++r) {
-        bool live = false;
-#pragma unroll
-        for (uint32_t j = 0; j < LV_PPL; ++j) live |= jv[j] < LV_WIN;
-        if (!__any(live)) break;
-        uint32_t rb = 0, nj[LV_PPL];
-#pragma unroll
-        for (uint32_t j = 0; j < LV_PPL; ++j) {
-          rb |= (uint32_t)W.R[j * WAVE + lane] << j;
-          nj[j] = jv[j] < LV_WIN ? (uint32_t)W.J16[jv[j]] : jv[j];
+      while (e < LV_WIN) {
+        const uint32_t sg = e / SEG;
+        const uint2 r = W.JC[(e % SEG) * WAVE + sg];
+        const uint32_t rx = rfl(r.x), ry = rfl(r.y);
+        if (lane == sg) {
+          mym = rx >> 16;
+          myacc = acc;
         }
-        wave_lds_sync();
-#pragma unroll
-        for (uint32_t j = 0; j < LV_PPL; ++j) {
-          if (((rb >> j) & 1u) && jv[j] < LV_WIN) W.R[jv[j]] = 1;  // idempotent: no atomics needed
-          jv[j] = nj[j];
-          W.J16[j * WAVE + lane] = (uint16_t)jv[j];
-        }
-        wave_lds_sync();
+        acc += ry;
+        if (acc >= lim) break;
+        e = rx & 0xFFFFu;
       }
-      // the true headers, in stream order (j-major, then lane): parse, count, place
-      uint32_t mine = 0;
+      // a dead header, or the stream's end, before n outputs
+      bad = acc < lim && (e == LV_J_DEAD || e == LV_J_END);
+      wave_lds_sync();  // the table's space now holds the run list
+      const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
+      const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
+      uint32_t k = rb;
+      uint64_t oa = (uint64_t)base + myacc;
 #pragma unroll
-      for (uint32_t j = 0; j < LV_PPL; ++j) mine |= (uint32_t)W.R[j * WAVE + lane] << j;
-      wave_lds_sync();  // the jump table's space now holds the run list
-#pragma unroll 1
-      for (uint32_t j = 0; j < LV_PPL; ++j) {
-        const uint32_t i = j * WAVE + lane;
-        uint32_t nx, c = 0, v = 0;
-        bool bp = false, hdr = (mine >> j) & 1u, dead = false;
-        if (hdr && !lv_parse4(W.stage, i + x.sb, x.W0 + i, slen, w, vb, nx, c, v, bp)) {
-          dead = true;  // a true header the window path does not take: fatal unless n comes first
-          hdr = false;
-        }
-        if (!hdr) c = 0;
-        const uint64_t hb = __ballot(hdr);
-        const uint64_t db = __ballot(dead);
-        if (!hb && !db) continue;  // no true header in this row
-        const uint32_t ir = (uint32_t)__builtin_popcountll(hb & ((2ull << lane) - 1ull));
-        const uint64_t ic = wave_incl_scan_cnt(c);
-        const uint64_t acc = (uint64_t)base + T + ic - c;
-        if (hdr) {
-          const uint32_t k = R + ir - 1u;
-          W.runs.rstart[k] = acc < 0xFFFFFFFFull ? (uint32_t)acc : 0xFFFFFFFFu;
+      for (uint32_t t = 0; t < SEG; ++t) {
+        if ((mym >> t) & 1u) {
+          const bool bp = (bpm >> t) & 1u;
+          const uint32_t v = pv[t];
+          W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
           W.runs.rinfo[k] = bp ? v : (R_RLE | v);
-          bad |= !lv_run_ok(bp, v, c, acc, n, slen, w);
+          bad |= !lv_run_ok(bp, v, pc[t], oa, n, slen, w);
+          ++k;
+          oa += pc[t];
         }
-        bad |= dead && acc < n;
-        R += (uint32_t)__builtin_popcountll(hb);
-        T += __shfl(ic, 63, 64);
-        if (db) break;  // nothing after a dead header is on the chain
       }
+      R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
+      T = acc;
     }
     if (__ballot(bad)) {
       if (lane == 0) lv_bail(rt, x.p, PF_PAGE);
