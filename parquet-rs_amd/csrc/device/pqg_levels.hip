@@ -88,7 +88,6 @@ struct LvWave {
       uint32_t rinfo[LV_RCAP];
     } runs;
   };
-  uint8_t R[LV_WIN];        // k_lv_emit: 1 = position reachable from the true entry
 };
 
 struct LvSmem {
@@ -1060,7 +1059,7 @@ __device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV
 
 // ------------------------------------------------------------------------------ k_lv_win
 // Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
-__global__ void __launch_bounds__(WG) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                const PageWork* __restrict__ pages, int npages,
                                                ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
   __shared__ LvSmem sm;
@@ -1728,7 +1727,7 @@ struct LvBaDictOut {
 // ------------------------------------------------------------------------------ k_lv_emit
 // Window path: windows g2 of the dense pages.
 template <int OUT>
-__global__ void __launch_bounds__(WG) k_lv_emit(const uint8_t* __restrict__ blob, uint64_t blob_len,
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_emit(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                 PageWork* pages, int npages, ColumnParams cp, int sel,
                                                 RunTables rt, LevelTables lt, uint8_t* __restrict__ out) {
   __shared__ LvSmem sm;
