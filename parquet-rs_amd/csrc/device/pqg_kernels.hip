@@ -260,10 +260,10 @@ struct LevelsPageMaker {
   __device__ void done(const QDesc&, uint32_t, TxLevels& em) { acc += em.nonnull; }
 };
 
-__global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                    ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
-                                                    int16_t* __restrict__ out) {
+__device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                        PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                        ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
+                                        int16_t* __restrict__ out) {
   __shared__ IndexSmem ism;
   __shared__ TileSmem sm;
   __shared__ int32_t st_s;
@@ -295,6 +295,19 @@ __global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ 
     const uint64_t nn = block_sum_u64(mk.acc, red);
     if (threadIdx.x == 0) pages[p].nonnull = nn;
   }
+}
+
+__device__ inline void scan_values(PageWork* pages, int npages, ChunkResult* res, int es, uint64_t cap_bytes);
+
+// scan_es >= 0 (a def stream, no rep stream after it): the grid's last workgroup also runs
+// k_scan_values (the non-null counts are final), one launch fewer per chunk.
+__global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    PageWork* pages, const uint32_t* __restrict__ tile_page,
+                                                    ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
+                                                    int16_t* __restrict__ out, uint32_t* ctr, int scan_es,
+                                                    uint64_t scan_cap) {
+  lv_fallback_page(blob, blob_len, pages, tile_page, cp, sel, rt, res, out);
+  if (scan_es >= 0 && last_workgroup(ctr)) scan_values(pages, (int)gridDim.x, res, scan_es, scan_cap);
 }
 
 // Tile expand of RLE_DICTIONARY indices with the dictionary gather.
@@ -413,9 +426,7 @@ __global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint3
 // ------------------------------------------------------------------------------ scan
 
 // Exclusive scan of per-page value counts -> value_out (single workgroup).
-__global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages,
-                                                    ChunkResult* res, int es,
-                                                    uint64_t cap_bytes) {
+__device__ inline void scan_values(PageWork* pages, int npages, ChunkResult* res, int es, uint64_t cap_bytes) {
   __shared__ uint64_t wsum[WG / 64];
   __shared__ uint64_t carry_s;
   if (threadIdx.x == 0) carry_s = 0;
@@ -448,6 +459,11 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages,
     __syncthreads();
   }
   if (threadIdx.x == 0) res->total_values = carry_s;
+}
+
+__global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages, ChunkResult* res, int es,
+                                                    uint64_t cap_bytes) {
+  scan_values(pages, npages, res, es, cap_bytes);
 }
 
 // ------------------------------------------------------------------------------ dictionary
@@ -576,14 +592,14 @@ hipError_t pqg_launch_page_counts(PageWork* pages, int npages, RunTables rt, int
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
                              int npages, uint32_t ntiles, ColumnParams cp, int which,
                              const uint32_t* tile_page, RunTables rt, LevelTables lt, int16_t* out,
-                             ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
+                             ChunkResult* res, hipStream_t s, hipEvent_t* kev, int scan_es, uint64_t scan_cap) {
   const int sel = which ? SS_REP : SS_DEF;
   if (kev) (void)hipEventRecord(kev[0], s);
   hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, -1, 0, rt, lt, out, res, s);
   if (kev) (void)hipEventRecord(kev[1], s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp, sel, rt, res,
-                     out);
+                     out, lt.ctr + 1, scan_es, scan_cap);
   return hipGetLastError();
 }
 

@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
 }
 
 // One workgroup: windows of the pages the walker left to the window path (wbase2).
-__global__ void __launch_bounds__(WG) k_lv_plan2(int npages, RunTables rt, LevelTables lt) {
+__device__ inline void lv_plan2_scan(int npages, RunTables rt, LevelTables lt) {
   lv_scan_windows(npages, lt.wbase2, [&](int p) -> uint32_t {
     return rt.pflag[p] == PF_PAGE ? lt.wbase[p + 1] - lt.wbase[p] : 0u;
   });
@@ -829,8 +829,8 @@ __device__ inline uint32_t lv_segscan_serial(LvSeg* seg, const uint2* srec, uint
   }
 }
 
-__global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+__device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
+                                       int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
   __shared__ uint64_t wout[WG / WAVE];
   __shared__ uint32_t wrun[WG / WAVE], wlast[WG / WAVE], wmin[WG / WAVE];
   __shared__ uint64_t c_out;
@@ -957,6 +957,14 @@ __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ b
   __syncthreads();
   if (verdict_s != 0)
     for (uint32_t q = tid; q < nseg; q += WG) seg[q].flags = 0;
+}
+
+// The grid's last workgroup also runs k_lv_plan2's scan (the windows of the pages left to the
+// window path), one launch fewer per level stream.
+__global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
+                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+  lv_segscan_page(blob, pages, npages, cp, sel, rt, lt);
+  if (last_workgroup(lt.ctr + 0)) lv_plan2_scan(npages, rt, lt);
 }
 
 // ------------------------------------------------------------------------------ k_lv_compact
@@ -2076,7 +2084,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
                          cp, sel, rt, lt, LvDictOut<4>{dict_page, o, res});
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_lv_plan2, dim3(1), dim3(WG), 0, s, npages, rt, lt);
+  // (k_lv_plan2's scan ran in k_lv_segscan's last workgroup)
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
   // window tables of 64 / 128 entry offsets (bit width 1 / 2) take the readlane walks
   const int lw = sel == SS_DEF ? cp.def_bit_width : sel == SS_REP ? cp.rep_bit_width : 1;

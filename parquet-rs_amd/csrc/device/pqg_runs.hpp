@@ -301,6 +301,25 @@ __device__ inline void ix_install(uint32_t* region, uint32_t lane, const uint4 (
 
 __device__ inline uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
+// True in exactly one workgroup of the grid, the last to arrive here, after every workgroup's
+// earlier global writes are visible to it: lets a one-workgroup pass that depends on the whole
+// grid (a scan over pages) run in the grid's last workgroup instead of its own launch. Every
+// workgroup of the grid must call it (no early exit before it); the ticket counter (zeroed once
+// at allocation) is reset by the last workgroup for the next launch using it.
+__device__ inline bool last_workgroup(uint32_t* ctr) {
+  __shared__ uint32_t last_s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this workgroup's writes before its ticket
+    const uint32_t t = atomicAdd(ctr, 1u);
+    last_s = t == gridDim.x * gridDim.y * gridDim.z - 1u;
+    if (last_s) atomicExch(ctr, 0u);
+  }
+  __syncthreads();
+  if (last_s) __threadfence();  // acquire: the other workgroups' writes (no stale cache lines)
+  return last_s != 0;
+}
+
 // One batch of k <= 64 consecutive headers of the chain (lane l: header at stream offset posv,
 // staged at region index posv - rbase): parse, prefix-sum output counts, make every check the
 // reference makes while reading them and write the run records, tile checkpoints and per-tile

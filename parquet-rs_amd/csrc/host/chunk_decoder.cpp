@@ -26,7 +26,7 @@ hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, Column
                                 RunTables, ChunkResult*, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
                              const uint32_t*, RunTables, LevelTables, int16_t*, ChunkResult*,
-                             hipStream_t, hipEvent_t*);
+                             hipStream_t, hipEvent_t*, int, uint64_t);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
                            hipStream_t);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
@@ -99,7 +99,7 @@ struct Slot {
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
   // level path (def, rep, RLE booleans): buffers of LevelTables (pqg_internal.hpp), grown on demand
-  static constexpr int LV_BUFS = 12;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense
+  static constexpr int LV_BUFS = 13;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr
   void* lvbuf[3][LV_BUFS] = {};
   size_t lvcap[3][LV_BUFS] = {};
   LevelTables lt(int k) const {
@@ -116,6 +116,7 @@ struct Slot {
     t.srec = (uint2*)lvbuf[k][9];
     t.spos = (uint32_t*)lvbuf[k][10];
     t.dense = (uint32_t*)lvbuf[k][11];
+    t.ctr = (uint32_t*)lvbuf[k][12];
     return t;
   }
 };
@@ -656,11 +657,14 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     const size_t need[Slot::LV_BUFS] = {(size_t)npages + 1, (size_t)npages + 1, nwin + npages + 1,
                                         64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1,
                                         (size_t)npages + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP,
-                                        (size_t)npages + 1};
+                                        (size_t)npages + 1, 16};
     const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2),
-                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4};
+                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4, 4};
+    const bool fresh_ctr = sl.lvbuf[k][12] == nullptr;
     for (int b = 0; b < Slot::LV_BUFS; ++b)
       if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
+    // the tickets start at zero once; every launch using them leaves them at zero
+    if (fresh_ctr) HIPCHK(hipMemsetAsync(sl.lvbuf[k][12], 0, sl.lvcap[k][12] * 4, s), "memset level tickets");
   }
   // Hybrid-stream flags: the level path (def, rep, RLE booleans) sets every page's flag and counts
   // the streams it hands back; dictionary indices always take the general decoder. k_prepare
@@ -713,19 +717,21 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (ctx->timing) hipEventRecord(ctx->ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, ini, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
+  // the value-offset scan runs in the def stream's last kernel when no rep stream follows it
+  const bool fused_scan = np && want_def && !want_rep && !ctx->timing;
   if (np && want_def) {
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              sl.lt(0), out->def_levels, ctx->d_res, s,
-                             ctx->timing ? &sl.ev[6] : nullptr),
+                             ctx->timing ? &sl.ev[6] : nullptr, fused_scan ? es : -1, out->values_capacity),
            "def levels");
     sl.kl = ctx->timing;
   }
   if (np && want_rep)
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
-                             sl.lt(1), out->rep_levels, ctx->d_res, s, nullptr),
+                             sl.lt(1), out->rep_levels, ctx->d_res, s, nullptr, -1, 0),
            "rep levels");
   if (ctx->timing) hipEventRecord(ctx->ev[2], s);
-  HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
+  if (!fused_scan) HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
   if (ctx->timing) hipEventRecord(ctx->ev[3], s);
   ctx->values_kernel = 0;
   if (np && vo && is_ba) {

@@ -199,6 +199,8 @@ struct LevelTables {
   uint2* win;        // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
   uint32_t* dense;   // [pages] 1: the stream's first 64 headers lie within 1 KiB (k_lv_probe): the
                      // window path takes it without a segment walk
+  uint32_t* ctr;     // [16] last-workgroup tickets (zero between launches): [0] k_lv_segscan,
+                     // [1] k_lv_fallback
 };
 
 // RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window

@@ -316,3 +316,32 @@ def test_level_streams_the_level_path_hands_back(oracle, ctx, nbytes):
         vals = rng.integers(-2 ** 31, 2 ** 31, size=nn, dtype=np.int64).astype(np.int32)
         pages.append(oracle.PageSpec(oracle.PAGE_DATA, lev + vals.tobytes(), n, oracle.PLAIN))
     _same(oracle, ctx, oracle.INT32, pages, max_def=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("long_run", [3000, 70000, 200000])
+def test_dense_level_windows_with_long_runs(oracle, ctx, long_run):
+    """Dense one-bit def-level streams (10% nulls: a header every few bytes, the window path) with
+    one long RLE run in the middle: the window holding it writes tens of thousands of outputs
+    from one run among hundreds of short ones. Runs of ones and of zeros; a dense page without a
+    long run after them."""
+    rng = np.random.default_rng(long_run)
+    pages = []
+    for k in range(4):
+        d1 = (rng.random(8 * (2500 + 125 * k)) > 0.1).astype(np.int16)
+        d3 = (rng.random(8 * 1875) > 0.1).astype(np.int16)
+        d1[-16:] = 1  # the prefix's encoding ends in an RLE run (no padded bit-packed group)
+        if k == 3:  # a dense page without a long run
+            defs = np.concatenate([d1, d3])
+            lev = oracle.level_encode(defs, 1)
+        else:
+            v = k % 2
+            body = (oracle.rle_encode(d1.astype(np.uint64), 1) + _leb_padded(long_run << 1, 3) + bytes([v]) +
+                    oracle.rle_encode(d3.astype(np.uint64), 1))
+            defs = np.concatenate([d1, np.full(long_run, v, np.int16), d3])
+            lev = len(body).to_bytes(4, "little") + body
+        n = len(defs)
+        nn = int(defs.sum())
+        vals = rng.integers(-2 ** 31, 2 ** 31, size=nn, dtype=np.int64).astype(np.int32)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, lev + vals.tobytes(), n, oracle.PLAIN))
+    _same(oracle, ctx, oracle.INT32, pages, max_def=1)
