@@ -700,9 +700,9 @@ def main(argv=None):
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "note": ("HIP events around pqg_launch_levels: the def-level kernel chain (k_lv_plan, "
-                              "k_lv_bound, k_lv_segwalk, k_lv_segscan, k_lv_compact, k_lv_plan2, k_lv_win, "
-                              "k_lv_stitch, k_lv_emit, k_lv_emit_walk + the general decoder's fallback "
-                              "kernels), one launch each per step; traffic = their PMC sum")
+                              "k_lv_bound, k_lv_segwalk, k_lv_segscan (+ the window scan in its last "
+                              "workgroup), k_lv_compact, k_lv_win, k_lv_stitch, k_lv_emit, k_lv_emit_walk, "
+                              "k_lv_fallback), one launch each per step; traffic = their PMC sum")
                      if name == "level path" else None,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms,
