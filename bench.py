@@ -1,19 +1,28 @@
 #!/usr/bin/env python3
 """Device-resident Parquet page-decode benchmark (BASELINE.json metric) on MI355X.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config levels|dict|delta] [...]
+  python bench.py [--gpus N --steps K --warmup W] [--config all|levels|dict|delta|alltypes] [...]
 
-A step is one decode of the whole synthetic column (BASELINE.json configs[1..3], 1e9
-levels/values per GPU) through the C ABI (pqg_decode_chunk), with the page bytes already
-resident in HBM. With --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
-N ranks through torch.distributed.run (before touching the GPU) and exits with their status;
-every rank decodes its own partition (its own row groups, seed + rank): weak scaling, no
-collective on the data path. Rank 0 prints one JSON line.
+A step is one decode of the whole synthetic workload through the C ABI with the page bytes
+already resident in HBM:
+  configs[1] (headline, `levels`): 1e9 one-bit def levels + 1e9 PLAIN INT32 values (p_null 0,
+      the literal config), 954 pages of 2^20 levels; p_null 0.5 / 0.1 variants alongside;
+  configs[2] (`dict`): RLE_DICTIONARY INT64, 65 536-entry dictionary, 1e9 indices;
+  configs[3] (`delta`): DELTA_BINARY_PACKED INT64, 1e9 values, 128-value mini-blocks;
+  configs[4] (`alltypes`): this GPU's share of the alltypes_plain-schema file (88 row groups of
+      2^23 rows, ~64 GiB decoded): row groups partitioned over the ranks.
+The default (`all`) times every config in one run; the JSON line's top level is configs[1], the
+others are under "configs". With --gpus N > 1 and no WORLD_SIZE in the environment, this process
+starts N ranks through torch.distributed.run (before touching the GPU) and exits with their
+status; every rank decodes its own partition: weak scaling, no collective on the data path (gloo
+carries the barrier and the max-over-ranks step time). Rank 0 prints one JSON line.
 
-The reported roofline is for the dominant kernel, timed with HIP events on the decode stream
-over the timed steps; the CPU baseline is the C restatement of parquet-rs's decode loop
-(oracle/, kind "port") on a bounded sample, one decoder per thread, at 1 thread and at every
-host core, batch sizes 32/64/128/1024 (benches/decoding.rs:103-123, record/reader.rs:33).
+ms_per_step is timed on the production kernel sequence with stage timing off; a second, shorter
+pass with HIP events on the decode stream (pqg_ctx_set_timing) gives the dominant kernel's time
+for the roofline. The CPU baseline is the C restatement of parquet-rs's decode loop (oracle/,
+kind "port") on a bounded sample, one decoder per thread, at 1 thread and at the host threads
+this process may use, batch sizes 32/64/128/1024 (benches/decoding.rs:103-123,
+record/reader.rs:33).
 """
 import argparse
 import ctypes as C
@@ -33,6 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 HBM_ACHIEVABLE_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
 METRIC = "decoded values/s + GB/s, device-resident page decode, 1/2/4/8 MI355X"
+FILE_ROW_GROUPS = 8          # config 5's file = FILE_ROW_GROUPS x --rowgroups row groups
 
 
 def parse(argv=None):
@@ -40,19 +50,19 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="levels", choices=["levels", "dict", "delta", "alltypes"])
+    ap.add_argument("--config", default="all", choices=["all", "levels", "dict", "delta", "alltypes"])
     ap.add_argument("--n", type=float, default=1e9, help="levels/values per GPU")
-    ap.add_argument("--p-null", type=float, default=0.5)
+    ap.add_argument("--p-null", type=float, default=0.0, help="configs[1]: null fraction of the def levels")
     ap.add_argument("--page-values", type=int, default=1 << 20)
     ap.add_argument("--dict-size", type=int, default=65536)
     ap.add_argument("--delta-bits", type=int, default=16)
     ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--mini-blocks", type=int, default=4)
-    ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0 / 0.1 variants")
+    ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0.5 / 0.1 variants")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--pcie", type=int, default=1, help="also time the host-to-host (PCIe) rate")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--threads", type=int, default=16, help="host threads (box CPU share: 16)")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline budget of the headline")
+    ap.add_argument("--threads", type=int, default=16, help="host threads at most (box CPU share: 16)")
     ap.add_argument("--seed", type=int, default=0x5EED0000)
     ap.add_argument("--rowgroups", type=int, default=11,
                     help="alltypes: row groups per GPU (11 x 2^23 rows ~ 8 GiB decoded: 1/8 of config 5)")
@@ -65,7 +75,7 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-from sharding import max_over_ranks, shard_seed  # noqa: E402  (row-group partition per rank)
+from sharding import max_over_ranks, row_groups_for_rank, shard_seed  # noqa: E402
 
 
 def _free_port():
@@ -87,6 +97,33 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd, env=env)
 
 
+def host_threads(cap):
+    """Threads the CPU legs use: at most `cap` (the box's CPU share) and at most the CPUs this
+    process may run on; with the affinity and cgroup quota that bound them, for the record."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    n = max(1, min(cap, aff, int(quota) if quota else aff))
+    return n, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "nproc": os.cpu_count(), "cap": cap}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 class Workload:
     """Synthetic pages generated on the host by the reference-identical writers of
     libpqgtools.so (tools/gen) and uploaded once to HBM."""
@@ -102,23 +139,24 @@ class Workload:
         self.p_null = p_null
         self.page_values = args.page_values
         self.dict_size, self.delta_bits = args.dict_size, args.delta_bits
+        th = host_threads(args.threads)[0]
         if kind == "levels":
             self.seed = shard_seed(args.seed + 2, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_levels_plain(
-                n, p_null, args.page_values, self.seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+                n, p_null, args.page_values, self.seed, th, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
             self.es = 4
         elif kind == "dict":
             self.seed = shard_seed(args.seed + 3, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64(
-                n, args.dict_size, args.page_values, self.seed, args.threads, blob, cap, pages, pcap, C.byref(info))
+                n, args.dict_size, args.page_values, self.seed, th, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
         else:
             self.seed = shard_seed(args.seed + 4, rank)
             gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64(
                 n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, self.seed,
-                args.threads, blob, cap, pages, pcap, C.byref(info))
+                th, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
         st = gen(None, 0, None, 0)
@@ -205,12 +243,12 @@ def check_values(ctx, w, stream):
     return {"pages_checked": checked, "status": st, "values": int(w.out.num_values)}
 
 
-def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
+def time_steps(ctx, w, stream, steps, warmup, dist=None):
+    """Seconds per step over `steps` decodes, production path (no stage events)."""
     import torch
     for _ in range(warmup):
         decode_once(ctx, w, stream)
     ctx.sync()
-    pqgpu.lib().pqg_reset_timings(ctx.h)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -223,25 +261,24 @@ def time_steps(pqgpu, ctx, w, stream, steps, warmup, dist=None):
     if dist is not None:
         dist.barrier()
     assert st == 0, (st, bad, ctx.error_message())
-    return (t1 - t0) / steps, ctx.timings()
+    return (t1 - t0) / steps
 
 
-def torch_device():
-    import torch
-    return torch.cuda.current_device()
+def time_stages(pqgpu, ctx, w, stream, n):
+    """Average stage / dominant-kernel device times over n decodes with HIP events on the decode
+    stream (the same kernel sequence as the production path)."""
+    ctx.set_timing(True)
+    pqgpu.lib().pqg_reset_timings(ctx.h)
+    for _ in range(n):
+        decode_once(ctx, w, stream)
+    st, bad = ctx.sync()
+    assert st == 0, (st, bad, ctx.error_message())
+    tm = ctx.timings()
+    ctx.set_timing(False)
+    return tm
 
 
-def cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
-
-
-def cpu_baseline(w, seconds, threads):
+def cpu_baseline(w, seconds, threads, thr_info):
     """parquet-rs's decode loop restated in C (oracle, kind "port"): ColumnReaderImpl::
     read_batch(batch) per reader, one reader per thread over disjoint pages (the reference's Rc
     types are !Send, so one reader per row group / thread is its only parallelism). Timed at 1
@@ -280,7 +317,7 @@ def cpu_baseline(w, seconds, threads):
         res[(th, b)] = (n / dt, npg, n, dt)
     head = res[(threads, 1024)]
     return {"value": head[0], "unit": "values/s" if w.kind != "levels" else "levels/s",
-            "cores": threads, "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "cores": threads, "kind": "port", "cpu_model": cpu_model(), "host_cpus": thr_info,
             "sample": f"{head[1]} of {w.npages} pages ({head[2]} levels/values), read_batch(1024), "
                       f"one reader per thread, {head[3]:.1f}s wall",
             "by_threads_batch": {f"{th}t_b{b}": round(v[0], 1) for (th, b), v in res.items()}}
@@ -318,15 +355,16 @@ def pcie_inclusive(ctx, w, stream, iters=3):
 LEVEL_PATH = ("k_lv_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
 
 
-def pmc_traffic(kind, kernel):
+def pmc_traffic(kind, kernel, variant=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this config
-    (profiles/<round>/<config>/kernels.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 +
-    WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). The def-level path is a chain of
-    kernels timed as one (HIP events around pqg_launch_levels): its traffic is their sum (every
-    kernel of the chain runs once per decode). None when not profiled."""
+    (profiles/<round>/<config>[_<variant>]/kernels.json, written by tools/pmc_traffic.py:
+    FETCH_SIZE x2 + WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). The def-level path
+    is a chain of kernels timed as one (HIP events around pqg_launch_levels): its traffic is their
+    sum (every kernel of the chain runs once per decode). None when not profiled."""
     base = kernel.split("<")[0]
+    sub = kind if variant is None else f"{kind}_{variant}"
     for rnd in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True):
-        path = os.path.join(ROOT, "profiles", rnd, kind, "kernels.json")
+        path = os.path.join(ROOT, "profiles", rnd, sub, "kernels.json")
         if not os.path.exists(path):
             continue
         try:
@@ -354,42 +392,133 @@ def copy_ceiling_gbs(nbytes=4 << 30):
     return L.pqg_copy_ceiling_gbs(nbytes, 10)
 
 
+def roofline(name, ms, nbytes, traffic, traffic_src, note=None):
+    achieved = nbytes / (ms * 1e-3) / 1e9 if ms else None
+    return {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+            "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms,
+            "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS if achieved else None, "note": note}
+
+
+LEVEL_NOTE = ("HIP events around pqg_launch_levels: the def-level kernel chain (k_lv_plan, k_lv_bound, "
+              "k_lv_segwalk, k_lv_segscan, k_lv_compact, k_lv_win, k_lv_stitch, k_lv_emit, k_lv_emit_walk, "
+              "k_lv_fallback + the fused value-offset scan), one launch each per step; traffic = their PMC sum")
+
+
+def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, steps=None, warmup=None,
+              cpu_seconds=None, extras=True):
+    """One of configs[1..3]: generate, check, time (production path), stage times, roofline, and
+    on rank 0 of a 1-GPU run the PCIe-inclusive rate and the CPU baseline."""
+    import torch
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    w = Workload(pqgpu, args, rank, kind, p_null=p_null)
+    checked = check_values(ctx, w, stream)
+    per_step = max_over_ranks(time_steps(ctx, w, stream, steps, warmup, dist), dist)
+    tm = time_stages(pqgpu, ctx, w, stream, max(3, steps // 4))
+    units = w.levels if kind == "levels" else w.values
+    step_bytes = w.in_bytes + w.out_bytes
+    variant = None
+    if kind == "levels":
+        lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
+        val_b = 2 * w.values * w.es               # PLAIN values in + out
+        variant = f"p{int(round(p_null * 100)):02d}"
+        stages = [("level path", tm.levels_kernel_ms, lev_b), ("k_plain_copy", tm.values_kernel_ms, val_b)]
+    elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
+        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
+    else:                  # deltas in + values out
+        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
+    rl = []
+    for name, ms, nb in stages:
+        tr, src = pmc_traffic(kind, name, variant)
+        rl.append(roofline(name, ms, nb, tr, src, LEVEL_NOTE if name == "level path" else None))
+    dom = max(rl, key=lambda r: r["avg_ms"] or 0)
+    res = {
+        "value": units * world / per_step,
+        "unit": "levels/s" if kind == "levels" else "values/s",
+        "ms_per_step": per_step * 1e3,
+        "gbps": step_bytes / per_step / 1e9 * world,
+        "config": {"workload": {"levels": "configs[1]: RLE/bit-packed def levels (max_def 1) + PLAIN INT32",
+                                "dict": "configs[2]: RLE_DICTIONARY INT64, 64K dictionary",
+                                "delta": "configs[3]: DELTA_BINARY_PACKED INT64"}[kind],
+                   "levels_per_gpu": w.levels, "values_per_gpu": w.values,
+                   "pages_per_gpu": w.npages, "page_values": args.page_values,
+                   "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes, "out_bytes_per_gpu": w.out_bytes,
+                   "block_size": args.block_size if kind == "delta" else None,
+                   "mini_blocks": args.mini_blocks if kind == "delta" else None,
+                   "gen_seconds": round(w.gen_s, 1),
+                   "parallelism": f"row-group partitions x{world}, no collective"},
+        "roofline": dom,
+        "roofline_stages": rl if len(rl) > 1 else None,
+        "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
+                      "values": tm.values_ms, "total": tm.total_ms,
+                      "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},
+        "value_check": checked,
+    }
+    if extras and rank == 0 and world == 1:
+        if args.pcie:
+            res["pcie_inclusive"] = pcie_inclusive(ctx, w, stream)
+        if args.cpu_baseline:
+            th, info = host_threads(args.threads)
+            res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds if cpu_seconds is None else cpu_seconds, th, info)
+    del w
+    torch.cuda.empty_cache()
+    return res
+
+
 def dry_run(args, world, rank, dist):
     """Launcher / partition / reduction plumbing without a GPU: every rank derives its own
-    partition seed, the max-over-ranks step time is reduced over gloo, rank 0 prints a line
-    marked dry_run with no value."""
+    partition (seed, config-5 row groups), the max-over-ranks step time is reduced over gloo,
+    rank 0 prints a line marked dry_run with no value."""
     seed = shard_seed(args.seed + 2, rank)
+    mine = alltypes_partition(args, world, rank)
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))
     per_step = max_over_ranks(time.perf_counter() - t0, dist)
-    seeds = [seed]
+    seeds, parts = [seed], [mine]
     if dist is not None:
-        seeds = [None] * world
+        seeds, parts = [None] * world, [None] * world
         dist.all_gather_object(seeds, seed)
+        dist.all_gather_object(parts, mine)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "values/s", "n_gpus": world,
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "levels/s", "n_gpus": world,
                           "steps": 0, "warmup": 0, "ms_per_step": per_step * 1e3, "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dry_run": True,
                           "config": {"workload": args.config, "partition_seeds": seeds,
+                                     "alltypes_row_groups": parts,
                                      "parallelism": f"row-group partitions x{world}, no collective"}}),
               flush=True)
 
 
-class AlltypesWorkload:
-    """Config 5 (one GPU's share): `rowgroups` row groups of the alltypes_plain schema, written by
-    the reference writer's defaults (tools/gen pqg_gen_alltypes), pages of all row groups in one
-    pinned host buffer and one device buffer; one pqg_decode_chunk per column chunk."""
+def alltypes_partition(args, world, rank):
+    """Row groups of config 5's file this rank decodes. The file has FILE_ROW_GROUPS x --rowgroups
+    row groups of --rg-rows rows (88 x 2^23 rows, ~64 GiB decoded); a run on `world` GPUs decodes
+    its first --rowgroups x world (all of it at 8 GPUs: weak scaling), split over the ranks by
+    sharding.row_groups_for_rank (contiguous, balanced by bytes; the synthetic row groups have
+    equal row counts and the same column mix, so rows stand in for their bytes)."""
+    file_rgs = FILE_ROW_GROUPS * args.rowgroups
+    job = min(file_rgs, args.rowgroups * world)
+    return row_groups_for_rank([args.rg_rows] * job, world, rank)
 
-    def __init__(self, pqgpu, args, rank):
+
+class AlltypesWorkload:
+    """Config 5 (one GPU's share): the row groups alltypes_partition assigns this rank, written by
+    the reference writer's defaults (tools/gen pqg_gen_alltypes), pages of all row groups in one
+    pinned host buffer and one device buffer; one pqg_rg_decode per row group."""
+
+    def __init__(self, pqgpu, args, rank, world):
         import torch
         import pqgtools
-        self.rows, self.R, self.p_null = args.rg_rows, args.rowgroups, args.at_p_null
-        self.seed = shard_seed(args.seed + 5, 0)
-        self.row0 = rank * self.R * self.rows  # this rank's row groups
+        self.rows, self.p_null = args.rg_rows, args.at_p_null
+        self.seed = shard_seed(args.seed + 5, 0)  # one file: every rank generates from the same seed
+        self.rg_index = alltypes_partition(args, world, rank)
+        self.R = len(self.rg_index)
+        self.row0s = [g * self.rows for g in self.rg_index]
+        self.job_rgs = min(FILE_ROW_GROUPS * args.rowgroups, args.rowgroups * world)
         self.cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+        th = host_threads(args.threads)[0]
         t0 = time.time()
-        rgs = [pqgtools.alltypes_row_group(self.rows, self.row0 + g * self.rows, self.p_null, self.seed,
-                                           args.threads) for g in range(self.R)]
+        rgs = [pqgtools.alltypes_row_group(self.rows, r0, self.p_null, self.seed, th) for r0 in self.row0s]
         self.gen_s = time.time() - t0
         self.base = []
         off = 0
@@ -430,7 +559,6 @@ class AlltypesWorkload:
             self.out.append(o)
         self.levels = self.R * self.rows * len(self.cols)  # cells: one level per row and column
         self.in_bytes = sum(i.blob_len for i in self.info)
-        es = {0: 1, 1: 4, 2: 8, 3: 12, 4: 4, 5: 8}
         self.out_bytes = 0
         for i in self.info:
             for j, (_, pt) in enumerate(pqgtools.ALLTYPES):
@@ -443,8 +571,8 @@ class AlltypesWorkload:
 
 
 def alltypes_check(ctx, w, stream):
-    """Decode row group 0 and compare every column (levels, values, BYTE_ARRAY offsets) with the
-    generator's own cells (pqg_truth_alltypes)."""
+    """Decode this rank's first row group and compare every column (levels, values, BYTE_ARRAY
+    offsets) with the generator's own cells (pqg_truth_alltypes)."""
     import pqgtools
     oa = w.decode_rg(ctx, 0, stream)
     st, bcol, bad = ctx.sync()
@@ -452,7 +580,7 @@ def alltypes_check(ctx, w, stream):
     for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
         nv, nb = w.info[0].num_values[j], w.info[0].value_bytes[j]
         assert oa[j].num_values == nv and oa[j].num_levels == w.rows, (name, oa[j].num_values, nv)
-        lv, vals, offs = pqgtools.alltypes_truth(w.row0, w.rows, j, w.p_null, w.seed, nb)
+        lv, vals, offs = pqgtools.alltypes_truth(w.row0s[0], w.rows, j, w.p_null, w.seed, nb)
         d_def, d_val, d_off, _ = w.out[0][j]
         assert np.array_equal(d_def[:w.rows].cpu().numpy(), lv), f"{name}: def levels differ"
         assert np.array_equal(d_val[:nb].cpu().numpy(), vals), f"{name}: values differ"
@@ -537,9 +665,9 @@ def alltypes_pcie(ctx, w, stream):
                     "decoded columns (three streams), one pass over all row groups"}
 
 
-def alltypes_cpu_baseline(w, threads):
-    """The C restatement of read_batch(1024) (oracle, kind "port") over row group 0's 11 column
-    chunks: one reader per chunk, at 1 thread and at `threads` threads."""
+def alltypes_cpu_baseline(w, threads, thr_info):
+    """The C restatement of read_batch(1024) (oracle, kind "port") over the first row group's 11
+    column chunks: one reader per chunk, at 1 thread and at `threads` threads."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     import pqgtools
@@ -564,34 +692,31 @@ def alltypes_cpu_baseline(w, threads):
             n = sum(ex.map(run, specs))
         res[th] = (n / (time.perf_counter() - t0), time.perf_counter() - t0)
     return {"value": res[threads][0], "unit": "values/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus": thr_info,
             "sample": f"row group 0 ({w.rows} rows x 11 columns), read_batch(1024), one reader per column "
                       f"chunk, {res[threads][1]:.1f}s wall",
             "by_threads": {f"{th}t_b1024": round(v[0], 1) for th, v in res.items()}}
 
 
-def main_alltypes(args, world, rank, dist, stream):
-    import pqgpu
-    w = AlltypesWorkload(pqgpu, args, rank)
-    ctx = pqgpu.RowGroupDecoder(torch_device(), args.streams)
+def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
+    import torch
+    w = AlltypesWorkload(pqgpu, args, rank, world)
+    ctx = pqgpu.RowGroupDecoder(torch.cuda.current_device(), args.streams)
     checked = alltypes_check(ctx, w, stream)
-    per_step = alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist)
-    per_step = max_over_ranks(per_step, dist, device="cuda")
+    per_step = max_over_ranks(alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist), dist)
     step_bytes = w.in_bytes + w.out_bytes
     achieved = step_bytes / per_step / 1e9
-    result = {
-        "metric": METRIC, "value": w.levels * world / per_step, "unit": "values/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+    res = {
+        "value": w.job_rgs * w.rows * len(w.cols) / per_step, "unit": "values/s (cells: one level + its value)",
+        "ms_per_step": per_step * 1e3, "gbps": step_bytes / per_step / 1e9 * world,
         "dtype": "int16 levels + native values (i32/i64/f32/f64/int96/bool bytes/byte arrays)",
-        "data": "synthetic alltypes_plain-schema row groups from the reference writer's defaults (SplitMix64 seeded)",
-        "gbps": step_bytes / per_step / 1e9 * world,
-        "config": {"workload": "configs[4]: alltypes_plain schema, one GPU's 1/8 share, row groups of "
-                               f"{w.rows} rows", "row_groups_per_gpu": w.R, "rows_per_gpu": w.R * w.rows,
-                   "cells_per_gpu": w.levels, "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes,
-                   "out_bytes_per_gpu": w.out_bytes, "chunk_decodes_per_step": w.R * len(w.cols),
-                   "gen_seconds": round(w.gen_s, 1), "streams": args.streams,
-                   "parallelism": f"row-group partitions x{world}, no collective"},
+        "config": {"workload": "configs[4]: alltypes_plain schema, this GPU's share of an "
+                               f"{FILE_ROW_GROUPS * args.rowgroups}-row-group file of {w.rows}-row row groups",
+                   "row_groups": w.rg_index, "row_groups_per_gpu": w.R, "job_row_groups": w.job_rgs,
+                   "rows_per_gpu": w.R * w.rows, "cells_per_gpu": w.levels, "p_null": w.p_null,
+                   "in_bytes_per_gpu": w.in_bytes, "out_bytes_per_gpu": w.out_bytes,
+                   "chunk_decodes_per_step": w.R * len(w.cols), "gen_seconds": round(w.gen_s, 1),
+                   "streams": args.streams, "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": "whole step (every chunk decode)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": step_bytes, "avg_ms": per_step * 1e3,
@@ -599,12 +724,16 @@ def main_alltypes(args, world, rank, dist, stream):
         "value_check": checked,
         "host_enqueue_ms_per_step": getattr(alltypes_steps, "host_ms", None),
     }
-    if rank == 0 and args.pcie and world == 1:
-        result["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)
-    if rank == 0 and args.cpu_baseline and world == 1:
-        result["cpu_baseline"] = alltypes_cpu_baseline(w, min(args.threads, os.cpu_count() or 1))
+    if extras and rank == 0 and world == 1:
+        if args.pcie:
+            res["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)
+        if args.cpu_baseline:
+            th, info = host_threads(args.threads)
+            res["cpu_baseline"] = alltypes_cpu_baseline(w, th, info)
     ctx.close()
-    return result
+    del w
+    torch.cuda.empty_cache()
+    return res
 
 
 def main(argv=None):
@@ -617,127 +746,58 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:  # barrier + max over ranks: two host scalars, gloo (no RCCL on this path)
+        import torch.distributed as td
+        td.init_process_group("gloo")
+        dist = td
     if args.dry_run:
-        dist = None
-        if world > 1:
-            import torch.distributed as td
-            td.init_process_group("gloo")
-            dist = td
         dry_run(args, world, rank, dist)
         if dist is not None:
             dist.destroy_process_group()
         return
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dist = td
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local if world > 1 else 0)
     import pqgpu
-    ctx = pqgpu.Context(torch.cuda.current_device(), timing=True)
     stream = torch.cuda.current_stream().cuda_stream
-
-    kind = args.config
-    if kind == "alltypes":
-        ctx.close()
-        result = main_alltypes(args, world, rank, dist, stream)
-        if rank == 0:
-            print(json.dumps(result), flush=True)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-    w = Workload(pqgpu, args, rank, kind, p_null=args.p_null if kind == "levels" else None)
-    checked = check_values(ctx, w, stream)
-    per_step, tm = time_steps(pqgpu, ctx, w, stream, args.steps, args.warmup, dist)
-    per_step = max_over_ranks(per_step, dist, device="cuda")
-    units = w.levels if kind == "levels" else w.values
-    value = units * world / per_step
-    step_bytes = w.in_bytes + w.out_bytes
-
-    # dominant kernel roofline: HIP events around that kernel's launch on the decode stream
-    # (pqg_timings.{levels,values}_kernel_ms), algorithmic bytes of that kernel per launch
-    if kind == "levels":
-        lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
-        val_b = 2 * w.values * w.es               # PLAIN values in + out
-        # the def-level path (pqg_levels.hip kernels) and the PLAIN copy
-        stages = [("level path", tm.levels_kernel_ms, lev_b),
-                  ("k_plain_copy", tm.values_kernel_ms, val_b)]
-    elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
-        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
-    else:                  # deltas in + values out
-        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
-    name, ms, nbytes = max(stages, key=lambda s: s[1])
-    traffic, traffic_src = pmc_traffic(kind, name)
-    achieved = nbytes / (ms * 1e-3) / 1e9
-
-    result = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "values/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": per_step * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": {"levels": "int16 levels + int32 values", "dict": "uint16 indices -> int64",
-                  "delta": "int64 (wrapping)"}[kind],
-        "data": "synthetic pages from reference-identical writers (SplitMix64 seeded)",
-        "gbps": step_bytes / per_step / 1e9 * world,
-        "config": {"workload": {"levels": "configs[1]: RLE/bit-packed def levels (max_def 1) + PLAIN INT32",
-                                "dict": "configs[2]: RLE_DICTIONARY INT64, 64K dictionary",
-                                "delta": "configs[3]: DELTA_BINARY_PACKED INT64"}[kind],
-                   "levels_per_gpu": w.levels, "values_per_gpu": w.values,
-                   "pages_per_gpu": w.npages, "page_values": args.page_values,
-                   "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes,
-                   "out_bytes_per_gpu": w.out_bytes,
-                   "block_size": args.block_size if kind == "delta" else None,
-                   "mini_blocks": args.mini_blocks if kind == "delta" else None,
-                   "parallelism": f"row-group partitions x{world}, no collective"},
-        "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "note": ("HIP events around pqg_launch_levels: the def-level kernel chain (k_lv_plan, "
-                              "k_lv_bound, k_lv_segwalk, k_lv_segscan (+ the window scan in its last "
-                              "workgroup), k_lv_compact, k_lv_win, k_lv_stitch, k_lv_emit, k_lv_emit_walk, "
-                              "k_lv_fallback), one launch each per step; traffic = their PMC sum")
-                     if name == "level path" else None,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "bytes_per_launch": nbytes, "avg_ms": ms,
-                     "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
-        "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
-                      "values": tm.values_ms, "total": tm.total_ms,
-                      "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},
-        "value_check": checked,
-    }
+    head = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "data": "synthetic pages from reference-identical writers (SplitMix64 seeded)"}
+    sub = {}
+    kinds = ["levels", "dict", "delta", "alltypes"] if args.config == "all" else [args.config]
+    ctx = pqgpu.Context(torch.cuda.current_device())
+    short_steps = max(5, args.steps // 2)
+    for kind in kinds:
+        if kind == "alltypes":
+            sub[kind] = run_alltypes(pqgpu, args, world, rank, dist, stream)
+        elif kind == "levels":
+            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "levels", p_null=args.p_null)
+            if args.variants:
+                var = {}
+                for p in (0.5, 0.1):
+                    r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "levels", p_null=p,
+                                  steps=short_steps, warmup=2, extras=False)
+                    var[f"p_null={p}"] = {"levels_per_s": r["value"], "ms_per_step": r["ms_per_step"],
+                                          "gbps": r["gbps"], "values_per_gpu": r["config"]["values_per_gpu"],
+                                          "roofline": r["roofline"], "roofline_stages": r["roofline_stages"],
+                                          "stages_ms": r["stages_ms"], "value_check": r["value_check"]}
+                sub[kind]["variants"] = var
+        else:
+            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, cpu_seconds=6.0)
+    ctx.close()
+    top = kinds[0]
+    result = dict(head)
+    result.update(sub[top])
+    result.setdefault("dtype", {"levels": "int16 levels + int32 values", "dict": "uint16 indices -> int64",
+                                "delta": "int64 (wrapping)"}.get(top))
+    if len(kinds) > 1:
+        result["configs"] = {k: sub[k] for k in kinds[1:]}
     if rank == 0:
         try:
             result["copy_ceiling_gbs"] = copy_ceiling_gbs()
         except Exception as e:  # pragma: no cover
             result["copy_ceiling_gbs"] = str(e)
-    if rank == 0 and args.pcie and world == 1:
-        result["pcie_inclusive"] = pcie_inclusive(ctx, w, stream)
-    if rank == 0 and args.cpu_baseline and world == 1:
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, min(args.threads, os.cpu_count() or 1))
-    if kind == "levels" and args.variants and world == 1:
-        var = {}
-        for p in (0.0, 0.1):
-            del w
-            torch.cuda.empty_cache()
-            wv = Workload(pqgpu, args, rank, "levels", p_null=p)
-            check_values(ctx, wv, stream)
-            ps, tv = time_steps(pqgpu, ctx, wv, stream, max(3, args.steps // 2), 2)
-            var[f"p_null={p}"] = {"levels_per_s": wv.levels / ps, "ms_per_step": ps * 1e3,
-                                  "gbps": (wv.in_bytes + wv.out_bytes) / ps / 1e9,
-                                  "levels_ms": tv.levels_ms, "values_ms": tv.values_ms,
-                                  "levels_kernel_ms": tv.levels_kernel_ms}
-            w = wv
-        result["variants"] = var
-    if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -138,7 +138,10 @@ int pqg_ctx_set_timing(pqg_ctx *ctx, int enabled);
 
 /* Enqueue the decode of one column chunk on `stream` (asynchronous). `blob` is a device
  * buffer of `blob_len` bytes holding every page payload; `pages` is host memory (copied
- * during the call). Returns immediately with PQG_OK or an argument error. */
+ * during the call). Returns immediately with PQG_OK or an argument error.
+ * `out` is written again later, when the decode's counters are delivered (by pqg_sync, or
+ * when the ctx reuses the decode's staging two decodes on): the pqg_output struct itself must
+ * stay valid until the pqg_sync that follows this call. */
 int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
                      uint64_t blob_len, const pqg_page *pages, uint32_t npages,
                      pqg_output *out, void *stream);
@@ -150,8 +153,9 @@ int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
 /* Record assembly on the device (the layout TypedTripletIter builds per batch,
  * record/triplet.rs:300-318, over a whole decoded chunk): spaced[i] = the value of level i when
  * def_levels[i] == max_def (values = the decode's dense fixed-width values, value_size 1 / 4 / 8
- * / 12 bytes), zero bytes otherwise. All pointers are device memory; enqueued on `stream`
- * (NULL: the ctx's stream) after the decode that produced them. */
+ * / 12 bytes), zero bytes otherwise. All pointers are device memory and required (values too,
+ * even when no level is non-null); enqueued on `stream` (NULL: the ctx's stream) after the
+ * decode that produced them. */
 int pqg_space_values(pqg_ctx *ctx, const int16_t *def_levels, uint64_t num_levels, int16_t max_def,
                      const void *values, int value_size, void *spaced, void *stream);
 /* Averages over all decodes since pqg_reset_timings (timing must be enabled). */
@@ -167,7 +171,8 @@ const char *pqg_error_message(pqg_ctx *ctx);
  * streams back into `stream` before returning. pages[j] / npages[j] / outs[j] are column j's
  * arguments of pqg_decode_chunk, all pages in the one device blob. Asynchronous: pqg_rg_sync
  * waits and fills every outs[j]; it returns the first failing column's status (lowest index)
- * and names that column and its page. */
+ * and names that column and its page. pages and outs (the arrays and the structs) must stay
+ * valid until that sync. */
 typedef struct pqg_rg_ctx pqg_rg_ctx;
 int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx **out);
 int pqg_rg_ctx_destroy(pqg_rg_ctx *g);
@@ -175,6 +180,10 @@ int pqg_rg_decode(pqg_rg_ctx *g, uint32_t ncols, const pqg_column *cols, const u
                   uint64_t blob_len, const pqg_page *const *pages, const uint32_t *npages,
                   pqg_output *outs, void *stream);
 int pqg_rg_sync(pqg_rg_ctx *g, int *bad_column, int *bad_page);
+/* pqg_rg_sync that also reports which pqg_rg_decode call (0 = the first since the last sync)
+ * failed. With several row groups in flight the failure reported is the one the reference meets
+ * first: the earliest failing row group, and in it the lowest failing column. */
+int pqg_rg_sync_call(pqg_rg_ctx *g, int *bad_call, int *bad_column, int *bad_page);
 const char *pqg_rg_error_message(pqg_rg_ctx *g);
 
 /* ---------------------------------------------------------------- host-side reader

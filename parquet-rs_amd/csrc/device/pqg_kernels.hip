@@ -784,6 +784,10 @@ __global__ void __launch_bounds__(WG) k_space_scatter(const int16_t* __restrict_
 
 extern "C" {
 
+// Tiles (SP_T levels each) pqg_launch_space needs `tiles` entries for: the host sizes its buffer
+// from this, not from a copy of the constant.
+uint64_t pqg_space_tiles(uint64_t n) { return (n + SP_T - 1) / SP_T; }
+
 hipError_t pqg_launch_space(const int16_t* def, uint64_t n, int16_t max_def, const void* values, int es,
                             uint64_t* tiles, void* spaced, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -42,6 +42,7 @@ hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_
 hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
                             ChunkResult*, hipStream_t);
 hipError_t pqg_launch_space(const int16_t*, uint64_t, int16_t, const void*, int, uint64_t*, void*, hipStream_t);
+uint64_t pqg_space_tiles(uint64_t n);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
                                   DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t,
                                   hipEvent_t*);
@@ -136,6 +137,7 @@ struct pqg_ctx {
   // first failure among decodes delivered at a slot's reuse, reported by the next pqg_sync
   int held_status = 0;
   int held_page = -1;
+  uint64_t held_seq = 0;
   std::string held_msg;
   double acc_ms[7] = {};
   uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
@@ -428,6 +430,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       if (st && !ctx->held_status) {
         ctx->held_status = st;
         ctx->held_page = page;
+        ctx->held_seq = sl.seq;
         ctx->held_msg = m;
       }
     }
@@ -710,7 +713,9 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     ini.val[nw_++] = 0u;
   }
   ini.dict_page = dict_page;
-  ini.dict_es = (np && vo && !is_ba && enc_present[PQG_RLE_DICTIONARY]) ? es : 0;
+  // configure_dictionary decodes the dictionary page whenever the reader reaches it, whatever the
+  // data pages' encodings and whether values are read (column/reader.rs:463-481)
+  ini.dict_es = (np && dict_page >= 0 && !is_ba) ? es : 0;
   ini.dense_def = need_lv[0] ? sl.lt(0).dense : nullptr;
   ini.dense_rep = need_lv[1] ? sl.lt(1).dense : nullptr;
   ini.dense_zero = (need_lv[2] && dict_lv) ? sl.lt(2).dense : nullptr;
@@ -718,7 +723,8 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, ini, s), "prepare");
   if (ctx->timing) hipEventRecord(ctx->ev[1], s);
   // the value-offset scan runs in the def stream's last kernel when no rep stream follows it
-  const bool fused_scan = np && want_def && !want_rep && !ctx->timing;
+  // (timed runs take the same kernel sequence: the stage events bracket the fused kernel)
+  const bool fused_scan = np && want_def && !want_rep;
   if (np && want_def) {
     HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
                              sl.lt(0), out->def_levels, ctx->d_res, s,
@@ -806,11 +812,11 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
 // Device-side record assembly of a decoded chunk (pqg_launch_space, device/pqg_kernels.hip).
 int pqg_space_values(pqg_ctx* ctx, const int16_t* def_levels, uint64_t num_levels, int16_t max_def,
                      const void* values, int value_size, void* spaced, void* stream) {
-  if (!ctx || (num_levels && (!def_levels || !spaced || (!values && max_def >= 0))) ||
+  if (!ctx || (num_levels && (!def_levels || !spaced || !values)) ||
       (value_size != 1 && value_size != 4 && value_size != 8 && value_size != 12))
     return PQG_ERR_INVALID;
   if (num_levels == 0) return PQG_OK;
-  const size_t nt = (size_t)((num_levels + 4095) / 4096);
+  const size_t nt = (size_t)pqg_space_tiles(num_levels);
   if (nt > ctx->sp_cap) {
     hipFree(ctx->sp_tiles);
     ctx->sp_tiles = nullptr;
@@ -823,18 +829,30 @@ int pqg_space_values(pqg_ctx* ctx, const int16_t* def_levels, uint64_t num_level
   return e == hipSuccess ? PQG_OK : set_err(ctx, PQG_ERR_HIP, "spacing launch: %s", hipGetErrorString(e));
 }
 
-int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
+// pqg_sync that also names the failing decode by its issue number (pqg_decode_seq); the
+// row-group decoder maps it back to its own call (row_group.cpp).
+int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq);
+
+int pqg_sync(pqg_ctx* ctx, int* first_bad_page) { return pqg_sync_seq(ctx, first_bad_page, nullptr); }
+
+// Issue number of the last decode enqueued on ctx (1, 2, ...; 0 before the first).
+uint64_t pqg_decode_seq(pqg_ctx* ctx) { return ctx ? ctx->seq : 0; }
+
+int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq) {
   if (!ctx) return PQG_ERR_INVALID;
   if (first_bad_page) *first_bad_page = -1;
+  if (bad_seq) *bad_seq = 0;
   Slot* order[2] = {&ctx->slot[ctx->cur ^ 1], &ctx->slot[ctx->cur]};
   if (order[0]->pending && order[1]->pending && order[0]->seq > order[1]->seq) std::swap(order[0], order[1]);
   if (!order[0]->pending && !order[1]->pending && !ctx->held_status)
     return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
   // every pending decode is delivered, in issue order; the first failure is reported
   int st = ctx->held_status, page = ctx->held_page;
+  uint64_t seq = ctx->held_seq;
   std::string msg = ctx->held_msg;
   ctx->held_status = 0;
   ctx->held_page = -1;
+  ctx->held_seq = 0;
   ctx->held_msg.clear();
   hipError_t herr = hipSuccess;
   for (Slot* sl : order) {
@@ -852,16 +870,19 @@ int pqg_sync(pqg_ctx* ctx, int* first_bad_page) {
     sl->used = false;
     int pg;
     std::string m;
+    const uint64_t sq = sl->seq;
     const int s2 = finish_slot(*sl, &pg, m);
     if (s2 && !st) {
       st = s2;
       page = pg;
+      seq = sq;
       msg = m;
     }
   }
   if (herr != hipSuccess) return hip_fail(ctx, herr, "hipEventSynchronize");
   ctx->msg = msg;
   if (first_bad_page) *first_bad_page = page;
+  if (bad_seq) *bad_seq = st ? seq : 0;
   return st;
 }
 

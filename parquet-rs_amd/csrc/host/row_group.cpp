@@ -27,6 +27,11 @@
 
 #include "../../../include/pqgpu.h"
 
+extern "C" {
+int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq);  // chunk_decoder.cpp
+uint64_t pqg_decode_seq(pqg_ctx* ctx);
+}
+
 // One host thread per stream: runs the enqueue jobs handed to it, one batch per decode call.
 struct RgWorker {
   std::thread th;
@@ -81,6 +86,10 @@ struct pqg_rg_ctx {
   hipEvent_t fork = nullptr;
   std::vector<pqg_ctx*> cols;   // one decode context per column index
   std::vector<int> issued;      // decodes pending per column
+  // per column, the decodes pending: (the column ctx's issue number, this decoder's call index
+  // since the last sync), so that a failure is reported at its (call, column)
+  std::vector<std::vector<std::pair<uint64_t, int>>> pend;
+  int calls_since_sync = 0;
   std::vector<RgWorker*> workers;
   uint64_t calls = 0;           // decode calls: rotates the stream assignment
   std::string msg;
@@ -151,7 +160,9 @@ int pqg_rg_decode(pqg_rg_ctx* g, uint32_t ncols, const pqg_column* cols, const u
     if (st) return rg_fail(g, st, "pqg_ctx_create");
     g->cols.push_back(c);
     g->issued.push_back(0);
+    g->pend.emplace_back();
   }
+  const int call = g->calls_since_sync++;
   hipStream_t caller = (hipStream_t)stream_v;
   if (hipEventRecord(g->fork, caller) != hipSuccess) return rg_fail(g, PQG_ERR_HIP, "fork event");
   const size_t K = g->streams.size();
@@ -203,6 +214,7 @@ int pqg_rg_decode(pqg_rg_ctx* g, uint32_t ncols, const pqg_column* cols, const u
       continue;
     }
     g->issued[j]++;
+    g->pend[j].emplace_back(pqg_decode_seq(g->cols[j]), call);
   }
   for (size_t k = 0; k < K; ++k) {
     if (hipEventRecord(g->join[k], g->streams[k]) != hipSuccess ||
@@ -212,26 +224,44 @@ int pqg_rg_decode(pqg_rg_ctx* g, uint32_t ncols, const pqg_column* cols, const u
   return first_err;
 }
 
-int pqg_rg_sync(pqg_rg_ctx* g, int* bad_column, int* bad_page) {
+// The failure reported is the one the reference meets first: the earliest row group (decode
+// call) with a failing column, and in it the lowest failing column index.
+int pqg_rg_sync_call(pqg_rg_ctx* g, int* bad_call, int* bad_column, int* bad_page) {
   if (!g) return PQG_ERR_INVALID;
+  if (bad_call) *bad_call = -1;
   if (bad_column) *bad_column = -1;
   if (bad_page) *bad_page = -1;
-  int first = PQG_OK;
+  int first = PQG_OK, fcall = 0x7FFFFFFF, fcol = -1;
   for (size_t j = 0; j < g->cols.size(); ++j) {
     if (!g->issued[j]) continue;
     g->issued[j] = 0;
     int page = -1;
-    const int st = pqg_sync(g->cols[j], &page);
-    if (st && !first) {
+    uint64_t seq = 0;
+    const int st = pqg_sync_seq(g->cols[j], &page, &seq);
+    int call = g->pend[j].empty() ? 0 : g->pend[j].back().second;
+    for (const auto& pc : g->pend[j])
+      if (pc.first == seq) call = pc.second;
+    g->pend[j].clear();
+    if (st && (call < fcall || (call == fcall && (int)j < fcol))) {
       first = st;
-      if (bad_column) *bad_column = (int)j;
+      fcall = call;
+      fcol = (int)j;
       if (bad_page) *bad_page = page;
       char buf[320];
-      snprintf(buf, sizeof(buf), "column %zu: %s", j, pqg_error_message(g->cols[j]));
+      snprintf(buf, sizeof(buf), "row group call %d, column %zu: %s", call, j, pqg_error_message(g->cols[j]));
       g->msg = buf;
     }
   }
+  g->calls_since_sync = 0;
+  if (first) {
+    if (bad_call) *bad_call = fcall;
+    if (bad_column) *bad_column = fcol;
+  }
   return first;
+}
+
+int pqg_rg_sync(pqg_rg_ctx* g, int* bad_column, int* bad_page) {
+  return pqg_rg_sync_call(g, nullptr, bad_column, bad_page);
 }
 
 }  // extern "C"

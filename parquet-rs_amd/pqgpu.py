@@ -67,7 +67,7 @@ EXPORTS = [
     "pqg_triplet_iter_read_next", "pqg_triplet_iter_has_next", "pqg_triplet_iter_def_level",
     "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
     "pqg_space_values", "pqg_rg_ctx_create", "pqg_rg_ctx_destroy", "pqg_rg_decode", "pqg_rg_sync",
-    "pqg_rg_error_message",
+    "pqg_rg_sync_call", "pqg_rg_error_message",
 ]
 
 _lib = None
@@ -127,6 +127,7 @@ def lib():
         L.pqg_rg_decode.argtypes = [vp, C.c_uint32, C.POINTER(Column), vp, u64, C.POINTER(C.POINTER(Page)),
                                     C.POINTER(C.c_uint32), C.POINTER(Output), vp]
         L.pqg_rg_sync.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.pqg_rg_sync_call.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.pqg_rg_error_message.argtypes = [vp]
         L.pqg_rg_error_message.restype = C.c_char_p
         _lib = L
@@ -164,6 +165,10 @@ class Context:
 
     def error_message(self):
         return lib().pqg_error_message(self.h).decode(errors="replace")
+
+    def set_timing(self, enabled):
+        """HIP events around the decode stages (pqg_get_timings); call with no decode pending."""
+        lib().pqg_ctx_set_timing(self.h, 1 if enabled else 0)
 
     def decode_async(self, column, blob, blob_len, pages, out, stream=0, npages=None):
         """Enqueue pqg_decode_chunk. `blob` is a device pointer (int), `pages` a ctypes Page
@@ -233,6 +238,13 @@ class RowGroupDecoder:
         st = lib().pqg_rg_sync(self.h, C.byref(col), C.byref(page))
         self._keep = self._keep[-1:]
         return st, col.value, page.value
+
+    def sync_call(self):
+        """(status, failing decode call since the last sync, bad column, bad page)."""
+        call, col, page = C.c_int(-1), C.c_int(-1), C.c_int(-1)
+        st = lib().pqg_rg_sync_call(self.h, C.byref(call), C.byref(col), C.byref(page))
+        self._keep = self._keep[-1:]
+        return st, call.value, col.value, page.value
 
 
 def make_pages(specs):

@@ -156,6 +156,36 @@ def test_gpu_row_group_decoder_reports_failing_column(rowgroup):
 
 
 @pytest.mark.gpu
+def test_gpu_row_group_decoder_reports_earliest_row_group():
+    """Two row groups in flight before one sync: the first fails on column 5 (bigint_col's data
+    page cut short), the second on column 1. The reference reads row group 0 first and stops at
+    its column 5, so pqg_rg_sync_call names call 0, column 5 (not the lower column of call 1)."""
+    import pqgpu
+    import torch
+    blob, pages, info = pqgtools.alltypes_row_group(70_000, ROW0, P_NULL, SEED, threads=8)
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob[:info.blob_len + 64])).cuda()
+    cols = [pqgpu.Column(pt, -1, 1, 0) for _, pt in pqgtools.ALLTYPES]
+    first, second = _rg_pages(pqgpu, pages, info), _rg_pages(pqgpu, pages, info)
+    first[5][1].nbytes = 40      # bigint_col: dictionary page, then its one data page
+    second[1][0].nbytes = 64     # bool_col: its PLAIN data page
+    rgd = pqgpu.RowGroupDecoder(0, 4)
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        sets = [_rg_outputs(torch, info, 70_000) for _ in range(2)]
+        rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, first, sets[0][1], s)
+        rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, second, sets[1][1], s)
+        st, call, bcol, bad = rgd.sync_call()
+        assert st != 0 and (call, bcol, bad) == (0, 5, 1), (st, call, bcol, bad, rgd.error_message())
+        # one row group failing alone: call 0, its column
+        rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, _rg_pages(pqgpu, pages, info), sets[0][1], s)
+        rgd.decode_async(cols, d_blob.data_ptr(), info.blob_len, second, sets[1][1], s)
+        st, call, bcol, bad = rgd.sync_call()
+        assert st != 0 and (call, bcol, bad) == (1, 1, 0), (st, call, bcol, bad)
+    finally:
+        rgd.close()
+
+
+@pytest.mark.gpu
 def test_gpu_row_group_pipeline():
     """The bench's config-5 loop at small scale: four row groups decoded by one row-group decoder
     (16 streams), alternating two launch streams and two output sets, so that row group g + 1 is

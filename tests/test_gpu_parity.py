@@ -250,7 +250,7 @@ def test_kat_vectors_on_gpu(oracle, ctx):
 
 
 @pytest.mark.parametrize("case", ["trunc_bp", "trunc_plain", "bad_dict_idx", "no_dict",
-                                  "bad_prefix", "delta_trunc"])
+                                  "bad_prefix", "delta_trunc", "trunc_dict_plain"])
 def test_errors_match_reference_class(oracle, ctx, case):
     """Malformed pages: the GPU path reports an error wherever the reference errors, panics
     or hangs; it never returns data there."""
@@ -271,6 +271,11 @@ def test_errors_match_reference_class(oracle, ctx, case):
         pages = [d, oracle.PageSpec(oracle.PAGE_DATA, bytes([3, 0x03, 0x88, 0xC6, 0xFA]), 8, oracle.RLE_DICTIONARY)]
     elif case == "no_dict":
         pages = [oracle.PageSpec(oracle.PAGE_DATA, bytes([1, 0x10, 0x01]), 8, oracle.RLE_DICTIONARY)]
+    elif case == "trunc_dict_plain":
+        # a dictionary page cut short, then PLAIN pages only: configure_dictionary still decodes
+        # the dictionary (column/reader.rs:463-481, decoding.rs:145-147) and returns EOF
+        d = oracle.PageSpec(oracle.PAGE_DICTIONARY, np.arange(5, dtype=np.int32).tobytes()[:-2], 5, oracle.PLAIN)
+        pages = [d, oracle.PageSpec(oracle.PAGE_DATA, np.arange(10, dtype=np.int32).tobytes(), 10, oracle.PLAIN)]
     elif case == "bad_prefix":
         pages = [oracle.PageSpec(oracle.PAGE_DATA, b"\xff\x00\x00\x00\x02\x01", 1, oracle.PLAIN)]
         max_def = 1
@@ -281,6 +286,8 @@ def test_errors_match_reference_class(oracle, ctx, case):
     got = pqgpu.decode_column(ctx, ptype, pages, max_def=max_def)
     assert ref["status"] != 0
     assert got["status"] != 0, "GPU decoded a page the reference rejects"
+    if case == "trunc_dict_plain":
+        assert ref["status"] == oracle.EOF and got["status"] == pqgpu.EOF and got["page"] == 0
 
 
 def test_large_chunk_properties(oracle, ctx):

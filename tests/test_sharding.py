@@ -78,6 +78,23 @@ def test_bench_launches_n_ranks_dry_run():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["dry_run"] is True and res["value"] is None
     assert len(set(res["config"]["partition_seeds"])) == 2
+    # config 5: the two ranks split the first 22 row groups of the one 88-row-group file
+    assert res["config"]["alltypes_row_groups"] == [list(range(11)), list(range(11, 22))]
+
+
+def test_bench_alltypes_partition_is_one_file():
+    """bench.alltypes_partition: at N GPUs the ranks split the first 11 N row groups of config 5's
+    88-row-group file (weak scaling), contiguous, each exactly once; at 8 GPUs the whole file."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    args = bench.parse([])
+    for world in (1, 2, 4, 8):
+        parts = [bench.alltypes_partition(args, world, r) for r in range(world)]
+        assert [g for p in parts for g in p] == list(range(11 * world))
+        assert all(len(p) == 11 for p in parts)
+    assert bench.alltypes_partition(args, 8, 7)[-1] == bench.FILE_ROW_GROUPS * 11 - 1
 
 
 def test_bench_refuses_debug_env():
