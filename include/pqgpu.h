@@ -146,10 +146,24 @@ int pqg_decode_chunk(pqg_ctx *ctx, const pqg_column *col, const uint8_t *blob,
                      uint64_t blob_len, const pqg_page *pages, uint32_t npages,
                      pqg_output *out, void *stream);
 
+/* Enqueue the decode of a batch of column chunks in one pass (asynchronous): chunk j is
+ * cols[j], its pages pages[j][0 .. npages[j]) (offsets into the one device blob) and its outputs
+ * outs[j], as pqg_decode_chunk takes them. The chunks share nothing (each is what one column
+ * reader of the reference decodes, file/reader.rs:252-260, 306-330); the batch runs every kernel
+ * once over all their pages, so one row group, or several, costs the launches of one chunk. The
+ * outs structs must stay valid until the pqg_sync that delivers them. */
+int pqg_decode_chunks(pqg_ctx *ctx, uint32_t nchunks, const pqg_column *cols, const uint8_t *blob,
+                      uint64_t blob_len, const pqg_page *const *pages, const uint32_t *npages,
+                      pqg_output *outs, void *stream);
+
 /* Wait for every decode enqueued on the ctx since the last pqg_sync, fill their outputs and
  * report the status of the first one (in issue order) that failed. On error *first_bad_page
  * names that decode's lowest failing page (the page the reference would fail on first). */
 int pqg_sync(pqg_ctx *ctx, int *first_bad_page);
+/* pqg_sync naming the failure fully: *bad_call = index of the failing decode call since the last
+ * sync (0 = the first), *bad_chunk = its lowest failing chunk (0 for pqg_decode_chunk),
+ * *bad_page = that chunk's lowest failing page. -1 when all succeeded. */
+int pqg_sync_detail(pqg_ctx *ctx, int *bad_call, int *bad_chunk, int *bad_page);
 /* Record assembly on the device (the layout TypedTripletIter builds per batch,
  * record/triplet.rs:300-318, over a whole decoded chunk): spaced[i] = the value of level i when
  * def_levels[i] == max_def (values = the decode's dense fixed-width values, value_size 1 / 4 / 8
@@ -164,15 +178,15 @@ int pqg_reset_timings(pqg_ctx *ctx);
 const char *pqg_error_message(pqg_ctx *ctx);
 
 /* ---------------------------------------------------------------- row groups
- * The column chunks of one row group decoded concurrently. The reference reads every column
- * chunk of a row group through its own page reader and column reader (file/reader.rs:252-260,
- * 306-330); they share nothing, so pqg_rg_decode forks `stream` onto `nstreams` HIP streams,
- * decodes column j with a context of its own (scratch reused across row groups) and joins the
- * streams back into `stream` before returning. pages[j] / npages[j] / outs[j] are column j's
- * arguments of pqg_decode_chunk, all pages in the one device blob. Asynchronous: pqg_rg_sync
- * waits and fills every outs[j]; it returns the first failing column's status (lowest index)
- * and names that column and its page. pages and outs (the arrays and the structs) must stay
- * valid until that sync. */
+ * The column chunks of one row group decoded together. The reference reads every column chunk
+ * of a row group through its own page reader and column reader (file/reader.rs:252-260,
+ * 306-330); they share nothing, so pqg_rg_decode is one pqg_decode_chunks of them on `stream`
+ * (two row groups may be in flight: the ctx has two staging slots; `nstreams` is accepted for
+ * compatibility, 1..16). pages[j] / npages[j] / outs[j] are column j's arguments of
+ * pqg_decode_chunk, all pages in the one device blob. Asynchronous: pqg_rg_sync waits and fills
+ * every outs[j]; it returns the first failing column's status (lowest index) and names that
+ * column and its page. pages and outs (the arrays and the structs) must stay valid until that
+ * sync. */
 typedef struct pqg_rg_ctx pqg_rg_ctx;
 int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx **out);
 int pqg_rg_ctx_destroy(pqg_rg_ctx *g);

@@ -154,6 +154,11 @@ __device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen,
   return sm.ctl[5] ? ST_PANIC : 0;
 }
 
+// Byte arrays of this chunk: FIXED_LEN_BYTE_ARRAY type length, 0 for BYTE_ARRAY.
+__device__ inline int ba_type_length(const ChunkWork& ck) {
+  return ck.cp.physical_type == T_FLBA ? ck.cp.type_length : 0;
+}
+
 // Sum of a page's output value lengths -> pages[p].nbytes_out.
 __device__ void page_bytes(DeltaSmem& sm, PageWork* pages, int p, uint64_t n, const uint32_t* len,
                            const uint32_t* pre) {
@@ -164,11 +169,18 @@ __device__ void page_bytes(DeltaSmem& sm, PageWork* pages, int p, uint64_t n, co
 }
 
 // Dictionary page of a BYTE_ARRAY / FLBA column: DictDecoder::set_dict decodes every entry
-// with PlainDecoder (decoding.rs:282-288).
+// with PlainDecoder (decoding.rs:282-288). One workgroup per chunk of the decode; the entries go
+// to the chunk's slots of the dictionary scratch (dscr_base on).
 __global__ void __launch_bounds__(WG) k_ba_dict_prep(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, int dict_page, int type_length,
-                                                     uint64_t* dsrc, uint32_t* dlen, ChunkResult* res) {
+                                                     PageWork* pages, ChunkWork* chunks, uint64_t* dsrc0,
+                                                     uint32_t* dlen0) {
   __shared__ DeltaSmem sm;
+  const ChunkWork& ck = chunks[blockIdx.x];
+  if (ck.es != 0 || ck.dict_page < 0 || !ck.val_out) return;
+  const int dict_page = ck.dict_page;
+  const int type_length = ba_type_length(ck);
+  uint64_t* dsrc = dsrc0 + ck.dscr_base;
+  uint32_t* dlen = dlen0 + ck.dscr_base;
   const PageWork dp = pages[dict_page];
   if (dp.status != 0) return;
   const uint64_t n = dp.num_values;
@@ -184,7 +196,7 @@ __global__ void __launch_bounds__(WG) k_ba_dict_prep(const uint8_t* __restrict__
   } else {
     st = plain_ba_walk(sm, blob, blob_len, S, dp.nbytes, n, dsrc, dlen);
   }
-  if (st && threadIdx.x == 0) report(pages, res, dict_page, st);
+  if (st && threadIdx.x == 0) report(pages, chunks, dict_page, st);
 }
 
 struct BaDictEmit {
@@ -212,32 +224,96 @@ struct BaDictEmit {
   }
 };
 
-// Dictionary indices -> (source, length) of the entry: wave expand pass over the tiles of the
-// index pass (k_run_index with SS_DICT); per quarter-tile byte totals go to rt.qcount.
+// Dictionary indices -> (source, length) of the entry: wave expand pass over the quarters of the
+// listed tiles (the index pass: k_run_index with SS_DICT); per quarter-tile byte totals go to
+// rt.qcount[4 t + q].
 __global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void k_wexpand_badict(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                       PageWork* pages, RunTables rt, int dict_page,
-                                                       const uint64_t* dsrc, const uint32_t* dlen,
-                                                       uint64_t* vsrc, uint32_t* vlen, ChunkResult* res) {
+                                                       PageWork* pages, ChunkWork* chunks, RunTables rt,
+                                                       const uint32_t* __restrict__ tl, const uint64_t* dsrc,
+                                                       const uint32_t* dlen, uint64_t* vsrc, uint32_t* vlen) {
   __shared__ WaveSmem sm;
-  const QDesc d = load_qdesc(&rt.desc[blockIdx.x]);
-  BaDictEmit em{dsrc, dlen, dict_page >= 0 ? pages[dict_page].num_values : 0u, vsrc, vlen, 0, 0};
-  if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, sm, em);
+  const uint32_t qi = 4u * tl[blockIdx.x >> 2] + (blockIdx.x & 3u);
+  const QDesc d = load_qdesc(&rt.desc[qi]);
+  BaDictEmit em{dsrc, dlen, 0u, vsrc, vlen, 0, 0};
+  if (d.qhi) {
+    const ChunkWork& ck = chunks[pages[d.page].chunk];
+    em.dsrc += ck.dscr_base;
+    em.dlen += ck.dscr_base;
+    em.src += ck.scr_base;
+    em.len += ck.scr_base;
+    em.ndict = pages[ck.dict_page].num_values;
+    wave_expand(blob, blob_len, d, rt.runs, sm, em);
+  }
   const uint64_t bad = __ballot(em.err != 0);
-  if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
+  if (bad && (threadIdx.x & 63) == 0) report(pages, chunks, (int)d.page, ST_PANIC);
   uint64_t b = em.bytes;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) b += __shfl_xor(b, off, 64);
-  if ((threadIdx.x & 63) == 0) rt.qcount[blockIdx.x] = (uint32_t)min(b, (uint64_t)0xFFFFFFFFu);
+  if ((threadIdx.x & 63) == 0) rt.qcount[qi] = (uint32_t)min(b, (uint64_t)0xFFFFFFFFu);
+}
+
+// Byte-array dictionary index streams the level path handed back, one workgroup per page (as
+// k_dict_fallback for fixed-width values): index walk, then each tile of the page expanded by the
+// workgroup's four waves (one quarter each), the page's byte total summed.
+__global__ void __launch_bounds__(WG) k_badict_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                        PageWork* pages, ChunkWork* chunks,
+                                                        const uint32_t* __restrict__ tile_page, RunTables rt,
+                                                        const uint64_t* dsrc, const uint32_t* dlen, uint64_t* vsrc,
+                                                        uint32_t* vlen) {
+  __shared__ IndexSmem ism;
+  __shared__ WaveSmem wsm[WG / 64];
+  __shared__ int32_t st_s;
+  __shared__ uint64_t red[WG / 64];
+  const int p = blockIdx.x;
+  if (rt.pflag[p] != PF_BAIL) return;
+  const PageWork pw = pages[p];
+  if (pw.status != 0) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.es != 0) return;
+  Stream s;
+  if (!get_stream(blob, pw, SS_DICT, ck.cp, s)) return;
+  if (ck.dict_page < 0) {  // "Decoder for dict should have been set"
+    if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
+    return;
+  }
+  if (pages[ck.dict_page].status != 0) return;
+  if (threadIdx.x < 64) {
+    const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
+                                 rt.nruns + pw.ltile0, ism);
+    if (threadIdx.x == 0) {
+      st_s = st;
+      if (st) report(pages, chunks, p, st);
+    }
+  }
+  __syncthreads();
+  if (st_s) return;
+  const uint32_t wid = threadIdx.x >> 6;
+  BaDictEmit em{dsrc + ck.dscr_base, dlen + ck.dscr_base, pages[ck.dict_page].num_values, vsrc + ck.scr_base,
+                vlen + ck.scr_base, 0, 0};
+  for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
+    const QDesc d = quarter_desc(blob, pages, chunks, tile_page, rt, SS_DICT, t, wid);
+    if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, wsm[wid], em);
+  }
+  const uint64_t bad = __ballot(em.err != 0);
+  if (bad && (threadIdx.x & 63) == 0) report(pages, chunks, p, ST_PANIC);
+  const uint64_t tb = block_sum_u64(em.bytes, red);
+  if (threadIdx.x == 0) pages[p].nbytes_out = tb;
 }
 
 __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                 PageWork* pages, int type_length, uint64_t* vsrc,
-                                                 uint32_t* vlen, uint32_t* vpre, ChunkResult* res) {
+                                                 PageWork* pages, ChunkWork* chunks, uint64_t* vsrc0,
+                                                 uint32_t* vlen0, uint32_t* vpre0) {
   __shared__ DeltaSmem sm;
   const int p = blockIdx.x;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.es != 0 || !ck.val_out) return;
+  const int type_length = ba_type_length(ck);
+  uint64_t* vsrc = vsrc0 + ck.scr_base;
+  uint32_t* vlen = vlen0 + ck.scr_base;
+  uint32_t* vpre = vpre0 + ck.scr_base;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   const uint64_t S = pw.base + pw.val_off;
   const uint32_t slen = pw.val_bytes;
@@ -314,50 +390,32 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
       return;  // dictionary pages of data (k_ba_dict_idx)
   }
   if (st) {
-    if (threadIdx.x == 0) report(pages, res, p, st);
+    if (threadIdx.x == 0) report(pages, chunks, p, st);
     return;
   }
   __syncthreads();
   page_bytes(sm, pages, p, n, len, dba ? vpre + vo : nullptr);
 }
 
-// Page byte offsets (exclusive scan of nbytes_out), the output capacity check and the final
-// offset entry. One workgroup.
-__global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, int npages, ChunkResult* res,
-                                                   uint64_t cap, int64_t* offsets) {
-  __shared__ uint64_t wsum[WG / 64];
-  __shared__ uint64_t carry_s;
-  if (threadIdx.x == 0) carry_s = 0;
-  __syncthreads();
-  for (int base = 0; base < npages; base += WG) {
-    const int p = base + threadIdx.x;
-    uint64_t x = 0;
-    if (p < npages) {
-      const int t = pages[p].page_type;
-      if (t == P_DATA || t == P_DATA_V2) x = pages[p].nbytes_out;
-    }
-    uint64_t s = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      uint64_t y = __shfl_up(s, off, 64);
-      if ((threadIdx.x & 63) >= (unsigned)off) s += y;
-    }
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = s;
-    __syncthreads();
-    uint64_t pre = carry_s;
-    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
-    if (p < npages) {
-      pages[p].byte_out = pre + s - x;
-      if (x > 0 && pre + s > cap && pages[p].status == 0) report(pages, res, p, ST_CAPACITY);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) carry_s += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    res->total_bytes = carry_s;
-    if (offsets) offsets[res->total_values] = (int64_t)carry_s;
-  }
+// Page byte offsets chunk by chunk (exclusive scan of nbytes_out restarted at each chunk's first
+// page), the output capacity check and each byte-array chunk's final offset entry. One workgroup.
+__global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, ChunkWork* chunks, int npages) {
+  seg_scan_pages(
+      pages, chunks, npages,
+      [&](int p) -> uint64_t {
+        const int t = pages[p].page_type;
+        return (t == P_DATA || t == P_DATA_V2) ? pages[p].nbytes_out : 0ull;
+      },
+      [&](int p, uint64_t excl, uint64_t incl) {
+        ChunkWork& ck = chunks[pages[p].chunk];
+        pages[p].byte_out = excl;
+        if (ck.es != 0) return;
+        if (incl > excl && incl > ck.val_cap && pages[p].status == 0) report(pages, chunks, p, ST_CAPACITY);
+        if ((uint32_t)p == ck.first_page + ck.npages - 1u) {
+          ck.res.total_bytes = incl;
+          if (ck.off_out) ck.off_out[ck.res.total_values] = (int64_t)incl;
+        }
+      });
 }
 
 // Gathers value slices into the output and writes their offsets (all encodings but
@@ -368,21 +426,26 @@ __global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, int npages, 
 //   k_ba_tscan  per page: the tiles' start offsets (page byte_out + exclusive scan);
 //   k_ba_copy   per tile: final offsets and the bytes.
 constexpr uint32_t BA_VPT = 16;            // values per thread
-constexpr uint32_t BA_T = BA_VPT * WG;     // values per tile
+constexpr uint32_t BA_T = BA_VPT * WG;     // values per tile: the pages' RUN_TILE tiles (ltile0, ntiles)
+static_assert(BA_T == RUN_TILE, "byte-array tiles are the page table's tiles");
 
-__device__ inline bool ba_page_ok(const PageWork& pw, const ChunkResult* res, uint64_t cap) {
-  return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) &&
-         pw.encoding != E_DELTA_BYTE_ARRAY && res->total_bytes <= cap;
+__device__ inline bool ba_page_ok(const PageWork& pw, const ChunkWork& ck) {
+  return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) && ck.es == 0 && ck.val_out &&
+         pw.encoding != E_DELTA_BYTE_ARRAY && ck.res.total_bytes <= ck.val_cap;
 }
 
-// Per page and tile of BA_T values: the tile's byte count (the offsets themselves are written
-// once, by k_ba_copy, from the scanned tile starts).
-__global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const uint32_t* __restrict__ vlen, uint64_t cap,
-                                                uint32_t maxt, uint64_t* __restrict__ tsum, ChunkResult* res) {
+// Per listed tile (gt, global) of a byte-array page: the tile's byte count into tsum[gt] (the
+// offsets themselves are written once, by k_ba_copy, from the scanned tile starts).
+__global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork* chunks,
+                                                const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
+                                                const uint32_t* __restrict__ vlen0, uint64_t* __restrict__ tsum) {
   __shared__ uint64_t red[WG / 64];
-  const uint32_t t = blockIdx.x, p = blockIdx.y;
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
-  if (!ba_page_ok(pw, res, cap)) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!ba_page_ok(pw, ck)) return;
+  const uint32_t t = gt - pw.ltile0;
+  const uint32_t* vlen = vlen0 + ck.scr_base;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
   uint64_t s = 0;
@@ -392,24 +455,25 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const uint32_t*
     s += i < n ? vlen[vo + i] : 0u;
   }
   const uint64_t tot = block_sum_u64(s, red);
-  if (threadIdx.x == 0) tsum[(uint64_t)p * maxt + t] = tot;
+  if (threadIdx.x == 0) tsum[gt] = tot;
 }
 
-__global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, uint64_t cap, uint32_t maxt,
-                                                 uint64_t* __restrict__ tsum, ChunkResult* res) {
+// Per byte-array page: its tiles' start offsets (page byte_out + exclusive scan of the tile sums).
+__global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWork* chunks, uint64_t* __restrict__ tsum) {
   __shared__ DeltaSmem sm;
   const uint32_t p = blockIdx.x;
   const PageWork pw = pages[p];
-  if (!ba_page_ok(pw, res, cap)) return;
+  if (!ba_page_ok(pw, chunks[pw.chunk])) return;
   const uint32_t nt = (uint32_t)((pw.nonnull + BA_T - 1) / BA_T);
   uint64_t carry = pw.byte_out;
+  uint64_t* ts = tsum + pw.ltile0;
   for (uint32_t b = 0; b < nt; b += WG) {
     const uint32_t t = b + threadIdx.x;
-    const uint64_t x = t < nt ? tsum[(uint64_t)p * maxt + t] : 0;
+    const uint64_t x = t < nt ? ts[t] : 0;
     uint64_t tot;
     const uint64_t pre = block_exscan(sm, x, tot);
     __syncthreads();  // every read of this pass's sums is done before the starts overwrite them
-    if (t < nt) tsum[(uint64_t)p * maxt + t] = carry + pre;
+    if (t < nt) ts[t] = carry + pre;
     carry += tot;
   }
 }
@@ -418,18 +482,23 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, uint64_t cap, 
 // the lengths, kept in LDS) written once to `offsets`, then the bytes: lanes take consecutive
 // values, so neighbouring lanes write neighbouring bytes.
 __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
-                                                const uint64_t* __restrict__ vsrc,
-                                                const uint32_t* __restrict__ vlen, uint64_t cap, uint32_t maxt,
-                                                const uint64_t* __restrict__ tsum, int64_t* __restrict__ offsets,
-                                                uint8_t* __restrict__ out, ChunkResult* res) {
+                                                const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                                const uint32_t* __restrict__ tl, const uint64_t* __restrict__ vsrc0,
+                                                const uint32_t* __restrict__ vlen0, const uint64_t* __restrict__ tsum) {
   __shared__ DeltaSmem sm;
   __shared__ uint64_t loff[BA_T];  // tile-relative byte offset of each value
-  const uint32_t t = blockIdx.x, p = blockIdx.y;
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
-  if (!ba_page_ok(pw, res, cap)) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!ba_page_ok(pw, ck)) return;
+  const uint32_t t = gt - pw.ltile0;
+  const uint64_t* vsrc = vsrc0 + ck.scr_base;
+  const uint32_t* vlen = vlen0 + ck.scr_base;
+  int64_t* __restrict__ offsets = ck.off_out;
+  uint8_t* __restrict__ out = ck.val_out;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
-  const uint64_t base = tsum[(uint64_t)p * maxt + t];
+  const uint64_t base = tsum[gt];
   const uint64_t i0 = (uint64_t)t * BA_T + (uint64_t)threadIdx.x * BA_VPT;
   uint32_t l[BA_VPT];
   uint64_t s = 0;
@@ -472,18 +541,22 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
 constexpr int DBA_PREV = 32768;
 
 __global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
-                                                 const uint64_t* __restrict__ vsrc,
-                                                 const uint32_t* __restrict__ vlen,
-                                                 const uint32_t* __restrict__ vpre, uint64_t cap,
-                                                 int64_t* __restrict__ offsets,
-                                                 uint8_t* __restrict__ out, ChunkResult* res) {
+                                                 ChunkWork* chunks, const uint64_t* __restrict__ vsrc0,
+                                                 const uint32_t* __restrict__ vlen0,
+                                                 const uint32_t* __restrict__ vpre0) {
   __shared__ uint8_t prev[DBA_PREV];
   const int p = blockIdx.x;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BYTE_ARRAY) return;
-  if (res->total_bytes > cap) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.es != 0 || !ck.val_out || ck.res.total_bytes > ck.val_cap) return;
+  const uint64_t* vsrc = vsrc0 + ck.scr_base;
+  const uint32_t* vlen = vlen0 + ck.scr_base;
+  const uint32_t* vpre = vpre0 + ck.scr_base;
+  int64_t* __restrict__ offsets = ck.off_out;
+  uint8_t* __restrict__ out = ck.val_out;
   const uint32_t lane = threadIdx.x;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   uint64_t d = pw.byte_out;
@@ -491,7 +564,7 @@ __global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blo
     const uint32_t pl = vpre[vo + i], sl = vlen[vo + i];
     const uint64_t tot = (uint64_t)pl + sl;
     if (tot > DBA_PREV) {  // values longer than the LDS buffer: not supported yet
-      if (lane == 0) report(pages, res, p, ST_NYI);
+      if (lane == 0) report(pages, chunks, p, ST_NYI);
       return;
     }
     const uint8_t* s = blob + vsrc[vo + i];
@@ -504,47 +577,59 @@ __global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blo
   }
 }
 
-// Dictionary pages: k_ba_dict_prep, then the caller's index pass (pqg_launch_run_index with
-// SS_DICT) between this and pqg_launch_bytes.
-extern "C" hipError_t pqg_launch_ba_dict_prep(const uint8_t* blob, uint64_t blob_len,
-                                              PageWork* pages, int dict_page, int type_length,
-                                              uint64_t* dsrc, uint32_t* dlen, ChunkResult* res,
-                                              hipStream_t s) {
-  if (dict_page >= 0)
-    hipLaunchKernelGGL(k_ba_dict_prep, dim3(1), dim3(WG), 0, s, blob, blob_len, pages, dict_page,
-                       type_length, dsrc, dlen, res);
+extern "C" {
+
+hipError_t pqg_launch_quarter_desc(const uint8_t* blob, PageWork* pages, ChunkWork* chunks, const uint32_t* tile_page,
+                                   const uint32_t* tl, uint32_t ntl, RunTables rt, int sel, hipStream_t s);
+hipError_t pqg_launch_page_counts(PageWork* pages, int npages, ChunkWork* chunks, RunTables rt, hipStream_t s);
+
+// Dictionary pages of the byte-array chunks (one workgroup per chunk of the decode).
+hipError_t pqg_launch_ba_dict_prep(const uint8_t* blob, uint64_t blob_len, PageWork* pages, ChunkWork* chunks,
+                                   int nchunks, uint64_t* dsrc, uint32_t* dlen, hipStream_t s) {
+  if (nchunks > 0)
+    hipLaunchKernelGGL(k_ba_dict_prep, dim3(nchunks), dim3(WG), 0, s, blob, blob_len, pages, chunks, dsrc, dlen);
   return hipGetLastError();
 }
 
-extern "C" hipError_t pqg_launch_badict_expand(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                               uint32_t ntiles, RunTables rt, int dict_page,
-                                               uint64_t* vsrc, uint32_t* vlen, uint64_t* dsrc,
-                                               uint32_t* dlen, ChunkResult* res, hipStream_t s) {
-  if (ntiles)
-    hipLaunchKernelGGL(k_wexpand_badict, dim3(ntiles * 4), dim3(64), 0, s, blob, blob_len, pages, rt,
-                       dict_page, dsrc, dlen, vsrc, vlen, res);
+// Byte-array dictionary indices off the level path: the pages it handed back (one workgroup per
+// page), then the general decoder's expand over the listed tiles of the chunks it does not take
+// (larger dictionaries; their index pass ran before), and the page byte totals of those.
+hipError_t pqg_launch_badict_general(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                     ChunkWork* chunks, const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl,
+                                     RunTables rt, uint64_t* dsrc, uint32_t* dlen, uint64_t* vsrc, uint32_t* vlen,
+                                     int lv, hipStream_t s) {
+  if (lv)
+    hipLaunchKernelGGL(k_badict_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, rt,
+                       dsrc, dlen, vsrc, vlen);
+  if (ntl) {
+    hipError_t e = pqg_launch_quarter_desc(blob, pages, chunks, tile_page, tl, ntl, rt, (int)SS_DICT, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_wexpand_badict, dim3(ntl * 4), dim3(64), 0, s, blob, blob_len, pages, chunks, rt, tl, dsrc,
+                       dlen, vsrc, vlen);
+    e = pqg_launch_page_counts(pages, npages, chunks, rt, s);
+    if (e != hipSuccess) return e;
+  }
   return hipGetLastError();
 }
 
-extern "C" hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                       int npages, int type_length, bool has_dba, uint64_t* vsrc,
-                                       uint32_t* vlen, uint32_t* vpre, uint64_t cap,
-                                       int64_t* offsets, uint8_t* out, uint64_t max_page_vals,
-                                       uint64_t* tsum, ChunkResult* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, type_length,
-                     vsrc, vlen, vpre, res);
-  hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, npages, res, cap, offsets);
-  const uint32_t maxt = (uint32_t)((max_page_vals + BA_T - 1) / BA_T);
-  if (maxt) {
-    hipLaunchKernelGGL(k_ba_tsum, dim3(maxt, npages), dim3(WG), 0, s, pages, vlen, cap, maxt, tsum, res);
-    hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, cap, maxt, tsum, res);
-    hipLaunchKernelGGL(k_ba_copy, dim3(maxt, npages), dim3(WG), 0, s, blob, pages, vsrc, vlen, cap, maxt, tsum,
-                       offsets, out, res);
+// Byte-array values of every byte-array chunk: lengths and sources of the PLAIN / DELTA_LENGTH /
+// DELTA_BYTE_ARRAY pages, page byte offsets, then the tiled copy over the listed tiles (the tiles
+// of the byte-array pages) and the DELTA_BYTE_ARRAY rebuild.
+hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                            const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, uint64_t* vsrc,
+                            uint32_t* vlen, uint32_t* vpre, uint64_t* tsum, hipStream_t s) {
+  hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
+  hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
+  if (ntl) {
+    hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vlen, tsum);
+    hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
+    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, vsrc, vlen, tsum);
   }
   if (has_dba)
-    hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, vsrc, vlen, vpre,
-                       cap, offsets, out, res);
+    hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, chunks, vsrc, vlen, vpre);
   return hipGetLastError();
 }
+
+}  // extern "C"
 
 }  // namespace pqg

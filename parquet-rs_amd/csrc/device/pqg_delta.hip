@@ -1,39 +1,7 @@
-// pqg_delta.hip — DELTA_BINARY_PACKED values (decoding.rs:392-619): one 256-thread workgroup
-// per page running the stream decoder of pqg_delta.hpp over the page's value stream.
+// pqg_delta.hip — DELTA_BINARY_PACKED values (decoding.rs:392-619) of the INT32 / INT64 chunks of
+// a decode (each kernel is instantiated per value size ES and takes the pages of chunks of that
+// size), output to each page's chunk buffer.
 #include "pqg_delta.hpp"
-
-namespace pqg {
-
-template <int ES>  // 4 = INT32, 8 = INT64
-__global__ void __launch_bounds__(WG) k_delta(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                              PageWork* pages, uint8_t* __restrict__ out,
-                                              ChunkResult* res) {
-  __shared__ DeltaSmem sm;
-  const int p = blockIdx.x;
-  const PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
-  DeltaInfo info;
-  // the decoder's set_data ignores num_values; read_batch asks for the non-null count
-  int32_t st = delta_stream<ES>(sm, blob, blob_len, pw.base + pw.val_off, pw.val_bytes, pw.nonnull,
-                                pw.nonnull, out + pw.value_out * ES, info);
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
-}
-
-extern "C" hipError_t pqg_launch_delta(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                       int npages, int es, uint8_t* out, ChunkResult* res,
-                                       hipStream_t s) {
-  if (es == 4)
-    hipLaunchKernelGGL(k_delta<4>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, out, res);
-  else if (es == 8)
-    hipLaunchKernelGGL(k_delta<8>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, out, res);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-}  // namespace pqg
 
 // =============================================================================== tiled path
 //
@@ -77,13 +45,13 @@ __device__ inline int vlq16(uint64_t lo, uint64_t hi, uint32_t avail, uint64_t& 
 
 template <int ES>
 __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages, DeltaTables dt, ChunkResult* res) {
+                                                    PageWork* pages, ChunkWork* chunks, DeltaTables dt) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
   const PageWork pw = pages[p];
   const uint32_t lane = threadIdx.x & 63;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
   if (dt.page[p].tiled == DP_DONE) return;  // decoded by k_delta_page
   DeltaPage info{0, 0, 0, 0, 0};
   if (pw.status != 0) {
@@ -120,7 +88,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   if (err) {
     if (lane == 0) {
       dt.page[p] = info;
-      report(pages, res, p, err);
+      report(pages, chunks, p, err);
     }
     return;
   }
@@ -252,7 +220,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   if (err) {
     if (lane == 0) {
       dt.page[p] = info;
-      report(pages, res, p, err);
+      report(pages, chunks, p, err);
     }
     return;
   }
@@ -284,7 +252,7 @@ struct DeltaExpandSmem {
 // per delta for widths <= 32) and their wrapping sum into s. False: nothing to do for tile t.
 template <int ES>
 __device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
-                                        uint64_t blob_len, PageWork* pages,
+                                        uint64_t blob_len, PageWork* pages, const ChunkWork* chunks,
                                         const uint32_t* __restrict__ tile_page, uint32_t ntiles,
                                         const DeltaTables& dt, uint32_t t, int& p, DeltaPage& info,
                                         uint32_t& lo, uint32_t& hi, uint64_t (&x)[DPT], uint64_t& s) {
@@ -292,7 +260,7 @@ __device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __re
   if (t >= ntiles) return false;
   p = (int)tile_page[t];
   const PageWork& pw = pages[p];
-  if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED) return false;
+  if (pw.status != 0 || pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return false;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return false;
   info = dt.page[p];
   if (info.tiled != 1u) return false;
@@ -428,14 +396,14 @@ __device__ inline bool delta_tile_front(DeltaExpandSmem& sm, const uint8_t* __re
 // Tile sums: wrapping sum of min_delta + delta over each tile's deltas -> dt.agg[t].
 template <int ES>
 __device__ inline void delta_sums_tile(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
-                                       uint64_t blob_len, PageWork* pages,
+                                       uint64_t blob_len, PageWork* pages, const ChunkWork* chunks,
                                        const uint32_t* __restrict__ tile_page, uint32_t ntiles,
                                        const DeltaTables& dt, uint32_t t) {
   int p;
   DeltaPage info;
   uint32_t lo, hi;
   uint64_t x[DPT], s;
-  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
+  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, chunks, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
     return;
   const uint64_t T = block_sum_u64(s, sm.wsum);
   if (threadIdx.x == 0) dt.agg[t] = T;
@@ -445,12 +413,13 @@ __device__ inline void delta_sums_tile(DeltaExpandSmem& sm, const uint8_t* __res
 // for this path the kernel exits at once).
 template <int ES>
 __global__ void __launch_bounds__(WG) k_delta_sums(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                   PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                   uint32_t ntiles, DeltaTables dt) {
+                                                   PageWork* pages, const ChunkWork* chunks,
+                                                   const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                   DeltaTables dt) {
   __shared__ DeltaExpandSmem sm;
   if (*dt.nfall == 0) return;
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    delta_sums_tile<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t);
+    delta_sums_tile<ES>(sm, blob, blob_len, pages, chunks, tile_page, ntiles, dt, t);
     __syncthreads();
   }
 }
@@ -496,17 +465,18 @@ __global__ void __launch_bounds__(WG) k_delta_tscan(const PageWork* pages, Delta
 // 16-byte chunks, chunk c by thread c % 256.
 template <int ES>
 __device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __restrict__ blob,
-                                         uint64_t blob_len, PageWork* pages,
+                                         uint64_t blob_len, PageWork* pages, const ChunkWork* chunks,
                                          const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                         const DeltaTables& dt, uint8_t* __restrict__ out, uint32_t t) {
+                                         const DeltaTables& dt, uint32_t t) {
   const int tid = threadIdx.x;
   int p;
   DeltaPage info;
   uint32_t lo, hi;
   uint64_t x[DPT], s;
-  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
+  if (!delta_tile_front<ES>(sm, blob, blob_len, pages, chunks, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
     return;
   const PageWork& pw = pages[p];
+  uint8_t* __restrict__ out = chunks[pw.chunk].val_out;
   // ---- workgroup scan of the thread sums
   uint64_t incl = s;
 #pragma unroll
@@ -572,13 +542,13 @@ __device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __r
 
 template <int ES>
 __global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                     uint32_t ntiles, DeltaTables dt,
-                                                     uint8_t* __restrict__ out) {
+                                                     PageWork* pages, const ChunkWork* chunks,
+                                                     const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                     DeltaTables dt) {
   __shared__ DeltaExpandSmem sm;
   if (*dt.nfall == 0) return;
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    delta_expand_tile<ES>(sm, blob, blob_len, pages, tile_page, ntiles, dt, out, t);
+    delta_expand_tile<ES>(sm, blob, blob_len, pages, chunks, tile_page, ntiles, dt, t);
     __syncthreads();
   }
 }
@@ -619,14 +589,14 @@ struct DeltaPageSmem {
 
 template <int ES>
 __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG) k_delta_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                   PageWork* pages, DeltaTables dt,
-                                                   uint8_t* __restrict__ out) {
+                                                   PageWork* pages, const ChunkWork* chunks, DeltaTables dt) {
   __shared__ DeltaPageSmem sm;
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
+  uint8_t* __restrict__ out = chunks[pw.chunk].val_out;
   DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
   if (pw.status != 0) {
     if (tid == 0) {
@@ -917,46 +887,44 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
 // Per-page fallback for pages the tiled path does not take (k_delta with a page filter).
 template <int ES>
 __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                   PageWork* pages, DeltaTables dt,
-                                                   uint8_t* __restrict__ out, ChunkResult* res) {
+                                                   PageWork* pages, ChunkWork* chunks, DeltaTables dt) {
   __shared__ DeltaSmem sm;
   const int p = blockIdx.x;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BINARY_PACKED) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
   if (dt.page[p].tiled) return;
   DeltaInfo info;
   int32_t st = delta_stream<ES>(sm, blob, blob_len, pw.base + pw.val_off, pw.val_bytes, pw.nonnull,
-                                pw.nonnull, out + pw.value_out * ES, info);
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
+                                pw.nonnull, chunks[pw.chunk].val_out + pw.value_out * ES, info);
+  if (st && threadIdx.x == 0) report(pages, chunks, p, st);
 }
 
+// The page pass; pages it leaves (irregular block shapes, errors) to the tiled kernels, which exit
+// at once when it left none (dt.nfall), then the per-page stream decoder for what those refuse.
 template <int ES>
-static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, uint8_t* out,
-                        ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
+static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, hipStream_t s, hipEvent_t* kev) {
   if (kev) (void)hipEventRecord(kev[0], s);
-  hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out);
+  hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, dt);
   if (kev) (void)hipEventRecord(kev[1], s);
-  hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, dt, res);
+  hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, chunks, dt);
   if (ntiles) {
     const dim3 tg(ntiles < 4096u ? ntiles : 4096u);  // grid-stride over the tiles
-    hipLaunchKernelGGL(k_delta_sums<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt);
+    hipLaunchKernelGGL(k_delta_sums<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, ntiles, dt);
     hipLaunchKernelGGL(k_delta_tscan, dim3(npages), dim3(WG), 0, s, pages, dt);
-    hipLaunchKernelGGL(k_delta_expand<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, tile_page, ntiles, dt, out);
+    hipLaunchKernelGGL(k_delta_expand<ES>, tg, dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, ntiles, dt);
   }
-  hipLaunchKernelGGL(k_delta_rest<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, dt, out, res);
+  hipLaunchKernelGGL(k_delta_rest<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, dt);
 }
 
-extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                             int npages, uint32_t ntiles, const uint32_t* tile_page,
-                                             DeltaTables dt, uint32_t epoch, int es, uint8_t* out,
-                                             ChunkResult* res, hipStream_t s, hipEvent_t* kev) {
-  (void)epoch;  // tile prefixes come from k_delta_tscan: no cross-workgroup flags
-  if (es == 8) delta_tiled<8>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s, kev);
-  else if (es == 4) delta_tiled<4>(blob, blob_len, pages, npages, ntiles, tile_page, dt, out, res, s, kev);
-  else return hipErrorInvalidValue;
+// es_mask: bit mask of the DELTA_BINARY_PACKED chunks' value sizes (4: INT32, 8: INT64).
+extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                             ChunkWork* chunks, uint32_t ntiles, const uint32_t* tile_page,
+                                             DeltaTables dt, uint32_t es_mask, hipStream_t s, hipEvent_t* kev) {
+  if (es_mask & 8u) delta_tiled<8>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, kev);
+  if (es_mask & 4u) delta_tiled<4>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, (es_mask & 8u) ? nullptr : kev);
   return hipGetLastError();
 }
 

@@ -10,13 +10,62 @@ namespace pqg {
 constexpr int WG = 256;       // threads per workgroup (4 waves of 64)
 constexpr int WAVE = 64;
 
-// Record the first error of a page and of the chunk. Results must not depend on which
+// Record the first error of a page and of its chunk. Results must not depend on which
 // workgroup reports first: the page status keeps the first code, the chunk keeps the
-// lowest bad page index.
-__device__ inline void report(PageWork* pages, ChunkResult* res, int page, int32_t code) {
+// lowest bad page index (chunk-relative).
+__device__ inline void report(PageWork* pages, ChunkWork* chunks, int page, int32_t code) {
   // the code that sets the page's status is the one the chunk reports for it
-  if (atomicCAS(&pages[page].status, 0, code) == 0)
-    atomicMin((unsigned long long*)&res->bad, ((unsigned long long)(uint32_t)page << 32) | (uint32_t)code);
+  if (atomicCAS(&pages[page].status, 0, code) == 0) {
+    ChunkWork& c = chunks[pages[page].chunk];
+    atomicMin((unsigned long long*)&c.res.bad,
+              ((unsigned long long)((uint32_t)page - c.first_page) << 32) | (uint32_t)code);
+  }
+}
+
+// The column parameters of page pw's chunk.
+__device__ inline const ColumnParams& pcp(const ChunkWork* chunks, const PageWork& pw) { return chunks[pw.chunk].cp; }
+
+// One workgroup (WG threads): exclusive scan of per-page counts over pages [0, npages) in order,
+// restarted at every chunk's first page. get(p) gives page p's count; put(p, excl, incl) receives
+// its chunk-relative exclusive and inclusive prefix.
+template <class Get, class Put>
+__device__ inline void seg_scan_pages(const PageWork* pages, const ChunkWork* chunks, int npages, Get get, Put put) {
+  __shared__ uint64_t sv[WG / 64];
+  __shared__ uint32_t sf[WG / 64];
+  __shared__ uint64_t carry_s;
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < npages; base += WG) {
+    const int p = base + (int)threadIdx.x;
+    const bool in = p < npages;
+    const uint64_t x = in ? get(p) : 0ull;
+    uint32_t f = in && (uint32_t)p == chunks[pages[p].chunk].first_page ? 1u : 0u;
+    uint64_t s = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // segmented inclusive scan: sums stop at a chunk start
+      const uint64_t y = __shfl_up(s, d, 64);
+      const uint32_t g = (uint32_t)__shfl_up((int)f, d, 64);
+      if (lane >= (uint32_t)d) {
+        if (!f) s += y;
+        f |= g;
+      }
+    }
+    if (lane == 63) {
+      sv[wid] = s;
+      sf[wid] = f;
+    }
+    __syncthreads();
+    if (!f) {  // no chunk start between the block's first page and this one: add what came before
+      uint64_t c = carry_s;
+      for (uint32_t k = 0; k < wid; ++k) c = sf[k] ? sv[k] : c + sv[k];
+      s += c;
+    }
+    if (in) put(p, s - x, s);
+    __syncthreads();
+    if (threadIdx.x == WG - 1) carry_s = s;
+    __syncthreads();
+  }
 }
 
 // Little-endian byte load from global memory, guarded by the blob size.

@@ -11,6 +11,12 @@
 //   k_plain_copy     PLAIN fixed-width values (decoding.rs:138-186, 228-247)
 //   k_plain_bool     PLAIN booleans (decoding.rs:188-204)
 //
+// A decode covers a batch of column chunks (pqg_decode_chunks; one for pqg_decode_chunk): every
+// kernel runs once over the pages of all of them, each page taking its column parameters,
+// dictionary and output buffers from its chunk (ChunkWork, pqg_internal.hpp). Kernels over tiles
+// of one kind of page take a host-built list of those tiles (tl, ntl) instead of a grid over
+// every tile of the batch.
+//
 // All work is integer/byte movement bound by HBM: no MFMA. The general RLE/bit-packing hybrid
 // decoder (index pass + grid-wide expand pass) is in pqg_runs.hpp / pqg_texpand.hpp; level
 // streams and RLE booleans take the fast path of pqg_levels.hip first.
@@ -18,25 +24,10 @@
 
 namespace pqg {
 
-
-
 // ------------------------------------------------------------------------------ prepare
 
 __device__ inline uint32_t rd_u32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-__device__ inline int type_size(int t, int tl) {
-  switch (t) {
-    case T_BOOLEAN: return 1;
-    case T_INT32: return 4;
-    case T_INT64: return 8;
-    case T_INT96: return 12;
-    case T_FLOAT: return 4;
-    case T_DOUBLE: return 8;
-    case T_FLBA: return tl;
-    default: return 0;
-  }
 }
 
 // One v1 level stream (levels.rs:191-211). `start` is the BufferPtr start of the slice
@@ -69,9 +60,10 @@ __device__ inline int64_t v1_level_stream(const uint8_t* page, uint32_t nbytes, 
 
 // Thread 0 of k_prepare: page p's layout (level streams, value section) into pages[p] and out.
 __device__ inline void prepare_page(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* __restrict__ pages,
-                                    int p, const ColumnParams& cp, ChunkResult* res, const PrepInit& ini,
-                                    PageWork& out) {
+                                    int p, ChunkWork* chunks, PageWork& out) {
   PageWork pw = pages[p];
+  ChunkWork& ck = chunks[pw.chunk];
+  const ColumnParams& cp = ck.cp;
   const int32_t host_status = pw.status;  // set by the host for pages the reference rejects
   pw.rep_kind = pw.def_kind = LK_NONE;
   pw.rep_off = pw.rep_bytes = pw.def_off = pw.def_bytes = 0;
@@ -124,25 +116,27 @@ __device__ inline void prepare_page(const uint8_t* __restrict__ blob, uint64_t b
     pw.val_off = 0;
     pw.val_bytes = pw.nbytes;
   }
-  // Values each page must yield: def == max_def count when levels are read (filled by
-  // k_rle_levels), else the page's level count (column/reader.rs:212-226).
+  // Values each page must yield: def == max_def count when levels are read (filled by the level
+  // path), else the page's level count (column/reader.rs:212-226).
   bool data = pw.page_type == P_DATA || pw.page_type == P_DATA_V2;
   if (data && !(cp.max_def > 0 && cp.want_def)) pw.nonnull = pw.num_values;
-  if (!err && p == ini.dict_page && ini.dict_es > 0) {  // DictDecoder::set_dict (was k_dict_check)
+  if (!err && p == ck.dict_page && ck.dict_es > 0) {  // DictDecoder::set_dict (decoding.rs:282-288)
     if (pw.encoding != E_PLAIN && pw.encoding != E_PLAIN_DICTIONARY) err = ST_NYI;
-    else if ((uint64_t)pw.num_values * (uint64_t)ini.dict_es > pw.nbytes) err = ST_EOF;
+    else if ((uint64_t)pw.num_values * (uint64_t)ck.dict_es > pw.nbytes) err = ST_EOF;
   }
   pw.status = err;
   pages[p] = pw;
   out = pw;
-  if (err) atomicMin((unsigned long long*)&res->bad, ((unsigned long long)(uint32_t)p << 32) | (uint32_t)err);
+  if (err)
+    atomicMin((unsigned long long*)&ck.res.bad,
+              ((unsigned long long)((uint32_t)p - ck.first_page) << 32) | (uint32_t)err);
 }
 
 // One wave per page: the lanes fill the page's tile -> page entries (a dictionary column's
 // single data page has thousands), lane 0 the rest.
 __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                                                uint32_t* __restrict__ tile_page, ChunkResult* res, PrepInit ini) {
+                                                PageWork* __restrict__ pages, int npages, ChunkWork* chunks,
+                                                uint32_t* __restrict__ tile_page, PrepInit ini) {
   const int p = blockIdx.x;
   if (p >= npages) return;
   {
@@ -151,7 +145,7 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
   }
   __shared__ PageWork pw_s;
   if (threadIdx.x == 0) {
-    prepare_page(blob, blob_len, pages, p, cp, res, ini, pw_s);
+    prepare_page(blob, blob_len, pages, p, chunks, pw_s);
     if (p == 0)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -163,6 +157,7 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
   }
   __syncthreads();
   // density probes of the level streams just located (wave-uniform from here)
+  const ColumnParams& cp = pcp(chunks, pw_s);
   for (int k = 0; k < 2; ++k) {
     uint32_t* dn = k == 0 ? ini.dense_def : ini.dense_rep;
     if (!dn) continue;
@@ -171,8 +166,10 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
     const int kind = k == 0 ? pw.def_kind : pw.rep_kind;
     const uint32_t slen = k == 0 ? pw.def_bytes : pw.rep_bytes;
     const uint32_t w = (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width);
+    const bool want = k == 0 ? cp.want_def : cp.want_rep;
     uint32_t dense = 0;
-    if (data && pw.status == 0 && kind == LK_RLE && w >= 1 && w <= 16 && pw.num_values && slen >= PROBE_SPAN + 64u)
+    if (want && data && pw.status == 0 && kind == LK_RLE && w >= 1 && w <= 16 && pw.num_values &&
+        slen >= PROBE_SPAN + 64u)
       dense = lv_probe_dense(blob, blob_len, pw.base + (k == 0 ? pw.def_off : pw.rep_off), w);
     if (threadIdx.x == 0) dn[p] = dense;
   }
@@ -182,67 +179,53 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
 
 // Index pass over stream `sel` of every page (one wave per page), pqg_runs.hpp.
 __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                  PageWork* pages, ColumnParams cp, int sel,
-                                                  int dict_page, RunTables rt, ChunkResult* res,
+                                                  PageWork* pages, ChunkWork* chunks, int sel, RunTables rt,
                                                   int bailed_only = 0) {
   __shared__ IndexSmem sm;
   const int p = blockIdx.x;
   if (bailed_only ? rt.pflag[p] != PF_BAIL : (*rt.nfall == 0 || pf_level_path(rt.pflag[p]))) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!bailed_only && sel == SS_DICT && ck.lvdict) return;  // the level path's chunk (its leftovers: k_*_fallback)
   Stream s;
-  if (!get_stream(blob, pw, sel, cp, s)) return;
+  if (!get_stream(blob, pw, sel, ck.cp, s)) return;
   if (sel == SS_DICT) {
-    if (dict_page < 0) {  // "Decoder for dict should have been set"
-      if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+    if (ck.dict_page < 0) {  // "Decoder for dict should have been set"
+      if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
       return;
     }
-    if (pages[dict_page].status != 0) return;
+    if (pages[ck.dict_page].status != 0) return;
   }
   const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0,
                               rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT, rt.nruns + pw.ltile0, sm,
-                              (cp.debug & 32) && cp.dbgbuf ? cp.dbgbuf + 2 * p : nullptr);
-  if (st && threadIdx.x == 0) report(pages, res, p, st);
+                              (ck.cp.debug & 32) && ck.cp.dbgbuf ? ck.cp.dbgbuf + 2 * p : nullptr);
+  if (st && threadIdx.x == 0) report(pages, chunks, p, st);
 }
 
-
-// Quarter-tile descriptors of stream `sel` (one thread per quarter), read by the wave expand
-// kernels.
+// Quarter-tile descriptors of stream `sel` over the listed tiles (one thread per quarter; desc
+// and its count slot at 4 t + q), read by the wave expand kernels.
 __global__ void __launch_bounds__(WG) k_quarter_desc(const uint8_t* __restrict__ blob, const PageWork* pages,
-                                                     const uint32_t* __restrict__ tile_page,
-                                                     uint32_t ntiles, RunTables rt, ColumnParams cp,
-                                                     int sel, int dict_page) {
+                                                     const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                                     const uint32_t* __restrict__ tl, uint32_t ntl, RunTables rt,
+                                                     int sel) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= ntiles * 4) return;
-  rt.desc[i] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, i >> 2, i & 3);
+  if (i >= ntl * 4) return;
+  const uint32_t t = tl[i >> 2];
+  rt.desc[4 * t + (i & 3)] = quarter_desc(blob, pages, chunks, tile_page, rt, sel, t, i & 3);
 }
 
-// Tile descriptors of stream `sel` (one thread per tile), read by the tile expand kernels.
+// Tile descriptors of stream `sel` over the listed tiles (one thread per tile), read by the tile
+// expand kernels.
 __global__ void __launch_bounds__(WG) k_tile_desc(const uint8_t* __restrict__ blob, const PageWork* pages,
-                                                  const uint32_t* __restrict__ tile_page,
-                                                  uint32_t ntiles, RunTables rt, ColumnParams cp,
-                                                  int sel, int dict_page) {
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  if (t >= ntiles || *rt.nfall == 0) return;
-  rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, dict_page, t, 0, RUN_TILE);
+                                                  const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                                  const uint32_t* __restrict__ tl, uint32_t ntl, RunTables rt,
+                                                  int sel) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= ntl || *rt.nfall == 0) return;
+  const uint32_t t = tl[i];
+  rt.desc[t] = quarter_desc(blob, pages, chunks, tile_page, rt, sel, t, 0, RUN_TILE);
 }
-
-// Tile expand of a level stream (which: SS_DEF / SS_REP), pqg_texpand.hpp, persistent grid.
-// Def levels also count the values read_batch will ask for: each wave writes its count of the
-// tile to qcount[4t + wave] (k_page_counts sums them per page).
-struct LevelsMaker {
-  int16_t* out;
-  int16_t maxl;
-  bool count;
-  uint32_t* qcount;
-  __device__ TxLevels make(const QDesc& d) { return TxLevels{out + d.out, maxl, count, 0u}; }
-  const uint32_t* pflag;
-  __device__ void done(const QDesc& d, uint32_t t, TxLevels& em) {
-    if (!count || (!d.qhi && pf_level_path(pflag[d.page]))) return;  // the level path wrote these counts
-    const uint32_t nn = wave_sum_u32(em.nonnull);
-    if ((threadIdx.x & 63) == 0) qcount[4 * t + (threadIdx.x >> 6)] = nn;
-  }
-};
 
 // Level streams the level path handed back (PF_BAIL: malformed input, unusual header forms), one
 // workgroup per page: wave 0 walks the page's header chain (run_index: every reference check,
@@ -261,9 +244,8 @@ struct LevelsPageMaker {
 };
 
 __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                        PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                        ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
-                                        int16_t* __restrict__ out) {
+                                        PageWork* pages, ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                        int sel, RunTables rt) {
   __shared__ IndexSmem ism;
   __shared__ TileSmem sm;
   __shared__ int32_t st_s;
@@ -272,21 +254,23 @@ __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64
   if (rt.pflag[p] != PF_BAIL) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
+  const ChunkWork& ck = chunks[pw.chunk];
   Stream s;
-  if (!get_stream(blob, pw, sel, cp, s)) return;
+  if (!get_stream(blob, pw, sel, ck.cp, s)) return;
   if (threadIdx.x < 64) {
     const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
                                  rt.nruns + pw.ltile0, ism);
     if (threadIdx.x == 0) {
       st_s = st;
-      if (st) report(pages, res, p, st);
+      if (st) report(pages, chunks, p, st);
     }
   }
   __syncthreads();
   if (st_s) return;
-  LevelsPageMaker mk{out, sel == SS_DEF ? cp.max_def : cp.max_rep, sel == SS_DEF, 0u};
+  LevelsPageMaker mk{sel == SS_DEF ? ck.def_out : ck.rep_out, sel == SS_DEF ? ck.cp.max_def : ck.cp.max_rep,
+                     sel == SS_DEF, 0u};
   for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
-    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, sel, -1, t, 0, RUN_TILE);
+    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, chunks, tile_page, rt, sel, t, 0, RUN_TILE);
     __syncthreads();  // (the descriptor is read by every thread of the workgroup)
     tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);
     __syncthreads();  // sm is refilled by the next tile
@@ -297,61 +281,57 @@ __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64
   }
 }
 
-__device__ inline void scan_values(PageWork* pages, int npages, ChunkResult* res, int es, uint64_t cap_bytes);
+__device__ inline void scan_values(PageWork* pages, ChunkWork* chunks, int npages);
 
-// scan_es >= 0 (a def stream, no rep stream after it): the grid's last workgroup also runs
-// k_scan_values (the non-null counts are final), one launch fewer per chunk.
+// scan != 0 (a def stream, no rep stream after it): the grid's last workgroup also runs
+// k_scan_values (the non-null counts are final), one launch fewer per decode.
 __global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                    PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                    ColumnParams cp, int sel, RunTables rt, ChunkResult* res,
-                                                    int16_t* __restrict__ out, uint32_t* ctr, int scan_es,
-                                                    uint64_t scan_cap) {
-  lv_fallback_page(blob, blob_len, pages, tile_page, cp, sel, rt, res, out);
-  if (scan_es >= 0 && last_workgroup(ctr)) scan_values(pages, (int)gridDim.x, res, scan_es, scan_cap);
+                                                    PageWork* pages, ChunkWork* chunks,
+                                                    const uint32_t* __restrict__ tile_page, int sel, RunTables rt,
+                                                    uint32_t* ctr, int scan) {
+  lv_fallback_page(blob, blob_len, pages, chunks, tile_page, sel, rt);
+  if (scan && last_workgroup(ctr)) scan_values(pages, chunks, (int)gridDim.x);
 }
 
-// Tile expand of RLE_DICTIONARY indices with the dictionary gather.
+// Tile expand of RLE_DICTIONARY indices with the dictionary gather: the tile's page names its
+// chunk, whose dictionary page and value buffer the emitter takes.
 template <int ES>
 struct DictMaker {
-  const uint8_t* dict;
-  uint32_t ndict;
-  bool aligned;
-  uint8_t* out;
+  const uint8_t* blob;
   PageWork* pages;
-  ChunkResult* res;
+  ChunkWork* chunks;
   __device__ TxDict<ES> make(const QDesc& d) {
-    return TxDict<ES>{dict, ndict, aligned, out + d.out * (uint64_t)ES, 0};
+    if (!d.qhi) return TxDict<ES>{nullptr, 0u, false, nullptr, 0};
+    const ChunkWork& ck = chunks[pages[d.page].chunk];
+    const PageWork& dp = pages[ck.dict_page];  // (quarter_desc gives work only with a valid dictionary)
+    return TxDict<ES>{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
+                      ck.val_out + d.out * (uint64_t)ES, 0};
   }
   __device__ void done(const QDesc& d, uint32_t, TxDict<ES>& em) {
     const uint64_t bad = __ballot(em.err != 0);
-    if (bad && (threadIdx.x & 63) == 0) report(pages, res, (int)d.page, ST_PANIC);
+    if (bad && (threadIdx.x & 63) == 0) report(pages, chunks, (int)d.page, ST_PANIC);
   }
 };
 
-#define PQG_TEXPAND_DICT(NAME, ATTR)                                                                  \
-  template <int ES>                                                                                   \
-  __global__ void ATTR __launch_bounds__(WG) NAME(const uint8_t* __restrict__ blob, uint64_t blob_len, \
-                                                  uint32_t ntiles, PageWork* pages, RunTables rt,     \
-                                                  int dict_page, uint8_t* __restrict__ out,           \
-                                                  ChunkResult* res) {                                 \
-    __shared__ TileSmem sm;                                                                         \
-    if (dict_page < 0) return;                                                                      \
-    const PageWork& dp = pages[dict_page];                                                          \
-    DictMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),   \
-                           out, pages, res};                                                        \
-    if (*rt.nfall == 0) return;                                                                     \
-    if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);       \
-  }
-PQG_TEXPAND_DICT(k_texpand_dict, )
+// One tile of the list per workgroup (the list holds the tiles of the chunks whose value size is ES).
+template <int ES>
+__global__ void __launch_bounds__(WG) k_texpand_dict(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     const uint32_t* __restrict__ tl, PageWork* pages,
+                                                     ChunkWork* chunks, RunTables rt) {
+  __shared__ TileSmem sm;
+  if (*rt.nfall == 0) return;
+  DictMaker<ES> mk{blob, pages, chunks};
+  tile_one(blob, blob_len, rt.desc, tl[blockIdx.x], rt.runs, sm, mk);
+}
 
 // Dictionary index streams the level path handed back, when they are expected to be rare (the
-// dictionary's index width is within the level path's limit): one workgroup per page, index walk
-// then the page's tiles with the gather, as k_lv_fallback does for levels.
+// dictionary's index width is within the level path's limit): one workgroup per page of a chunk
+// of ES-byte values, index walk then the page's tiles with the gather, as k_lv_fallback does for
+// levels.
 template <int ES>
 __global__ void __launch_bounds__(WG) k_dict_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                      PageWork* pages, const uint32_t* __restrict__ tile_page,
-                                                      ColumnParams cp, int dict_page, RunTables rt,
-                                                      uint8_t* __restrict__ out, ChunkResult* res) {
+                                                      PageWork* pages, ChunkWork* chunks,
+                                                      const uint32_t* __restrict__ tile_page, RunTables rt) {
   __shared__ IndexSmem ism;
   __shared__ TileSmem sm;
   __shared__ int32_t st_s;
@@ -359,133 +339,120 @@ __global__ void __launch_bounds__(WG) k_dict_fallback(const uint8_t* __restrict_
   if (rt.pflag[p] != PF_BAIL) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.es != ES) return;
   Stream s;
-  if (!get_stream(blob, pw, SS_DICT, cp, s)) return;
-  if (dict_page < 0) {  // "Decoder for dict should have been set"
-    if (threadIdx.x == 0) report(pages, res, p, ST_PANIC);
+  if (!get_stream(blob, pw, SS_DICT, ck.cp, s)) return;
+  if (ck.dict_page < 0) {  // "Decoder for dict should have been set"
+    if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
     return;
   }
-  if (pages[dict_page].status != 0) return;
+  if (pages[ck.dict_page].status != 0) return;
   if (threadIdx.x < 64) {
     const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
                                  rt.nruns + pw.ltile0, ism);
     if (threadIdx.x == 0) {
       st_s = st;
-      if (st) report(pages, res, p, st);
+      if (st) report(pages, chunks, p, st);
     }
   }
   __syncthreads();
   if (st_s) return;
-  const PageWork& dp = pages[dict_page];
-  DictMaker<ES> mk{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0), out, pages, res};
+  DictMaker<ES> mk{blob, pages, chunks};
   for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
-    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, tile_page, rt, cp, SS_DICT, dict_page, t, 0, RUN_TILE);
+    if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, chunks, tile_page, rt, SS_DICT, t, 0, RUN_TILE);
     __syncthreads();
     tile_one(blob, blob_len, rt.desc, t, rt.runs, sm, mk);
     __syncthreads();
   }
 }
 
-// Tile expand of RLE booleans (data page v2 values).
+// Tile expand of RLE booleans (data page v2 values) over the listed tiles.
 struct BoolMaker {
-  uint8_t* out;
-  __device__ TxBool make(const QDesc& d) { return TxBool{out + d.out}; }
+  PageWork* pages;
+  ChunkWork* chunks;
+  __device__ TxBool make(const QDesc& d) {
+    return TxBool{d.qhi ? chunks[pages[d.page].chunk].val_out + d.out : nullptr};
+  }
   __device__ void done(const QDesc&, uint32_t, TxBool&) {}
 };
 
 __global__ void __launch_bounds__(WG) k_texpand_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     uint32_t ntiles, RunTables rt, uint8_t* __restrict__ out) {
+                                                     const uint32_t* __restrict__ tl, PageWork* pages,
+                                                     ChunkWork* chunks, RunTables rt) {
   __shared__ TileSmem sm;
   if (*rt.nfall == 0) return;
-  BoolMaker mk{out};
-  if (blockIdx.x < ntiles) tile_one(blob, blob_len, rt.desc, blockIdx.x, rt.runs, sm, mk);
+  BoolMaker mk{pages, chunks};
+  tile_one(blob, blob_len, rt.desc, tl[blockIdx.x], rt.runs, sm, mk);
 }
 
-static inline dim3 tx_grid(uint32_t ntiles) { return dim3(ntiles); }  // one tile per workgroup
-
-// Per-page sum of the quarter-tile counts -> pages[p].nonnull (field 0) / nbytes_out (1).
-__global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const uint32_t* __restrict__ qcount,
+// Per-page sum of the quarter-tile byte counts -> pages[p].nbytes_out, for the dictionary pages
+// of the byte-array chunks the general decoder expanded (k_wexpand_badict).
+__global__ void __launch_bounds__(WG) k_page_counts(PageWork* pages, const ChunkWork* chunks,
+                                                    const uint32_t* __restrict__ qcount,
                                                     const uint32_t* __restrict__ pflag,
-                                                    const uint32_t* __restrict__ nfall, int field) {
+                                                    const uint32_t* __restrict__ nfall) {
   __shared__ uint64_t red[WG / 64];
   if (*nfall == 0) return;  // every stream done by the level path, which set the counts
   const int p = blockIdx.x;
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_RLE_DICTIONARY) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.es != 0 || ck.lvdict) return;  // (the level path's chunks: counted by their emit or fallback)
   if (pf_level_path(pflag[p])) return;
   const uint32_t q0 = pw.ltile0 * 4u, nq = pw.ntiles * 4u;
   uint64_t s = 0;
   for (uint32_t i = threadIdx.x; i < nq; i += WG) s += qcount[q0 + i];
   const uint64_t t = block_sum_u64(s, red);
-  if (threadIdx.x == 0) {
-    if (field == 0) pages[p].nonnull = t;
-    else pages[p].nbytes_out = t;
-  }
+  if (threadIdx.x == 0) pages[p].nbytes_out = t;
 }
 
 // ------------------------------------------------------------------------------ scan
 
-// Exclusive scan of per-page value counts -> value_out (single workgroup).
-__device__ inline void scan_values(PageWork* pages, int npages, ChunkResult* res, int es, uint64_t cap_bytes) {
-  __shared__ uint64_t wsum[WG / 64];
-  __shared__ uint64_t carry_s;
-  if (threadIdx.x == 0) carry_s = 0;
-  __syncthreads();
-  for (int base = 0; base < npages; base += WG) {
-    int p = base + threadIdx.x;
-    uint64_t x = 0;
-    if (p < npages) {
-      int t = pages[p].page_type;
-      if (t == P_DATA || t == P_DATA_V2) x = pages[p].nonnull;
-    }
-    // inclusive wave scan
-    uint64_t s = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      uint64_t y = __shfl_up(s, off, 64);
-      if ((threadIdx.x & 63) >= (unsigned)off) s += y;
-    }
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = s;
-    __syncthreads();
-    uint64_t pre = carry_s;
-    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += wsum[k];
-    if (p < npages) {
-      pages[p].value_out = pre + s - x;
-      if (es > 0 && x > 0 && (pre + s) * (uint64_t)es > cap_bytes && pages[p].status == 0)
-        report(pages, res, p, ST_CAPACITY);
-    }
-    __syncthreads();
-    if (threadIdx.x == WG - 1) carry_s = pre + s;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) res->total_values = carry_s;
+// Value offsets per page, chunk by chunk (exclusive scan of the data pages' non-null counts,
+// restarted at each chunk's first page), each chunk's total and its capacity check (single
+// workgroup).
+__device__ inline void scan_values(PageWork* pages, ChunkWork* chunks, int npages) {
+  seg_scan_pages(
+      pages, chunks, npages,
+      [&](int p) -> uint64_t {
+        const int t = pages[p].page_type;
+        return (t == P_DATA || t == P_DATA_V2) ? pages[p].nonnull : 0ull;
+      },
+      [&](int p, uint64_t excl, uint64_t incl) {
+        ChunkWork& ck = chunks[pages[p].chunk];
+        pages[p].value_out = excl;
+        const uint64_t es = (uint64_t)ck.es;
+        if (es > 0 && incl > excl && incl * es > ck.val_cap && pages[p].status == 0) report(pages, chunks, p, ST_CAPACITY);
+        if ((uint32_t)p == ck.first_page + ck.npages - 1u) ck.res.total_values = incl;
+      });
 }
 
-__global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, int npages, ChunkResult* res, int es,
-                                                    uint64_t cap_bytes) {
-  scan_values(pages, npages, res, es, cap_bytes);
+__global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, ChunkWork* chunks, int npages) {
+  scan_values(pages, chunks, npages);
 }
-
-// ------------------------------------------------------------------------------ dictionary
 
 // ------------------------------------------------------------------------------ PLAIN
 
-// Copies each page's `nonnull * es` value bytes to out + value_out * es. grid.y = page,
-// grid.x strides 16-byte output chunks. Source alignment is arbitrary (the value section
-// follows the level streams): dword loads + v_alignbyte; the destination is chunked on
-// 16-byte boundaries of the output so stores are dwordx4 except at page edges.
+// Copies each page's `nonnull * es` value bytes to its chunk's values + value_out * es. grid.y =
+// page, grid.x strides 16-byte output chunks. Source alignment is arbitrary (the value section
+// follows the level streams): dword loads + v_alignbyte; the destination is chunked on 16-byte
+// boundaries of the output so stores are dwordx4 except at page edges.
 __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ blob,
-                                                   uint64_t blob_len, PageWork* pages, int es,
-                                                   int enc_filter, uint8_t* __restrict__ out,
-                                                   ChunkResult* res) {
+                                                   uint64_t blob_len, PageWork* pages, ChunkWork* chunks) {
   const int p = blockIdx.y;
   const PageWork& pwr = pages[p];
   if (pwr.status != 0) return;
   if (pwr.page_type != P_DATA && pwr.page_type != P_DATA_V2) return;
-  if (pwr.encoding != enc_filter) return;
+  if (pwr.encoding != E_PLAIN) return;
+  const ChunkWork& ck = chunks[pwr.chunk];
+  const int es = ck.es;
+  if (es <= 0 || ck.cp.physical_type == T_BOOLEAN || !ck.val_out) return;
+  uint8_t* __restrict__ out = ck.val_out;
   const uint64_t nbytes = pwr.nonnull * (uint64_t)es;
   if (nbytes > pwr.val_bytes) {  // eof_err!("Not enough bytes to decode")
-    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, res, p, ST_EOF);
+    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, p, ST_EOF);
     return;
   }
   const uint64_t src = pwr.base + pwr.val_off;
@@ -526,16 +493,18 @@ __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ b
 
 // PLAIN booleans: LSB-first bits from the value section, one byte (0/1) per value.
 __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ blob,
-                                                   PageWork* pages, uint8_t* __restrict__ out,
-                                                   ChunkResult* res) {
+                                                   PageWork* pages, ChunkWork* chunks) {
   const int p = blockIdx.y;
   const PageWork& pw = pages[p];
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_PLAIN) return;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (ck.cp.physical_type != T_BOOLEAN || !ck.val_out) return;
+  uint8_t* __restrict__ out = ck.val_out;
   const uint64_t n = pw.nonnull;
   if ((n + 7) / 8 > pw.val_bytes && n > (uint64_t)pw.val_bytes * 8) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, res, p, ST_EOF);
+    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, p, ST_EOF);
     return;
   }
   const uint8_t* src = blob + pw.base + pw.val_off;
@@ -553,148 +522,121 @@ __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ b
 
 extern "C" {
 
-hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                         ColumnParams cp, int sel, int dict_page, int es, RunTables rt, LevelTables lt, void* out,
-                         ChunkResult* res, hipStream_t s);
+hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                         int sel, uint32_t widths, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* vsrc,
+                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s);
 
-hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                              int npages, ColumnParams cp, uint32_t* tile_page, ChunkResult* res,
-                              PrepInit ini, hipStream_t s) {
-  hipLaunchKernelGGL(k_prepare, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, npages, cp, tile_page, res, ini);
+hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                              ChunkWork* chunks, uint32_t* tile_page, PrepInit ini, hipStream_t s) {
+  hipLaunchKernelGGL(k_prepare, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, npages, chunks, tile_page, ini);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_run_index(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                int npages, ColumnParams cp, int sel, int dict_page, RunTables rt,
-                                ChunkResult* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, sel,
-                     dict_page, rt, res);
+hipError_t pqg_launch_run_index(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                ChunkWork* chunks, int sel, RunTables rt, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, chunks, sel, rt, 0);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_tile_desc(const uint8_t* blob, PageWork* pages, uint32_t ntiles,
-                                const uint32_t* tile_page, RunTables rt, ColumnParams cp, int sel,
-                                int dict_page, hipStream_t s) {
-  if (ntiles)
-    hipLaunchKernelGGL(k_quarter_desc, dim3((ntiles * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
-                       ntiles, rt, cp, sel, dict_page);
+hipError_t pqg_launch_quarter_desc(const uint8_t* blob, PageWork* pages, ChunkWork* chunks, const uint32_t* tile_page,
+                                   const uint32_t* tl, uint32_t ntl, RunTables rt, int sel, hipStream_t s) {
+  if (ntl)
+    hipLaunchKernelGGL(k_quarter_desc, dim3((ntl * 4 + WG - 1) / WG), dim3(WG), 0, s, blob, pages, chunks, tile_page,
+                       tl, ntl, rt, sel);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_page_counts(PageWork* pages, int npages, RunTables rt, int field, hipStream_t s) {
-  hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, rt.qcount, rt.pflag, rt.nfall, field);
+hipError_t pqg_launch_page_counts(PageWork* pages, int npages, ChunkWork* chunks, RunTables rt, hipStream_t s) {
+  hipLaunchKernelGGL(k_page_counts, dim3(npages), dim3(WG), 0, s, pages, chunks, rt.qcount, rt.pflag, rt.nfall);
   return hipGetLastError();
 }
 
-// Level stream `which` (0 def, 1 rep): the window-parallel level path (levels + per-page non-null
-// counts, pqg_levels.hip), then the general hybrid decoder for the streams it hands back
-// (k_run_index walks only those; the tiled kernels exit at once when there are none).
-hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                             int npages, uint32_t ntiles, ColumnParams cp, int which,
-                             const uint32_t* tile_page, RunTables rt, LevelTables lt, int16_t* out,
-                             ChunkResult* res, hipStream_t s, hipEvent_t* kev, int scan_es, uint64_t scan_cap) {
+// Level stream `which` (0 def, 1 rep) of every chunk that reads it: the window-parallel level path
+// (levels + per-page non-null counts, pqg_levels.hip), then the general hybrid decoder for the
+// streams it hands back (one workgroup per handed-back page; the others exit at once). `widths`:
+// bit mask of the streams' bit widths (1 << w). scan: the value-offset scan runs in that last
+// kernel's last workgroup.
+hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                             int which, uint32_t widths, const uint32_t* tile_page, RunTables rt, LevelTables lt,
+                             hipStream_t s, hipEvent_t* kev, int scan) {
   const int sel = which ? SS_REP : SS_DEF;
   if (kev) (void)hipEventRecord(kev[0], s);
-  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, sel, -1, 0, rt, lt, out, res, s);
-  if (kev) (void)hipEventRecord(kev[1], s);
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, chunks, sel, widths, nullptr, nullptr, nullptr, nullptr,
+                               rt, lt, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp, sel, rt, res,
-                     out, lt.ctr + 1, scan_es, scan_cap);
+  hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, sel, rt,
+                     lt.ctr + 1, scan);
+  if (kev) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkResult* res, int es,
-                           uint64_t cap_bytes, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan_values, dim3(1), dim3(WG), 0, s, pages, npages, res, es, cap_bytes);
+hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkWork* chunks, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_values, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
   return hipGetLastError();
 }
 
-// RLE_DICTIONARY values. 4- and 8-byte values take the hybrid-stream path (pqg_levels.hip: segment
-// walks, then a gather per output); its pages the general decoder takes back (dense or malformed
-// streams, indices wider than 16 bits), and other value sizes, take the index pass and tiled
-// expand.
-hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                           uint32_t ntiles, ColumnParams cp, int dict_page, int es,
-                           const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
-                           ChunkResult* res, hipStream_t s, hipEvent_t* kev, int small_dict) {
-  // (the dictionary page's checks ran in k_prepare)
-  bool lvpath = es == 4 || es == 8;
-#ifdef PQG_DIAG
-  if (cp.debug & 256) lvpath = false;
-#endif
+// RLE_DICTIONARY values of fixed-width chunks. Chunks of 4- and 8-byte values with a dictionary of
+// at most 2^dict_maxw entries take the hybrid-stream path (pqg_launch_lv with SS_DICT, launched by
+// the host for every dictionary chunk on it), their rare leftovers one workgroup per page here
+// (lv_es: bit mask of those value sizes). The other chunks' pages (larger dictionaries: wider
+// indices, gathers served from L2; other value sizes) take the tiled expand over the listed
+// tiles (tl_all: every such tile; tl[i] / ntl[i]: those of value size 1, 4, 8, 12), their index
+// pass (pqg_launch_run_index with SS_DICT) having run before.
+hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                           const uint32_t* tile_page, uint32_t lv_es, const uint32_t* const* tl,
+                           const uint32_t* ntl, const uint32_t* tl_all, uint32_t ntl_all, RunTables rt,
+                           hipStream_t s, hipEvent_t* kev) {
+  // (the dictionary pages' checks ran in k_prepare)
   if (kev) (void)hipEventRecord(kev[0], s);
-  if (lvpath) {
-    const hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, es, rt, lt, out, res, s);
-    if (e != hipSuccess) return e;
-    if (small_dict) {  // the level path takes (nearly) every page: its rare leftovers in one launch
-      if (es == 8)
-        hipLaunchKernelGGL((k_dict_fallback<8>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp,
-                           dict_page, rt, out, res);
-      else
-        hipLaunchKernelGGL((k_dict_fallback<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, tile_page, cp,
-                           dict_page, rt, out, res);
-      if (kev) (void)hipEventRecord(kev[1], s);
-      return hipGetLastError();
-    }
-  }
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_DICT,
-                     dict_page, rt, res, lvpath ? 1 : 0);
-  if (!ntiles) {
-    if (kev) (void)hipEventRecord(kev[1], s);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
-                     ntiles, rt, cp, (int)SS_DICT, dict_page);
-  const dim3 g = tx_grid(ntiles);
-  switch (es) {
-    case 1: hipLaunchKernelGGL((k_texpand_dict<1>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
-    case 4: hipLaunchKernelGGL((k_texpand_dict<4>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
-    case 8: hipLaunchKernelGGL((k_texpand_dict<8>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
-    case 12: hipLaunchKernelGGL((k_texpand_dict<12>), g, dim3(WG), 0, s, blob, blob_len, ntiles, pages, rt, dict_page, out, res); break;
-    default: return hipErrorInvalidValue;
+  if (lv_es & 8)
+    hipLaunchKernelGGL((k_dict_fallback<8>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, rt);
+  if (lv_es & 4)
+    hipLaunchKernelGGL((k_dict_fallback<4>), dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, rt);
+  if (ntl_all) {
+    hipLaunchKernelGGL(k_tile_desc, dim3((ntl_all + WG - 1) / WG), dim3(WG), 0, s, blob, pages, chunks, tile_page,
+                       tl_all, ntl_all, rt, (int)SS_DICT);
+    if (ntl[0]) hipLaunchKernelGGL((k_texpand_dict<1>), dim3(ntl[0]), dim3(WG), 0, s, blob, blob_len, tl[0], pages, chunks, rt);
+    if (ntl[1]) hipLaunchKernelGGL((k_texpand_dict<4>), dim3(ntl[1]), dim3(WG), 0, s, blob, blob_len, tl[1], pages, chunks, rt);
+    if (ntl[2]) hipLaunchKernelGGL((k_texpand_dict<8>), dim3(ntl[2]), dim3(WG), 0, s, blob, blob_len, tl[2], pages, chunks, rt);
+    if (ntl[3]) hipLaunchKernelGGL((k_texpand_dict<12>), dim3(ntl[3]), dim3(WG), 0, s, blob, blob_len, tl[3], pages, chunks, rt);
   }
   if (kev) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_plain_copy(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                                 int npages, int es, int enc, uint64_t max_page_bytes,
-                                 uint8_t* out, ChunkResult* res, hipStream_t s) {
-  uint64_t chunks = (max_page_bytes + 16 * WG - 1) / (16 * WG) + 1;
-  if (chunks > 4096) chunks = 4096;
-  hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)chunks, npages), dim3(WG), 0, s, blob,
-                     blob_len, pages, es, enc, out, res);
+hipError_t pqg_launch_plain_copy(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                 ChunkWork* chunks, uint64_t max_page_bytes, hipStream_t s) {
+  uint64_t nch = (max_page_bytes + 16 * WG - 1) / (16 * WG) + 1;
+  if (nch > 4096) nch = 4096;
+  hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)nch, npages), dim3(WG), 0, s, blob, blob_len, pages, chunks);
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npages,
-                                 uint64_t max_page_values, uint8_t* out, ChunkResult* res,
-                                 hipStream_t s) {
-  uint64_t chunks = (max_page_values + 8 * WG - 1) / (8 * WG) + 1;
-  if (chunks > 4096) chunks = 4096;
-  hipLaunchKernelGGL(k_plain_bool, dim3((unsigned)chunks, npages), dim3(WG), 0, s, blob, pages,
-                     out, res);
+hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npages, ChunkWork* chunks,
+                                 uint64_t max_page_values, hipStream_t s) {
+  uint64_t nch = (max_page_values + 8 * WG - 1) / (8 * WG) + 1;
+  if (nch > 4096) nch = 4096;
+  hipLaunchKernelGGL(k_plain_bool, dim3((unsigned)nch, npages), dim3(WG), 0, s, blob, pages, chunks);
   return hipGetLastError();
 }
 
 // RLE booleans (data page v2 values, RleValueDecoder<bool>): the level path (one byte per value)
-// with the general hybrid decoder for the streams it hands back.
-hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
-                               int npages, uint32_t ntiles, ColumnParams cp,
-                               const uint32_t* tile_page, RunTables rt, LevelTables lt, uint8_t* out,
-                               ChunkResult* res, hipStream_t s) {
-  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, cp, SS_BOOL, -1, 0, rt, lt, out, res, s);
+// with the general hybrid decoder for the streams it hands back, over the listed tiles (the tiles
+// of the pages of RLE-encoded BOOLEAN chunks).
+hipError_t pqg_launch_rle_bool(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                               const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, RunTables rt,
+                               LevelTables lt, hipStream_t s) {
+  hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, chunks, SS_BOOL, 2u, nullptr, nullptr, nullptr, nullptr,
+                               rt, lt, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, cp, SS_BOOL,
-                     -1, rt, res, 1);
-  if (ntiles) {
-    hipLaunchKernelGGL(k_tile_desc, dim3((ntiles + WG - 1) / WG), dim3(WG), 0, s, blob, pages, tile_page,
-                       ntiles, rt, cp, (int)SS_BOOL, -1);
-    hipLaunchKernelGGL(k_texpand_bool, tx_grid(ntiles), dim3(WG), 0, s, blob, blob_len, ntiles, rt, out);
+  hipLaunchKernelGGL(k_run_index, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, chunks, (int)SS_BOOL, rt, 1);
+  if (ntl) {
+    hipLaunchKernelGGL(k_tile_desc, dim3((ntl + WG - 1) / WG), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, ntl,
+                       rt, (int)SS_BOOL);
+    hipLaunchKernelGGL(k_texpand_bool, dim3(ntl), dim3(WG), 0, s, blob, blob_len, tl, pages, chunks, rt);
   }
   return hipGetLastError();
 }
-
 
 }  // extern "C"
 

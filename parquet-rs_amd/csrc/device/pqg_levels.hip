@@ -210,12 +210,14 @@ __device__ inline uint32_t lv_page_of(const uint32_t* __restrict__ wbase, uint32
 }
 
 // Streams this path takes (wide streams: k_lv_bound's wide mode finds their segment starts).
-// Dictionary indices up to cp.dict_maxw bits: wider indices into 4- / 8-byte values (a large
-// dictionary, its gathers served from L2) expand faster through the general decoder's tiles.
-__device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int sel, const ColumnParams& cp,
+// Dictionary indices of the chunks the host gave this path (ChunkWork::lvdict: a dictionary of
+// at most 2^dict_maxw entries), up to dict_maxw bits: wider indices into 4- / 8-byte values (a
+// large dictionary, its gathers served from L2) expand faster through the general decoder's tiles.
+__device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int sel, const ChunkWork* chunks,
                                  Stream& s) {
-  return get_stream(blob, pw, sel, cp, s) && pw.status == 0 && !s.err && s.kind == LK_RLE &&
-         lv_width_ok((uint32_t)s.w) && (sel != SS_DICT || (uint32_t)s.w <= cp.dict_maxw);
+  const ChunkWork& ck = chunks[pw.chunk];
+  return get_stream(blob, pw, sel, ck.cp, s) && pw.status == 0 && !s.err && s.kind == LK_RLE &&
+         lv_width_ok((uint32_t)s.w) && (sel != SS_DICT || (ck.lvdict && (uint32_t)s.w <= ck.cp.dict_maxw));
 }
 
 // Hand page p to the general decoder (once).
@@ -282,32 +284,38 @@ __device__ inline void lv_scan_windows(int npages, uint32_t* wbase, F nwin_of) {
 // One wave per page of an RLE boolean stream: the density probe (pqg_runs.hpp lv_probe_dense);
 // the def / rep streams are probed by k_prepare, dictionary indices (no window path) never.
 __global__ void __launch_bounds__(WG) k_lv_probe(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                 const PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                                                 int sel, LevelTables lt) {
+                                                 const PageWork* __restrict__ pages, int npages,
+                                                 const ChunkWork* chunks, int sel, LevelTables lt) {
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;  // (uniform: scalar readlane indices)
   const uint32_t p = blockIdx.x * (WG / WAVE) + wid;
   if (p >= (uint32_t)npages) return;
   Stream st;
   uint32_t dense = 0;
-  if (lv_stream(blob, pages[p], sel, cp, st) && st.n && st.slen >= LW_SPAN + 64u)
+  if (lv_stream(blob, pages[p], sel, chunks, st) && st.n && st.slen >= LW_SPAN + 64u)
     dense = lv_probe_dense(blob, blob_len, st.S, rfl((uint32_t)st.w));
   if (lane == 0) lt.dense[p] = dense;
 }
 
 // ------------------------------------------------------------------------------ k_lv_plan
 // One workgroup: per page the stream's windows (exclusive scan into wbase), and the page flag:
-// PF_PAGE (level path) or PF_BAIL (general decoder). Def streams start their count at 0.
-__global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
-                                                ColumnParams cp, int sel, int dict_page, RunTables rt,
-                                                LevelTables lt) {
+// PF_PAGE (level path) or PF_BAIL (general decoder); 0 for pages without the stream and, for
+// dictionary indices, pages of chunks the general decoder takes (ChunkWork::lvdict 0). Def
+// streams start their count at 0.
+__device__ inline bool lv_nodict(const PageWork* pages, const ChunkWork& ck, int sel) {
   // dictionary indices without a usable dictionary: the general decoder reports it
-  const bool nodict = sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0);
+  return sel == SS_DICT && (ck.dict_page < 0 || pages[ck.dict_page].status != 0);
+}
+
+__global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
+                                                const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   lv_scan_windows(npages, lt.wbase, [&](int p) -> uint32_t {
     const PageWork& pw = pages[p];
+    const ChunkWork& ck = chunks[pw.chunk];
+    const bool nodict = lv_nodict(pages, ck, sel);
     Stream s;
     uint32_t flag = 0, nw = 0;
-    if (get_stream(blob, pw, sel, cp, s)) {
-      if (!nodict && lv_stream(blob, pw, sel, cp, s) && (s.n == 0 || s.slen > 0)) {
+    if (get_stream(blob, pw, sel, ck.cp, s) && (sel != SS_DICT || ck.lvdict)) {
+      if (!nodict && lv_stream(blob, pw, sel, chunks, s) && (s.n == 0 || s.slen > 0)) {
         flag = PF_PAGE;
         nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
         if (sel == SS_DEF) pages[p].nonnull = 0;
@@ -321,7 +329,9 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
   });
   lv_scan_windows(npages, lt.sbase, [&](int p) -> uint32_t {
     Stream s;
-    if (nodict || lt.dense[p] || !lv_stream(blob, pages[p], sel, cp, s) || !s.n || !s.slen) return 0u;
+    if (lv_nodict(pages, chunks[pages[p].chunk], sel) || lt.dense[p] || !lv_stream(blob, pages[p], sel, chunks, s) ||
+        !s.n || !s.slen)
+      return 0u;
     const uint32_t sw = lw_segw((uint32_t)s.w);
     return ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
   });
@@ -392,12 +402,12 @@ __device__ inline void lv_jump(LvWave& W, const LvWin& x, uint32_t (&jv)[LV_PPL]
 
 // Segment s of the level streams: page, segment of the page; false unless the page is still
 // on the level path's sparse candidates.
-__device__ inline bool lv_seg_of(const uint8_t* blob, const PageWork* pages, uint32_t npages, const ColumnParams& cp,
+__device__ inline bool lv_seg_of(const uint8_t* blob, const PageWork* pages, uint32_t npages, const ChunkWork* chunks,
                                  int sel, const RunTables& rt, const LevelTables& lt, uint32_t s, uint32_t& p,
                                  uint32_t& j, Stream& st) {
   p = lv_page_of(lt.sbase, npages, s);
   j = s - lt.sbase[p];
-  return rt.pflag[p] == PF_PAGE && lv_stream(blob, pages[p], sel, cp, st);
+  return rt.pflag[p] == PF_PAGE && lv_stream(blob, pages[p], sel, chunks, st);
 }
 
 // ------------------------------------------------------------------------------ k_lv_bound
@@ -422,8 +432,8 @@ constexpr uint32_t LB_PER = 7;                   // wide streams: full bit-packe
                                                  // place the true chain
 
 __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                 const PageWork* __restrict__ pages, int npages, ColumnParams cp,
-                                                 int sel, RunTables rt, LevelTables lt) {
+                                                 const PageWork* __restrict__ pages, int npages,
+                                                 const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   __shared__ uint32_t stg[WG / WAVE][LB_STG / 4];
   __shared__ uint32_t hist_s[WG / WAVE][LB_BINS];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
@@ -433,7 +443,7 @@ __global__ void __launch_bounds__(WG) k_lv_bound(const uint8_t* __restrict__ blo
   for (uint32_t s = blockIdx.x * (WG / WAVE) + wid; s < total; s += gridDim.x * (WG / WAVE)) {
     LvWin x;
     uint32_t j;
-    if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, s, x.p, j, x.s) || j == 0) continue;
+    if (!lv_seg_of(blob, pages, (uint32_t)npages, chunks, sel, rt, lt, s, x.p, j, x.s) || j == 0) continue;
     x.k = j * lw_segw((uint32_t)x.s.w);
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen;
@@ -548,7 +558,7 @@ __device__ inline void lv_hops(uint32_t& addr, uint32_t alim, uint32_t& k, uint3
 // RLE value or payload offset) and header offsets.
 __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                    const PageWork* __restrict__ pages, int npages,
-                                                   ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+                                                   const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   __shared__ uint32_t stg[WG / WAVE][LW_STG / 4];
   __shared__ uint4 lent_s[WG / WAVE][LW_STG / 8];  // per staged byte (u16): 2 * hop length of a one-byte header
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
@@ -558,7 +568,7 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
   for (uint32_t sidx = blockIdx.x * (WG / WAVE) + wid; sidx < total; sidx += gridDim.x * (WG / WAVE)) {
   uint32_t p, j;
   Stream s;
-  if (!lv_seg_of(blob, pages, (uint32_t)npages, cp, sel, rt, lt, sidx, p, j, s)) continue;
+  if (!lv_seg_of(blob, pages, (uint32_t)npages, chunks, sel, rt, lt, sidx, p, j, s)) continue;
   LvSeg& sg = lt.seg[sidx];
   const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
   const uint32_t start = j == 0 ? 0u : lt.bexit[sidx];
@@ -591,6 +601,7 @@ __global__ void __launch_bounds__(WG) k_lv_segwalk(const uint8_t* __restrict__ b
 #ifdef PQG_DIAG
   // diagnostics (PQG_DEBUG bit 7): per segment s_memtime cycles in region installs, hop loops,
   // batches, and the headers walked
+  const ColumnParams& cp = pcp(chunks, pages[p]);
   const bool stamps = (cp.debug & 128) && cp.dbgbuf;
   uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, t_reg = 0, t_hop = 0, t_bat = 0, nhops = 0;
 #define LW_STAMP(acc)                                      \
@@ -830,7 +841,7 @@ __device__ inline uint32_t lv_segscan_serial(LvSeg* seg, const uint2* srec, uint
 }
 
 __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                       int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+                                       int npages, const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   __shared__ uint64_t wout[WG / WAVE];
   __shared__ uint32_t wrun[WG / WAVE], wlast[WG / WAVE], wmin[WG / WAVE];
   __shared__ uint64_t c_out;
@@ -838,7 +849,7 @@ __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const P
   const uint32_t p = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   Stream s;
-  if (!lv_stream(blob, pages[p], sel, cp, s)) return;
+  if (!lv_stream(blob, pages[p], sel, chunks, s)) return;
   if (lt.dense[p]) return;  // the window path's (k_lv_probe)
   const uint32_t n = s.n, w = (uint32_t)s.w;
   const uint32_t s0 = lt.sbase[p], nseg = lt.sbase[p + 1] - s0;
@@ -962,8 +973,9 @@ __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const P
 // The grid's last workgroup also runs k_lv_plan2's scan (the windows of the pages left to the
 // window path), one launch fewer per level stream.
 __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                                   int npages, ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
-  lv_segscan_page(blob, pages, npages, cp, sel, rt, lt);
+                                                   int npages, const ChunkWork* chunks, int sel, RunTables rt,
+                                                   LevelTables lt) {
+  lv_segscan_page(blob, pages, npages, chunks, sel, rt, lt);
   if (last_workgroup(lt.ctr + 0)) lv_plan2_scan(npages, rt, lt);
 }
 
@@ -1069,7 +1081,7 @@ __device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV
 // Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                const PageWork* __restrict__ pages, int npages,
-                                               ColumnParams cp, int sel, RunTables rt, LevelTables lt) {
+                                               const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   __shared__ LvSmem sm;
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
@@ -1078,7 +1090,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     LvWin x;
     x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
     const PageWork& pw = pages[x.p];
-    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, cp, x.s)) continue;
+    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, chunks, x.s)) continue;
     x.k = g2 - lt.wbase2[x.p];
     const uint32_t g = lt.wbase[x.p] + x.k;
     x.W0 = x.k * LV_WIN;
@@ -1086,7 +1098,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
     // table of the entry offsets: (exit offset from W0 or terminal code | headers << 16, outputs)
     const uint32_t ent = lv_ent(w);
-    uint2* tab = lt.tab + (uint64_t)g * ent;
+    uint2* tab = lt.tab + (uint64_t)g * lt.tstride;
     if (w == 1) {  // 64 entry offsets: lane e follows entry e across the segments
       uint32_t pc[LV_SEG], pv[LV_SEG], bpm;
       lv_seg_build(W, x, pc, pv, bpm);
@@ -1134,11 +1146,11 @@ constexpr uint32_t SC_MMAX = 6;     // windows per wave with readlane walks (EPL
 constexpr uint32_t SC_SPEC = 0x80000000u;  // composition left the composable form
 
 __device__ inline bool lv_stitch_serial(const uint2* __restrict__ tab, uint2* win, uint32_t nw, uint32_t ent,
-                                        uint32_t n, uint32_t slen) {
+                                        uint32_t stride, uint32_t n, uint32_t slen) {
   uint32_t cur = 0, e = 0;
   uint64_t acc = 0;
   while (cur < nw) {
-    const uint2 t = tab[(uint64_t)cur * ent + e];
+    const uint2 t = tab[(uint64_t)cur * stride + e];
     win[cur] = make_uint2(e | (t.x & 0xFFFF0000u), (uint32_t)acc);  // entry | headers << 16
     acc += t.y;
     if (acc >= n) return true;
@@ -1161,9 +1173,10 @@ __device__ inline uint32_t sc_rl(const uint32_t (&v)[EPL], uint32_t e) {
   return e >= 64u ? b : a;
 }
 
-template <uint32_t EPL>  // entries per lane (ent / 64): 1, 2 (readlane walks) or 0 (any ent, LDS walks)
+template <uint32_t EPL>  // entries per lane (ent / 64): 1, 2 (readlane walks: streams of bit width 1 / 2) or
+                        // 0 (any ent, LDS walks: wider streams)
 __global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                                     int npages, ColumnParams cp, int sel, RunTables rt,
+                                                     int npages, const ChunkWork* chunks, int sel, RunTables rt,
                                                      LevelTables lt) {
   __shared__ uint2 tb[SC_ENT];
   __shared__ uint2 F[SC_FENT];  // per composing wave and entry offset: (exit entry | SC_SPEC, outputs)
@@ -1175,7 +1188,8 @@ __global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   const PageWork& pw = pages[p];
   Stream s;
-  if (!lv_stream(blob, pw, sel, cp, s)) return;
+  if (!lv_stream(blob, pw, sel, chunks, s)) return;
+  if (EPL == 1 ? s.w != 1 : EPL == 2 ? s.w != 2 : s.w <= 2) return;  // another launch's width
   const uint32_t k0 = lt.wbase[p], nw = lt.wbase[p + 1] - k0;
   uint2* win = lt.win + k0;
   for (uint32_t k = tid; k < nw; k += SC_WG) win[k] = make_uint2(LV_NONE, 0u);
@@ -1186,16 +1200,18 @@ __global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__
   const uint32_t m = (CW + amax - 1) / amax;               // windows per wave
   const uint32_t A = (CW + m - 1) / m;                     // composing waves
   const uint32_t nch = (nw + CW - 1) / CW;
-  const uint2* tab = lt.tab + (uint64_t)k0 * ent;
+  const uint32_t ts = lt.tstride;  // table row stride (>= ent; rows of ent entries are staged)
+  const uint32_t lge = 31u - __builtin_clz(ent);  // (ent: a power of two)
+  const uint2* tab = lt.tab + (uint64_t)k0 * ts;
   constexpr uint32_t PF = SC_ENT / SC_WG;
   uint2 pf[PF];
   auto fetch = [&](uint32_t c) {
     const uint32_t cnt = min(CW, nw - c * CW) * ent;
-    const uint2* src = tab + (uint64_t)c * CW * ent;
+    const uint2* src = tab + (uint64_t)c * CW * ts;
 #pragma unroll
     for (uint32_t i = 0; i < PF; ++i) {
       const uint32_t idx = tid + i * SC_WG;
-      pf[i] = idx < cnt ? src[idx] : make_uint2(LV_J_DEAD, 0u);
+      pf[i] = idx < cnt ? src[(uint64_t)(idx >> lge) * ts + (idx & (ent - 1u))] : make_uint2(LV_J_DEAD, 0u);
     }
   };
   fetch(0);
@@ -1338,7 +1354,7 @@ __global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__
   }
   if (tid == 0) {
     bool ok = ok_s != 0;
-    if (serial_s) ok = lv_stitch_serial(tab, win, nw, ent, n, slen);
+    if (serial_s) ok = lv_stitch_serial(tab, win, nw, ent, ts, n, slen);
     if (!ok) lv_bail(rt, p, PF_PAGE);
   }
 }
@@ -1519,13 +1535,20 @@ __device__ inline uint32_t lv_write_wide(const LvRuns& rl, const uint32_t* stage
   return cnt;
 }
 
+// Output buffer of stream `sel` of a chunk: def / rep levels, RLE booleans.
+__device__ inline uint8_t* lv_out(const ChunkWork& ck, int sel) {
+  return sel == SS_DEF ? (uint8_t*)ck.def_out : sel == SS_REP ? (uint8_t*)ck.rep_out : ck.val_out;
+}
+
 // Outputs of one window from its run list, and the def count.
 template <int OUT>
 __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                 uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo, int sel,
-                                const ColumnParams& cp, PageWork* pages, uint8_t* __restrict__ out) {
+                                const ChunkWork* chunks, PageWork* pages) {
+  const ChunkWork& ck = chunks[pages[x.p].chunk];
+  uint8_t* __restrict__ out = lv_out(ck, sel);
   const bool count = sel == SS_DEF;
-  const uint32_t maxl = sel == SS_DEF ? (uint32_t)cp.max_def : (uint32_t)cp.max_rep;
+  const uint32_t maxl = sel == SS_DEF ? (uint32_t)ck.cp.max_def : (uint32_t)ck.cp.max_rep;
   uint32_t cnt = x.s.w == 1 ? lv_write1<OUT>(rl, stage, blob, blob_len, x, base, endo, out)
                             : lv_write_wide<OUT>(rl, stage, blob, blob_len, x, base, endo, maxl, count, out);
   if (count) {
@@ -1637,47 +1660,29 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
 template <int OUT>
 struct LvLevelOut {
   static constexpr bool PIPE = true;  // k_lv_emit_walk prefetches the next window (registers to spare)
-  uint8_t* out;
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
-                             const LvWin& x, uint32_t base, uint32_t endo, int sel, const ColumnParams& cp,
+                             const LvWin& x, uint32_t base, uint32_t endo, int sel, const ChunkWork* chunks,
                              PageWork* pages) const {
-    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, cp, pages, out);
-  }
-};
-
-template <int ES>
-struct LvDictOut {
-  static constexpr bool PIPE = false;  // (its gathers hold the registers the prefetch would take)
-  int dict_page;  // the chunk's PLAIN dictionary page (k_lv_plan checked it)
-  uint8_t* out;
-  ChunkResult* res;
-  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
-                             const LvWin& x, uint32_t base, uint32_t endo, int, const ColumnParams&,
-                             PageWork* pages) const {
-    const PageWork& dp = pages[dict_page];
-    const bool aligned = (dp.base % ES) == 0;
-    const uint32_t bad = lv_write_dict<ES>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base,
-                                           dp.num_values, aligned, out);
-    if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, res, (int)x.p, ST_PANIC);
+    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, chunks, pages);
   }
 };
 
 // BYTE_ARRAY / FLBA dictionary indices (decoding.rs:256-315 over the entries k_ba_dict_prep
 // decoded): per output the entry's source address and length (the byte-array scan and copy,
-// pqg_bytes.hip, take it from there), and the page's byte total.
-struct LvBaDictOut {
-  static constexpr bool PIPE = false;
-  int dict_page;
-  const uint64_t* dsrc;
-  const uint32_t* dlen;
-  uint64_t* vsrc;
-  uint32_t* vlen;
-  ChunkResult* res;
-  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
-                             const LvWin& x, uint32_t base, uint32_t endo, int, const ColumnParams&,
-                             PageWork* pages) const {
+// pqg_bytes.hip, take it from there), and the page's byte total. Scratch slots: the chunk's
+// scr_base (values) and dscr_base (dictionary entries) on.
+__device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+                                       const LvWin& x, uint32_t base, uint32_t endo, const ChunkWork& ck,
+                                       PageWork* pages, ChunkWork* chunks, const uint64_t* __restrict__ dsrc0,
+                                       const uint32_t* __restrict__ dlen0, uint64_t* __restrict__ vsrc0,
+                                       uint32_t* __restrict__ vlen0) {
+  {
+    const uint64_t* dsrc = dsrc0 + ck.dscr_base;
+    const uint32_t* dlen = dlen0 + ck.dscr_base;
+    uint64_t* vsrc = vsrc0 + ck.scr_base;
+    uint32_t* vlen = vlen0 + ck.scr_base;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t ndict = pages[dict_page].num_values;
+    const uint32_t ndict = pages[ck.dict_page].num_values;
     const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
     const uint64_t go = x.s.out;
     uint32_t lgn = 1;
@@ -1728,7 +1733,37 @@ struct LvBaDictOut {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off, 64);
     if (lane == 0 && bytes) atomicAdd((unsigned long long*)&pages[x.p].nbytes_out, (unsigned long long)bytes);
-    if (__ballot(bad) && lane == 0) report(pages, res, (int)x.p, ST_PANIC);
+    if (__ballot(bad) && lane == 0) report(pages, chunks, (int)x.p, ST_PANIC);
+  }
+}
+
+// Dictionary indices of every chunk on this path (ChunkWork::lvdict), by the chunk's value type:
+// 4- / 8-byte values gathered from its PLAIN dictionary page (k_prepare checked it), byte arrays
+// as entry addresses and lengths.
+struct LvDictOut {
+  static constexpr bool PIPE = false;  // (its gathers hold the registers the prefetch would take)
+  const uint64_t* dsrc;
+  const uint32_t* dlen;
+  uint64_t* vsrc;
+  uint32_t* vlen;
+  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+                             const LvWin& x, uint32_t base, uint32_t endo, int, const ChunkWork* chunks,
+                             PageWork* pages) const {
+    const ChunkWork& ck = chunks[pages[x.p].chunk];
+    if (ck.es == 0) {
+      lv_write_badict(rl, stage, blob, blob_len, x, base, endo, ck, pages, const_cast<ChunkWork*>(chunks), dsrc, dlen,
+                      vsrc, vlen);
+      return;
+    }
+    const PageWork& dp = pages[ck.dict_page];
+    uint32_t bad;
+    if (ck.es == 8)
+      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base, dp.num_values,
+                             (dp.base % 8) == 0, ck.val_out);
+    else
+      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base, dp.num_values,
+                             (dp.base % 4) == 0, ck.val_out);
+    if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)x.p, ST_PANIC);
   }
 };
 
@@ -1736,8 +1771,8 @@ struct LvBaDictOut {
 // Window path: windows g2 of the dense pages.
 template <int OUT>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_emit(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                PageWork* pages, int npages, ColumnParams cp, int sel,
-                                                RunTables rt, LevelTables lt, uint8_t* __restrict__ out) {
+                                                PageWork* pages, int npages, const ChunkWork* chunks, int sel,
+                                                RunTables rt, LevelTables lt) {
   __shared__ LvSmem sm;
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
@@ -1746,7 +1781,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     LvWin x;
     x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
     const PageWork& pw = pages[x.p];
-    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, cp, x.s)) continue;
+    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, chunks, x.s)) continue;
     x.k = g2 - lt.wbase2[x.p];
     const uint2 wi = lt.win[lt.wbase[x.p] + x.k];
     if (wi.x == LV_NONE) continue;  // no true header in this window
@@ -1839,8 +1874,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (endo <= base || R == 0) continue;
-    lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel, cp,
-                  pages, out);
+    lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
+                  chunks, pages);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
@@ -1922,8 +1957,8 @@ __device__ inline void le_install(const LeLoad& f, LeWave& E) {
 
 template <class Writer>
 __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, int npages, ColumnParams cp, int sel,
-                                                     RunTables rt, LevelTables lt, Writer wr) {
+                                                     PageWork* pages, int npages, const ChunkWork* chunks,
+                                                     int sel, RunTables rt, LevelTables lt, Writer wr) {
   __shared__ LeWave sm[WG / WAVE];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LeWave& E = sm[wid];
@@ -1936,7 +1971,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   uint32_t wb = lt.wbase[p], pend = lt.wbase[p + 1];
   LvWin x;
   x.p = p;
-  bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
+  bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
   LeLoad nf;  // the next window's loads, issued while the current one is written
   nf.ok = false;
   uint32_t nb0 = 0, nb1 = 0, nbk = 0;  // run bounds (wfirst) of window nbk of the page, read ahead
@@ -1947,7 +1982,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       wb = pend;
       pend = lt.wbase[p + 1];
       x.p = p;
-      walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, cp, x.s);
+      walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
       nf.ok = false;
       nbv = false;
     }
@@ -1978,7 +2013,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       lv_stage(blob, blob_len, x, E.stage, le_nch(w));  // ends with a wave LDS sync (run list too)
       const uint32_t base = E.rstart[0];
       const uint32_t endo = endn < x.s.n ? endn : x.s.n;
-      if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp, pages);
+      if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages);
       wave_lds_sync();
       continue;
     }
@@ -2030,78 +2065,60 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     const uint32_t base = E.rstart[0];
     const uint32_t endn = E.endn;
     const uint32_t endo = endn < x.s.n ? endn : x.s.n;
-    if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, cp, pages);
+    if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
 
 // Plan, segment starts and walks, page scan, run compaction: every page of stream `sel` ends
 // walked (PF_WALK, its run list built), dense (PF_PAGE) or handed back (PF_BAIL).
-static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ColumnParams cp,
-                     int sel, int dict_page, RunTables rt, LevelTables lt, uint32_t wgrid, hipStream_t s) {
+static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, const ChunkWork* chunks,
+                     int sel, RunTables rt, LevelTables lt, uint32_t wgrid, hipStream_t s) {
   if (sel == SS_BOOL)  // (def / rep: k_prepare probed them; dictionary indices: cleared there)
     hipLaunchKernelGGL(k_lv_probe, dim3((npages + WG / WAVE - 1) / (WG / WAVE)), dim3(WG), 0, s, blob, blob_len,
-                       pages, npages, cp, sel, lt);
-  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, cp, sel, dict_page, rt, lt);
-  hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segscan, dim3(npages), dim3(WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+                       pages, npages, chunks, sel, lt);
+  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_segscan, dim3(npages), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
 }
 
 extern "C" {
 
-// BYTE_ARRAY / FLBA dictionary indices on the hybrid-stream path (walked pages only: dense or
-// malformed streams go back to the general decoder): per value its entry's address and length.
-hipError_t pqg_launch_lv_badict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                                ColumnParams cp, int dict_page, RunTables rt, LevelTables lt, const uint64_t* dsrc,
-                                const uint32_t* dlen, uint64_t* vsrc, uint32_t* vlen, ChunkResult* res,
-                                hipStream_t s) {
+// Hybrid-stream path of stream `sel` over every chunk of the decode: plan, segment starts and
+// walks, page scan, run compaction, window path for the dense pages, emits. Def / rep levels:
+// int16 out (+ def counts); RLE booleans: bytes out; dictionary indices (SS_DICT, the chunks with
+// ChunkWork::lvdict): 4- / 8-byte dictionary values, or byte-array entry addresses and lengths
+// (scratch dsrc/dlen -> vsrc/vlen). widths: bit mask (1 << w) of the level streams' bit widths.
+hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
+                         int sel, uint32_t widths, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* vsrc,
+                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s) {
   if (npages <= 0) return hipSuccess;
   const uint32_t wgrid = 256u * 8u;
-  lv_front(blob, blob_len, pages, npages, cp, SS_DICT, dict_page, rt, lt, wgrid, s);
-  hipLaunchKernelGGL(k_lv_emit_walk<LvBaDictOut>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
-                     (int)SS_DICT, rt, lt, LvBaDictOut{dict_page, dsrc, dlen, vsrc, vlen, res});
-  return hipGetLastError();
-}
-
-// Hybrid-stream path of stream `sel`: plan, segment starts and walks, page scan, run compaction,
-// window path for the dense pages, emits. Def / rep levels: int16 out (+ def counts); RLE
-// booleans: bytes out; dictionary indices (SS_DICT, es 4 or 8): dictionary values out.
-hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                         ColumnParams cp, int sel, int dict_page, int es, RunTables rt, LevelTables lt, void* out,
-                         ChunkResult* res, hipStream_t s) {
-  if (npages <= 0) return hipSuccess;
-  const uint32_t wgrid = 256u * 8u;
-  lv_front(blob, blob_len, pages, npages, cp, sel, dict_page, rt, lt, wgrid, s);
-  uint8_t* o = (uint8_t*)out;
+  lv_front(blob, blob_len, pages, npages, chunks, sel, rt, lt, wgrid, s);
   if (sel == SS_DICT) {  // (dense dictionary streams went to the general decoder)
-    if (es == 8)
-      hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut<8>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
-                         cp, sel, rt, lt, LvDictOut<8>{dict_page, o, res});
-    else
-      hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut<4>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
-                         cp, sel, rt, lt, LvDictOut<4>{dict_page, o, res});
+    hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks,
+                       sel, rt, lt, LvDictOut{dsrc, dlen, vsrc, vlen});
     return hipGetLastError();
   }
   // (k_lv_plan2's scan ran in k_lv_segscan's last workgroup)
-  hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
   // window tables of 64 / 128 entry offsets (bit width 1 / 2) take the readlane walks
-  const int lw = sel == SS_DEF ? cp.def_bit_width : sel == SS_REP ? cp.rep_bit_width : 1;
-  if (lw == 1)
-    hipLaunchKernelGGL(k_lv_stitch<1>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
-  else if (lw == 2)
-    hipLaunchKernelGGL(k_lv_stitch<2>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
-  else
-    hipLaunchKernelGGL(k_lv_stitch<0>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, cp, sel, rt, lt);
+  if (widths & 2u)
+    hipLaunchKernelGGL(k_lv_stitch<1>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
+  if (widths & 4u)
+    hipLaunchKernelGGL(k_lv_stitch<2>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
+  if (widths & ~7u)
+    hipLaunchKernelGGL(k_lv_stitch<0>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
   if (sel == SS_BOOL) {
-    hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
-    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
-                       sel, rt, lt, LvLevelOut<1>{o});
+    hipLaunchKernelGGL(k_lv_emit<1>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
+                       chunks, sel, rt, lt, LvLevelOut<1>{});
   } else {
-    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp, sel, rt, lt, o);
-    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, cp,
-                       sel, rt, lt, LvLevelOut<2>{o});
+    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
+                       chunks, sel, rt, lt, LvLevelOut<2>{});
   }
   return hipGetLastError();
 }

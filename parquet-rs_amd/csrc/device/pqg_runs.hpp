@@ -52,7 +52,7 @@ __device__ inline bool get_stream(const uint8_t* blob, const PageWork& pw, int s
   s.kind = LK_RLE;
   if (sel == SS_DEF || sel == SS_REP) {
     const int kind = sel == SS_DEF ? pw.def_kind : pw.rep_kind;
-    if (kind == LK_NONE) return false;
+    if (kind == LK_NONE || !(sel == SS_DEF ? cp.want_def : cp.want_rep)) return false;
     s.kind = kind;
     s.S = pw.base + (sel == SS_DEF ? pw.def_off : pw.rep_off);
     s.slen = sel == SS_DEF ? pw.def_bytes : pw.rep_bytes;
@@ -797,9 +797,8 @@ __device__ inline uint32_t wave_stage(const uint8_t* __restrict__ blob, uint64_t
 
 // Descriptor of outputs [q * span, (q + 1) * span) of tile t for stream `sel` (k_quarter_desc:
 // one thread per quarter; k_tile_desc: one thread per tile with span = RUN_TILE).
-__device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
-                                     const uint32_t* tile_page, const RunTables& rt,
-                                     const ColumnParams& cp, int sel, int dict_page, uint32_t t,
+__device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages, const ChunkWork* chunks,
+                                     const uint32_t* tile_page, const RunTables& rt, int sel, uint32_t t,
                                      uint32_t q, uint32_t span = WX_OUT) {
   QDesc d{};
   const uint32_t p = tile_page[t];
@@ -807,9 +806,10 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   d.page = p;
   if (pw.status != 0) return d;
   if (rt.pflag && pf_level_path(rt.pflag[p])) return d;  // decoded by the level path
-  if (sel == SS_DICT && (dict_page < 0 || pages[dict_page].status != 0)) return d;
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (sel == SS_DICT && (ck.dict_page < 0 || pages[ck.dict_page].status != 0)) return d;
   Stream s;
-  if (!get_stream(blob, pw, sel, cp, s) || s.err) return d;
+  if (!get_stream(blob, pw, sel, ck.cp, s) || s.err) return d;
   const uint32_t k = t - pw.ltile0;
   const uint32_t lo = k * RUN_TILE + q * span;
   if (lo >= s.n) return d;

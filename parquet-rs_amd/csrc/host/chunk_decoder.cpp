@@ -1,9 +1,16 @@
-// chunk_decoder.cpp — pqg_ctx / pqg_decode_chunk / pqg_sync: the host half of the C ABI.
+// chunk_decoder.cpp — pqg_ctx / pqg_decode_chunk(s) / pqg_sync: the host half of the C ABI.
 //
-// Replaces ColumnReaderImpl's decode driving (column/reader.rs:159-488) for a whole chunk:
-// validates the page sequence the way read_new_page / set_current_page_encoding /
-// configure_dictionary would (column/reader.rs:269-488, decoding.rs:60-79), uploads the page
-// table, and enqueues the kernels of device/*.hip on one HIP stream.
+// Replaces ColumnReaderImpl's decode driving (column/reader.rs:159-488) for whole column chunks:
+// validates each chunk's page sequence the way read_new_page / set_current_page_encoding /
+// configure_dictionary would (column/reader.rs:269-488, decoding.rs:60-79), uploads one page
+// table for the decode, and enqueues the kernels of device/*.hip on one HIP stream.
+//
+// A decode is a batch of column chunks (pqg_decode_chunks; pqg_decode_chunk is a batch of one):
+// the chunks share nothing in the reference (every column chunk has its own page reader and
+// column reader, file/reader.rs:252-260, 306-330), so their pages go into one page table (each
+// page naming its chunk, ChunkWork in pqg_internal.hpp) and every kernel runs once over all of
+// them. A row group of 11 columns, or several row groups, then costs the ~30 launches one chunk
+// costs instead of ~30 per chunk.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -20,90 +27,88 @@
 using namespace pqg;
 
 extern "C" {
-hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, uint32_t*,
-                              ChunkResult*, PrepInit, hipStream_t);
-hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, int,
-                                RunTables, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                             const uint32_t*, RunTables, LevelTables, int16_t*, ChunkResult*,
-                             hipStream_t, hipEvent_t*, int, uint64_t);
-hipError_t pqg_launch_scan(PageWork*, int, ChunkResult*, int es, uint64_t cap_bytes,
-                           hipStream_t);
-hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams, int,
-                           int, const uint32_t*, RunTables, LevelTables, uint8_t*, ChunkResult*, hipStream_t,
-                           hipEvent_t*, int);
-hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, int, int, uint64_t,
-                                 uint8_t*, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, uint64_t, uint8_t*,
-                                 ChunkResult*, hipStream_t);
-hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, uint32_t, ColumnParams,
-                               const uint32_t*, RunTables, LevelTables, uint8_t*, ChunkResult*,
-                               hipStream_t);
-hipError_t pqg_launch_delta(const uint8_t*, uint64_t, PageWork*, int, int, uint8_t*,
-                            ChunkResult*, hipStream_t);
+hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint32_t*, PrepInit, hipStream_t);
+hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, RunTables, hipStream_t);
+hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, uint32_t, const uint32_t*,
+                             RunTables, LevelTables, hipStream_t, hipEvent_t*, int);
+hipError_t pqg_launch_scan(PageWork*, int, ChunkWork*, hipStream_t);
+hipError_t pqg_launch_lv(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, uint32_t, const uint64_t*,
+                         const uint32_t*, uint64_t*, uint32_t*, RunTables, LevelTables, hipStream_t);
+hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
+                           const uint32_t* const*, const uint32_t*, const uint32_t*, uint32_t, RunTables, hipStream_t,
+                           hipEvent_t*);
+hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint64_t, hipStream_t);
+hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, ChunkWork*, uint64_t, hipStream_t);
+hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
+                               uint32_t, RunTables, LevelTables, hipStream_t);
+hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint32_t, const uint32_t*,
+                                  DeltaTables, uint32_t, hipStream_t, hipEvent_t*);
 hipError_t pqg_launch_space(const int16_t*, uint64_t, int16_t, const void*, int, uint64_t*, void*, hipStream_t);
 uint64_t pqg_space_tiles(uint64_t n);
-hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, uint32_t, const uint32_t*,
-                                  DeltaTables, uint32_t, int, uint8_t*, ChunkResult*, hipStream_t,
-                                  hipEvent_t*);
-hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, int, int, uint64_t*,
-                                   uint32_t*, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, int, bool, uint64_t*, uint32_t*,
-                            uint32_t*, uint64_t, int64_t*, uint8_t*, uint64_t, uint64_t*, ChunkResult*,
-                            hipStream_t);
-hipError_t pqg_launch_badict_expand(const uint8_t*, uint64_t, PageWork*, uint32_t, RunTables, int,
-                                    uint64_t*, uint32_t*, uint64_t*, uint32_t*, ChunkResult*, hipStream_t);
-hipError_t pqg_launch_tile_desc(const uint8_t*, PageWork*, uint32_t, const uint32_t*, RunTables,
-                                ColumnParams, int, int, hipStream_t);
-hipError_t pqg_launch_page_counts(PageWork*, int, RunTables, int, hipStream_t);
-hipError_t pqg_launch_lv_badict(const uint8_t*, uint64_t, PageWork*, int, ColumnParams, int, RunTables,
-                                LevelTables, const uint64_t*, const uint32_t*, uint64_t*, uint32_t*,
-                                ChunkResult*, hipStream_t);
+hipError_t pqg_launch_ba_dict_prep(const uint8_t*, uint64_t, PageWork*, ChunkWork*, int, uint64_t*, uint32_t*,
+                                   hipStream_t);
+hipError_t pqg_launch_badict_general(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*,
+                                     const uint32_t*, uint32_t, RunTables, uint64_t*, uint32_t*, uint64_t*, uint32_t*,
+                                     int, hipStream_t);
+hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
+                            uint32_t, bool, uint64_t*, uint32_t*, uint32_t*, uint64_t*, hipStream_t);
 }
+
+// Stream kinds of the hybrid-stream tables: def, rep, dictionary indices, RLE booleans.
+enum { K_DEF = 0, K_REP = 1, K_DICT = 2, K_BOOL = 3, K_N = 4 };
+constexpr int SS_DICT = 2;  // device/pqg_runs.hpp StreamSel: dictionary indices
+
+// Tile lists the kernels over one kind of page take (host-built, uploaded with the page table):
+// general-path dictionary tiles by value size (1, 4, 8, 12) and all of them, byte-array
+// dictionary tiles off the level path, byte-array copy tiles, RLE boolean tiles.
+enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_N };
+
+// What the host knows of one chunk of a decode until its results are delivered.
+struct ChunkHost {
+  pqg_output* out = nullptr;
+  uint64_t total_levels = 0;  // the level count read_batch reports (column/reader.rs:259)
+  int host_status = 0;        // what the host checks found before the launch
+  int host_bad_page = -1;
+  std::string host_msg;
+};
 
 // Two staging slots so consecutive async decodes never overwrite pinned memory that an
 // in-flight H2D/D2H copy still reads (slot i is reused only after its last decode ended).
 struct Slot {
-  PageWork* d_pages = nullptr;
-  size_t pages_cap = 0;
-  PageWork* h_pages = nullptr;  // pinned staging
-  ChunkResult* d_res = nullptr;
-  ChunkResult* h_res = nullptr;  // pinned
+  uint8_t* d_tab = nullptr;  // page table | chunk table | tile lists (one H2D copy)
+  uint8_t* h_tab = nullptr;  // pinned staging
+  size_t tab_cap = 0;
+  ChunkWork* h_res = nullptr;  // pinned: the chunk table copied back after the decode
+  size_t res_cap = 0;
   hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the def-level path / values kernel
   bool kl = false, kv = false;  // events 6-7 / 8-9 recorded by the last decode
   bool used = false;     // a decode was enqueued and its timings not yet harvested
   bool pending = false;  // a decode was enqueued and its results not yet delivered
   uint64_t seq = 0;      // issue order of that decode
-  // the decode's own result delivery (pqg_sync, or the slot's reuse): its output struct, the
-  // level count read_batch reports, and what the host checks found before the launch
-  pqg_output* out = nullptr;
-  uint64_t total_levels = 0;
-  int host_status = 0;
-  int host_bad_page = -1;
-  std::string host_msg;
-  // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix;
-  // per dictionary entry source address and length
+  int call = 0;          // its index among the decodes since the last pqg_sync
+  std::vector<ChunkHost> ch;  // per chunk of that decode
+  // BYTE_ARRAY / FLBA scratch: per value source address, length, DELTA_BYTE_ARRAY prefix (slots
+  // per chunk from ChunkWork::scr_base); per dictionary entry source and length (dscr_base)
   uint64_t* vsrc = nullptr;
   uint32_t* vlen = nullptr;
   uint32_t* vpre = nullptr;
-  uint64_t* tsum = nullptr;  // BYTE_ARRAY copy: per page and tile of 4096 values, bytes then start
-  size_t tsumcap = 0;
   size_t vcap = 0;
   uint64_t* dsrc = nullptr;
   uint32_t* dlen = nullptr;
   size_t dcap = 0;
-  // hybrid-stream expand tiles: tile -> page map and one checkpoint array per stream kind
+  uint64_t* tsum = nullptr;  // byte-array copy: per tile, bytes then start
+  // hybrid-stream expand tiles: tile -> page map and the index-pass tables per stream kind
   uint32_t* tile_page = nullptr;
-  RunTables rt[3] = {};  // def, rep, values (index-pass outputs)
+  RunTables rt[K_N] = {};
   size_t tcap = 0;
   size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
-  // level path (def, rep, RLE booleans): buffers of LevelTables (pqg_internal.hpp), grown on demand
+  // level path (pqg_levels.hip): buffers of LevelTables per stream kind, grown on demand
   static constexpr int LV_BUFS = 13;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr
-  void* lvbuf[3][LV_BUFS] = {};
-  size_t lvcap[3][LV_BUFS] = {};
-  LevelTables lt(int k) const {
+  void* lvbuf[K_N][LV_BUFS] = {};
+  size_t lvcap[K_N][LV_BUFS] = {};
+  LevelTables lt(int k, uint32_t tstride) const {
     LevelTables t{};
     t.wbase = (uint32_t*)lvbuf[k][0];
     t.wbase2 = (uint32_t*)lvbuf[k][1];
@@ -118,6 +123,7 @@ struct Slot {
     t.spos = (uint32_t*)lvbuf[k][10];
     t.dense = (uint32_t*)lvbuf[k][11];
     t.ctr = (uint32_t*)lvbuf[k][12];
+    t.tstride = tstride;
     return t;
   }
 };
@@ -126,22 +132,16 @@ struct pqg_ctx {
   int device = 0;
   Slot slot[2];
   int cur = 0;          // slot of the last decode
-  PageWork* d_pages = nullptr;
-  PageWork* h_pages = nullptr;
-  ChunkResult* d_res = nullptr;
-  ChunkResult* h_res = nullptr;
-  hipEvent_t* ev = nullptr;
   hipStream_t stream = nullptr;
   bool timing = false;
   uint64_t seq = 0;     // decodes issued
+  int calls = 0;        // decodes issued since the last pqg_sync
   // first failure among decodes delivered at a slot's reuse, reported by the next pqg_sync
   int held_status = 0;
-  int held_page = -1;
-  uint64_t held_seq = 0;
+  int held_call = -1, held_chunk = -1, held_page = -1;
   std::string held_msg;
   double acc_ms[7] = {};
-  uint32_t epoch = 0;  // decode counter: look-back flags of older decodes never match
-  uint64_t* dbgbuf = nullptr;  // diagnostics (PQG_DEBUG bit 4)
+  uint64_t* dbgbuf = nullptr;  // diagnostics (PQG_DIAG builds)
   size_t dbg_cap = 0;
   uint32_t dbg_n = 0;
   uint64_t acc_n = 0;
@@ -183,33 +183,46 @@ static const char* status_name(int st) {
   return st >= 0 && st < 9 ? names[st] : "?";
 }
 
-// Delivers the results of slot sl's finished decode into its output struct; returns its status
-// (the host checks' status when they rejected a page no later than the first failing one)
-// and writes the failing page and a message.
-static int finish_slot(Slot& sl, int* page_out, std::string& msg) {
-  const ChunkResult& r = *sl.h_res;
-  pqg_output* out = sl.out;
-  out->num_levels = sl.total_levels;
-  out->num_values = r.total_values;
-  out->num_bytes = r.total_bytes;
-  int st = 0, page = -1;
-  if (r.bad != ~0ull) {
-    page = (int)(r.bad >> 32);
-    st = (int)(uint32_t)r.bad;
-  }
-  if (sl.host_status && (page < 0 || sl.host_bad_page <= page)) {
-    page = sl.host_bad_page;
-    st = sl.host_status;
-    msg = sl.host_msg;
-  } else if (st) {
-    char buf[160];
-    snprintf(buf, sizeof(buf), "page %d: %s (reference: %s)", page, status_name(st),
-             st == PQG_ERR_PANIC ? "panics" : st == PQG_ERR_HANG ? "loops forever" : "returns Err");
-    msg = buf;
+// Delivers the results of slot sl's finished decode into its chunks' output structs; returns the
+// status of its first failing chunk (lowest index; per chunk the host checks' status when they
+// rejected a page no later than the first failing one) and writes that chunk, its page and a
+// message.
+static int finish_slot(Slot& sl, int* chunk_out, int* page_out, std::string& msg) {
+  int st0 = 0, chunk0 = -1, page0 = -1;
+  for (size_t j = 0; j < sl.ch.size(); ++j) {
+    const ChunkHost& h = sl.ch[j];
+    const ChunkResult& r = sl.h_res[j].res;
+    pqg_output* out = h.out;
+    out->num_levels = h.total_levels;
+    out->num_values = r.total_values;
+    out->num_bytes = r.total_bytes;
+    int st = 0, page = -1;
+    if (r.bad != ~0ull) {
+      page = (int)(r.bad >> 32);
+      st = (int)(uint32_t)r.bad;
+    }
+    std::string m;
+    if (h.host_status && (page < 0 || h.host_bad_page <= page)) {
+      page = h.host_bad_page;
+      st = h.host_status;
+      m = h.host_msg;
+    } else if (st) {
+      char buf[160];
+      snprintf(buf, sizeof(buf), "page %d: %s (reference: %s)", page, status_name(st),
+               st == PQG_ERR_PANIC ? "panics" : st == PQG_ERR_HANG ? "loops forever" : "returns Err");
+      m = buf;
+    }
+    if (st && !st0) {
+      st0 = st;
+      chunk0 = (int)j;
+      page0 = page;
+      msg = m;
+    }
   }
   sl.pending = false;
-  *page_out = page;
-  return st;
+  *chunk_out = chunk0;
+  *page_out = page0;
+  return st0;
 }
 
 #define HIPCHK(expr, what)                      \
@@ -246,6 +259,17 @@ static int value_size(int t, int tl) {
   }
 }
 
+static void free_run_tables(RunTables& r) {
+  hipFree(r.ck);
+  hipFree(r.runs);
+  hipFree(r.nruns);
+  hipFree(r.desc);
+  hipFree(r.qcount);
+  hipFree(r.pflag);
+  hipFree(r.nfall);
+  r = RunTables{};
+}
+
 extern "C" {
 
 int pqg_ctx_create(int device, pqg_ctx** out) {
@@ -258,14 +282,8 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     delete ctx;
     return PQG_ERR_HIP;
   }
-  for (Slot& sl : ctx->slot) {
-    if (hipMalloc(&sl.d_res, sizeof(ChunkResult)) != hipSuccess ||
-        hipHostMalloc(&sl.h_res, sizeof(ChunkResult), hipHostMallocDefault) != hipSuccess) {
-      delete ctx;
-      return PQG_ERR_HIP;
-    }
+  for (Slot& sl : ctx->slot)
     for (auto& ev : sl.ev) hipEventCreate(&ev);
-  }
   ctx->cur = 1;
   *out = ctx;
   return PQG_OK;
@@ -276,9 +294,8 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
   hipSetDevice(ctx->device);
   for (Slot& sl : ctx->slot) {
     if (sl.used || sl.pending) hipEventSynchronize(sl.ev[5]);
-    hipFree(sl.d_pages);
-    hipHostFree(sl.h_pages);
-    hipFree(sl.d_res);
+    hipFree(sl.d_tab);
+    hipHostFree(sl.h_tab);
     hipHostFree(sl.h_res);
     hipFree(sl.vsrc);
     hipFree(sl.vlen);
@@ -287,27 +304,20 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
     hipFree(sl.tile_page);
-    for (RunTables& t : sl.rt) {
-      hipFree(t.ck);
-      hipFree(t.runs);
-      hipFree(t.nruns);
-      hipFree(t.desc);
-      hipFree(t.qcount);
-      hipFree(t.pflag);
-      hipFree(t.nfall);
-    }
+    for (RunTables& t : sl.rt) free_run_tables(t);
     hipFree(sl.dt.page);
     hipFree(sl.dt.blocks);
     hipFree(sl.dt.agg);
     hipFree(sl.dt.inc);
     hipFree(sl.dt.flag);
     hipFree(sl.dt.nfall);
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < K_N; ++k) {
       for (void* b : sl.lvbuf[k]) hipFree(b);
     }
     for (auto& ev : sl.ev) hipEventDestroy(ev);
   }
   hipFree(ctx->sp_tiles);
+  hipFree(ctx->dbgbuf);
   delete ctx;
   return PQG_OK;
 }
@@ -319,6 +329,8 @@ int pqg_ctx_set_timing(pqg_ctx* ctx, int enabled) {
 }
 
 const char* pqg_error_message(pqg_ctx* ctx) { return ctx ? ctx->msg.c_str() : "null ctx"; }
+
+}  // extern "C"
 
 // Host-side checks that read_new_page / set_current_page_encoding / configure_dictionary /
 // get_decoder would make before touching page bytes. Returns the status of the first page
@@ -387,12 +399,11 @@ static int validate_pages(const pqg_column* col, const pqg_page* pages, uint32_t
   return PQG_OK;
 }
 
-int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, uint64_t blob_len,
-                     const pqg_page* pages, uint32_t npages, pqg_output* out, void* stream_v) {
-  if (!ctx || !col || !out || (npages && !pages)) return PQG_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream_v;
-  // ---- argument checks first: a rejected call leaves the context (and a decode still in
-  // flight on it) untouched, so a later pqg_sync reports that decode's own status
+// Argument checks of one chunk: a rejected call leaves the context (and decodes still in flight
+// on it) untouched.
+static int check_chunk(pqg_ctx* ctx, uint32_t j, const pqg_column* col, const pqg_page* pages, uint32_t npages,
+                       const pqg_output* out) {
+  if (!col || !out || (npages && !pages)) return set_err(ctx, PQG_ERR_INVALID, "chunk %u: null argument", j);
   auto misaligned = [](const void* p) { return p && ((uintptr_t)p & 15u); };
   if (misaligned(out->def_levels) || misaligned(out->rep_levels) || misaligned(out->values))
     return set_err(ctx, PQG_ERR_INVALID, "output buffers must be 16-byte aligned");
@@ -403,14 +414,36 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
   if ((t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) && out->values) {
     uint64_t nlev = 0;
     for (uint32_t i = 0; i < npages; ++i)
-      if (pages[i].page_type == PQG_PAGE_DATA || pages[i].page_type == PQG_PAGE_DATA_V2)
-        nlev += pages[i].num_values;
+      if (pages[i].page_type == PQG_PAGE_DATA || pages[i].page_type == PQG_PAGE_DATA_V2) nlev += pages[i].num_values;
     if (!out->offsets || out->offsets_capacity < nlev + 1)
       return set_err(ctx, PQG_ERR_INVALID, "BYTE_ARRAY/FLBA output needs offsets[num_levels + 1]");
   }
+  return PQG_OK;
+}
+
+// Grows a device buffer to at least `need` elements (+1/8 headroom).
+static int grow(pqg_ctx* ctx, void** p, size_t* cap, size_t need, size_t elem, const char* what) {
+  if (need <= *cap) return PQG_OK;
+  hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t c = need + need / 8 + 1024;
+  HIPCHK(hipMalloc(p, c * elem), what);
+  *cap = c;
+  return PQG_OK;
+}
+
+// The decode of a batch of column chunks (see the top of this file).
+static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const uint8_t* blob, uint64_t blob_len,
+                        const pqg_page* const* pages, const uint32_t* npages, pqg_output* outs, hipStream_t s) {
+  if (!ctx || (nc && (!cols || !pages || !npages || !outs))) return PQG_ERR_INVALID;
+  for (uint32_t j = 0; j < nc; ++j) {
+    const int st = check_chunk(ctx, j, &cols[j], pages[j], npages[j], &outs[j]);
+    if (st) return st;
+  }
   HIPCHK(hipSetDevice(ctx->device), "hipSetDevice");
   ctx->stream = s;
-  out->num_levels = out->num_values = out->num_bytes = 0;
+  for (uint32_t j = 0; j < nc; ++j) outs[j].num_levels = outs[j].num_values = outs[j].num_bytes = 0;
 
   // ---- staging slot: wait until its previous decode has finished, harvest its timings and
   // deliver its results (a failure is held for the next pqg_sync)
@@ -424,187 +457,268 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     }
     sl.used = false;
     if (sl.pending) {
-      int page;
+      int chunk, page;
       std::string m;
-      const int st = finish_slot(sl, &page, m);
+      const int st = finish_slot(sl, &chunk, &page, m);
       if (st && !ctx->held_status) {
         ctx->held_status = st;
+        ctx->held_call = sl.call;
+        ctx->held_chunk = chunk;
         ctx->held_page = page;
-        ctx->held_seq = sl.seq;
         ctx->held_msg = m;
       }
     }
   }
-  sl.out = out;
-  sl.host_status = 0;
-  sl.host_bad_page = -1;
-  sl.host_msg.clear();
-  // page table and the chunk result go up in one copy: the result sits after the pages
-  const size_t res_off = ((size_t)npages * sizeof(PageWork) + 63) & ~(size_t)63;
-  if (npages > sl.pages_cap) {
-    size_t cap = npages < 1024 ? 1024 : npages;
-    hipFree(sl.d_pages);
-    hipHostFree(sl.h_pages);
-    sl.d_pages = nullptr;
-    sl.h_pages = nullptr;
-    const size_t bytes = ((cap * sizeof(PageWork) + 63) & ~(size_t)63) + sizeof(ChunkResult);
-    HIPCHK(hipMalloc(&sl.d_pages, bytes), "hipMalloc pages");
-    HIPCHK(hipHostMalloc(&sl.h_pages, bytes, hipHostMallocDefault), "hipHostMalloc");
-    sl.pages_cap = cap;
-  }
-  ctx->d_pages = sl.d_pages;
-  ctx->h_pages = sl.h_pages;
-  ctx->d_res = (ChunkResult*)((char*)sl.d_pages + res_off);
-  ctx->h_res = sl.h_res;
-  ctx->ev = sl.ev;
   sl.kl = sl.kv = false;
-  int bad = -1, dict_page = -1;
-  std::string why;
-  int vst = validate_pages(col, pages, npages, &bad, &dict_page, why);
-  uint64_t level_out = 0, max_page_bytes = 0, max_page_vals = 0;
-  uint32_t total_tiles = 0;
-  bool enc_present[16] = {};
-  uint64_t nwin = 0;           // level-path windows, upper bound (a stream is part of its page)
-  for (uint32_t i = 0; i < npages; ++i) {
-    PageWork& w = ctx->h_pages[i];
-    memset(&w, 0, sizeof(w));
-    w.base = pages[i].offset;
-    w.nbytes = pages[i].nbytes;
-    w.num_values = pages[i].num_values;
-    w.page_type = pages[i].page_type;
-    w.encoding = pages[i].encoding;
-    if (w.page_type != PQG_PAGE_DICTIONARY && w.encoding == PQG_PLAIN_DICTIONARY)
-      w.encoding = PQG_RLE_DICTIONARY;  // column/reader.rs:391-393
-    w.def_encoding = pages[i].def_encoding;
-    w.rep_encoding = pages[i].rep_encoding;
-    w.def_len = pages[i].def_len;
-    w.rep_len = pages[i].rep_len;
-    w.level_out = level_out;
-    w.ltile0 = total_tiles;
-    w.ntiles = 0;
-    if (w.page_type == PQG_PAGE_DATA || w.page_type == PQG_PAGE_DATA_V2) {
-      w.ntiles = (uint32_t)(((uint64_t)w.num_values + RUN_TILE - 1) / RUN_TILE);
-      total_tiles += w.ntiles;
-      level_out += w.num_values;
-      if (w.encoding >= 0 && w.encoding < 16) enc_present[w.encoding] = true;
-      if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
-      if (w.num_values > max_page_vals) max_page_vals = w.num_values;
-      nwin += (w.nbytes + LV_WIN - 1) / LV_WIN;
-    }
-    if (vst && (int)i == bad) w.status = vst;
-    if (vst && (int)i > bad) w.status = -1;  // never reached by the reference
-  }
-  if (vst) {
-    sl.host_status = vst;
-    sl.host_bad_page = bad;
-    sl.host_msg = why;
-  }
-  const bool want_def = col->max_def > 0 && out->def_levels;
-  const bool want_rep = col->max_rep > 0 && out->rep_levels;
-  const uint64_t lev_needed = level_out;
-  // read_batch reports levels only for the streams it reads (column/reader.rs:259)
-  sl.total_levels = (want_def || want_rep) ? lev_needed : 0;
 
-  ColumnParams cp{};
-  cp.physical_type = t;
-  cp.type_length = col->type_length;
-  cp.max_def = col->max_def;
-  cp.max_rep = col->max_rep;
-  cp.def_bit_width = log2_ceil((uint64_t)(int64_t)col->max_def + 1);
-  cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
-  cp.want_def = want_def;
-  cp.want_rep = want_rep;
-  // byte-array entries (address + length per value) take every index width; 4- / 8-byte values
-  // up to 8 bits (wider: a large dictionary, gathered faster by the tiled expand)
-  cp.dict_maxw = (t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY) ? 16u : 8u;
-  // Diagnostic kernel modes exist only in a PQG_DIAG build (make DIAG=1); the shipped library
-  // never reads the environment and always runs the production path.
+  // ---- the batch's shape: pages, tiles, windows, per-chunk parameters and scratch slots
+  uint32_t np = 0;
+  for (uint32_t j = 0; j < nc; ++j) np += npages[j];
+  sl.ch.assign(nc, ChunkHost{});
+  std::vector<ChunkWork> cw(nc);
+  std::vector<uint32_t> tl[TL_N];
+  std::vector<PageWork> pw(np);
+  uint32_t total_tiles = 0;
+  uint64_t nwin = 0, max_page_bytes = 0, max_page_vals = 0, scr = 0, dscr = 0;
+  uint32_t def_w = 0, rep_w = 0;  // bit masks of the level streams' widths
+  bool any_def = false, any_rep = false, any_plain = false, any_pbool = false, any_ba = false, any_dba = false;
+  bool any_badict = false, ba_lv = false, any_rbool = false, fixed_gen = false;
+  uint32_t lv_es = 0, delta_es = 0;  // value sizes of the level-path dictionary chunks / DELTA chunks
+  int nlvdict = 0;
 #ifdef PQG_DIAG
   static const int dbg_env = getenv("PQG_DEBUG") ? atoi(getenv("PQG_DEBUG")) : 0;
 #else
-  const int dbg_env = 0;
+  const int dbg_env = 0;  // diagnostic kernel modes exist only in a PQG_DIAG build (make DIAG=1)
 #endif
-  cp.debug = dbg_env;
-  cp.dbgbuf = nullptr;
+  uint32_t p0 = 0;
+  for (uint32_t j = 0; j < nc; ++j) {
+    const pqg_column* col = &cols[j];
+    const pqg_page* pg = pages[j];
+    const uint32_t n = npages[j];
+    pqg_output* out = &outs[j];
+    ChunkHost& h = sl.ch[j];
+    ChunkWork& c = cw[j];
+    memset(&c, 0, sizeof(c));
+    h.out = out;
+    const int t = col->physical_type;
+    const bool is_ba = t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY;
+    const int es = is_ba ? 0 : value_size(t, col->type_length);
+    int bad = -1, dict_page = -1;
+    std::string why;
+    const int vst = validate_pages(col, pg, n, &bad, &dict_page, why);
+    if (vst) {
+      h.host_status = vst;
+      h.host_bad_page = bad;
+      h.host_msg = why;
+    }
+    ColumnParams& cp = c.cp;
+    cp.physical_type = t;
+    cp.type_length = col->type_length;
+    cp.max_def = col->max_def;
+    cp.max_rep = col->max_rep;
+    cp.def_bit_width = log2_ceil((uint64_t)(int64_t)col->max_def + 1);
+    cp.rep_bit_width = log2_ceil((uint64_t)(int64_t)col->max_rep + 1);
+    cp.want_def = col->max_def > 0 && out->def_levels;
+    cp.want_rep = col->max_rep > 0 && out->rep_levels;
+    // byte-array entries (address + length per value) take every index width; 4- / 8-byte values
+    // up to 8 bits (wider: a large dictionary, gathered faster by the tiled expand)
+    cp.dict_maxw = is_ba ? 16u : 8u;
+    cp.debug = dbg_env;
+    c.def_out = out->def_levels;
+    c.rep_out = out->rep_levels;
+    c.val_out = (uint8_t*)out->values;
+    c.off_out = out->offsets;
+    c.val_cap = out->values_capacity;
+    c.es = es;
+    c.first_page = p0;
+    c.npages = n;
+    c.dict_page = dict_page < 0 ? -1 : (int32_t)(p0 + dict_page);
+    c.res.bad = ~0ull;
+    // configure_dictionary decodes the dictionary page whenever the reader reaches it, whatever
+    // the data pages' encodings and whether values are read (column/reader.rs:463-481)
+    c.dict_es = (dict_page >= 0 && !is_ba) ? es : 0;
+    const bool vo = out->values != nullptr;
+    bool enc[16] = {};
+    uint64_t lev = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      PageWork& w = pw[p0 + i];
+      memset(&w, 0, sizeof(w));
+      w.base = pg[i].offset;
+      w.nbytes = pg[i].nbytes;
+      w.num_values = pg[i].num_values;
+      w.page_type = pg[i].page_type;
+      w.encoding = pg[i].encoding;
+      if (w.page_type != PQG_PAGE_DICTIONARY && w.encoding == PQG_PLAIN_DICTIONARY)
+        w.encoding = PQG_RLE_DICTIONARY;  // column/reader.rs:391-393
+      w.def_encoding = pg[i].def_encoding;
+      w.rep_encoding = pg[i].rep_encoding;
+      w.def_len = pg[i].def_len;
+      w.rep_len = pg[i].rep_len;
+      w.level_out = lev;
+      w.ltile0 = total_tiles;
+      w.chunk = j;
+      if (w.page_type == PQG_PAGE_DATA || w.page_type == PQG_PAGE_DATA_V2) {
+        w.ntiles = (uint32_t)(((uint64_t)w.num_values + RUN_TILE - 1) / RUN_TILE);
+        total_tiles += w.ntiles;
+        lev += w.num_values;
+        if (w.encoding >= 0 && w.encoding < 16) enc[w.encoding] = true;
+        if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
+        if (w.num_values > max_page_vals) max_page_vals = w.num_values;
+        nwin += (w.nbytes + LV_WIN - 1) / LV_WIN;
+      }
+      if (vst && (int)i == bad) w.status = vst;
+      if (vst && (int)i > bad) w.status = -1;  // never reached by the reference
+    }
+    // read_batch reports levels only for the streams it reads (column/reader.rs:259)
+    h.total_levels = (cp.want_def || cp.want_rep) ? lev : 0;
+    if (cp.want_def) {
+      any_def = true;
+      def_w |= 1u << cp.def_bit_width;
+    }
+    if (cp.want_rep) {
+      any_rep = true;
+      rep_w |= 1u << cp.rep_bit_width;
+    }
+    if (n && vo) {
+      const uint32_t ndict = dict_page >= 0 ? pg[dict_page].num_values : 0u;
+      auto list_tiles = [&](int which, int encoding) {  // tiles of this chunk's data pages (of an encoding)
+        for (uint32_t i = 0; i < n; ++i) {
+          const PageWork& w = pw[p0 + i];
+          if (w.ntiles && (encoding < 0 || w.encoding == encoding))
+            for (uint32_t k = 0; k < w.ntiles; ++k) tl[which].push_back(w.ltile0 + k);
+        }
+      };
+      if (is_ba) {
+        any_ba = true;
+        c.scr_base = scr;
+        scr += lev ? lev : 1;
+        list_tiles(TL_BA, -1);
+        if (enc[PQG_DELTA_BYTE_ARRAY]) any_dba = true;
+        if (enc[PQG_RLE_DICTIONARY]) {
+          any_badict = true;
+          c.dscr_base = dscr;
+          dscr += ndict ? ndict : 1;
+          if (dict_page >= 0 && ndict <= (1u << cp.dict_maxw)) {
+            c.lvdict = 1;
+            ba_lv = true;
+          } else {  // (no dictionary page: the index pass reports the reference's panic)
+            list_tiles(TL_BADICT, PQG_RLE_DICTIONARY);
+          }
+        }
+      } else {
+        if (enc[PQG_PLAIN]) {
+          if (t == PQG_BOOLEAN) any_pbool = true;
+          else any_plain = true;
+        }
+        if (enc[PQG_RLE_DICTIONARY]) {
+          if ((es == 4 || es == 8) && dict_page >= 0 && ndict <= (1u << cp.dict_maxw)) {
+            c.lvdict = 1;
+            lv_es |= (uint32_t)es;
+          } else {
+            fixed_gen = true;
+            list_tiles(es == 1 ? TL_D1 : es == 4 ? TL_D4 : es == 8 ? TL_D8 : TL_D12, PQG_RLE_DICTIONARY);
+            list_tiles(TL_DALL, PQG_RLE_DICTIONARY);
+          }
+        }
+        if (enc[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64)) delta_es |= (uint32_t)es;
+        if (enc[PQG_RLE] && t == PQG_BOOLEAN) {
+          any_rbool = true;
+          list_tiles(TL_BOOL, PQG_RLE);
+        }
+      }
+      if (c.lvdict) ++nlvdict;
+    }
+    p0 += n;
+  }
+#ifdef PQG_DIAG
   if (dbg_env & (16 | 32 | 64 | 128)) {
-    size_t need = (size_t)(total_tiles * 4 > (uint64_t)npages * 2 ? total_tiles * 4 : (uint64_t)npages * 2) * 16;
-    if (need < (size_t)npages * 64) need = (size_t)npages * 64;
-    if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + npages + 1) * 32;  // per level-stream segment
+    size_t need = (size_t)(total_tiles * 4 > (uint64_t)np * 2 ? total_tiles * 4 : (uint64_t)np * 2) * 16;
+    if (need < (size_t)np * 64) need = (size_t)np * 64;
+    if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + np + 1) * 32;  // per level-stream segment
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
       HIPCHK(hipMalloc(&ctx->dbgbuf, need), "hipMalloc dbg");
       ctx->dbg_cap = need;
     }
-    ctx->dbg_n = (dbg_env & 32) ? (uint32_t)npages : total_tiles * 4;
-    cp.dbgbuf = ctx->dbgbuf;
+    ctx->dbg_n = (dbg_env & 32) ? np : total_tiles * 4;
+    for (ChunkWork& c : cw) c.cp.dbgbuf = ctx->dbgbuf;
+  }
+#endif
+
+  // ---- staging: page table | chunk table | tile lists, one H2D copy
+  const size_t pw_bytes = ((size_t)np * sizeof(PageWork) + 63) & ~(size_t)63;
+  const size_t cw_bytes = ((size_t)nc * sizeof(ChunkWork) + 63) & ~(size_t)63;
+  size_t tl_off[TL_N], tl_total = 0;
+  for (int k = 0; k < TL_N; ++k) {
+    tl_off[k] = tl_total;
+    tl_total += tl[k].size();
+  }
+  const size_t tab_bytes = pw_bytes + cw_bytes + tl_total * 4 + 64;
+  if (tab_bytes > sl.tab_cap) {
+    hipFree(sl.d_tab);
+    hipHostFree(sl.h_tab);
+    sl.d_tab = sl.h_tab = nullptr;
+    sl.tab_cap = 0;
+    const size_t cap = tab_bytes < (1u << 20) ? (1u << 20) : tab_bytes + tab_bytes / 4;
+    HIPCHK(hipMalloc(&sl.d_tab, cap), "hipMalloc page table");
+    HIPCHK(hipHostMalloc(&sl.h_tab, cap, hipHostMallocDefault), "hipHostMalloc page table");
+    sl.tab_cap = cap;
+  }
+  if ((size_t)nc > sl.res_cap) {
+    hipHostFree(sl.h_res);
+    sl.h_res = nullptr;
+    sl.res_cap = 0;
+    const size_t cap = nc < 64 ? 64 : (size_t)nc * 2;
+    HIPCHK(hipHostMalloc(&sl.h_res, cap * sizeof(ChunkWork), hipHostMallocDefault), "hipHostMalloc results");
+    sl.res_cap = cap;
+  }
+  PageWork* d_pages = (PageWork*)sl.d_tab;
+  ChunkWork* d_chunks = (ChunkWork*)(sl.d_tab + pw_bytes);
+  const uint32_t* d_tl = (const uint32_t*)(sl.d_tab + pw_bytes + cw_bytes);
+  const uint32_t* tlp[TL_N];
+  uint32_t ntl[TL_N];
+  for (int k = 0; k < TL_N; ++k) {
+    tlp[k] = d_tl + tl_off[k];
+    ntl[k] = (uint32_t)tl[k].size();
   }
 
-  ChunkResult r0{};
-  r0.total_levels = sl.total_levels;
-  r0.bad = ~0ull;
-  r0.dict_page = dict_page < 0 ? 0xFFFFFFFFu : (uint32_t)dict_page;
-  *(ChunkResult*)((char*)ctx->h_pages + res_off) = r0;
-  HIPCHK(hipMemcpyAsync(ctx->d_pages, ctx->h_pages, res_off + sizeof(ChunkResult), hipMemcpyHostToDevice, s),
-         "H2D pages");
-
-  const bool is_ba = t == PQG_BYTE_ARRAY || t == PQG_FIXED_LEN_BYTE_ARRAY;
-  const int es = is_ba ? 0 : value_size(t, col->type_length);
-  const int np = (int)npages;
-  if (is_ba && out->values) {
-    size_t need = lev_needed ? lev_needed : 1;
-    if (need > sl.vcap) {
-      hipFree(sl.vsrc);
+  // ---- scratch, grown on demand
+  const int ni = (int)np;
+  if (any_ba) {
+    int st;
+    const size_t vcap0 = sl.vcap;
+    if ((st = grow(ctx, (void**)&sl.vsrc, &sl.vcap, scr, 8, "hipMalloc vsrc"))) return st;
+    if (sl.vcap != vcap0) {  // vlen / vpre share vsrc's capacity
       hipFree(sl.vlen);
       hipFree(sl.vpre);
-      sl.vsrc = nullptr;
       sl.vlen = sl.vpre = nullptr;
-      HIPCHK(hipMalloc(&sl.vsrc, need * 8), "hipMalloc vsrc");
-      HIPCHK(hipMalloc(&sl.vlen, need * 4), "hipMalloc vlen");
-      HIPCHK(hipMalloc(&sl.vpre, need * 4), "hipMalloc vpre");
-      sl.vcap = need;
+      HIPCHK(hipMalloc(&sl.vlen, sl.vcap * 4), "hipMalloc vlen");
+      HIPCHK(hipMalloc(&sl.vpre, sl.vcap * 4), "hipMalloc vpre");
     }
-    const size_t tneed = (size_t)np * ((max_page_vals + 4095) / 4096) + 1;
-    if (tneed > sl.tsumcap) {
-      hipFree(sl.tsum);
-      sl.tsum = nullptr;
-      sl.tsumcap = 0;
-      HIPCHK(hipMalloc(&sl.tsum, tneed * 8), "hipMalloc byte-array tiles");
-      sl.tsumcap = tneed;
-    }
-    size_t dn = dict_page >= 0 && pages[dict_page].num_values ? pages[dict_page].num_values : 1;
-    if (dn > sl.dcap) {
-      hipFree(sl.dsrc);
+    const size_t dcap0 = sl.dcap;
+    if ((st = grow(ctx, (void**)&sl.dsrc, &sl.dcap, dscr ? dscr : 1, 8, "hipMalloc dsrc"))) return st;
+    if (sl.dcap != dcap0) {
       hipFree(sl.dlen);
-      sl.dsrc = nullptr;
       sl.dlen = nullptr;
-      HIPCHK(hipMalloc(&sl.dsrc, dn * 8), "hipMalloc dsrc");
-      HIPCHK(hipMalloc(&sl.dlen, dn * 4), "hipMalloc dlen");
-      sl.dcap = dn;
+      HIPCHK(hipMalloc(&sl.dlen, sl.dcap * 4), "hipMalloc dlen");
     }
   }
-  // expand-tile bookkeeping of the hybrid streams (tile -> page, checkpoints per stream kind)
-  if (total_tiles + 1 > sl.tcap) {
+  // expand-tile bookkeeping (tile -> page, byte-array tile sums, index tables per stream kind)
+  if ((size_t)total_tiles + 1 > sl.tcap) {
     hipFree(sl.tile_page);
+    hipFree(sl.tsum);
     sl.tile_page = nullptr;
-    for (RunTables& r : sl.rt) {
-      hipFree(r.ck);
-      hipFree(r.runs);
-      hipFree(r.nruns);
-      hipFree(r.desc);
-      hipFree(r.qcount);
-      hipFree(r.pflag);
-      hipFree(r.nfall);
-      r = RunTables{};
-    }
+    sl.tsum = nullptr;
+    for (RunTables& r : sl.rt) free_run_tables(r);
     sl.tcap = 0;
     sl.pfcap = 0;
-    size_t cap = (size_t)total_tiles + 1024;
+    const size_t cap = (size_t)total_tiles + 1024;
     HIPCHK(hipMalloc(&sl.tile_page, cap * sizeof(uint32_t)), "hipMalloc tile_page");
+    HIPCHK(hipMalloc(&sl.tsum, cap * sizeof(uint64_t)), "hipMalloc byte-array tiles");
     sl.tcap = cap;
   }
-  // run tables are allocated per stream kind on first use
-  auto tables = [&](int k) -> hipError_t {
+  auto tables = [&](int k) -> hipError_t {  // run tables per stream kind, on first use
     RunTables& r = sl.rt[k];
     if (r.ck) return hipSuccess;
     hipError_t e = hipMalloc(&r.ck, (sl.tcap + 1) * sizeof(RunCkpt));
@@ -615,8 +729,7 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     if (e == hipSuccess) e = hipMalloc(&r.nfall, sizeof(uint32_t));
     return e;
   };
-  // page-pass flags, sized by pages (all stream kinds together)
-  if ((size_t)np > sl.pfcap) {
+  if ((size_t)np > sl.pfcap) {  // page-pass flags, sized by pages
     const size_t pc = (size_t)np < 4096 ? 4096 : (size_t)np * 2;
     for (RunTables& r : sl.rt) {
       hipFree(r.pflag);
@@ -626,65 +739,47 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
     for (RunTables& r : sl.rt) HIPCHK(hipMalloc(&r.pflag, pc * sizeof(uint32_t)), "hipMalloc page flags");
     sl.pfcap = pc;
   }
-  const bool hybrid_values = enc_present[PQG_RLE_DICTIONARY] || (enc_present[PQG_RLE] && t == PQG_BOOLEAN);
-  if (want_def) HIPCHK(tables(0), "hipMalloc run tables");
-  if (want_rep) HIPCHK(tables(1), "hipMalloc run tables");
-  if (hybrid_values && out->values) HIPCHK(tables(2), "hipMalloc run tables");
-  const uint32_t nt = total_tiles;
-  // Level path buffers (normalized streams) per stream kind, grown on demand.
-  const bool rle_bool = enc_present[PQG_RLE] && t == PQG_BOOLEAN && out->values;
-  // 4- / 8-byte dictionary values: their index streams take the same path (pqg_launch_dict)
-  bool dict_lv = enc_present[PQG_RLE_DICTIONARY] && !is_ba && out->values && (es == 4 || es == 8);
-  // byte-array dictionary indices: entry addresses and lengths from the same path
-  bool badict_lv = enc_present[PQG_RLE_DICTIONARY] && is_ba && out->values;
-#ifdef PQG_DIAG
-  if (cp.debug & 256) dict_lv = badict_lv = false;  // diagnostics: dictionary indices through the general decoder
-#endif
-  dict_lv = dict_lv || badict_lv;
-  const bool need_lv[3] = {want_def, want_rep, rle_bool || dict_lv};
-  auto grow = [&](void** p, size_t* cap, size_t need, size_t elem, const char* what) -> int {
-    if (need <= *cap) return PQG_OK;
-    hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    const size_t c = need + need / 8 + 1024;
-    HIPCHK(hipMalloc(p, c * elem), what);
-    *cap = c;
-    return PQG_OK;
-  };
-  for (int k = 0; k < 3; ++k) {
+  const bool dict_any = nlvdict > 0 || fixed_gen || any_badict;
+  const bool need_tables[K_N] = {any_def, any_rep, dict_any, any_rbool};
+  for (int k = 0; k < K_N; ++k)
+    if (need_tables[k]) HIPCHK(tables(k), "hipMalloc run tables");
+  // level path buffers per stream kind, grown on demand; window tables of a uniform row stride
+  uint32_t tstride[K_N] = {64, 64, 64, 64};
+  for (int w = 1; w <= 31; ++w) {
+    if ((def_w >> w) & 1u) tstride[K_DEF] = lv_ent((uint32_t)w) > tstride[K_DEF] ? lv_ent((uint32_t)w) : tstride[K_DEF];
+    if ((rep_w >> w) & 1u) tstride[K_REP] = lv_ent((uint32_t)w) > tstride[K_REP] ? lv_ent((uint32_t)w) : tstride[K_REP];
+  }
+  const bool need_lv[K_N] = {any_def, any_rep, nlvdict > 0, any_rbool};
+  for (int k = 0; k < K_N; ++k) {
     if (!need_lv[k]) continue;
     int st;
-    const size_t ent = lv_ent(k == 2 ? 1u : (uint32_t)(k == 0 ? cp.def_bit_width : cp.rep_bit_width));
-    const size_t nseg = nwin / LW_SEGW + npages + 1;  // segments, upper bound
-    const size_t need[Slot::LV_BUFS] = {(size_t)npages + 1, (size_t)npages + 1, nwin + npages + 1,
-                                        64 * (nwin + 2 * (size_t)npages) + 1, (nwin + 1) * ent, nwin + 1,
-                                        (size_t)npages + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP,
-                                        (size_t)npages + 1, 16};
+    const size_t ent = tstride[k];
+    const size_t nseg = nwin / LW_SEGW + np + 1;  // segments, upper bound
+    const size_t need[Slot::LV_BUFS] = {(size_t)np + 1, (size_t)np + 1, nwin + np + 1,
+                                        64 * (nwin + 2 * (size_t)np) + 1, (nwin + 1) * ent, nwin + 1,
+                                        (size_t)np + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP,
+                                        (size_t)np + 1, 16};
     const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2),
                                         4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4, 4};
     const bool fresh_ctr = sl.lvbuf[k][12] == nullptr;
-    for (int b = 0; b < Slot::LV_BUFS; ++b)
-      if ((st = grow(&sl.lvbuf[k][b], &sl.lvcap[k][b], need[b], elem[b], "hipMalloc level tables"))) return st;
+    for (int bb = 0; bb < Slot::LV_BUFS; ++bb)
+      if ((st = grow(ctx, &sl.lvbuf[k][bb], &sl.lvcap[k][bb], need[bb], elem[bb], "hipMalloc level tables"))) return st;
     // the tickets start at zero once; every launch using them leaves them at zero
     if (fresh_ctr) HIPCHK(hipMemsetAsync(sl.lvbuf[k][12], 0, sl.lvcap[k][12] * 4, s), "memset level tickets");
   }
-  // Hybrid-stream flags: the level path (def, rep, RLE booleans) sets every page's flag and counts
-  // the streams it hands back; dictionary indices always take the general decoder. k_prepare
-  // sets them (no memset launches), and runs the fixed-width dictionary page's checks.
+  // Hybrid-stream counters and flags, set by k_prepare (no memset launches): the level path (def,
+  // rep, dictionary indices, RLE booleans) sets every page's flag and counts the streams it hands
+  // back; the general dictionary path's kernels run when it has listed tiles.
   PrepInit ini{};
   int nw_ = 0, nz = 0;
-  for (int k = 0; k < 3; ++k) {
-    if (!sl.rt[k].nfall) continue;
-    const bool lvpath = k < 2 || rle_bool || dict_lv;
+  for (int k = 0; k < K_N; ++k) {
+    if (!need_tables[k]) continue;
     ini.word[nw_] = sl.rt[k].nfall;
-    ini.val[nw_++] = lvpath ? 0u : 0xFFFFFFFFu;
-    if (!lvpath) ini.pzero[nz++] = sl.rt[k].pflag;
+    ini.val[nw_++] = (k == K_DICT && (ntl[TL_DALL] || ntl[TL_BADICT])) ? 1u : 0u;
+    if (!need_lv[k]) ini.pzero[nz++] = sl.rt[k].pflag;
   }
-  uint8_t* vo = (uint8_t*)out->values;
-  const bool delta_vals = np && vo && !is_ba && enc_present[PQG_DELTA_BINARY_PACKED] && (t == PQG_INT32 || t == PQG_INT64);
-  if (delta_vals) {  // DELTA_BINARY_PACKED tables (tiled fallback path), grown on demand
-    if (nt > sl.dt_tcap || (size_t)np > sl.dt_pcap) {
+  if (delta_es) {  // DELTA_BINARY_PACKED tables (tiled fallback path), grown on demand
+    if (total_tiles > sl.dt_tcap || (size_t)np > sl.dt_pcap) {
       hipFree(sl.dt.page);
       hipFree(sl.dt.blocks);
       hipFree(sl.dt.agg);
@@ -700,113 +795,121 @@ int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, u
       HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
       HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
       HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
-      HIPCHK(hipMemsetAsync(sl.dt.flag, 0, tc * sizeof(uint32_t), s), "memset delta flags");
       sl.dt_tcap = tc;
       sl.dt_pcap = pc;
     }
-    ctx->epoch = (ctx->epoch + 1) & 0x3FFFFFFFu;
-    if (ctx->epoch == 0) {  // wrapped: flags from 2^30 decodes ago could match
-      HIPCHK(hipMemsetAsync(sl.dt.flag, 0, sl.dt_tcap * sizeof(uint32_t), s), "memset delta flags");
-      ctx->epoch = 1;
-    }
     ini.word[nw_] = sl.dt.nfall;
     ini.val[nw_++] = 0u;
+    sl.dt.dbg = (dbg_env & 32) ? ctx->dbgbuf : nullptr;
   }
-  ini.dict_page = dict_page;
-  // configure_dictionary decodes the dictionary page whenever the reader reaches it, whatever the
-  // data pages' encodings and whether values are read (column/reader.rs:463-481)
-  ini.dict_es = (np && dict_page >= 0 && !is_ba) ? es : 0;
-  ini.dense_def = need_lv[0] ? sl.lt(0).dense : nullptr;
-  ini.dense_rep = need_lv[1] ? sl.lt(1).dense : nullptr;
-  ini.dense_zero = (need_lv[2] && dict_lv) ? sl.lt(2).dense : nullptr;
-  if (ctx->timing) hipEventRecord(ctx->ev[0], s);
-  if (np) HIPCHK(pqg_launch_prepare(blob, blob_len, ctx->d_pages, np, cp, sl.tile_page, ctx->d_res, ini, s), "prepare");
-  if (ctx->timing) hipEventRecord(ctx->ev[1], s);
+  ini.dense_def = need_lv[K_DEF] ? sl.lt(K_DEF, 0).dense : nullptr;
+  ini.dense_rep = need_lv[K_REP] ? sl.lt(K_REP, 0).dense : nullptr;
+  ini.dense_zero = need_lv[K_DICT] ? sl.lt(K_DICT, 0).dense : nullptr;
+
+  // ---- upload the tables
+  memcpy(sl.h_tab, pw.data(), (size_t)np * sizeof(PageWork));
+  memcpy(sl.h_tab + pw_bytes, cw.data(), (size_t)nc * sizeof(ChunkWork));
+  for (int k = 0; k < TL_N; ++k)
+    if (!tl[k].empty()) memcpy(sl.h_tab + pw_bytes + cw_bytes + tl_off[k] * 4, tl[k].data(), tl[k].size() * 4);
+  HIPCHK(hipMemcpyAsync(sl.d_tab, sl.h_tab, pw_bytes + cw_bytes + tl_total * 4, hipMemcpyHostToDevice, s), "H2D pages");
+
+  // ---- kernels
+  const uint8_t* b = blob;
+  hipEvent_t* ev = sl.ev;
+  if (ctx->timing) hipEventRecord(ev[0], s);
+  if (np) HIPCHK(pqg_launch_prepare(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, ini, s), "prepare");
+  if (ctx->timing) hipEventRecord(ev[1], s);
   // the value-offset scan runs in the def stream's last kernel when no rep stream follows it
-  // (timed runs take the same kernel sequence: the stage events bracket the fused kernel)
-  const bool fused_scan = np && want_def && !want_rep;
-  if (np && want_def) {
-    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 0, sl.tile_page, sl.rt[0],
-                             sl.lt(0), out->def_levels, ctx->d_res, s,
-                             ctx->timing ? &sl.ev[6] : nullptr, fused_scan ? es : -1, out->values_capacity),
+  const bool fused_scan = np && any_def && !any_rep;
+  if (np && any_def) {
+    HIPCHK(pqg_launch_levels(b, blob_len, d_pages, ni, d_chunks, 0, def_w, sl.tile_page, sl.rt[K_DEF],
+                             sl.lt(K_DEF, tstride[K_DEF]), s, ctx->timing ? &ev[6] : nullptr, fused_scan ? 1 : 0),
            "def levels");
     sl.kl = ctx->timing;
   }
-  if (np && want_rep)
-    HIPCHK(pqg_launch_levels(blob, blob_len, ctx->d_pages, np, nt, cp, 1, sl.tile_page, sl.rt[1],
-                             sl.lt(1), out->rep_levels, ctx->d_res, s, nullptr, -1, 0),
+  if (np && any_rep)
+    HIPCHK(pqg_launch_levels(b, blob_len, d_pages, ni, d_chunks, 1, rep_w, sl.tile_page, sl.rt[K_REP],
+                             sl.lt(K_REP, tstride[K_REP]), s, nullptr, 0),
            "rep levels");
-  if (ctx->timing) hipEventRecord(ctx->ev[2], s);
-  if (!fused_scan) HIPCHK(pqg_launch_scan(ctx->d_pages, np, ctx->d_res, es, out->values_capacity, s), "scan");
-  if (ctx->timing) hipEventRecord(ctx->ev[3], s);
+  if (ctx->timing) hipEventRecord(ev[2], s);
+  if (np && !fused_scan) HIPCHK(pqg_launch_scan(d_pages, ni, d_chunks, s), "scan");
+  if (ctx->timing) hipEventRecord(ev[3], s);
   ctx->values_kernel = 0;
-  if (np && vo && is_ba) {
-    ctx->values_kernel = enc_present[PQG_RLE_DICTIONARY] ? PQG_RLE_DICTIONARY
-                         : enc_present[PQG_DELTA_BYTE_ARRAY] ? PQG_DELTA_BYTE_ARRAY
-                         : enc_present[PQG_DELTA_LENGTH_BYTE_ARRAY] ? PQG_DELTA_LENGTH_BYTE_ARRAY
-                                                                     : PQG_PLAIN;
-    const int tl = t == PQG_FIXED_LEN_BYTE_ARRAY ? col->type_length : 0;
-    if (enc_present[PQG_RLE_DICTIONARY]) {
-      HIPCHK(pqg_launch_ba_dict_prep(blob, blob_len, ctx->d_pages, dict_page, tl, sl.dsrc, sl.dlen,
-                                     ctx->d_res, s), "byte-array dictionary");
-      if (badict_lv)  // (nfall 0: the flags the plan sets decide which pages the index pass takes)
-        HIPCHK(pqg_launch_lv_badict(blob, blob_len, ctx->d_pages, np, cp, dict_page, sl.rt[2], sl.lt(2), sl.dsrc,
-                                    sl.dlen, sl.vsrc, sl.vlen, ctx->d_res, s), "dictionary indices");
-      HIPCHK(pqg_launch_run_index(blob, blob_len, ctx->d_pages, np, cp, 2 /* SS_DICT */, dict_page,
-                                  sl.rt[2], ctx->d_res, s), "dictionary index pass");
-      HIPCHK(pqg_launch_tile_desc(blob, ctx->d_pages, nt, sl.tile_page, sl.rt[2], cp, 2, dict_page, s),
-             "dictionary tiles");
-      HIPCHK(pqg_launch_badict_expand(blob, blob_len, ctx->d_pages, nt, sl.rt[2], dict_page, sl.vsrc,
-                                      sl.vlen, sl.dsrc, sl.dlen, ctx->d_res, s), "dictionary expand");
-      HIPCHK(pqg_launch_page_counts(ctx->d_pages, np, sl.rt[2], 1, s), "dictionary byte counts");
-    }
-    HIPCHK(pqg_launch_bytes(blob, blob_len, ctx->d_pages, np, tl, enc_present[PQG_DELTA_BYTE_ARRAY],
-                            sl.vsrc, sl.vlen, sl.vpre, out->values_capacity, out->offsets, vo, max_page_vals,
-                            sl.tsum, ctx->d_res, s),
-           "byte arrays");
-  } else if (np && vo) {
-    if (enc_present[PQG_PLAIN]) {
-      ctx->values_kernel = PQG_PLAIN;
-      if (t == PQG_BOOLEAN)
-        HIPCHK(pqg_launch_plain_bool(blob, ctx->d_pages, np, max_page_vals, vo, ctx->d_res, s), "plain bool");
-      else if (es > 0) {
-        if (ctx->timing) hipEventRecord(sl.ev[8], s);
-        HIPCHK(pqg_launch_plain_copy(blob, blob_len, ctx->d_pages, np, es, PQG_PLAIN, max_page_bytes, vo,
-                                     ctx->d_res, s), "plain");
-        if (ctx->timing) hipEventRecord(sl.ev[9], s);
-        sl.kv = true;
-      }
-    }
-    if (enc_present[PQG_RLE_DICTIONARY]) {
+  if (np) {
+    const RunTables& rd = sl.rt[K_DICT];
+    if (any_badict)
+      HIPCHK(pqg_launch_ba_dict_prep(b, blob_len, d_pages, d_chunks, (int)nc, sl.dsrc, sl.dlen, s),
+             "byte-array dictionary");
+    if (nlvdict)  // every dictionary chunk the level path takes, fixed-width and byte-array, in one pass
+      HIPCHK(pqg_launch_lv(b, blob_len, d_pages, ni, d_chunks, SS_DICT, 0u, sl.dsrc, sl.dlen, sl.vsrc, sl.vlen, rd,
+                           sl.lt(K_DICT, 64), s),
+             "dictionary indices");
+    if (ntl[TL_DALL] || ntl[TL_BADICT])  // the general path's index pass, both kinds together
+      HIPCHK(pqg_launch_run_index(b, blob_len, d_pages, ni, d_chunks, SS_DICT, rd, s), "dictionary index pass");
+    if (lv_es || fixed_gen) {
       ctx->values_kernel = PQG_RLE_DICTIONARY;
-      // a dictionary of at most 2^dict_maxw entries: the writer's index width is within the level
-      // path's limit, so the general decoder only sees the rare pages it hands back
-      const int small_dict = dict_page >= 0 && pages[dict_page].num_values <= (1u << cp.dict_maxw);
-      HIPCHK(pqg_launch_dict(blob, blob_len, ctx->d_pages, np, nt, cp, dict_page, es, sl.tile_page,
-                             sl.rt[2], sl.lt(2), vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr, small_dict),
+      const uint32_t* dl[4] = {tlp[TL_D1], tlp[TL_D4], tlp[TL_D8], tlp[TL_D12]};
+      const uint32_t dn[4] = {ntl[TL_D1], ntl[TL_D4], ntl[TL_D8], ntl[TL_D12]};
+      HIPCHK(pqg_launch_dict(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, lv_es, dl, dn, tlp[TL_DALL],
+                             ntl[TL_DALL], rd, s, ctx->timing ? &ev[8] : nullptr),
              "dict");
       sl.kv = ctx->timing;
     }
-    if (delta_vals) {
-      ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
-      sl.dt.dbg = (cp.debug & 32) ? cp.dbgbuf : nullptr;
-      HIPCHK(pqg_launch_delta_tiled(blob, blob_len, ctx->d_pages, np, nt, sl.tile_page, sl.dt, ctx->epoch,
-                                    es, vo, ctx->d_res, s, ctx->timing ? &sl.ev[8] : nullptr), "delta");
-      sl.kv = true;
+    if (any_badict)
+      HIPCHK(pqg_launch_badict_general(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BADICT],
+                                       ntl[TL_BADICT], rd, sl.dsrc, sl.dlen, sl.vsrc, sl.vlen, ba_lv ? 1 : 0, s),
+             "byte-array dictionary indices");
+    if (any_ba) {
+      if (!ctx->values_kernel) ctx->values_kernel = any_dba ? PQG_DELTA_BYTE_ARRAY : PQG_PLAIN;
+      HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba,
+                              sl.vsrc, sl.vlen, sl.vpre, sl.tsum, s),
+             "byte arrays");
     }
-    if (enc_present[PQG_RLE] && t == PQG_BOOLEAN) {
-      ctx->values_kernel = PQG_RLE;
-      HIPCHK(pqg_launch_rle_bool(blob, blob_len, ctx->d_pages, np, nt, cp, sl.tile_page, sl.rt[2],
-                                 sl.lt(2), vo, ctx->d_res, s), "rle bool");
+    if (any_plain) {
+      ctx->values_kernel = PQG_PLAIN;
+      if (ctx->timing) hipEventRecord(ev[8], s);
+      HIPCHK(pqg_launch_plain_copy(b, blob_len, d_pages, ni, d_chunks, max_page_bytes, s), "plain");
+      if (ctx->timing) hipEventRecord(ev[9], s);
+      sl.kv = ctx->timing;
+    }
+    if (any_pbool) HIPCHK(pqg_launch_plain_bool(b, d_pages, ni, d_chunks, max_page_vals, s), "plain bool");
+    if (delta_es) {
+      ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
+      HIPCHK(pqg_launch_delta_tiled(b, blob_len, d_pages, ni, d_chunks, total_tiles, sl.tile_page, sl.dt, delta_es, s,
+                                    ctx->timing ? &ev[8] : nullptr),
+             "delta");
+      sl.kv = ctx->timing;
+    }
+    if (any_rbool) {
+      if (!ctx->values_kernel) ctx->values_kernel = PQG_RLE;
+      HIPCHK(pqg_launch_rle_bool(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BOOL], ntl[TL_BOOL],
+                                 sl.rt[K_BOOL], sl.lt(K_BOOL, 64), s),
+             "rle bool");
     }
   }
-  if (ctx->timing) hipEventRecord(ctx->ev[4], s);
-  HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(ChunkResult), hipMemcpyDeviceToHost, s), "D2H res");
-  HIPCHK(hipEventRecord(ctx->ev[5], s), "event");
+  if (ctx->timing) hipEventRecord(ev[4], s);
+  if (nc)
+    HIPCHK(hipMemcpyAsync(sl.h_res, d_chunks, (size_t)nc * sizeof(ChunkWork), hipMemcpyDeviceToHost, s),
+           "D2H results");
+  HIPCHK(hipEventRecord(ev[5], s), "event");
   sl.used = true;
   sl.pending = true;
   sl.seq = ++ctx->seq;
+  sl.call = ctx->calls++;
   return PQG_OK;
+}
+
+extern "C" {
+
+int pqg_decode_chunk(pqg_ctx* ctx, const pqg_column* col, const uint8_t* blob, uint64_t blob_len,
+                     const pqg_page* pages, uint32_t npages, pqg_output* out, void* stream) {
+  if (!ctx || !col || !out || (npages && !pages)) return PQG_ERR_INVALID;
+  return decode_batch(ctx, 1, col, blob, blob_len, &pages, &npages, out, (hipStream_t)stream);
+}
+
+int pqg_decode_chunks(pqg_ctx* ctx, uint32_t nchunks, const pqg_column* cols, const uint8_t* blob, uint64_t blob_len,
+                      const pqg_page* const* pages, const uint32_t* npages, pqg_output* outs, void* stream) {
+  return decode_batch(ctx, nchunks, cols, blob, blob_len, pages, npages, outs, (hipStream_t)stream);
 }
 
 // Device-side record assembly of a decoded chunk (pqg_launch_space, device/pqg_kernels.hip).
@@ -829,30 +932,22 @@ int pqg_space_values(pqg_ctx* ctx, const int16_t* def_levels, uint64_t num_level
   return e == hipSuccess ? PQG_OK : set_err(ctx, PQG_ERR_HIP, "spacing launch: %s", hipGetErrorString(e));
 }
 
-// pqg_sync that also names the failing decode by its issue number (pqg_decode_seq); the
-// row-group decoder maps it back to its own call (row_group.cpp).
-int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq);
-
-int pqg_sync(pqg_ctx* ctx, int* first_bad_page) { return pqg_sync_seq(ctx, first_bad_page, nullptr); }
-
-// Issue number of the last decode enqueued on ctx (1, 2, ...; 0 before the first).
-uint64_t pqg_decode_seq(pqg_ctx* ctx) { return ctx ? ctx->seq : 0; }
-
-int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq) {
+int pqg_sync_detail(pqg_ctx* ctx, int* bad_call, int* bad_chunk, int* bad_page) {
   if (!ctx) return PQG_ERR_INVALID;
-  if (first_bad_page) *first_bad_page = -1;
-  if (bad_seq) *bad_seq = 0;
+  if (bad_call) *bad_call = -1;
+  if (bad_chunk) *bad_chunk = -1;
+  if (bad_page) *bad_page = -1;
   Slot* order[2] = {&ctx->slot[ctx->cur ^ 1], &ctx->slot[ctx->cur]};
   if (order[0]->pending && order[1]->pending && order[0]->seq > order[1]->seq) std::swap(order[0], order[1]);
-  if (!order[0]->pending && !order[1]->pending && !ctx->held_status)
+  if (!order[0]->pending && !order[1]->pending && !ctx->held_status) {
+    ctx->calls = 0;
     return set_err(ctx, PQG_ERR_INVALID, "no decode pending");
+  }
   // every pending decode is delivered, in issue order; the first failure is reported
-  int st = ctx->held_status, page = ctx->held_page;
-  uint64_t seq = ctx->held_seq;
+  int st = ctx->held_status, call = ctx->held_call, chunk = ctx->held_chunk, page = ctx->held_page;
   std::string msg = ctx->held_msg;
   ctx->held_status = 0;
-  ctx->held_page = -1;
-  ctx->held_seq = 0;
+  ctx->held_call = ctx->held_chunk = ctx->held_page = -1;
   ctx->held_msg.clear();
   hipError_t herr = hipSuccess;
   for (Slot* sl : order) {
@@ -868,23 +963,30 @@ int pqg_sync_seq(pqg_ctx* ctx, int* first_bad_page, uint64_t* bad_seq) {
       ctx->acc_n++;
     }
     sl->used = false;
-    int pg;
+    int ch, pg;
     std::string m;
-    const uint64_t sq = sl->seq;
-    const int s2 = finish_slot(*sl, &pg, m);
+    const int c = sl->call;
+    const int s2 = finish_slot(*sl, &ch, &pg, m);
     if (s2 && !st) {
       st = s2;
+      call = c;
+      chunk = ch;
       page = pg;
-      seq = sq;
       msg = m;
     }
   }
+  ctx->calls = 0;
   if (herr != hipSuccess) return hip_fail(ctx, herr, "hipEventSynchronize");
   ctx->msg = msg;
-  if (first_bad_page) *first_bad_page = page;
-  if (bad_seq) *bad_seq = st ? seq : 0;
+  if (st) {
+    if (bad_call) *bad_call = call;
+    if (bad_chunk) *bad_chunk = chunk;
+    if (bad_page) *bad_page = page;
+  }
   return st;
 }
+
+int pqg_sync(pqg_ctx* ctx, int* first_bad_page) { return pqg_sync_detail(ctx, nullptr, nullptr, first_bad_page); }
 
 // Average per-stage device time over every decode since the last reset (HIP events recorded
 // on the decode stream between the stages).
@@ -904,14 +1006,13 @@ int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
   return PQG_OK;
 }
 
-// Diagnostics: average per-wave phase cycles of the last decode's wave expand kernel
-// (PQG_DEBUG bit 4). out[0..2] = desc, expand, tail cycles; out[3] = waves.
 // Diagnostics: raw copy of the debug buffer (PQG_DIAG builds; u64 words).
 int pqg_debug_read(pqg_ctx* ctx, uint64_t* out, size_t n) {
   if (!ctx || !ctx->dbgbuf || !out || n * 8 > ctx->dbg_cap) return PQG_ERR_INVALID;
   return hipMemcpy(out, ctx->dbgbuf, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 
+// Diagnostics: average per-wave phase cycles of the last decode (PQG_DIAG builds).
 int pqg_debug_stamps(pqg_ctx* ctx, double* out4) {
   if (!ctx || !ctx->dbgbuf || !out4) return PQG_ERR_INVALID;
   std::vector<uint32_t> h((size_t)ctx->dbg_n * 4);

@@ -59,9 +59,12 @@ struct PageWork {
   int32_t status;
   // ---- levels kernel / scan
   uint64_t nonnull;     // values this page must yield (def == max_def count, or num_values)
-  uint64_t value_out;   // index of this page's first value in the value output
+  uint64_t value_out;   // index of this page's first value in its chunk's value output
   uint64_t byte_out;    // BYTE_ARRAY/FLBA: first byte of this page's values in the byte output
   uint64_t nbytes_out;  // BYTE_ARRAY/FLBA: bytes this page produces
+  // ---- host-filled
+  uint32_t chunk;       // the column chunk of the batch this page belongs to (ChunkWork index)
+  uint32_t pad1;
 };
 
 // Chunk-level result, copied to pinned host memory at the end of a decode.
@@ -72,8 +75,6 @@ struct PrepInit {
   uint32_t* word[4];
   uint32_t val[4];
   uint32_t* pzero[3];
-  int32_t dict_page;
-  int32_t dict_es;
   // level-path density probe (LevelTables::dense) of the def / rep streams, run by k_prepare's
   // wave right after it locates them; dense_zero: a stream kind's array cleared instead
   uint32_t* dense_def;
@@ -85,9 +86,8 @@ struct ChunkResult {
   uint64_t total_levels;
   uint64_t total_values;
   uint64_t total_bytes;
-  uint64_t bad;            // lowest failing page and its status: (page << 32) | status; ~0 when clean
-  uint32_t dict_page;      // index of the dictionary page or UINT32_MAX
-  uint32_t pad;
+  uint64_t bad;            // lowest failing page (chunk-relative) and its status: (page << 32) | status;
+                           // ~0 when clean
 };
 
 // Outputs per expand tile of the RLE/bit-packed hybrid decoder (device/pqg_runs.hpp).
@@ -195,12 +195,14 @@ struct LevelTables {
   uint32_t* wbase2;  // [pages + 1] the same over the pages the walker left to the window path
   uint32_t* wfirst;  // [windows + pages] walked pages: first run of each window, then the run count
   uint2* rec;        // [64 * (windows + 2 * pages)] walked pages' runs: (first output, info)
-  uint2* tab;        // [windows * entries] per window and entry offset: (exit offset, outputs)
+  uint2* tab;        // [windows * tstride] per window and entry offset: (exit offset, outputs)
   uint2* win;        // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
   uint32_t* dense;   // [pages] 1: the stream's first 64 headers lie within 1 KiB (k_lv_probe): the
                      // window path takes it without a segment walk
   uint32_t* ctr;     // [16] last-workgroup tickets (zero between launches): [0] k_lv_segscan,
                      // [1] k_lv_fallback
+  uint32_t tstride;  // tab entries per window: lv_ent of the widest stream of the decode (the
+                     // streams of a batch's chunks may differ in bit width)
 };
 
 // RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window
@@ -221,6 +223,28 @@ struct ColumnParams {
   int32_t debug;     // diagnostics switches (PQG_DEBUG), 0 in production
   uint32_t dict_maxw;  // widest dictionary index stream the hybrid-stream path takes
   uint64_t* dbgbuf;  // diagnostics: per-wave s_memtime phases (PQG_DEBUG bit 4)
+};
+
+// One column chunk of a decode (pqg_decode_chunk: one; pqg_decode_chunks: a batch of column
+// chunks, e.g. every chunk of one or more row groups, decoded by one pass of every kernel). Its
+// pages are [first_page, first_page + npages) of the decode's page table; outputs are the
+// caller's, indexed by the pages' chunk-relative level_out / value_out / byte_out.
+struct ChunkWork {
+  ColumnParams cp;
+  int16_t* def_out;
+  int16_t* rep_out;
+  uint8_t* val_out;      // fixed-width values / byte-array bytes
+  int64_t* off_out;      // byte-array offsets
+  uint64_t val_cap;      // bytes val_out holds
+  uint64_t scr_base;     // byte arrays: first per-value slot of this chunk in the source/length scratch
+  uint64_t dscr_base;    // byte arrays: first dictionary-entry slot in the dictionary scratch
+  int32_t dict_page;     // page-table index of the chunk's dictionary page, or -1
+  int32_t es;            // fixed value size in bytes (0: BYTE_ARRAY / FLBA)
+  int32_t dict_es;       // k_prepare's fixed-width dictionary page check: value size, 0 = none
+  uint32_t first_page;
+  uint32_t npages;
+  uint32_t lvdict;       // 1: its dictionary indices take the hybrid-stream (level) path
+  ChunkResult res;       // filled by the kernels, copied back after the decode
 };
 
 }  // namespace pqg

@@ -58,7 +58,8 @@ class Timings(C.Structure):
 
 
 EXPORTS = [
-    "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_sync",
+    "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_decode_chunks",
+    "pqg_sync", "pqg_sync_detail",
     "pqg_get_timings", "pqg_reset_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
@@ -86,7 +87,10 @@ def lib():
         L.pqg_ctx_set_timing.argtypes = [vp, i32]
         L.pqg_decode_chunk.argtypes = [vp, C.POINTER(Column), vp, u64, C.POINTER(Page), C.c_uint32,
                                        C.POINTER(Output), vp]
+        L.pqg_decode_chunks.argtypes = [vp, C.c_uint32, C.POINTER(Column), vp, u64, C.POINTER(C.POINTER(Page)),
+                                        C.POINTER(C.c_uint32), C.POINTER(Output), vp]
         L.pqg_sync.argtypes = [vp, C.POINTER(C.c_int)]
+        L.pqg_sync_detail.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.pqg_get_timings.argtypes = [vp, C.POINTER(Timings)]
         L.pqg_reset_timings.argtypes = [vp]
         L.pqg_error_message.argtypes = [vp]
@@ -179,10 +183,33 @@ class Context:
         if st:
             raise PqgError(st, self.error_message())
 
+    def decode_chunks_async(self, columns, blob, blob_len, page_arrays, outs, stream=0):
+        """Enqueue pqg_decode_chunks: a batch of column chunks (Column, ctypes Page array, Output
+        per chunk), every page in the device blob at `blob`. Returns the Output array the
+        library fills at sync (keep it alive until then)."""
+        n = len(columns)
+        cols = (Column * n)(*columns)
+        pp = (C.POINTER(Page) * n)(*[C.cast(a, C.POINTER(Page)) for a in page_arrays])
+        npg = (C.c_uint32 * n)(*[len(a) for a in page_arrays])
+        oa = (Output * n)(*outs)
+        st = lib().pqg_decode_chunks(self.h, n, cols, C.c_void_p(blob), blob_len, pp, npg, oa, C.c_void_p(stream))
+        self._keep = getattr(self, "_keep", []) + [(cols, pp, npg, oa, page_arrays)]
+        if st:
+            raise PqgError(st, self.error_message())
+        return oa
+
     def sync(self):
         bad = C.c_int(-1)
         st = lib().pqg_sync(self.h, C.byref(bad))
+        self._keep = getattr(self, "_keep", [])[-2:]
         return st, bad.value
+
+    def sync_detail(self):
+        """(status, failing call since the last sync, its chunk, that chunk's page)."""
+        call, chunk, page = C.c_int(-1), C.c_int(-1), C.c_int(-1)
+        st = lib().pqg_sync_detail(self.h, C.byref(call), C.byref(chunk), C.byref(page))
+        self._keep = getattr(self, "_keep", [])[-2:]
+        return st, call.value, chunk.value, page.value
 
     def timings(self):
         t = Timings()
