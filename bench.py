@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--at-p-null", type=float, default=0.05, help="alltypes: null fraction per column")
     ap.add_argument("--streams", type=int, default=16,
                     help="alltypes: HIP streams the row-group decoder spreads the column chunks over")
+    ap.add_argument("--at-batch", default="step", choices=["step", "rg"],
+                    help="alltypes: one pqg_decode_chunks over every chunk of the step (step) or one "
+                         "pqg_rg_decode per row group on two alternating streams (rg)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
     return ap.parse_args(argv)
@@ -542,11 +545,23 @@ class AlltypesWorkload:
         dev = torch.device("cuda", torch.cuda.current_device())
         self.d_blob = torch.empty(off + 64, dtype=torch.uint8, device=dev)
         self.d_blob.copy_(self.h_blob)
-        # outputs: two sets (the PCIe pipeline decodes row group g + 1 while g drains)
+        # pages of every row group with offsets into the one device blob (the batched step)
+        self.shifted = []
+        for g in range(self.R):
+            per = []
+            for arr in self.chunks[g]:
+                sh = (pqgpu.Page * len(arr))()
+                for i in range(len(arr)):
+                    sh[i] = arr[i]
+                    sh[i].offset = arr[i].offset + self.base[g]
+                per.append(sh)
+            self.shifted.append(per)
+        # outputs: one set per row group for the batched step; the row-group path and the PCIe
+        # pipeline use sets 0 and 1 (row group g + 1 decodes while g drains)
         self.vcap = [max(i.value_bytes[j] for i in self.info) + 64 for j in range(len(self.cols))]
         self.ncap = [self.rows + 1] * len(self.cols)  # BYTE_ARRAY offsets: num_levels + 1 (pqgpu.h)
         self.out = []
-        for _ in range(2):
+        for _ in range(max(2, self.R) if args.at_batch == "step" else 2):
             o = []
             for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
                 d_def = torch.empty(self.rows + 64, dtype=torch.int16, device=dev)
@@ -565,44 +580,71 @@ class AlltypesWorkload:
                 self.out_bytes += 2 * self.rows + i.value_bytes[j] + (8 * (i.num_values[j] + 1) if pt == 6 else 0)
 
     def decode_rg(self, rgd, g, stream, oset=0):
-        """pqg_rg_decode of row group g: its 11 column chunks over the decoder's streams."""
+        """pqg_rg_decode of row group g: its 11 column chunks in one batched decode."""
         return rgd.decode_async(self.cols, self.d_blob.data_ptr() + self.base[g], self.info[g].blob_len,
                                 self.chunks[g], [o[3] for o in self.out[oset]], stream)
 
+    def decode_step(self, ctx, stream):
+        """Every column chunk of every row group of the share in one pqg_decode_chunks (row group
+        g into output set g)."""
+        cols, arrays, outs = [], [], []
+        for g in range(self.R):
+            for j, col in enumerate(self.cols):
+                cols.append(col)
+                arrays.append(self.shifted[g][j])
+                outs.append(self.out[g][j][3])
+        return ctx.decode_chunks_async(cols, self.d_blob.data_ptr(), self.blob_len, arrays, outs, stream)
 
-def alltypes_check(ctx, w, stream):
-    """Decode this rank's first row group and compare every column (levels, values, BYTE_ARRAY
-    offsets) with the generator's own cells (pqg_truth_alltypes)."""
+
+def alltypes_check(ctx, w, stream, batch_ctx=None):
+    """Decode this rank's row groups and compare every column (levels, values, BYTE_ARRAY
+    offsets) of the first and the last with the generator's own cells (pqg_truth_alltypes):
+    through the batched step when batch_ctx is given, else row group 0 through pqg_rg_decode."""
     import pqgtools
-    oa = w.decode_rg(ctx, 0, stream)
-    st, bcol, bad = ctx.sync()
-    assert st == 0, (st, bcol, bad, ctx.error_message())
-    for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
-        nv, nb = w.info[0].num_values[j], w.info[0].value_bytes[j]
-        assert oa[j].num_values == nv and oa[j].num_levels == w.rows, (name, oa[j].num_values, nv)
-        lv, vals, offs = pqgtools.alltypes_truth(w.row0s[0], w.rows, j, w.p_null, w.seed, nb)
-        d_def, d_val, d_off, _ = w.out[0][j]
-        assert np.array_equal(d_def[:w.rows].cpu().numpy(), lv), f"{name}: def levels differ"
-        assert np.array_equal(d_val[:nb].cpu().numpy(), vals), f"{name}: values differ"
-        if offs is not None:
-            assert np.array_equal(d_off[:nv + 1].cpu().numpy(), offs), f"{name}: offsets differ"
-    return {"row_groups_checked": 1, "columns": len(pqgtools.ALLTYPES), "status": st}
+    if batch_ctx is not None:
+        oa_all = w.decode_step(batch_ctx, stream)
+        st, call, chunk, bad = batch_ctx.sync_detail()
+        assert st == 0, (st, call, chunk, bad, batch_ctx.error_message())
+        groups = sorted({0, w.R - 1})
+    else:
+        oa_all = w.decode_rg(ctx, 0, stream)
+        st, bcol, bad = ctx.sync()
+        assert st == 0, (st, bcol, bad, ctx.error_message())
+        groups = [0]
+    nc = len(pqgtools.ALLTYPES)
+    for g in groups:
+        for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+            o = oa_all[g * nc + j] if batch_ctx is not None else oa_all[j]
+            nv, nb = w.info[g].num_values[j], w.info[g].value_bytes[j]
+            assert o.num_values == nv and o.num_levels == w.rows, (g, name, o.num_values, nv)
+            lv, vals, offs = pqgtools.alltypes_truth(w.row0s[g], w.rows, j, w.p_null, w.seed, nb)
+            d_def, d_val, d_off, _ = w.out[g][j]
+            assert np.array_equal(d_def[:w.rows].cpu().numpy(), lv), f"{name}: def levels differ"
+            assert np.array_equal(d_val[:nb].cpu().numpy(), vals), f"{name}: values differ"
+            if offs is not None:
+                assert np.array_equal(d_off[:nv + 1].cpu().numpy(), offs), f"{name}: offsets differ"
+    return {"row_groups_checked": len(groups), "columns": nc, "status": st,
+            "path": "pqg_decode_chunks (whole step)" if batch_ctx is not None else "pqg_rg_decode"}
 
 
-def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
-    """Every row group of the share per step. Row groups alternate between two launch streams
-    and two output sets, so row group g + 1's column chunks start while g's still run (each
-    column's decodes stay in order on its own stream inside the row-group decoder)."""
+def alltypes_steps(ctx, w, stream, steps, warmup, dist=None, batch_ctx=None):
+    """Every row group of the share per step: one batched decode of all their column chunks
+    (batch_ctx), or one row-group decode per row group alternating between two launch streams and
+    two output sets, so that row group g + 1's kernels start while g's still run."""
     import torch
     lanes = [stream, torch.cuda.Stream().cuda_stream]
 
     def one_pass():
+        if batch_ctx is not None:
+            w.decode_step(batch_ctx, stream)
+            return
         for g in range(w.R):
             w.decode_rg(ctx, g, lanes[g % 2], g % 2)
 
+    sync = (lambda: batch_ctx.sync_detail()) if batch_ctx is not None else (lambda: ctx.sync())
     for _ in range(warmup):
         one_pass()
-    ctx.sync()
+    sync()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -610,59 +652,86 @@ def alltypes_steps(ctx, w, stream, steps, warmup, dist=None):
     for _ in range(steps):
         one_pass()
     th = time.perf_counter()
-    st, bcol, bad = ctx.sync()
+    r = sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    assert st == 0, (st, bcol, bad, ctx.error_message())
+    assert r[0] == 0, r
     alltypes_steps.host_ms = (th - t0) / steps * 1e3  # enqueue time per step (host side)
+    # the enqueue alone: with the GPU idle, no wait for a staging slot is inside it
+    enq = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        one_pass()
+        enq.append(time.perf_counter() - te)
+        sync()
+    alltypes_steps.enqueue_ms = min(enq) * 1e3
     return (t1 - t0) / steps
 
 
-def alltypes_pcie(ctx, w, stream):
-    """Host-to-host rate: pinned page bytes of row group g + 1 go up (H2D stream) while row group g
-    decodes; its decoded columns come back (D2H stream) into two alternating pinned buffers."""
-    import torch
-    s_dec = torch.cuda.ExternalStream(stream)
-    s_up, s_dn = torch.cuda.Stream(), torch.cuda.Stream()
-    h_out = []
-    for k in range(2):
-        h_out.append([(torch.empty(d.numel(), dtype=d.dtype).pin_memory(),
-                       torch.empty(v.numel(), dtype=v.dtype).pin_memory(),
-                       torch.empty(o.numel(), dtype=o.dtype).pin_memory() if o is not None else None)
-                      for d, v, o, _ in w.out[k]])
-    up = [torch.cuda.Event() for _ in range(w.R)]
-    dec = [torch.cuda.Event() for _ in range(w.R)]
-    free = [torch.cuda.Event() for _ in range(2)]
-    torch.cuda.synchronize()
+def alltypes_file_pipeline(pqgpu, w, args, groups=6):
+    """PCIe-inclusive rate through the product API (pqg_rgr_*, csrc/host/rg_reader.cpp): `groups`
+    row groups of this workload written as an uncompressed parquet file, then read file -> pinned
+    staging (host threads) -> H2D -> batched decode -> D2H into pinned host buffers, two row groups
+    in flight. The file is in the page cache (just written): the rate excludes disk."""
+    import tempfile
+    import pqgtools
+    th = host_threads(args.threads)[0]
+    path = os.path.join(tempfile.gettempdir(), f"pqg_bench_alltypes_{os.getpid()}.parquet")
+    groups = min(groups, max(2, w.R))
     t0 = time.perf_counter()
-    with torch.cuda.stream(s_up):  # every row group's upload, in order, on its own stream
-        for g in range(w.R):
-            lo, hi = w.base[g], w.base[g] + w.info[g].blob_len
-            w.d_blob[lo:hi].copy_(w.h_blob[lo:hi], non_blocking=True)
-            up[g].record(s_up)
-    for g in range(w.R):
-        s_dec.wait_event(up[g])
-        if g >= 2:
-            s_dec.wait_event(free[g % 2])
-        w.decode_rg(ctx, g, stream, g % 2)
-        dec[g].record(s_dec)
-        with torch.cuda.stream(s_dn):
-            s_dn.wait_event(dec[g])
-            for (d, v, o, _), (hd, hv, ho) in zip(w.out[g % 2], h_out[g % 2]):
-                hd.copy_(d, non_blocking=True)
-                hv.copy_(v, non_blocking=True)
-                if o is not None:
-                    ho.copy_(o, non_blocking=True)
-            free[g % 2].record(s_dn)
-    st, bcol, bad = ctx.sync()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    assert st == 0, (st, bcol, bad)
-    return {"values_per_s": w.levels / dt, "ms": dt * 1e3, "pcie_bytes": w.in_bytes + w.out_bytes,
-            "note": "pinned H2D of row group g+1 overlapped with the decode of g and the D2H of its "
-                    "decoded columns (three streams), one pass over all row groups"}
+    pqgtools.write_alltypes_file(path, w.rows, groups, row0=w.row0s[0], p_null=w.p_null, seed=w.seed, codec=0,
+                                 threads=th)
+    write_s = time.perf_counter() - t0
+    res = {"row_groups": groups, "rows_per_group": w.rows, "file_bytes": os.path.getsize(path),
+           "write_seconds": round(write_s, 1), "host_threads": th}
+    try:
+        r = pqgpu.FileReader(path)
+        for host_output in (True, False):
+            rd = pqgpu.RowGroupReader(r, host_threads=th, host_output=host_output)
+            rd.submit(0)  # warm: buffers sized, pages faulted in
+            assert rd.wait()[0] == 0, rd.error()
+            s0 = rd.stats()
+            t0 = time.perf_counter()
+            nxt = 0
+            for _ in range(min(2, groups)):
+                rd.submit(nxt)
+                nxt += 1
+            for g in range(groups):
+                st, rg, col, page = rd.wait()
+                assert st == 0 and rg == g, (st, rg, col, page, rd.error())
+                if nxt < groups:
+                    rd.submit(nxt)
+                    nxt += 1
+            dt = time.perf_counter() - t0
+            s1 = rd.stats()
+            if host_output:  # the last row group's columns against the generator's cells
+                g = groups - 1
+                for j, (name, pt) in enumerate(pqgtools.ALLTYPES):
+                    out = rd.host_arrays(j, pt)
+                    nb = out["num_bytes"] if pt == 6 else out["values"].nbytes
+                    lv, vals, offs = pqgtools.alltypes_truth(w.row0s[0] + g * w.rows, w.rows, j, w.p_null, w.seed,
+                                                             max(nb, 1))
+                    assert np.array_equal(out["def_levels"], lv), name
+                    assert out["values"].tobytes() == vals[:nb].tobytes(), name
+            key = "to_host" if host_output else "to_device"
+            fb = s1["file_bytes"] - s0["file_bytes"]
+            ob = s1["output_bytes"] - s0["output_bytes"]
+            res[key] = {"values_per_s": groups * w.rows * len(w.cols) / dt, "ms": dt * 1e3,
+                        "ms_per_row_group": dt * 1e3 / groups,
+                        "file_gbps": fb / dt / 1e9, "output_gbps": ob / dt / 1e9,
+                        "host_ms_per_row_group": (s1["host_ms"] - s0["host_ms"]) / groups,
+                        "checked": host_output}
+            rd.close()
+        r.close()
+    finally:
+        os.unlink(path)
+    res["note"] = ("pqg_rgr: headers + page fill into pinned staging on host threads, async H2D, one "
+                   "pqg_decode_chunks per row group, async D2H (to_host) into pinned buffers; row group "
+                   "g+1 staged while g decodes")
+    return res
 
 
 def alltypes_cpu_baseline(w, threads, thr_info):
@@ -702,8 +771,11 @@ def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
     import torch
     w = AlltypesWorkload(pqgpu, args, rank, world)
     ctx = pqgpu.RowGroupDecoder(torch.cuda.current_device(), args.streams)
-    checked = alltypes_check(ctx, w, stream)
-    per_step = max_over_ranks(alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist), dist)
+    bctx = pqgpu.Context(torch.cuda.current_device()) if args.at_batch == "step" else None
+    checked = alltypes_check(ctx, w, stream, bctx)
+    if bctx is not None:
+        checked["row_group_path"] = alltypes_check(ctx, w, stream)  # the row-group decoder too
+    per_step = max_over_ranks(alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist, bctx), dist)
     step_bytes = w.in_bytes + w.out_bytes
     achieved = step_bytes / per_step / 1e9
     res = {
@@ -716,21 +788,27 @@ def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
                    "rows_per_gpu": w.R * w.rows, "cells_per_gpu": w.levels, "p_null": w.p_null,
                    "in_bytes_per_gpu": w.in_bytes, "out_bytes_per_gpu": w.out_bytes,
                    "chunk_decodes_per_step": w.R * len(w.cols), "gen_seconds": round(w.gen_s, 1),
-                   "streams": args.streams, "parallelism": f"row-group partitions x{world}, no collective"},
+                   "decode_calls_per_step": 1 if bctx is not None else w.R,
+                   "batch": "pqg_decode_chunks of every chunk of the step" if bctx is not None
+                            else "pqg_rg_decode per row group, two streams",
+                   "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": "whole step (every chunk decode)", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": step_bytes, "avg_ms": per_step * 1e3,
                      "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
         "value_check": checked,
-        "host_enqueue_ms_per_step": getattr(alltypes_steps, "host_ms", None),
+        "host_enqueue_ms_per_step": getattr(alltypes_steps, "enqueue_ms", None),
+        "host_ms_per_step_in_loop": getattr(alltypes_steps, "host_ms", None),
     }
     if extras and rank == 0 and world == 1:
         if args.pcie:
-            res["pcie_inclusive"] = alltypes_pcie(ctx, w, stream)
+            res["pcie_inclusive"] = alltypes_file_pipeline(pqgpu, w, args)
         if args.cpu_baseline:
             th, info = host_threads(args.threads)
             res["cpu_baseline"] = alltypes_cpu_baseline(w, th, info)
     ctx.close()
+    if bctx is not None:
+        bctx.close()
     del w
     torch.cuda.empty_cache()
     return res

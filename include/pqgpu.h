@@ -236,6 +236,51 @@ int pqg_column_reader_read_batch(pqg_column_reader *cr, size_t batch_size, int16
                                  int16_t *rep, void *values, uint64_t values_bytes_cap,
                                  uint32_t *lengths, size_t *values_read, size_t *levels_read);
 
+/* ---------------------------------------------------------------- file -> device row groups
+ * The product path of whole row groups, from the file to device (and host) memory, pipelined:
+ * page headers of every column parsed and the payloads copied or decompressed (SNAPPY, GZIP) by
+ * `host_threads` threads straight into pinned staging (SerializedPageReader::get_next_page,
+ * file/reader.rs:420-522, for all of a row group's chunks, file/reader.rs:252-260, 306-330), one
+ * async H2D copy, one batched decode of the row group's column chunks (pqg_decode_chunks), and
+ * with PQG_RGR_HOST_OUTPUT async D2H copies of every output into pinned host buffers.
+ * pqg_rgr_submit returns once the row group is staged and its copies and decode are enqueued; up
+ * to two row groups may be in flight, so submitting g + 1 before waiting for g overlaps g + 1's
+ * host work and H2D copy with g's decode. pqg_rgr_wait waits for the oldest row group in flight,
+ * returns its status (the first failure the reference would meet reading its columns in order:
+ * the lowest failing column, and in it the lowest failing page, be it a header / decompression
+ * failure or a decode failure) and makes its outputs current for pqg_rgr_column. Current outputs
+ * stay valid until the next pqg_rgr_wait. Staging, device blobs and outputs are kept across row
+ * groups (grown, never shrunk). The file reader must outlive the pqg_rgr. */
+typedef struct pqg_rgr pqg_rgr;
+#define PQG_RGR_HOST_OUTPUT 1
+typedef struct {
+  const int16_t *def_levels; /* device; NULL when the column has no such levels */
+  const int16_t *rep_levels;
+  const void *values;        /* dense non-null values (BYTE_ARRAY/FLBA: concatenated bytes) */
+  const int64_t *offsets;    /* BYTE_ARRAY/FLBA: num_values + 1 byte offsets */
+  const int16_t *host_def_levels; /* pinned host copies (PQG_RGR_HOST_OUTPUT), else NULL */
+  const int16_t *host_rep_levels;
+  const void *host_values;
+  const int64_t *host_offsets;
+  uint64_t num_levels, num_values, num_bytes;
+} pqg_rgr_output;
+typedef struct {
+  uint64_t row_groups;   /* submitted */
+  uint64_t file_bytes;   /* column chunk bytes read from the file (compressed) */
+  uint64_t staged_bytes; /* uncompressed page bytes copied H2D */
+  uint64_t output_bytes; /* levels, values and offsets of waited row groups */
+  double host_ms;        /* host time in submit: headers, copies / decompression, tables */
+} pqg_rgr_stats;
+int pqg_rgr_open(pqg_file_reader *r, int device, int host_threads, int flags, pqg_rgr **out);
+int pqg_rgr_close(pqg_rgr *g);
+int pqg_rgr_submit(pqg_rgr *g, int row_group);
+int pqg_rgr_wait(pqg_rgr *g, int *row_group, int *bad_column, int *bad_page);
+/* Outputs of column `col` of the current row group; returns the row group's status for a column at
+ * or after its failing column (whose outputs are then partial), PQG_OK otherwise. */
+int pqg_rgr_column(pqg_rgr *g, int col, pqg_rgr_output *out);
+int pqg_rgr_get_stats(pqg_rgr *g, pqg_rgr_stats *out);
+const char *pqg_rgr_error(pqg_rgr *g);
+
 /* Record assembly's leaf iterator: TypedTripletIter (record/triplet.rs:168-330) over a column
  * reader. read_next (triplet.rs:270-294) advances one (definition level, repetition level,
  * value) triplet, refilling `batch_size` levels at a time through read_batch and spacing the

@@ -207,6 +207,7 @@ struct BaDictEmit {
   uint32_t* len;
   uint64_t bytes;
   int32_t err;
+  bool index_only;  // the level path's chunks: the index in the length slot (BaSrc)
   __device__ void operator()(uint64_t g, const uint32_t* v, uint32_t mask) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -217,8 +218,12 @@ struct BaDictEmit {
         continue;
       }
       const uint32_t l = dlen[idx];
-      src[g + j] = dsrc[idx];
-      len[g + j] = l;
+      if (index_only) {
+        len[g + j] = idx;
+      } else {
+        src[g + j] = dsrc[idx];
+        len[g + j] = l;
+      }
       bytes += l;
     }
   }
@@ -234,7 +239,7 @@ __global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(64) void
   __shared__ WaveSmem sm;
   const uint32_t qi = 4u * tl[blockIdx.x >> 2] + (blockIdx.x & 3u);
   const QDesc d = load_qdesc(&rt.desc[qi]);
-  BaDictEmit em{dsrc, dlen, 0u, vsrc, vlen, 0, 0};
+  BaDictEmit em{dsrc, dlen, 0u, vsrc, vlen, 0, 0, false};
   if (d.qhi) {
     const ChunkWork& ck = chunks[pages[d.page].chunk];
     em.dsrc += ck.dscr_base;
@@ -289,7 +294,7 @@ __global__ void __launch_bounds__(WG) k_badict_fallback(const uint8_t* __restric
   if (st_s) return;
   const uint32_t wid = threadIdx.x >> 6;
   BaDictEmit em{dsrc + ck.dscr_base, dlen + ck.dscr_base, pages[ck.dict_page].num_values, vsrc + ck.scr_base,
-                vlen + ck.scr_base, 0, 0};
+                vlen + ck.scr_base, 0, 0, ck.lvdict != 0};
   for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
     const QDesc d = quarter_desc(blob, pages, chunks, tile_page, rt, SS_DICT, t, wid);
     if (d.qhi) wave_expand(blob, blob_len, d, rt.runs, wsm[wid], em);
@@ -434,25 +439,45 @@ __device__ inline bool ba_page_ok(const PageWork& pw, const ChunkWork& ck) {
          pw.encoding != E_DELTA_BYTE_ARRAY && ck.res.total_bytes <= ck.val_cap;
 }
 
+// Value k of a byte-array page (k: its index among the chunk's values): source address and length.
+// The dictionary pages of the level path's chunks (ChunkWork::lvdict) keep the value's dictionary
+// index in the length slot (4 bytes per value instead of 12): the entry comes from the chunk's
+// dictionary scratch (k_ba_dict_prep).
+struct BaSrc {
+  const uint64_t* vsrc;
+  const uint32_t* vlen;
+  const uint64_t* dsrc;
+  const uint32_t* dlen;
+  bool via_dict;
+  __device__ BaSrc(const ChunkWork& ck, const PageWork& pw, const uint64_t* vsrc0, const uint32_t* vlen0,
+                   const uint64_t* dsrc0, const uint32_t* dlen0)
+      : vsrc(vsrc0 + ck.scr_base), vlen(vlen0 + ck.scr_base), dsrc(dsrc0 + ck.dscr_base),
+        dlen(dlen0 + ck.dscr_base), via_dict(pw.encoding == E_RLE_DICTIONARY && ck.lvdict) {}
+  __device__ uint32_t len(uint64_t k) const { return via_dict ? dlen[vlen[k]] : vlen[k]; }
+  __device__ uint64_t src(uint64_t k) const { return via_dict ? dsrc[vlen[k]] : vsrc[k]; }
+};
+
 // Per listed tile (gt, global) of a byte-array page: the tile's byte count into tsum[gt] (the
 // offsets themselves are written once, by k_ba_copy, from the scanned tile starts).
 __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork* chunks,
                                                 const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
-                                                const uint32_t* __restrict__ vlen0, uint64_t* __restrict__ tsum) {
+                                                const uint64_t* vsrc0, const uint32_t* __restrict__ vlen0,
+                                                const uint64_t* dsrc0, const uint32_t* dlen0,
+                                                uint64_t* __restrict__ tsum) {
   __shared__ uint64_t red[WG / 64];
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pw, ck)) return;
   const uint32_t t = gt - pw.ltile0;
-  const uint32_t* vlen = vlen0 + ck.scr_base;
+  const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
   uint64_t s = 0;
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
     const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
-    s += i < n ? vlen[vo + i] : 0u;
+    s += i < n ? bs.len(vo + i) : 0u;
   }
   const uint64_t tot = block_sum_u64(s, red);
   if (threadIdx.x == 0) tsum[gt] = tot;
@@ -478,52 +503,77 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWor
   }
 }
 
-// Per page and tile: the values' byte offsets (tile start from k_ba_tscan + an in-tile scan of
-// the lengths, kept in LDS) written once to `offsets`, then the bytes: lanes take consecutive
-// values, so neighbouring lanes write neighbouring bytes.
+// Per listed tile of a byte-array page: the values' byte offsets (tile start from k_ba_tscan + an
+// in-tile scan of the lengths) and their bytes. Lengths come in coalesced (lanes on consecutive
+// values) into LDS, laid out with one pad word per 16 so that each thread's 16 consecutive values
+// are read without bank conflicts for its scan; the offsets go out coalesced from LDS; then lanes
+// take consecutive values for the copy, so neighbouring lanes write neighbouring bytes.
+__device__ inline uint32_t ba_pad(uint32_t j) { return j + (j >> 4); }
+
 __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
                                                 const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
                                                 const uint32_t* __restrict__ tl, const uint64_t* __restrict__ vsrc0,
-                                                const uint32_t* __restrict__ vlen0, const uint64_t* __restrict__ tsum) {
-  __shared__ DeltaSmem sm;
-  __shared__ uint64_t loff[BA_T];  // tile-relative byte offset of each value
+                                                const uint32_t* __restrict__ vlen0, const uint64_t* dsrc0,
+                                                const uint32_t* dlen0, const uint64_t* __restrict__ tsum) {
+  __shared__ uint32_t lens[BA_T + BA_T / 16];   // value lengths (padded layout)
+  __shared__ uint64_t loff[BA_T + BA_T / 16];   // tile-relative byte offset of each value (padded)
+  __shared__ uint64_t wsum[WG / 64];
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pw, ck)) return;
   const uint32_t t = gt - pw.ltile0;
-  const uint64_t* vsrc = vsrc0 + ck.scr_base;
-  const uint32_t* vlen = vlen0 + ck.scr_base;
+  const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
   int64_t* __restrict__ offsets = ck.off_out;
   uint8_t* __restrict__ out = ck.val_out;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
-  if ((uint64_t)t * BA_T >= n) return;
+  const uint64_t t0 = (uint64_t)t * BA_T;
+  if (t0 >= n) return;
+  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
   const uint64_t base = tsum[gt];
-  const uint64_t i0 = (uint64_t)t * BA_T + (uint64_t)threadIdx.x * BA_VPT;
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint32_t j = k * WG + tid;
+    lens[ba_pad(j)] = j < cnt ? bs.len(vo + t0 + j) : 0u;
+  }
+  __syncthreads();
   uint32_t l[BA_VPT];
   uint64_t s = 0;
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {
-    l[k] = i0 + k < n ? vlen[vo + i0 + k] : 0u;
+    l[k] = lens[tid * 17u + k];  // value tid * 16 + k
     s += l[k];
   }
-  uint64_t tot;
-  uint64_t pre = block_exscan(sm, s, tot);
+  // workgroup exclusive scan of the thread sums
+  uint64_t incl = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if ((tid & 63) >= (uint32_t)off) incl += y;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  __syncthreads();
+  uint64_t pre = incl - s;
+  for (uint32_t w = 0; w < (tid >> 6); ++w) pre += wsum[w];
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {
-    if (i0 + k < n) offsets[vo + i0 + k] = (int64_t)(base + pre);
-    loff[threadIdx.x * BA_VPT + k] = pre;
+    loff[tid * 17u + k] = pre;
     pre += l[k];
   }
   __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {  // offsets, coalesced
+    const uint32_t j = k * WG + tid;
+    if (j < cnt) offsets[vo + t0 + j] = (int64_t)(base + loff[ba_pad(j)]);
+  }
 #pragma unroll 1
   for (uint32_t k = 0; k < BA_VPT; ++k) {
-    const uint32_t j = k * WG + threadIdx.x;
-    const uint64_t i = (uint64_t)t * BA_T + j;
-    if (i >= n) break;
-    const uint64_t d = base + loff[j];
-    const uint32_t ln = vlen[vo + i];
-    const uint8_t* sp = blob + vsrc[vo + i];
+    const uint32_t j = k * WG + tid;
+    if (j >= cnt) break;
+    const uint64_t d = base + loff[ba_pad(j)];
+    const uint32_t ln = lens[ba_pad(j)];
+    const uint8_t* sp = blob + bs.src(vo + t0 + j);
     uint8_t* o = out + d;
     uint32_t q = 0;
     for (; q + 8 <= ln; q += 8) {
@@ -617,13 +667,16 @@ hipError_t pqg_launch_badict_general(const uint8_t* blob, uint64_t blob_len, Pag
 // of the byte-array pages) and the DELTA_BYTE_ARRAY rebuild.
 hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                             const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, uint64_t* vsrc,
-                            uint32_t* vlen, uint32_t* vpre, uint64_t* tsum, hipStream_t s) {
+                            uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* tsum,
+                            hipStream_t s) {
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
   if (ntl) {
-    hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vlen, tsum);
+    hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
+                       tsum);
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
-    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, vsrc, vlen, tsum);
+    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
+                       tsum);
   }
   if (has_dba)
     hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, chunks, vsrc, vlen, vpre);

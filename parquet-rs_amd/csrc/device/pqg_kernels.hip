@@ -435,28 +435,27 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, ChunkWork* 
 
 // ------------------------------------------------------------------------------ PLAIN
 
-// Copies each page's `nonnull * es` value bytes to its chunk's values + value_out * es. grid.y =
-// page, grid.x strides 16-byte output chunks. Source alignment is arbitrary (the value section
-// follows the level streams): dword loads + v_alignbyte; the destination is chunked on 16-byte
-// boundaries of the output so stores are dwordx4 except at page edges.
-__global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ blob,
-                                                   uint64_t blob_len, PageWork* pages, ChunkWork* chunks) {
-  const int p = blockIdx.y;
+// PLAIN fixed-width values: grid.y over the listed pages (PLAIN pages of fixed-width chunks),
+// grid.x over 16-byte chunks of a page's output: the page's `nonnull * es` value bytes go to its
+// chunk's values + value_out * es. Source alignment is arbitrary (the value section follows the
+// level streams): dword loads + v_alignbyte; the destination is chunked on 16-byte boundaries of
+// the output so stores are dwordx4 except at page edges.
+__global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, ChunkWork* chunks,
+                                                   const uint32_t* __restrict__ pl) {
+  const uint32_t p = pl[blockIdx.y];
   const PageWork& pwr = pages[p];
   if (pwr.status != 0) return;
-  if (pwr.page_type != P_DATA && pwr.page_type != P_DATA_V2) return;
-  if (pwr.encoding != E_PLAIN) return;
   const ChunkWork& ck = chunks[pwr.chunk];
-  const int es = ck.es;
-  if (es <= 0 || ck.cp.physical_type == T_BOOLEAN || !ck.val_out) return;
+  const uint64_t es = (uint64_t)ck.es;
   uint8_t* __restrict__ out = ck.val_out;
-  const uint64_t nbytes = pwr.nonnull * (uint64_t)es;
+  const uint64_t nbytes = pwr.nonnull * es;
   if (nbytes > pwr.val_bytes) {  // eof_err!("Not enough bytes to decode")
-    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, p, ST_EOF);
+    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, (int)p, ST_EOF);
     return;
   }
   const uint64_t src = pwr.base + pwr.val_off;
-  const uint64_t dst = pwr.value_out * (uint64_t)es;
+  const uint64_t dst = pwr.value_out * es;
   const uint64_t dend = dst + nbytes;
   const uint64_t c0 = dst & ~15ull;
   for (uint64_t c = c0 + ((uint64_t)blockIdx.x * WG + threadIdx.x) * 16ull; c < dend;
@@ -491,29 +490,46 @@ __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ b
   }
 }
 
-// PLAIN booleans: LSB-first bits from the value section, one byte (0/1) per value.
-__global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ blob,
-                                                   PageWork* pages, ChunkWork* chunks) {
-  const int p = blockIdx.y;
+// PLAIN booleans (decoding.rs:188-204 via BitReader::get_batch::<bool>): LSB-first bits of the
+// value section, one byte (0/1) per value, one workgroup per listed tile; every 16-byte chunk of
+// the output (aligned on the chunk's buffer) from the 16 bits at its values' bit offset.
+__global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                   PageWork* pages, ChunkWork* chunks,
+                                                   const uint32_t* __restrict__ tile_page,
+                                                   const uint32_t* __restrict__ tl) {
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork& pw = pages[p];
   if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_PLAIN) return;
   const ChunkWork& ck = chunks[pw.chunk];
-  if (ck.cp.physical_type != T_BOOLEAN || !ck.val_out) return;
   uint8_t* __restrict__ out = ck.val_out;
   const uint64_t n = pw.nonnull;
   if ((n + 7) / 8 > pw.val_bytes && n > (uint64_t)pw.val_bytes * 8) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, p, ST_EOF);
+    if (threadIdx.x == 0 && gt == pw.ltile0) report(pages, chunks, (int)p, ST_EOF);
     return;
   }
-  const uint8_t* src = blob + pw.base + pw.val_off;
-  for (uint64_t k = (uint64_t)blockIdx.x * WG + threadIdx.x; k * 8 < n;
-       k += (uint64_t)gridDim.x * WG) {
-    uint32_t byte = src[k];
-    for (int j = 0; j < 8; ++j) {
-      uint64_t i = k * 8 + j;
-      if (i < n) out[pw.value_out + i] = (byte >> j) & 1u;
+  const uint64_t v0 = (uint64_t)(gt - pw.ltile0) * RUN_TILE;
+  if (v0 >= n) return;
+  const uint64_t v1 = v0 + RUN_TILE < n ? v0 + RUN_TILE : n;
+  const uint64_t src = pw.base + pw.val_off;
+  const uint64_t dst = pw.value_out;
+  const uint64_t lo_b = dst + v0, hi_b = dst + v1;
+  for (uint64_t c = (lo_b & ~15ull) + (uint64_t)threadIdx.x * 16ull; c < hi_b; c += (uint64_t)WG * 16ull) {
+    const uint64_t lo = c < lo_b ? lo_b : c;
+    const uint64_t hi = (c + 16 < hi_b) ? c + 16 : hi_b;
+    if (lo == c && hi == c + 16) {
+      const uint64_t vi = c - dst;  // value (bit) index of the chunk's first output
+      const uint64_t a = src + (vi >> 3);
+      const uint32_t x = (gbyte(blob, blob_len, a) | (gbyte(blob, blob_len, a + 1) << 8) |
+                          (gbyte(blob, blob_len, a + 2) << 16)) >> (vi & 7u);
+      uint32_t d[4];
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t) d[t] = (((x >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
+      *reinterpret_cast<uint4*>(out + c) = make_uint4(d[0], d[1], d[2], d[3]);
+    } else {
+      for (uint64_t b = lo; b < hi; ++b) {
+        const uint64_t vi = b - dst;
+        out[b] = (uint8_t)((blob[src + (vi >> 3)] >> (vi & 7u)) & 1u);
+      }
     }
   }
 }
@@ -604,19 +620,18 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
   return hipGetLastError();
 }
 
-hipError_t pqg_launch_plain_copy(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                                 ChunkWork* chunks, uint64_t max_page_bytes, hipStream_t s) {
-  uint64_t nch = (max_page_bytes + 16 * WG - 1) / (16 * WG) + 1;
-  if (nch > 4096) nch = 4096;
-  hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)nch, npages), dim3(WG), 0, s, blob, blob_len, pages, chunks);
-  return hipGetLastError();
-}
-
-hipError_t pqg_launch_plain_bool(const uint8_t* blob, PageWork* pages, int npages, ChunkWork* chunks,
-                                 uint64_t max_page_values, hipStream_t s) {
-  uint64_t nch = (max_page_values + 8 * WG - 1) / (8 * WG) + 1;
-  if (nch > 4096) nch = 4096;
-  hipLaunchKernelGGL(k_plain_bool, dim3((unsigned)nch, npages), dim3(WG), 0, s, blob, pages, chunks);
+// PLAIN values: fixed-width over the listed pages (pl, npl; max_bytes: the largest of them) and
+// booleans over the listed tiles (tlb, ntlb).
+hipError_t pqg_launch_plain(const uint8_t* blob, uint64_t blob_len, PageWork* pages, ChunkWork* chunks,
+                            const uint32_t* tile_page, const uint32_t* pl, uint32_t npl, uint64_t max_bytes,
+                            const uint32_t* tlb, uint32_t ntlb, hipStream_t s) {
+  if (npl) {
+    uint64_t nch = (max_bytes + 16 * WG - 1) / (16 * WG) + 1;
+    if (nch > 4096) nch = 4096;
+    hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)nch, npl), dim3(WG), 0, s, blob, blob_len, pages, chunks, pl);
+  }
+  if (ntlb)
+    hipLaunchKernelGGL(k_plain_bool, dim3(ntlb), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tlb);
   return hipGetLastError();
 }
 

@@ -1540,15 +1540,17 @@ __device__ inline uint8_t* lv_out(const ChunkWork& ck, int sel) {
   return sel == SS_DEF ? (uint8_t*)ck.def_out : sel == SS_REP ? (uint8_t*)ck.rep_out : ck.val_out;
 }
 
-// Outputs of one window from its run list, and the def count.
+// Max level of stream `sel` (the def count's test, column/reader.rs:212-226).
+__device__ inline uint32_t lv_maxl(const ChunkWork& ck, int sel) {
+  return sel == SS_DEF ? (uint32_t)ck.cp.max_def : sel == SS_REP ? (uint32_t)ck.cp.max_rep : 1u;
+}
+
+// Outputs of one window from its run list (into out, the page's chunk buffer), and the def count.
 template <int OUT>
 __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                 uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo, int sel,
-                                const ChunkWork* chunks, PageWork* pages) {
-  const ChunkWork& ck = chunks[pages[x.p].chunk];
-  uint8_t* __restrict__ out = lv_out(ck, sel);
+                                uint32_t maxl, PageWork* pages, uint8_t* __restrict__ out) {
   const bool count = sel == SS_DEF;
-  const uint32_t maxl = sel == SS_DEF ? (uint32_t)ck.cp.max_def : (uint32_t)ck.cp.max_rep;
   uint32_t cnt = x.s.w == 1 ? lv_write1<OUT>(rl, stage, blob, blob_len, x, base, endo, out)
                             : lv_write_wide<OUT>(rl, stage, blob, blob_len, x, base, endo, maxl, count, out);
   if (count) {
@@ -1596,6 +1598,30 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
       full[u] = ohi - olo == V;
       for (uint32_t sp = lgn; sp; sp >>= 1)
         if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
+      const uint32_t st0 = rl.rstart[a], inf0 = rl.rinfo[a];
+      if (full[u] && rl.rstart[a + 1] >= ohi) {
+        // the group inside one run: one index, or V consecutive fields of one 8-byte read
+        // (V * w + 7 <= 39 bits: w <= 8 on this path)
+        uint64_t bits;
+        uint32_t sh;
+        if (inf0 & R_RLE) {
+          bits = inf0 & 0x7FFFFFFFu;
+          sh = 0;
+        } else {
+          const uint64_t bit = (uint64_t)inf0 * 8ull + (uint64_t)(olo - st0) * w;
+          bits = lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u);
+          sh = w;
+        }
+        const uint32_t m = (inf0 & R_RLE) ? 0x7FFFFFFFu : wm;
+#pragma unroll
+        for (uint32_t j = 0; j < V; ++j) {
+          const uint32_t idx = (uint32_t)(bits >> (j * sh)) & m;
+          id[u][j] = idx < ndict ? idx : 0u;  // (out of the dictionary: the page fails, ST_PANIC)
+          bad |= idx >= ndict ? 1u : 0u;
+        }
+        msk[u] = (1u << V) - 1u;
+        continue;
+      }
       uint32_t b = a;
 #pragma unroll
       for (uint32_t j = 0; j < V; ++j) {
@@ -1656,31 +1682,39 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
   return bad;
 }
 
-// What the walked-page emit writes: levels / booleans, or dictionary values.
+// What the walked-page emit writes: levels / booleans, or dictionary values. page() takes the
+// per-page state (the chunk's buffer and parameters) when the emit moves to another page, so
+// that a window's writes start without a dependent load.
 template <int OUT>
 struct LvLevelOut {
   static constexpr bool PIPE = true;  // k_lv_emit_walk prefetches the next window (registers to spare)
+  uint8_t* out;
+  uint32_t maxl;
+  __device__ void page(const ChunkWork& ck, const PageWork*, const uint8_t*, int sel) {
+    out = lv_out(ck, sel);
+    maxl = lv_maxl(ck, sel);
+  }
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
-                             const LvWin& x, uint32_t base, uint32_t endo, int sel, const ChunkWork* chunks,
+                             const LvWin& x, uint32_t base, uint32_t endo, int sel, const ChunkWork*,
                              PageWork* pages) const {
-    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, chunks, pages);
+    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, maxl, pages, out);
   }
 };
 
 // BYTE_ARRAY / FLBA dictionary indices (decoding.rs:256-315 over the entries k_ba_dict_prep
-// decoded): per output the entry's source address and length (the byte-array scan and copy,
-// pqg_bytes.hip, take it from there), and the page's byte total. Scratch slots: the chunk's
-// scr_base (values) and dscr_base (dictionary entries) on.
+// decoded): per output the entry's index, in the value-length slot (the byte-array scan and copy,
+// pqg_bytes.hip BaSrc, take the entry's address and length from there), and the page's byte total.
+// Scratch slots: the chunk's scr_base (values) and dscr_base (dictionary entries) on.
 __device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                                        const LvWin& x, uint32_t base, uint32_t endo, const ChunkWork& ck,
                                        PageWork* pages, ChunkWork* chunks, const uint64_t* __restrict__ dsrc0,
                                        const uint32_t* __restrict__ dlen0, uint64_t* __restrict__ vsrc0,
                                        uint32_t* __restrict__ vlen0) {
   {
-    const uint64_t* dsrc = dsrc0 + ck.dscr_base;
     const uint32_t* dlen = dlen0 + ck.dscr_base;
-    uint64_t* vsrc = vsrc0 + ck.scr_base;
     uint32_t* vlen = vlen0 + ck.scr_base;
+    (void)dsrc0;
+    (void)vsrc0;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t ndict = pages[ck.dict_page].num_values;
     const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
@@ -1713,20 +1747,14 @@ __device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, 
         if (idx >= ndict) bad = 1;  // dict[idx] out of bounds: the reference panics
         else id[u] = idx;
       }
-      uint64_t sv[U];
       uint32_t lv[U];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
-        if (id[u] != 0xFFFFFFFFu) {
-          sv[u] = dsrc[id[u]];
-          lv[u] = dlen[id[u]];
-        }
+        if (id[u] != 0xFFFFFFFFu) lv[u] = dlen[id[u]];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
         if (id[u] != 0xFFFFFFFFu) {
-          const uint64_t g = go + ob + u * WAVE;
-          vsrc[g] = sv[u];
-          vlen[g] = lv[u];
+          vlen[go + ob + u * WAVE] = id[u];  // the index (BaSrc in pqg_bytes.hip takes the entry)
           bytes += lv[u];
         }
     }
@@ -1746,23 +1774,33 @@ struct LvDictOut {
   const uint32_t* dlen;
   uint64_t* vsrc;
   uint32_t* vlen;
+  const ChunkWork* ck;  // the current page's chunk, value size, buffer and dictionary (page())
+  uint8_t* val_out;
+  const uint8_t* dict;
+  uint32_t ndict;
+  int es;
+  __device__ void page(const ChunkWork& c, const PageWork* pages, const uint8_t* blob, int) {
+    ck = &c;
+    es = c.es;
+    val_out = c.val_out;
+    const PageWork& dp = pages[c.dict_page];
+    dict = blob + dp.base;
+    ndict = dp.num_values;
+  }
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                              const LvWin& x, uint32_t base, uint32_t endo, int, const ChunkWork* chunks,
                              PageWork* pages) const {
-    const ChunkWork& ck = chunks[pages[x.p].chunk];
-    if (ck.es == 0) {
-      lv_write_badict(rl, stage, blob, blob_len, x, base, endo, ck, pages, const_cast<ChunkWork*>(chunks), dsrc, dlen,
+    if (es == 0) {
+      lv_write_badict(rl, stage, blob, blob_len, x, base, endo, *ck, pages, const_cast<ChunkWork*>(chunks), dsrc, dlen,
                       vsrc, vlen);
       return;
     }
-    const PageWork& dp = pages[ck.dict_page];
+    const uint64_t da = (uint64_t)(dict - blob);
     uint32_t bad;
-    if (ck.es == 8)
-      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base, dp.num_values,
-                             (dp.base % 8) == 0, ck.val_out);
+    if (es == 8)
+      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 8) == 0, val_out);
     else
-      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, blob + dp.base, dp.num_values,
-                             (dp.base % 4) == 0, ck.val_out);
+      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 4) == 0, val_out);
     if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)x.p, ST_PANIC);
   }
 };
@@ -1874,8 +1912,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (endo <= base || R == 0) continue;
+    const ChunkWork& ck = chunks[pw.chunk];
     lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
-                  chunks, pages);
+                  lv_maxl(ck, sel), pages, lv_out(ck, sel));
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
@@ -1972,6 +2011,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   LvWin x;
   x.p = p;
   bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
+  if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel);
   LeLoad nf;  // the next window's loads, issued while the current one is written
   nf.ok = false;
   uint32_t nb0 = 0, nb1 = 0, nbk = 0;  // run bounds (wfirst) of window nbk of the page, read ahead
@@ -1983,6 +2023,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       pend = lt.wbase[p + 1];
       x.p = p;
       walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
+      if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel);
       nf.ok = false;
       nbv = false;
     }

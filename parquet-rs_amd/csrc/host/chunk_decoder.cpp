@@ -37,8 +37,8 @@ hipError_t pqg_launch_lv(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, i
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
                            const uint32_t* const*, const uint32_t*, const uint32_t*, uint32_t, RunTables, hipStream_t,
                            hipEvent_t*);
-hipError_t pqg_launch_plain_copy(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint64_t, hipStream_t);
-hipError_t pqg_launch_plain_bool(const uint8_t*, PageWork*, int, ChunkWork*, uint64_t, hipStream_t);
+hipError_t pqg_launch_plain(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, const uint32_t*, uint32_t,
+                            uint64_t, const uint32_t*, uint32_t, hipStream_t);
 hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
                                uint32_t, RunTables, LevelTables, hipStream_t);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint32_t, const uint32_t*,
@@ -51,7 +51,8 @@ hipError_t pqg_launch_badict_general(const uint8_t*, uint64_t, PageWork*, int, C
                                      const uint32_t*, uint32_t, RunTables, uint64_t*, uint32_t*, uint64_t*, uint32_t*,
                                      int, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
-                            uint32_t, bool, uint64_t*, uint32_t*, uint32_t*, uint64_t*, hipStream_t);
+                            uint32_t, bool, uint64_t*, uint32_t*, uint32_t*, const uint64_t*, const uint32_t*, uint64_t*,
+                            hipStream_t);
 }
 
 // Stream kinds of the hybrid-stream tables: def, rep, dictionary indices, RLE booleans.
@@ -60,8 +61,9 @@ constexpr int SS_DICT = 2;  // device/pqg_runs.hpp StreamSel: dictionary indices
 
 // Tile lists the kernels over one kind of page take (host-built, uploaded with the page table):
 // general-path dictionary tiles by value size (1, 4, 8, 12) and all of them, byte-array
-// dictionary tiles off the level path, byte-array copy tiles, RLE boolean tiles.
-enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_N };
+// dictionary tiles off the level path, byte-array copy tiles, RLE boolean tiles, PLAIN
+// fixed-width pages (a page list) and PLAIN boolean tiles.
+enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_N };
 
 // What the host knows of one chunk of a decode until its results are delivered.
 struct ChunkHost {
@@ -479,7 +481,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   std::vector<uint32_t> tl[TL_N];
   std::vector<PageWork> pw(np);
   uint32_t total_tiles = 0;
-  uint64_t nwin = 0, max_page_bytes = 0, max_page_vals = 0, scr = 0, dscr = 0;
+  uint64_t nwin = 0, plain_max = 0, scr = 0, dscr = 0;
   uint32_t def_w = 0, rep_w = 0;  // bit masks of the level streams' widths
   bool any_def = false, any_rep = false, any_plain = false, any_pbool = false, any_ba = false, any_dba = false;
   bool any_badict = false, ba_lv = false, any_rbool = false, fixed_gen = false;
@@ -562,8 +564,6 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
         total_tiles += w.ntiles;
         lev += w.num_values;
         if (w.encoding >= 0 && w.encoding < 16) enc[w.encoding] = true;
-        if (w.nbytes > max_page_bytes) max_page_bytes = w.nbytes;
-        if (w.num_values > max_page_vals) max_page_vals = w.num_values;
         nwin += (w.nbytes + LV_WIN - 1) / LV_WIN;
       }
       if (vst && (int)i == bad) w.status = vst;
@@ -607,8 +607,19 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
         }
       } else {
         if (enc[PQG_PLAIN]) {
-          if (t == PQG_BOOLEAN) any_pbool = true;
-          else any_plain = true;
+          if (t == PQG_BOOLEAN) {
+            any_pbool = true;
+            list_tiles(TL_PBOOL, PQG_PLAIN);
+          } else if (es > 0) {
+            any_plain = true;
+            for (uint32_t i = 0; i < n; ++i) {
+              const PageWork& w = pw[p0 + i];
+              if (w.ntiles && w.encoding == PQG_PLAIN) {
+                tl[TL_PLAIN].push_back(p0 + i);
+                if (w.nbytes > plain_max) plain_max = w.nbytes;
+              }
+            }
+          }
         }
         if (enc[PQG_RLE_DICTIONARY]) {
           if ((es == 4 || es == 8) && dict_page >= 0 && ndict <= (1u << cp.dict_maxw)) {
@@ -862,17 +873,18 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     if (any_ba) {
       if (!ctx->values_kernel) ctx->values_kernel = any_dba ? PQG_DELTA_BYTE_ARRAY : PQG_PLAIN;
       HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba,
-                              sl.vsrc, sl.vlen, sl.vpre, sl.tsum, s),
+                              sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, s),
              "byte arrays");
     }
-    if (any_plain) {
-      ctx->values_kernel = PQG_PLAIN;
-      if (ctx->timing) hipEventRecord(ev[8], s);
-      HIPCHK(pqg_launch_plain_copy(b, blob_len, d_pages, ni, d_chunks, max_page_bytes, s), "plain");
-      if (ctx->timing) hipEventRecord(ev[9], s);
-      sl.kv = ctx->timing;
+    if (any_plain || any_pbool) {
+      if (any_plain) ctx->values_kernel = PQG_PLAIN;
+      if (ctx->timing && any_plain) hipEventRecord(ev[8], s);
+      HIPCHK(pqg_launch_plain(b, blob_len, d_pages, d_chunks, sl.tile_page, tlp[TL_PLAIN], ntl[TL_PLAIN], plain_max,
+                              tlp[TL_PBOOL], ntl[TL_PBOOL], s),
+             "plain");
+      if (ctx->timing && any_plain) hipEventRecord(ev[9], s);
+      sl.kv = ctx->timing && any_plain;
     }
-    if (any_pbool) HIPCHK(pqg_launch_plain_bool(b, d_pages, ni, d_chunks, max_page_vals, s), "plain bool");
     if (delta_es) {
       ctx->values_kernel = PQG_DELTA_BINARY_PACKED;
       HIPCHK(pqg_launch_delta_tiled(b, blob_len, d_pages, ni, d_chunks, total_tiles, sl.tile_page, sl.dt, delta_es, s,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <map>
 #include <memory>
@@ -20,24 +21,9 @@
 #include <vector>
 
 #include "file_reader.hpp"
+#include "staging.hpp"
 
 using namespace pqg;
-
-struct ChunkPages {
-  std::vector<uint8_t> blob;
-  std::vector<pqg_page> pages;
-  int status = 0;
-  std::string err;
-};
-
-struct pqg_file_reader {
-  std::vector<uint8_t> owned;
-  const uint8_t* data = nullptr;
-  uint64_t len = 0;
-  FileMeta meta;
-  std::string err;
-  std::map<std::pair<int, int>, std::unique_ptr<ChunkPages>> chunks;
-};
 
 struct pqg_column_reader {
   pqg_column col{};
@@ -53,6 +39,25 @@ struct pqg_column_reader {
   uint64_t bad_level = ~0ull;  // first level index of the failing page
   std::string err;
 };
+
+struct ColumnStaging {
+  int device = -1;
+  hipStream_t s = nullptr;
+  Buf h_blob, d_blob, d_def, d_rep, d_val, d_off, h_def, h_rep, h_val, h_off;
+  ColumnStaging() { h_blob.host = h_def.host = h_rep.host = h_val.host = h_off.host = true; }
+  ~ColumnStaging() {
+    if (s) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
+    for (Buf* b : {&h_blob, &d_blob, &d_def, &d_rep, &d_val, &d_off, &h_def, &h_rep, &h_val, &h_off}) b->release();
+  }
+};
+
+pqg_file_reader::~pqg_file_reader() {
+  delete staging;
+  if (map) munmap(map, map_len);
+}
 
 static int value_size(int t, int tl) {
   switch (t) {
@@ -105,15 +110,28 @@ int pqg_file_open(const char* path, pqg_file_reader** out) {
     *out = r;
     return PQG_ERR_GENERAL;
   }
-  std::vector<uint8_t> buf;
-  uint8_t tmp[1 << 16];
-  size_t n;
-  while ((n = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
-  fclose(f);
   pqg_file_reader* r = new pqg_file_reader();
-  r->owned.swap(buf);
-  r->data = r->owned.data();
-  r->len = r->owned.size();
+  // mapped, not read: a row group's pages are then read from the page cache by the threads that
+  // fill the pinned staging (pqg_rgr_*), and a large file costs no copy at open
+  fseek(f, 0, SEEK_END);
+  const long sz = ftell(f);
+  if (sz > 0) {
+    void* m = mmap(nullptr, (size_t)sz, PROT_READ, MAP_PRIVATE, fileno(f), 0);
+    if (m != MAP_FAILED) {
+      r->map = m;
+      r->map_len = (size_t)sz;
+      r->data = (const uint8_t*)m;
+      r->len = (uint64_t)sz;
+    }
+  }
+  if (!r->map && sz > 0) {  // not mappable: read it
+    fseek(f, 0, SEEK_SET);
+    r->owned.resize((size_t)sz);
+    r->owned.resize(fread(r->owned.data(), 1, (size_t)sz, f));
+    r->data = r->owned.data();
+    r->len = r->owned.size();
+  }
+  fclose(f);
   int st = parse_file_metadata(r->data, r->len, r->meta, r->err);
   *out = r;
   return st;
@@ -167,7 +185,9 @@ int pqg_chunk_blob(pqg_file_reader* r, int rg, int col, const uint8_t** blob, ui
   return PQG_OK;
 }
 
-// Decodes the whole chunk on the ctx's device, then keeps the decoded streams on the host.
+// Decodes the whole chunk on the ctx's device, then keeps the decoded streams on the host. The
+// page bytes go through the file's pinned staging (async H2D), the outputs come back into pinned
+// buffers (async D2H) on the staging stream; device and pinned buffers are reused chunk after chunk.
 int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
                            pqg_column_reader** out) {
   if (!valid_chunk(r, rg, col) || !ctx || !out) return PQG_ERR_INVALID;
@@ -191,72 +211,87 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
     if (p.page_type == PQG_PAGE_DATA || p.page_type == PQG_PAGE_DATA_V2) cr->total_levels += p.num_values;
   }
   const uint64_t n = cr->total_levels;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (!r->staging || r->staging->device != dev) {
+    delete r->staging;
+    r->staging = new ColumnStaging();
+    r->staging->device = dev;
+    if (hipStreamCreateWithFlags(&r->staging->s, hipStreamNonBlocking) != hipSuccess) {
+      r->err = "hipStreamCreate failed";
+      return PQG_ERR_HIP;
+    }
+  }
+  ColumnStaging& S = *r->staging;
   // BYTE_ARRAY output bytes are bounded by the page bytes except for DELTA_BYTE_ARRAY prefix
   // sharing and dictionary repeats; the decode reports the exact size on CAPACITY, so retry once.
   uint64_t vcap = cr->is_ba && l.physical_type == PQG_BYTE_ARRAY ? c->blob.size() + 64
                                                                  : (uint64_t)cr->es * n + 64;
+  const size_t blen = c->blob.size();
+  bool ok = S.h_blob.need(blen + 64) == hipSuccess && S.d_blob.need(blen + 64) == hipSuccess &&
+            S.d_def.need(n * 2 + 64) == hipSuccess && S.d_rep.need(n * 2 + 64) == hipSuccess &&
+            S.h_def.need(n * 2 + 64) == hipSuccess && S.h_rep.need(n * 2 + 64) == hipSuccess &&
+            (!cr->is_ba || (S.d_off.need((n + 1) * 8 + 64) == hipSuccess && S.h_off.need((n + 1) * 8 + 64) == hipSuccess));
+  if (ok) {
+    memcpy(S.h_blob.p, c->blob.data(), blen);
+    ok = hipMemcpyAsync(S.d_blob.p, S.h_blob.p, blen, hipMemcpyHostToDevice, S.s) == hipSuccess;
+  }
+  if (!ok) {
+    r->err = "HIP allocation/copy failed";
+    return PQG_ERR_HIP;
+  }
   int st = PQG_OK, bad = -1;
   std::string msg;
+  pqg_output o{};
   for (int attempt = 0; attempt < 2; ++attempt) {
-    void *d_blob = nullptr, *d_def = nullptr, *d_rep = nullptr, *d_val = nullptr, *d_off = nullptr;
-    auto cleanup = [&]() {
-      hipFree(d_blob);
-      hipFree(d_def);
-      hipFree(d_rep);
-      hipFree(d_val);
-      hipFree(d_off);
-    };
-    bool ok = hipMalloc(&d_blob, c->blob.size() + 64) == hipSuccess &&
-              hipMemcpy(d_blob, c->blob.data(), c->blob.size(), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMalloc(&d_def, n * 2 + 64) == hipSuccess && hipMalloc(&d_rep, n * 2 + 64) == hipSuccess &&
-              hipMalloc(&d_val, vcap) == hipSuccess &&
-              (!cr->is_ba || hipMalloc(&d_off, (n + 1) * 8 + 64) == hipSuccess);
-    if (!ok) {
-      cleanup();
-      r->err = "HIP allocation/copy failed";
+    if (S.d_val.need(vcap) != hipSuccess) {
+      r->err = "HIP allocation failed";
       return PQG_ERR_HIP;
     }
-    pqg_output o{};
-    o.def_levels = l.max_def > 0 ? (int16_t*)d_def : nullptr;
-    o.rep_levels = l.max_rep > 0 ? (int16_t*)d_rep : nullptr;
-    o.values = d_val;
+    o = pqg_output{};
+    o.def_levels = l.max_def > 0 ? (int16_t*)S.d_def.p : nullptr;
+    o.rep_levels = l.max_rep > 0 ? (int16_t*)S.d_rep.p : nullptr;
+    o.values = S.d_val.p;
     o.values_capacity = vcap;
-    o.offsets = (int64_t*)d_off;
+    o.offsets = cr->is_ba ? (int64_t*)S.d_off.p : nullptr;
     o.offsets_capacity = cr->is_ba ? n + 1 : 0;
-    st = pqg_decode_chunk(ctx, &cr->col, (const uint8_t*)d_blob, c->blob.size(), c->pages.data(),
-                          (uint32_t)c->pages.size(), &o, nullptr);
+    st = pqg_decode_chunk(ctx, &cr->col, (const uint8_t*)S.d_blob.p, blen, c->pages.data(),
+                          (uint32_t)c->pages.size(), &o, S.s);
     if (st == PQG_OK) st = pqg_sync(ctx, &bad);
     msg = pqg_error_message(ctx);
     if (st == PQG_ERR_CAPACITY && attempt == 0 && o.num_bytes > vcap) {
       vcap = o.num_bytes + 64;
-      cleanup();
       continue;
     }
-    if (st == PQG_ERR_HIP || st == PQG_ERR_INVALID) {
-      cleanup();
-      r->err = msg;
-      return st;
-    }
-    cr->total_values = o.num_values;
-    cr->def.resize(n);
-    cr->rep.resize(n);
-    uint64_t vb = cr->is_ba ? o.num_bytes : o.num_values * (uint64_t)cr->es;
-    if (vb > vcap) vb = vcap;
-    cr->values.resize(vb);
-    ok = true;
-    if (l.max_def > 0 && n) ok &= hipMemcpy(cr->def.data(), d_def, n * 2, hipMemcpyDeviceToHost) == hipSuccess;
-    if (l.max_rep > 0 && n) ok &= hipMemcpy(cr->rep.data(), d_rep, n * 2, hipMemcpyDeviceToHost) == hipSuccess;
-    if (vb) ok &= hipMemcpy(cr->values.data(), d_val, vb, hipMemcpyDeviceToHost) == hipSuccess;
-    if (cr->is_ba) {
-      cr->offsets.resize(o.num_values + 1);
-      ok &= hipMemcpy(cr->offsets.data(), d_off, (o.num_values + 1) * 8, hipMemcpyDeviceToHost) == hipSuccess;
-    }
-    cleanup();
-    if (!ok) {
-      r->err = "HIP copy failed";
-      return PQG_ERR_HIP;
-    }
     break;
+  }
+  if (st == PQG_ERR_HIP || st == PQG_ERR_INVALID) {
+    r->err = msg;
+    return st;
+  }
+  cr->total_values = o.num_values;
+  uint64_t vb = cr->is_ba ? o.num_bytes : o.num_values * (uint64_t)cr->es;
+  if (vb > vcap) vb = vcap;
+  const uint64_t noff = cr->is_ba ? o.num_values + 1 : 0;
+  ok = S.h_val.need(vb + 64) == hipSuccess;
+  if (ok && l.max_def > 0 && n) ok = hipMemcpyAsync(S.h_def.p, S.d_def.p, n * 2, hipMemcpyDeviceToHost, S.s) == hipSuccess;
+  if (ok && l.max_rep > 0 && n) ok = hipMemcpyAsync(S.h_rep.p, S.d_rep.p, n * 2, hipMemcpyDeviceToHost, S.s) == hipSuccess;
+  if (ok && vb) ok = hipMemcpyAsync(S.h_val.p, S.d_val.p, vb, hipMemcpyDeviceToHost, S.s) == hipSuccess;
+  if (ok && noff) ok = hipMemcpyAsync(S.h_off.p, S.d_off.p, noff * 8, hipMemcpyDeviceToHost, S.s) == hipSuccess;
+  if (ok) ok = hipStreamSynchronize(S.s) == hipSuccess;
+  if (!ok) {
+    r->err = "HIP copy failed";
+    return PQG_ERR_HIP;
+  }
+  cr->def.resize(n);
+  cr->rep.resize(n);
+  if (l.max_def > 0 && n) memcpy(cr->def.data(), S.h_def.p, n * 2);
+  if (l.max_rep > 0 && n) memcpy(cr->rep.data(), S.h_rep.p, n * 2);
+  cr->values.resize(vb);
+  if (vb) memcpy(cr->values.data(), S.h_val.p, vb);
+  if (noff) {
+    cr->offsets.resize(noff);
+    memcpy(cr->offsets.data(), S.h_off.p, noff * 8);
   }
   cr->status = st;
   cr->err = msg;

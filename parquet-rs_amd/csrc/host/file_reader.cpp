@@ -449,7 +449,15 @@ static int snappy_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64
         err = "snappy: bad copy";
         return PQG_ERR_GENERAL;
       }
-      for (uint64_t k = 0; k < len; ++k) out[op + k] = out[op - off + k];  // may overlap
+      if (off >= len) {
+        memcpy(out + op, out + op - off, len);
+      } else if (off >= 8) {  // overlapping: 8-byte steps never read bytes not yet written
+        uint64_t k = 0;
+        for (; k + 8 <= len; k += 8) memcpy(out + op + k, out + op - off + k, 8);
+        for (; k < len; ++k) out[op + k] = out[op - off + k];
+      } else {
+        for (uint64_t k = 0; k < len; ++k) out[op + k] = out[op - off + k];  // a short repeat
+      }
       op += len;
     }
   }
@@ -497,8 +505,8 @@ int decompress(int codec, const uint8_t* in, uint64_t in_len, uint8_t* out, uint
   return PQG_OK;
 }
 
-int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMeta& cc,
-                     std::vector<uint8_t>& blob, std::vector<pqg_page>& pages, std::string& err) {
+int plan_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMeta& cc,
+                     std::vector<PagePlan>& plan, uint64_t& blob_len, std::string& err) {
   // get_column_page_reader, file/reader.rs:314-330
   int64_t start = cc.has_dict_offset ? cc.dictionary_page_offset : cc.data_page_offset;
   int64_t len = cc.total_compressed_size;
@@ -507,7 +515,7 @@ int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
     return PQG_ERR_EOF;
   }
   const uint8_t* p = file + start;
-  uint64_t avail = (uint64_t)len, pos = 0;
+  uint64_t avail = (uint64_t)len, pos = 0, at = 0;
   int64_t seen = 0;
   // SerializedPageReader::get_next_page, file/reader.rs:420-522
   while (seen < cc.num_values) {
@@ -533,22 +541,16 @@ int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
       err = "failed to fill whole buffer";  // read_exact
       return PQG_ERR_EOF;
     }
-    const uint8_t* src = p + pos;
+    PagePlan pp;
+    pp.src = p + pos;
+    pp.prefix = offset;
+    pp.clen = clen;
+    pp.decompress = cc.codec != 0 && can_decompress;
     pos += offset + clen;
-    // 64-byte aligned payload in the blob
-    uint64_t at = (blob.size() + 63) & ~63ull;
-    uint64_t out_len = (cc.codec != 0 && can_decompress) ? offset + ulen : offset + clen;
-    blob.resize(at + out_len);
-    memcpy(blob.data() + at, src, offset);
-    if (cc.codec != 0 && can_decompress) {
-      st = decompress(cc.codec, src + offset, clen, blob.data() + at + offset, ulen, err);
-      if (st) return st;
-    } else {
-      memcpy(blob.data() + at + offset, src + offset, clen);
-    }
-    pqg_page pg;
+    const uint64_t out_len = pp.decompress ? offset + ulen : offset + clen;
+    pqg_page& pg = pp.page;
     memset(&pg, 0, sizeof(pg));
-    pg.offset = at;
+    pg.offset = at;  // 64-byte aligned payload in the chunk's blob
     pg.nbytes = (uint32_t)out_len;
     if (h.type == PQG_PAGE_DICTIONARY && h.has_dict) {
       pg.page_type = PQG_PAGE_DICTIONARY;
@@ -572,12 +574,36 @@ int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
       err = "page header without its page-type header";  // assert! in the reference
       return PQG_ERR_PANIC;
     } else {
-      blob.resize(at);  // unknown page type (INDEX_PAGE): skipped (file/reader.rs:512-515)
-      continue;
+      continue;  // unknown page type (INDEX_PAGE): skipped (file/reader.rs:512-515)
     }
-    pages.push_back(pg);
+    plan.push_back(pp);
+    at = (at + out_len + 63) & ~63ull;
   }
-  blob.resize(blob.size() + 64, 0);  // tail slack
+  blob_len = at + 64;  // tail slack
+  return PQG_OK;
+}
+
+int fill_page(const PagePlan& pp, int codec, uint8_t* chunk_blob, std::string& err) {
+  uint8_t* dst = chunk_blob + pp.page.offset;
+  memcpy(dst, pp.src, pp.prefix);  // v2 levels are never compressed
+  if (pp.decompress)
+    return decompress(codec, pp.src + pp.prefix, pp.clen, dst + pp.prefix, pp.page.nbytes - pp.prefix, err);
+  memcpy(dst + pp.prefix, pp.src + pp.prefix, pp.clen);
+  return PQG_OK;
+}
+
+int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMeta& cc,
+                     std::vector<uint8_t>& blob, std::vector<pqg_page>& pages, std::string& err) {
+  std::vector<PagePlan> plan;
+  uint64_t len = 0;
+  int st = plan_chunk_pages(file, file_len, cc, plan, len, err);
+  if (st) return st;
+  blob.assign(len, 0);
+  for (const PagePlan& pp : plan) {
+    st = fill_page(pp, cc.codec, blob.data(), err);
+    if (st) return st;
+    pages.push_back(pp.page);
+  }
   return PQG_OK;
 }
 

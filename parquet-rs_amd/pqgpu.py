@@ -57,6 +57,20 @@ class Timings(C.Structure):
                 ("levels_kernel_ms", C.c_float), ("values_kernel_ms", C.c_float)]
 
 
+class RgrOutput(C.Structure):
+    _fields_ = [("def_levels", C.c_void_p), ("rep_levels", C.c_void_p), ("values", C.c_void_p),
+                ("offsets", C.c_void_p), ("host_def_levels", C.c_void_p), ("host_rep_levels", C.c_void_p),
+                ("host_values", C.c_void_p), ("host_offsets", C.c_void_p), ("num_levels", C.c_uint64),
+                ("num_values", C.c_uint64), ("num_bytes", C.c_uint64)]
+
+
+class RgrStats(C.Structure):
+    _fields_ = [("row_groups", C.c_uint64), ("file_bytes", C.c_uint64), ("staged_bytes", C.c_uint64),
+                ("output_bytes", C.c_uint64), ("host_ms", C.c_double)]
+
+
+RGR_HOST_OUTPUT = 1
+
 EXPORTS = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_decode_chunks",
     "pqg_sync", "pqg_sync_detail",
@@ -68,7 +82,8 @@ EXPORTS = [
     "pqg_triplet_iter_read_next", "pqg_triplet_iter_has_next", "pqg_triplet_iter_def_level",
     "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
     "pqg_space_values", "pqg_rg_ctx_create", "pqg_rg_ctx_destroy", "pqg_rg_decode", "pqg_rg_sync",
-    "pqg_rg_sync_call", "pqg_rg_error_message",
+    "pqg_rg_sync_call", "pqg_rg_error_message", "pqg_rgr_open", "pqg_rgr_close", "pqg_rgr_submit",
+    "pqg_rgr_wait", "pqg_rgr_column", "pqg_rgr_get_stats", "pqg_rgr_error",
 ]
 
 _lib = None
@@ -134,6 +149,14 @@ def lib():
         L.pqg_rg_sync_call.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.pqg_rg_error_message.argtypes = [vp]
         L.pqg_rg_error_message.restype = C.c_char_p
+        L.pqg_rgr_open.argtypes = [vp, i32, i32, i32, C.POINTER(vp)]
+        L.pqg_rgr_close.argtypes = [vp]
+        L.pqg_rgr_submit.argtypes = [vp, i32]
+        L.pqg_rgr_wait.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.pqg_rgr_column.argtypes = [vp, i32, C.POINTER(RgrOutput)]
+        L.pqg_rgr_get_stats.argtypes = [vp, C.POINTER(RgrStats)]
+        L.pqg_rgr_error.argtypes = [vp]
+        L.pqg_rgr_error.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -423,6 +446,80 @@ class FileReader:
 
     def column_reader(self, rg, j, ctx):
         return ColumnReader(self, rg, j, ctx)
+
+
+class RowGroupReader:
+    """pqg_rgr_*: whole row groups from a FileReader to device memory (and, with host_output, to
+    pinned host memory), pipelined: submit(g + 1) before wait() overlaps g + 1's page reading,
+    decompression and H2D copy with g's decode (file/reader.rs:252-260, 306-330, 420-522)."""
+
+    def __init__(self, reader, device=0, host_threads=8, host_output=True):
+        self.reader = reader  # keeps the file open while the pqg_rgr lives
+        self.h = C.c_void_p()
+        st = lib().pqg_rgr_open(reader.h, device, host_threads, RGR_HOST_OUTPUT if host_output else 0,
+                                C.byref(self.h))
+        if st:
+            raise PqgError(st, "pqg_rgr_open failed")
+        self.host_output = host_output
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pqg_rgr_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self):
+        return lib().pqg_rgr_error(self.h).decode(errors="replace")
+
+    def submit(self, rg):
+        st = lib().pqg_rgr_submit(self.h, rg)
+        if st:
+            raise PqgError(st, self.error())
+
+    def wait(self):
+        """(status, row group, bad column, bad page) of the oldest row group in flight."""
+        rg, col, page = C.c_int(), C.c_int(), C.c_int()
+        st = lib().pqg_rgr_wait(self.h, C.byref(rg), C.byref(col), C.byref(page))
+        if st == INVALID or st == HIP:
+            raise PqgError(st, self.error())
+        return st, rg.value, col.value, page.value
+
+    def column(self, j):
+        """(status, RgrOutput) of column j of the current (last waited) row group."""
+        o = RgrOutput()
+        st = lib().pqg_rgr_column(self.h, j, C.byref(o))
+        return st, o
+
+    def host_arrays(self, j, ptype):
+        """Column j's host outputs as numpy arrays: {levels, values, offsets} (copies)."""
+        import numpy as np
+        st, o = self.column(j)
+        res = {"status": st, "num_levels": o.num_levels, "num_values": o.num_values, "num_bytes": o.num_bytes}
+
+        def arr(ptr, n, dt):
+            if not ptr or n == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(n,)).copy()
+        res["def_levels"] = arr(o.host_def_levels, o.num_levels, np.int16) if o.host_def_levels else None
+        res["rep_levels"] = arr(o.host_rep_levels, o.num_levels, np.int16) if o.host_rep_levels else None
+        if ptype in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY):
+            res["offsets"] = arr(o.host_offsets, o.num_values + 1, np.int64)
+            res["values"] = arr(o.host_values, o.num_bytes, np.uint8)
+        else:
+            nb = o.num_values * VALUE_SIZE[ptype]
+            res["values"] = arr(o.host_values, nb, np.uint8)
+        return res
+
+    def stats(self):
+        s = RgrStats()
+        lib().pqg_rgr_get_stats(self.h, C.byref(s))
+        return {k: getattr(s, k) for k, _ in RgrStats._fields_}
 
 
 class ColumnReader:

@@ -74,6 +74,11 @@ void pqg_alltypes_free(void *handle);
 /* Raw content of column `col` over rows [row0, row0 + rows): levels (0/1), the non-null values'
  * bytes (PLAIN form; BYTE_ARRAY: the bytes alone, with int64 offsets[values + 1]). Returns the
  * non-null count. Any output pointer may be NULL. */
+/* Row groups [row0 / rows_per_group, ...) of the alltypes workload written as a parquet file
+ * (row group g = pqg_gen_alltypes(rows_per_group, row0 + g * rows_per_group, ...)); codec 0 none,
+ * 1 SNAPPY, 2 GZIP. Returns PQG_OK or a PQG_ERR_* status. */
+int pqg_write_alltypes_file(const char *path, uint64_t rows_per_group, uint32_t row_groups, uint64_t row0,
+                            double p_null, uint64_t seed, int codec, int threads);
 uint64_t pqg_truth_alltypes(uint64_t row0, uint64_t rows, int col, double p_null, uint64_t seed,
                             int16_t *levels, uint8_t *values, int64_t *offsets);
 

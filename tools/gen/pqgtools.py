@@ -11,7 +11,8 @@ LIB_PATH = os.path.join(_HERE, "libpqgtools.so")
 EXPORTS = ["pqg_encode_rle", "pqg_encode_levels_v1", "pqg_encode_delta", "pqg_encode_dict_indices",
            "pqg_gen_levels_plain", "pqg_gen_dict_int64", "pqg_gen_delta_int64",
            "pqg_truth_levels_plain", "pqg_truth_dict_int64", "pqg_truth_delta_int64",
-           "pqg_gen_alltypes", "pqg_alltypes_copy", "pqg_alltypes_free", "pqg_truth_alltypes"]
+           "pqg_gen_alltypes", "pqg_alltypes_copy", "pqg_alltypes_free", "pqg_truth_alltypes",
+           "pqg_write_alltypes_file"]
 
 # alltypes_plain schema (data/alltypes_plain.parquet): 11 OPTIONAL leaves, physical types
 ALLTYPES = [("id", 1), ("bool_col", 0), ("tinyint_col", 1), ("smallint_col", 1), ("int_col", 1),
@@ -72,6 +73,7 @@ def lib():
         L.pqg_alltypes_free.argtypes = [vp]
         L.pqg_truth_alltypes.restype = u64
         L.pqg_truth_alltypes.argtypes = [u64, u64, i32, C.c_double, u64, vp, vp, vp]
+        L.pqg_write_alltypes_file.argtypes = [C.c_char_p, u64, u32, u64, C.c_double, u64, i32, i32]
         _lib = L
     return _lib
 
@@ -109,3 +111,12 @@ def alltypes_truth(row0, rows, col, p_null, seed, value_bytes):
     nv = L.pqg_truth_alltypes(row0, rows, col, p_null, seed, lv.ctypes.data, vals.ctypes.data,
                               offs.ctypes.data if ba else None)
     return lv, vals[:value_bytes], (offs[:nv + 1] if ba else None)
+
+
+def write_alltypes_file(path, rows_per_group, row_groups, row0=0, p_null=0.0, seed=0x5EED0005, codec=0,
+                        threads=16):
+    """The alltypes workload's row groups as a parquet file (codec 0 none, 1 SNAPPY, 2 GZIP)."""
+    st = lib().pqg_write_alltypes_file(os.fsencode(path), rows_per_group, row_groups, row0, p_null, seed,
+                                       codec, threads)
+    if st:
+        raise RuntimeError("pqg_write_alltypes_file failed: %d" % st)
