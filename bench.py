@@ -73,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--at-batch", default="step", choices=["step", "rg"],
                     help="alltypes: one pqg_decode_chunks over every chunk of the step (step) or one "
                          "pqg_rg_decode per row group on two alternating streams (rg)")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")
     return ap.parse_args(argv)
@@ -723,6 +725,9 @@ def alltypes_file_pipeline(pqgpu, w, args, groups=6):
                         "ms_per_row_group": dt * 1e3 / groups,
                         "file_gbps": fb / dt / 1e9, "output_gbps": ob / dt / 1e9,
                         "host_ms_per_row_group": (s1["host_ms"] - s0["host_ms"]) / groups,
+                        "per_row_group_ms": {k: round((s1[k] - s0[k]) / groups, 3)
+                                             for k in ("plan_ms", "fill_ms", "enqueue_ms", "sync_ms",
+                                                       "d2h_wait_ms")},
                         "checked": host_output}
             rd.close()
         r.close()
@@ -772,6 +777,8 @@ def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
     w = AlltypesWorkload(pqgpu, args, rank, world)
     ctx = pqgpu.RowGroupDecoder(torch.cuda.current_device(), args.streams)
     bctx = pqgpu.Context(torch.cuda.current_device()) if args.at_batch == "step" else None
+    if bctx is not None:
+        bctx.set_overlap(args.overlap)
     checked = alltypes_check(ctx, w, stream, bctx)
     if bctx is not None:
         checked["row_group_path"] = alltypes_check(ctx, w, stream)  # the row-group decoder too
@@ -844,6 +851,7 @@ def main(argv=None):
     sub = {}
     kinds = ["levels", "dict", "delta", "alltypes"] if args.config == "all" else [args.config]
     ctx = pqgpu.Context(torch.cuda.current_device())
+    ctx.set_overlap(args.overlap)
     short_steps = max(5, args.steps // 2)
     for kind in kinds:
         if kind == "alltypes":

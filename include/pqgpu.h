@@ -135,6 +135,12 @@ typedef struct {
 int pqg_ctx_create(int device, pqg_ctx **out);
 int pqg_ctx_destroy(pqg_ctx *ctx);
 int pqg_ctx_set_timing(pqg_ctx *ctx, int enabled);
+/* PLAIN fixed-width values of chunks read with def levels, whose data pages are all PLAIN: copied
+ * on a side stream while the def levels decode, at the offsets the value sections' sizes give
+ * (a page's value section holds exactly its non-null values in every file the reference writes);
+ * the value-offset scan checks every such page and the chunks where a count or offset differs are
+ * copied again at the true offsets. enabled = 0 copies after the levels only. Default 1. */
+int pqg_ctx_set_overlap(pqg_ctx *ctx, int enabled);
 
 /* Enqueue the decode of one column chunk on `stream` (asynchronous). `blob` is a device
  * buffer of `blob_len` bytes holding every page payload; `pages` is host memory (copied
@@ -270,6 +276,11 @@ typedef struct {
   uint64_t staged_bytes; /* uncompressed page bytes copied H2D */
   uint64_t output_bytes; /* levels, values and offsets of waited row groups */
   double host_ms;        /* host time in submit: headers, copies / decompression, tables */
+  double plan_ms;        /*   of which page headers */
+  double fill_ms;        /*   of which page copies / decompression (the thread pool) */
+  double enqueue_ms;     /* submit: H2D, decode and D2H enqueue */
+  double sync_ms;        /* wait: for the decode */
+  double d2h_wait_ms;    /* wait: for the D2H copies (PQG_RGR_HOST_OUTPUT) */
 } pqg_rgr_stats;
 int pqg_rgr_open(pqg_file_reader *r, int device, int host_threads, int flags, pqg_rgr **out);
 int pqg_rgr_close(pqg_rgr *g);

@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(WG) k_scan_bytes(PageWork* pages, ChunkWork* c
         if (incl > excl && incl > ck.val_cap && pages[p].status == 0) report(pages, chunks, p, ST_CAPACITY);
         if ((uint32_t)p == ck.first_page + ck.npages - 1u) {
           ck.res.total_bytes = incl;
-          if (ck.off_out) ck.off_out[ck.res.total_values] = (int64_t)incl;
+          if (ck.off_out) gp(ck.off_out)[ck.res.total_values] = (int64_t)incl;
         }
       });
 }
@@ -504,28 +504,57 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWor
 }
 
 // Per listed tile of a byte-array page: the values' byte offsets (tile start from k_ba_tscan + an
-// in-tile scan of the lengths) and their bytes. Lengths come in coalesced (lanes on consecutive
-// values) into LDS, laid out with one pad word per 16 so that each thread's 16 consecutive values
-// are read without bank conflicts for its scan; the offsets go out coalesced from LDS; then lanes
-// take consecutive values for the copy, so neighbouring lanes write neighbouring bytes.
+// in-tile scan of the lengths) and their bytes.
+//  - lengths come in coalesced (lanes on consecutive values) into LDS, laid out with one pad word
+//    per 16 so that each thread's 16 consecutive values are read without bank conflicts for its
+//    scan; their tile-relative offsets replace them in place (32-bit: a tile's bytes come from
+//    one page, < 4 GiB); the offsets go out coalesced from LDS;
+//  - values of at most BA_SMALL bytes (the common case: short strings) are staged: per round of
+//    BA_RN values, each thread loads its BA_RV consecutive values (16 bytes each, all loads in
+//    flight together, no store between them to wait for) and writes their bytes into an LDS image
+//    of the round's output, aligned as the output is; the workgroup then stores the image with
+//    16-byte stores (byte stores at the round's two ends only);
+//  - longer values are copied value by value, 8 bytes at a time.
 __device__ inline uint32_t ba_pad(uint32_t j) { return j + (j >> 4); }
 
-__global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
+constexpr uint32_t BA_RV = 4;                     // values per thread per staged round
+constexpr uint32_t BA_RN = BA_RV * WG;            // values per round
+constexpr uint32_t BA_SMALL = 16;                 // longest value the staged rounds take
+constexpr uint32_t BA_IMG = BA_RN * BA_SMALL + 16; // bytes of a round's output image
+
+__device__ inline void ba_load16(const uint8_t* __restrict__ blob, uint64_t blob_len, uint64_t a, uint32_t ln,
+                                 uint64_t& x0, uint64_t& x1) {
+  x0 = x1 = 0;
+  if (ln == 0) return;
+  if (a + 16 <= blob_len) {
+    __builtin_memcpy(&x0, blob + a, 8);
+    __builtin_memcpy(&x1, blob + a + 8, 8);
+  } else {
+    for (uint32_t q = 0; q < ln && a + q < blob_len; ++q) {
+      const uint64_t b = blob[a + q];
+      if (q < 8) x0 |= b << (8 * q);
+      else x1 |= b << (8 * (q - 8));
+    }
+  }
+}
+
+__global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
                                                 const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
                                                 const uint32_t* __restrict__ tl, const uint64_t* __restrict__ vsrc0,
                                                 const uint32_t* __restrict__ vlen0, const uint64_t* dsrc0,
                                                 const uint32_t* dlen0, const uint64_t* __restrict__ tsum) {
-  __shared__ uint32_t lens[BA_T + BA_T / 16];   // value lengths (padded layout)
-  __shared__ uint64_t loff[BA_T + BA_T / 16];   // tile-relative byte offset of each value (padded)
+  __shared__ uint32_t loff[BA_T + BA_T / 16 + 1];  // lengths, then tile-relative offsets (padded)
+  __shared__ __attribute__((aligned(16))) uint8_t img[BA_IMG];
   __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint32_t wmax[WG / 64];
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pw, ck)) return;
   const uint32_t t = gt - pw.ltile0;
   const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
-  int64_t* __restrict__ offsets = ck.off_out;
-  uint8_t* __restrict__ out = ck.val_out;
+  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   const uint64_t t0 = (uint64_t)t * BA_T;
   if (t0 >= n) return;
@@ -535,53 +564,122 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {
     const uint32_t j = k * WG + tid;
-    lens[ba_pad(j)] = j < cnt ? bs.len(vo + t0 + j) : 0u;
+    loff[ba_pad(j)] = j < cnt ? bs.len(vo + t0 + j) : 0u;
   }
   __syncthreads();
   uint32_t l[BA_VPT];
   uint64_t s = 0;
+  uint32_t mx = 0;
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {
-    l[k] = lens[tid * 17u + k];  // value tid * 16 + k
+    l[k] = loff[tid * 17u + k];  // value tid * 16 + k
     s += l[k];
+    mx = l[k] > mx ? l[k] : mx;
   }
-  // workgroup exclusive scan of the thread sums
+  // workgroup exclusive scan of the thread sums, and the longest value
   uint64_t incl = s;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const uint64_t y = __shfl_up(incl, off, 64);
     if ((tid & 63) >= (uint32_t)off) incl += y;
   }
-  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
-  __syncthreads();
-  uint64_t pre = incl - s;
-  for (uint32_t w = 0; w < (tid >> 6); ++w) pre += wsum[w];
 #pragma unroll
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    loff[tid * 17u + k] = pre;
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)mx, off, 64);
+    mx = y > mx ? y : mx;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+  __syncthreads();
+  uint64_t pre = incl - s, total = 0;
+  uint32_t maxlen = 0;
+  for (uint32_t w = 0; w < WG / 64; ++w) {
+    if (w < (tid >> 6)) pre += wsum[w];
+    total += wsum[w];
+    maxlen = wmax[w] > maxlen ? wmax[w] : maxlen;
+  }
+  if (total >> 32) {  // (a tile of > 4 GiB: offsets from registers, values copied one by one)
+    uint64_t d = pre;
+#pragma unroll 1
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      const uint32_t j = tid * BA_VPT + k;
+      if (j >= cnt) break;
+      offsets[vo + t0 + j] = (int64_t)(base + d);
+      const uint8_t* sp = blob + bs.src(vo + t0 + j);
+      for (uint64_t q = 0; q < l[k]; ++q) out[base + d + q] = sp[q];
+      d += l[k];
+    }
+    return;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {  // lengths -> offsets, in place (each thread its own)
+    loff[tid * 17u + k] = (uint32_t)pre;
     pre += l[k];
   }
+  if (tid == WG - 1) loff[ba_pad(BA_T)] = (uint32_t)total;
   __syncthreads();
 #pragma unroll
   for (uint32_t k = 0; k < BA_VPT; ++k) {  // offsets, coalesced
     const uint32_t j = k * WG + tid;
     if (j < cnt) offsets[vo + t0 + j] = (int64_t)(base + loff[ba_pad(j)]);
   }
+  if (maxlen > BA_SMALL) {  // long values: value by value, lanes on consecutive values
 #pragma unroll 1
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    const uint32_t j = k * WG + tid;
-    if (j >= cnt) break;
-    const uint64_t d = base + loff[ba_pad(j)];
-    const uint32_t ln = lens[ba_pad(j)];
-    const uint8_t* sp = blob + bs.src(vo + t0 + j);
-    uint8_t* o = out + d;
-    uint32_t q = 0;
-    for (; q + 8 <= ln; q += 8) {
-      uint64_t x;
-      __builtin_memcpy(&x, sp + q, 8);
-      __builtin_memcpy(o + q, &x, 8);
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      const uint32_t j = k * WG + tid;
+      if (j >= cnt) break;
+      const uint32_t d0 = loff[ba_pad(j)], ln = loff[ba_pad(j + 1)] - d0;
+      const uint8_t* sp = blob + bs.src(vo + t0 + j);
+      gptr<uint8_t> o = out + base + d0;
+      uint32_t q = 0;
+      for (; q + 8 <= ln; q += 8) {
+        uint64_t x;
+        __builtin_memcpy(&x, sp + q, 8);
+        __builtin_memcpy(o + q, &x, 8);
+      }
+      for (; q < ln; ++q) o[q] = sp[q];
     }
-    for (; q < ln; ++q) o[q] = sp[q];
+    return;
+  }
+#pragma unroll 1
+  for (uint32_t r0 = 0; r0 < cnt; r0 += BA_RN) {
+    const uint32_t r1 = r0 + BA_RN < cnt ? r0 + BA_RN : cnt;
+    const uint32_t R0 = loff[ba_pad(r0)], R1 = loff[ba_pad(r1)];
+    const uint64_t gA = base + R0, gB = base + R1;  // the round's output bytes
+    const uint32_t sh = (uint32_t)(gA & 15u);        // image byte i = output byte gA - sh + i
+    uint64_t x[BA_RV][2];
+    uint32_t dd[BA_RV], ln[BA_RV];
+#pragma unroll
+    for (uint32_t i = 0; i < BA_RV; ++i) {  // loads of the thread's values, all in flight
+      const uint32_t j = r0 + tid * BA_RV + i;
+      ln[i] = 0;
+      dd[i] = 0;
+      if (j < r1) {
+        dd[i] = loff[ba_pad(j)];
+        ln[i] = loff[ba_pad(j + 1)] - dd[i];
+        ba_load16(blob, blob_len, bs.src(vo + t0 + j), ln[i], x[i][0], x[i][1]);
+      } else {
+        x[i][0] = x[i][1] = 0;
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < BA_RV; ++i) {  // their bytes into the image
+      const uint32_t b0 = dd[i] - R0 + sh;
+      for (uint32_t q = 0; q < ln[i]; ++q)
+        img[b0 + q] = (uint8_t)((q < 8 ? x[i][0] >> (8 * q) : x[i][1] >> (8 * (q - 8))) & 0xFFu);
+    }
+    __syncthreads();
+    const uint64_t c0 = gA & ~15ull;
+    for (uint64_t c = c0 + (uint64_t)tid * 16u; c < gB; c += (uint64_t)WG * 16u) {
+      const uint32_t ii = (uint32_t)(c - c0);
+      if (c >= gA && c + 16 <= gB) {
+        gst16(out + c, *reinterpret_cast<const uint4*>(img + ii));
+      } else {
+        for (uint32_t q = 0; q < 16; ++q)
+          if (c + q >= gA && c + q < gB) out[c + q] = img[ii + q];
+      }
+    }
+    __syncthreads();  // (the next round's bytes reuse the image)
   }
 }
 
@@ -605,8 +703,8 @@ __global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blo
   const uint64_t* vsrc = vsrc0 + ck.scr_base;
   const uint32_t* vlen = vlen0 + ck.scr_base;
   const uint32_t* vpre = vpre0 + ck.scr_base;
-  int64_t* __restrict__ offsets = ck.off_out;
-  uint8_t* __restrict__ out = ck.val_out;
+  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
   const uint32_t lane = threadIdx.x;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   uint64_t d = pw.byte_out;
@@ -675,7 +773,8 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
     hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
                        tsum);
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
-    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
+    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vsrc, vlen,
+                       dsrc, dlen,
                        tsum);
   }
   if (has_dba)

@@ -476,7 +476,7 @@ __device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __r
   if (!delta_tile_front<ES>(sm, blob, blob_len, pages, chunks, tile_page, ntiles, dt, t, p, info, lo, hi, x, s))
     return;
   const PageWork& pw = pages[p];
-  uint8_t* __restrict__ out = chunks[pw.chunk].val_out;
+  const gptr<uint8_t> __restrict__ out = gp(chunks[pw.chunk].val_out);
   // ---- workgroup scan of the thread sums
   uint64_t incl = s;
 #pragma unroll
@@ -496,7 +496,7 @@ __device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __r
     val[j] = acc;
   }
   const uint32_t cnt = hi - lo;
-  uint8_t* const ob = out + (pw.value_out + lo) * (uint64_t)ES;
+  const gptr<uint8_t> ob = out + (pw.value_out + lo) * (uint64_t)ES;
   constexpr uint32_t HALF = DELTA_TILE / 2;  // values per half
   constexpr uint32_t CPT = DPT * ES / 16;    // 16-byte chunks per thread
   constexpr uint32_t NCH = HALF * ES / 16;   // chunks per half
@@ -523,16 +523,16 @@ __device__ inline void delta_expand_tile(DeltaExpandSmem& sm, const uint8_t* __r
       const uint32_t ci = (uint32_t)tid + r * WG;
       const uint4 q = sm.outq[ci ^ ((ci / CPT) & 7u)];
       const uint32_t v0 = h * HALF + ci * (16 / ES);  // first tile value of the chunk
-      uint8_t* dst = ob + (uint64_t)v0 * ES;
+      gptr<uint8_t> dst = ob + (uint64_t)v0 * ES;
       if (v0 + 16 / ES <= cnt) {
-        *reinterpret_cast<uint4*>(dst) = q;
+        gst16(dst, q);
       } else if (v0 < cnt) {
         const uint32_t qa[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (uint32_t e = 0; e < 16 / ES; ++e) {
           if (v0 + e >= cnt) break;
-          if (ES == 8) reinterpret_cast<uint64_t*>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
-          else reinterpret_cast<uint32_t*>(dst)[e] = qa[e];
+          if (ES == 8) reinterpret_cast<gptr<uint64_t>>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
+          else reinterpret_cast<gptr<uint32_t>>(dst)[e] = qa[e];
         }
       }
     }
@@ -596,7 +596,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
-  uint8_t* __restrict__ out = chunks[pw.chunk].val_out;
+  const gptr<uint8_t> __restrict__ out = gp(chunks[pw.chunk].val_out);
   DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
   if (pw.status != 0) {
     if (tid == 0) {
@@ -642,10 +642,10 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
   const uint32_t need = nn > 0 ? nn - 1 : 0u;  // deltas
   const uint32_t wmax = ES == 4 ? 32u : 64u;
   const uint64_t first = (uint64_t)unzigzag(fz);
-  uint8_t* const ob = out + pw.value_out * (uint64_t)ES;
+  const gptr<uint8_t> ob = out + pw.value_out * (uint64_t)ES;
   if (tid == 0 && nn > 0) {  // value 0
-    if (ES == 8) *reinterpret_cast<uint64_t*>(ob) = first;
-    else *reinterpret_cast<uint32_t*>(ob) = (uint32_t)first;
+    if (ES == 8) *reinterpret_cast<gptr<uint64_t>>(ob) = first;
+    else *reinterpret_cast<gptr<uint32_t>>(ob) = (uint32_t)first;
   }
   uint4 pv[DPG_CH];
   uint64_t SB = (S + q) & ~15ull;  // stage base of the current tile (absolute)
@@ -828,7 +828,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
     }
     // ---- stores through the stage buffer: quarter qq = wave qq's values [1024 qq, + 1024)
     const uint32_t cnt = D1 - D0;
-    uint8_t* const tb = ob + (uint64_t)(D0 + 1) * ES;
+    const gptr<uint8_t> tb = ob + (uint64_t)(D0 + 1) * ES;
     constexpr uint32_t CPT = DPT * ES / 16;  // 16-byte chunks per thread
     constexpr uint32_t QV = DPG_T / 4;       // values per quarter
     constexpr uint32_t NCH = QV * ES / 16;   // chunks per quarter
@@ -856,16 +856,16 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
         if (ci < NCH) {
           const uint4 v4 = sm.stq[ci ^ ((ci / CPT) & 7u)];
           const uint32_t v0 = (uint32_t)qq * QV + ci * (16 / ES);
-          uint8_t* dst = tb + (uint64_t)v0 * ES;
+          gptr<uint8_t> dst = tb + (uint64_t)v0 * ES;
           if (v0 + 16 / ES <= cnt) {
-            *reinterpret_cast<uint4*>(dst) = v4;
+            gst16(dst, v4);
           } else if (v0 < cnt) {
             const uint32_t qa[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
             for (uint32_t e = 0; e < 16 / ES; ++e) {
               if (v0 + e >= cnt) break;
-              if (ES == 8) reinterpret_cast<uint64_t*>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
-              else reinterpret_cast<uint32_t*>(dst)[e] = qa[e];
+              if (ES == 8) reinterpret_cast<gptr<uint64_t>>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
+              else reinterpret_cast<gptr<uint32_t>>(dst)[e] = qa[e];
             }
           }
         }

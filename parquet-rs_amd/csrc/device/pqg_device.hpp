@@ -5,6 +5,24 @@
 
 #include "../pqg_internal.hpp"
 
+// Global-memory pointers. Output buffers reached through ChunkWork (pointers loaded from memory,
+// or held in a struct argument) are generic to the compiler, which then emits flat stores; a flat
+// store counts in lgkmcnt as well as vmcnt, so every LDS wait after it waits for the store too.
+// Store paths take their output as gptr<T> (gp() at the point the pointer is read).
+#define PQG_AS1 __attribute__((address_space(1)))
+template <class T>
+using gptr = PQG_AS1 T*;
+template <class T>
+__device__ __forceinline__ gptr<T> gp(T* p) {
+  return (gptr<T>)p;
+}
+// One 16-byte streaming store (never split by the compiler into element stores).
+typedef uint32_t pqg_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void gst16(gptr<uint8_t> p, uint4 v) {
+  const pqg_u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<gptr<pqg_u32x4>>(p));
+}
+
 namespace pqg {
 
 constexpr int WG = 256;       // threads per workgroup (4 waves of 64)

@@ -120,6 +120,7 @@ __device__ inline void prepare_page(const uint8_t* __restrict__ blob, uint64_t b
   // path), else the page's level count (column/reader.rs:212-226).
   bool data = pw.page_type == P_DATA || pw.page_type == P_DATA_V2;
   if (data && !(cp.max_def > 0 && cp.want_def)) pw.nonnull = pw.num_values;
+  pw.spec_n = (!err && data && ck.spec && pw.encoding == E_PLAIN && ck.es > 0) ? pw.val_bytes / (uint32_t)ck.es : 0;
   if (!err && p == ck.dict_page && ck.dict_es > 0) {  // DictDecoder::set_dict (decoding.rs:282-288)
     if (pw.encoding != E_PLAIN && pw.encoding != E_PLAIN_DICTIONARY) err = ST_NYI;
     else if ((uint64_t)pw.num_values * (uint64_t)ck.dict_es > pw.nbytes) err = ST_EOF;
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(WG) k_tile_desc(const uint8_t* __restrict__ bl
 // to it only on unusual input, so the latency of a serial page matters less than three launches
 // on every decode.
 struct LevelsPageMaker {
-  int16_t* out;
+  gptr<int16_t> out;
   int16_t maxl;
   bool count;
   uint32_t acc;  // this thread's outputs == maxl
@@ -267,7 +268,7 @@ __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64
   }
   __syncthreads();
   if (st_s) return;
-  LevelsPageMaker mk{sel == SS_DEF ? ck.def_out : ck.rep_out, sel == SS_DEF ? ck.cp.max_def : ck.cp.max_rep,
+  LevelsPageMaker mk{gp(sel == SS_DEF ? ck.def_out : ck.rep_out), sel == SS_DEF ? ck.cp.max_def : ck.cp.max_rep,
                      sel == SS_DEF, 0u};
   for (uint32_t t = pw.ltile0; t < pw.ltile0 + pw.ntiles; ++t) {
     if (threadIdx.x == 0) rt.desc[t] = quarter_desc(blob, pages, chunks, tile_page, rt, sel, t, 0, RUN_TILE);
@@ -305,7 +306,7 @@ struct DictMaker {
     const ChunkWork& ck = chunks[pages[d.page].chunk];
     const PageWork& dp = pages[ck.dict_page];  // (quarter_desc gives work only with a valid dictionary)
     return TxDict<ES>{blob + dp.base, dp.num_values, ((dp.base % (ES == 12 ? 4 : ES)) == 0),
-                      ck.val_out + d.out * (uint64_t)ES, 0};
+                      gp(ck.val_out) + d.out * (uint64_t)ES, 0};
   }
   __device__ void done(const QDesc& d, uint32_t, TxDict<ES>& em) {
     const uint64_t bad = __ballot(em.err != 0);
@@ -372,7 +373,7 @@ struct BoolMaker {
   PageWork* pages;
   ChunkWork* chunks;
   __device__ TxBool make(const QDesc& d) {
-    return TxBool{d.qhi ? chunks[pages[d.page].chunk].val_out + d.out : nullptr};
+    return TxBool{d.qhi ? gp(chunks[pages[d.page].chunk].val_out) + d.out : gptr<uint8_t>(nullptr)};
   }
   __device__ void done(const QDesc&, uint32_t, TxBool&) {}
 };
@@ -423,6 +424,10 @@ __device__ inline void scan_values(PageWork* pages, ChunkWork* chunks, int npage
       [&](int p, uint64_t excl, uint64_t incl) {
         ChunkWork& ck = chunks[pages[p].chunk];
         pages[p].value_out = excl;
+        // a speculative PLAIN copy at the wrong offset or count: the chunk is copied again (mode 2)
+        if (ck.spec && (pages[p].page_type == P_DATA || pages[p].page_type == P_DATA_V2) &&
+            pages[p].encoding == E_PLAIN && (pages[p].spec_out != excl || pages[p].spec_n != incl - excl))
+          atomicOr(&ck.spec_bad, 1u);
         const uint64_t es = (uint64_t)ck.es;
         if (es > 0 && incl > excl && incl * es > ck.val_cap && pages[p].status == 0) report(pages, chunks, p, ST_CAPACITY);
         if ((uint32_t)p == ck.first_page + ck.npages - 1u) ck.res.total_values = incl;
@@ -433,6 +438,14 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, ChunkWork* 
   scan_values(pages, chunks, npages);
 }
 
+// Speculative value offsets of the PLAIN pages of ChunkWork::spec chunks: the exclusive prefix of
+// the value sections' value counts, chunk by chunk (single workgroup, right after k_prepare).
+__global__ void __launch_bounds__(WG) k_spec_scan(PageWork* pages, ChunkWork* chunks, int npages) {
+  seg_scan_pages(
+      pages, chunks, npages, [&](int p) -> uint64_t { return pages[p].spec_n; },
+      [&](int p, uint64_t excl, uint64_t) { pages[p].spec_out = excl; });
+}
+
 // ------------------------------------------------------------------------------ PLAIN
 
 // PLAIN fixed-width values: grid.y over the listed pages (PLAIN pages of fixed-width chunks),
@@ -440,29 +453,47 @@ __global__ void __launch_bounds__(WG) k_scan_values(PageWork* pages, ChunkWork* 
 // chunk's values + value_out * es. Source alignment is arbitrary (the value section follows the
 // level streams): dword loads + v_alignbyte; the destination is chunked on 16-byte boundaries of
 // the output so stores are dwordx4 except at page edges.
+//
+// mode 0: at the page's value offset (after the level decode and the offset scan);
+// mode 1 (speculative, ChunkWork::spec chunks, on a side stream beside the level decode): the
+//   value section's values (spec_n) at the offsets their counts give (spec_out), so the copy does
+//   not wait for the def levels; the offset scan flags the chunk when a page's count or offset
+//   turns out different (ChunkWork::spec_bad);
+// mode 2: the pages of flagged chunks again, as mode 0.
 __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                    PageWork* pages, ChunkWork* chunks,
-                                                   const uint32_t* __restrict__ pl) {
+                                                   const uint32_t* __restrict__ pl, int mode) {
   const uint32_t p = pl[blockIdx.y];
   const PageWork& pwr = pages[p];
   if (pwr.status != 0) return;
   const ChunkWork& ck = chunks[pwr.chunk];
+  if (mode == 2 && !ck.spec_bad) return;
   const uint64_t es = (uint64_t)ck.es;
-  uint8_t* __restrict__ out = ck.val_out;
-  const uint64_t nbytes = pwr.nonnull * es;
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
+  const uint64_t nv = mode == 1 ? pwr.spec_n : pwr.nonnull;
+  const uint64_t nbytes = nv * es;
   if (nbytes > pwr.val_bytes) {  // eof_err!("Not enough bytes to decode")
     if (blockIdx.x == 0 && threadIdx.x == 0) report(pages, chunks, (int)p, ST_EOF);
     return;
   }
   const uint64_t src = pwr.base + pwr.val_off;
-  const uint64_t dst = pwr.value_out * es;
+  const uint64_t dst = (mode == 1 ? pwr.spec_out : pwr.value_out) * es;
+  if (mode == 1 && dst + nbytes > ck.val_cap) return;  // (the offset scan flags it: copied again)
   const uint64_t dend = dst + nbytes;
   const uint64_t c0 = dst & ~15ull;
-  for (uint64_t c = c0 + ((uint64_t)blockIdx.x * WG + threadIdx.x) * 16ull; c < dend;
-       c += (uint64_t)gridDim.x * WG * 16ull) {
-    const uint64_t lo = c < dst ? dst : c;
-    const uint64_t hi = (c + 16 < dend) ? c + 16 : dend;
-    if (lo == c && hi == c + 16) {
+  // PC_U chunks per lane per step (WG * 16 bytes apart: each wave-instruction stays contiguous),
+  // their loads all issued before the stores
+  constexpr uint32_t PC_U = 4;
+  const uint64_t stepb = (uint64_t)WG * 16ull;
+  for (uint64_t cb = c0 + (uint64_t)blockIdx.x * stepb * PC_U + threadIdx.x * 16ull; cb < dend;
+       cb += (uint64_t)gridDim.x * stepb * PC_U) {
+    uint4 v[PC_U];
+    bool full[PC_U];
+#pragma unroll
+    for (uint32_t u = 0; u < PC_U; ++u) {
+      const uint64_t c = cb + u * stepb;
+      full[u] = c >= dst && c + 16 <= dend;
+      if (!full[u]) continue;
       const uint64_t s = src + (c - dst);
       const uint64_t sal = s & ~3ull;
       const uint32_t sh = (uint32_t)(s - sal);
@@ -475,17 +506,23 @@ __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ b
 #pragma unroll
         for (int k = 0; k < 5; ++k)
           w[k] = gbyte(blob, blob_len, sal + 4 * k) | (gbyte(blob, blob_len, sal + 4 * k + 1) << 8) |
-                 (gbyte(blob, blob_len, sal + 4 * k + 2) << 16) |
-                 (gbyte(blob, blob_len, sal + 4 * k + 3) << 24);
+                 (gbyte(blob, blob_len, sal + 4 * k + 2) << 16) | (gbyte(blob, blob_len, sal + 4 * k + 3) << 24);
       }
-      uint4 v;
-      v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-      v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-      v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-      v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
-      *reinterpret_cast<uint4*>(out + c) = v;
-    } else {
-      for (uint64_t b = lo; b < hi; ++b) out[b] = blob[src + (b - dst)];
+      v[u].x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+      v[u].y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      v[u].z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+      v[u].w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PC_U; ++u) {
+      const uint64_t c = cb + u * stepb;
+      if (full[u]) {
+        gst16(out + c, v[u]);
+      } else if (c < dend) {  // a chunk shared with a neighbouring page: its bytes only
+        const uint64_t lo = c < dst ? dst : c;
+        const uint64_t hi = (c + 16 < dend) ? c + 16 : dend;
+        for (uint64_t b = lo; b < hi; ++b) out[b] = blob[src + (b - dst)];
+      }
     }
   }
 }
@@ -501,7 +538,7 @@ __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ b
   const PageWork& pw = pages[p];
   if (pw.status != 0) return;
   const ChunkWork& ck = chunks[pw.chunk];
-  uint8_t* __restrict__ out = ck.val_out;
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
   const uint64_t n = pw.nonnull;
   if ((n + 7) / 8 > pw.val_bytes && n > (uint64_t)pw.val_bytes * 8) {
     if (threadIdx.x == 0 && gt == pw.ltile0) report(pages, chunks, (int)p, ST_EOF);
@@ -524,7 +561,7 @@ __global__ void __launch_bounds__(WG) k_plain_bool(const uint8_t* __restrict__ b
       uint32_t d[4];
 #pragma unroll
       for (uint32_t t = 0; t < 4; ++t) d[t] = (((x >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
-      *reinterpret_cast<uint4*>(out + c) = make_uint4(d[0], d[1], d[2], d[3]);
+      gst16(out + c, make_uint4(d[0], d[1], d[2], d[3]));
     } else {
       for (uint64_t b = lo; b < hi; ++b) {
         const uint64_t vi = b - dst;
@@ -626,12 +663,33 @@ hipError_t pqg_launch_plain(const uint8_t* blob, uint64_t blob_len, PageWork* pa
                             const uint32_t* tile_page, const uint32_t* pl, uint32_t npl, uint64_t max_bytes,
                             const uint32_t* tlb, uint32_t ntlb, hipStream_t s) {
   if (npl) {
-    uint64_t nch = (max_bytes + 16 * WG - 1) / (16 * WG) + 1;
+    uint64_t nch = (max_bytes + 64 * WG - 1) / (64 * WG) + 1;  // 4 x 16 bytes per lane (k_plain_copy)
     if (nch > 4096) nch = 4096;
-    hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)nch, npl), dim3(WG), 0, s, blob, blob_len, pages, chunks, pl);
+    hipLaunchKernelGGL(k_plain_copy, dim3((unsigned)nch, npl), dim3(WG), 0, s, blob, blob_len, pages, chunks, pl, 0);
   }
   if (ntlb)
     hipLaunchKernelGGL(k_plain_bool, dim3(ntlb), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tlb);
+  return hipGetLastError();
+}
+
+// The speculative PLAIN copy of ChunkWork::spec chunks (pages pl, npl): offsets scan + copy on
+// `side` (mode 1), launched after k_prepare; the re-copy of flagged chunks (mode 2) on `s` once the
+// offset scan has run there and the side stream's copy is joined.
+hipError_t pqg_launch_plain_spec(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
+                                 ChunkWork* chunks, const uint32_t* pl, uint32_t npl, uint64_t max_bytes,
+                                 hipStream_t side) {
+  hipLaunchKernelGGL(k_spec_scan, dim3(1), dim3(WG), 0, side, pages, chunks, npages);
+  // one workgroup per page: the copy holds a few workgroups per CU and leaves the rest of the
+  // chip to the level decode it runs beside (a full-size grid takes every CU and the level
+  // kernels wait for it)
+  (void)max_bytes;
+  hipLaunchKernelGGL(k_plain_copy, dim3(1, npl), dim3(WG), 0, side, blob, blob_len, pages, chunks, pl, 1);
+  return hipGetLastError();
+}
+
+hipError_t pqg_launch_plain_fix(const uint8_t* blob, uint64_t blob_len, PageWork* pages, ChunkWork* chunks,
+                                const uint32_t* pl, uint32_t npl, hipStream_t s) {
+  hipLaunchKernelGGL(k_plain_copy, dim3(8, npl), dim3(WG), 0, s, blob, blob_len, pages, chunks, pl, 2);
   return hipGetLastError();
 }
 

@@ -1403,7 +1403,7 @@ struct LvRuns {
 template <int OUT>
 __device__ inline uint32_t lv_write1(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                      uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
-                                     uint8_t* __restrict__ out) {
+                                     gptr<uint8_t> __restrict__ out) {
   constexpr uint32_t V = 16u / OUT;        // outputs per 16-byte chunk
   constexpr uint32_t NQ = 64u * 32u / (V * 64u);  // store instructions per step (4 / 2)
   const uint32_t lane = threadIdx.x & 63u;
@@ -1448,12 +1448,12 @@ __device__ inline uint32_t lv_write1(const LvRuns& rl, const uint32_t* stage, co
         for (uint32_t t = 0; t < 4; ++t)
           d[t] = OUT == 2 ? (((cb >> (2u * t)) & 3u) * 0x8001u) & 0x10001u
                           : (((cb >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
-        *reinterpret_cast<uint4*>(out + gc * OUT) = make_uint4(d[0], d[1], d[2], d[3]);
+        gst16(out + gc * OUT, make_uint4(d[0], d[1], d[2], d[3]));
       } else {
         for (uint32_t j = 0; j < V; ++j) {
           const uint64_t gi = gc + j;
           if (gi >= lo && gi < hi) {
-            if (OUT == 2) reinterpret_cast<int16_t*>(out)[gi] = (int16_t)((cb >> j) & 1u);
+            if (OUT == 2) reinterpret_cast<gptr<int16_t>>(out)[gi] = (int16_t)((cb >> j) & 1u);
             else out[gi] = (uint8_t)((cb >> j) & 1u);
           }
         }
@@ -1468,7 +1468,7 @@ __device__ inline uint32_t lv_write1(const LvRuns& rl, const uint32_t* stage, co
 template <int OUT>
 __device__ inline uint32_t lv_write_wide(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                          uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
-                                         uint32_t maxl, bool count, uint8_t* __restrict__ out) {
+                                         uint32_t maxl, bool count, gptr<uint8_t> __restrict__ out) {
   constexpr uint32_t G = 16u / OUT;  // outputs per 16-byte store
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
@@ -1520,13 +1520,13 @@ __device__ inline uint32_t lv_write_wide(const LvRuns& rl, const uint32_t* stage
                  ((f[4 * t + 3] & 0xFFu) << 24);
         v = make_uint4(q[0], q[1], q[2], q[3]);
       }
-      *reinterpret_cast<uint4*>(out + gl * OUT) = v;
+      gst16(out + gl * OUT, v);
     } else {
 #pragma unroll
       for (uint32_t j = 0; j < G; ++j) {
         const uint32_t oo = f0 + j;
         if (oo >= olo && oo < ohi) {
-          if (OUT == 2) reinterpret_cast<int16_t*>(out)[gl + j] = (int16_t)f[j];
+          if (OUT == 2) reinterpret_cast<gptr<int16_t>>(out)[gl + j] = (int16_t)f[j];
           else out[gl + j] = (uint8_t)f[j];
         }
       }
@@ -1549,7 +1549,7 @@ __device__ inline uint32_t lv_maxl(const ChunkWork& ck, int sel) {
 template <int OUT>
 __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                 uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo, int sel,
-                                uint32_t maxl, PageWork* pages, uint8_t* __restrict__ out) {
+                                uint32_t maxl, PageWork* pages, gptr<uint8_t> __restrict__ out) {
   const bool count = sel == SS_DEF;
   uint32_t cnt = x.s.w == 1 ? lv_write1<OUT>(rl, stage, blob, blob_len, x, base, endo, out)
                             : lv_write_wide<OUT>(rl, stage, blob, blob_len, x, base, endo, maxl, count, out);
@@ -1567,7 +1567,7 @@ template <int ES>
 __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                          uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
                                          const uint8_t* __restrict__ dict, uint32_t ndict, bool aligned,
-                                         uint8_t* __restrict__ out) {
+                                         const uint32_t* ldict, gptr<uint8_t> __restrict__ out) {
   using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
   constexpr uint32_t V = 16u / ES;  // outputs per 16-byte store
   const uint32_t lane = threadIdx.x & 63u;
@@ -1598,30 +1598,6 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
       full[u] = ohi - olo == V;
       for (uint32_t sp = lgn; sp; sp >>= 1)
         if (a + sp < rl.R && rl.rstart[a + sp] <= olo) a += sp;
-      const uint32_t st0 = rl.rstart[a], inf0 = rl.rinfo[a];
-      if (full[u] && rl.rstart[a + 1] >= ohi) {
-        // the group inside one run: one index, or V consecutive fields of one 8-byte read
-        // (V * w + 7 <= 39 bits: w <= 8 on this path)
-        uint64_t bits;
-        uint32_t sh;
-        if (inf0 & R_RLE) {
-          bits = inf0 & 0x7FFFFFFFu;
-          sh = 0;
-        } else {
-          const uint64_t bit = (uint64_t)inf0 * 8ull + (uint64_t)(olo - st0) * w;
-          bits = lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u);
-          sh = w;
-        }
-        const uint32_t m = (inf0 & R_RLE) ? 0x7FFFFFFFu : wm;
-#pragma unroll
-        for (uint32_t j = 0; j < V; ++j) {
-          const uint32_t idx = (uint32_t)(bits >> (j * sh)) & m;
-          id[u][j] = idx < ndict ? idx : 0u;  // (out of the dictionary: the page fails, ST_PANIC)
-          bad |= idx >= ndict ? 1u : 0u;
-        }
-        msk[u] = (1u << V) - 1u;
-        continue;
-      }
       uint32_t b = a;
 #pragma unroll
       for (uint32_t j = 0; j < V; ++j) {
@@ -1652,7 +1628,12 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
       for (uint32_t j = 0; j < V; ++j) {
         T t = 0;
         if ((msk[u] >> j) & 1u) {
-          if (aligned) {
+          if (ldict) {  // the dictionary in LDS (LvDictOut::page): no global load to wait for
+            if constexpr (ES == 8)
+              t = (uint64_t)ldict[2 * id[u][j]] | ((uint64_t)ldict[2 * id[u][j] + 1] << 32);
+            else
+              t = ldict[id[u][j]];
+          } else if (aligned) {
             t = reinterpret_cast<const T*>(dict)[id[u][j]];
           } else {
             const uint8_t* pv = dict + (uint64_t)id[u][j] * ES;
@@ -1671,11 +1652,11 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
           v = make_uint4((uint32_t)f[u][0], (uint32_t)(f[u][0] >> 32), (uint32_t)f[u][1], (uint32_t)(f[u][1] >> 32));
         else
           v = make_uint4(f[u][0], f[u][1], f[u][2], f[u][3]);
-        *reinterpret_cast<uint4*>(out + gl * ES) = v;
+        gst16(out + gl * ES, v);
       } else {
 #pragma unroll
         for (uint32_t j = 0; j < V; ++j)
-          if ((msk[u] >> j) & 1u) reinterpret_cast<T*>(out)[gl + j] = f[u][j];
+          if ((msk[u] >> j) & 1u) reinterpret_cast<gptr<T>>(out)[gl + j] = f[u][j];
       }
     }
   }
@@ -1690,14 +1671,15 @@ struct LvLevelOut {
   static constexpr bool PIPE = true;  // k_lv_emit_walk prefetches the next window (registers to spare)
   uint8_t* out;
   uint32_t maxl;
-  __device__ void page(const ChunkWork& ck, const PageWork*, const uint8_t*, int sel) {
+  static constexpr uint32_t XW = 1;  // per-wave LDS words it uses (none)
+  __device__ void page(const ChunkWork& ck, const PageWork*, const uint8_t*, int sel, uint32_t*) {
     out = lv_out(ck, sel);
     maxl = lv_maxl(ck, sel);
   }
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                              const LvWin& x, uint32_t base, uint32_t endo, int sel, const ChunkWork*,
-                             PageWork* pages) const {
-    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, maxl, pages, out);
+                             PageWork* pages, const uint32_t*) const {
+    lv_write<OUT>(rl, stage, blob, blob_len, x, base, endo, sel, maxl, pages, gp(out));
   }
 };
 
@@ -1709,10 +1691,10 @@ __device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, 
                                        const LvWin& x, uint32_t base, uint32_t endo, const ChunkWork& ck,
                                        PageWork* pages, ChunkWork* chunks, const uint64_t* __restrict__ dsrc0,
                                        const uint32_t* __restrict__ dlen0, uint64_t* __restrict__ vsrc0,
-                                       uint32_t* __restrict__ vlen0) {
+                                       uint32_t* __restrict__ vlen0, const uint32_t* ldlen) {
   {
-    const uint32_t* dlen = dlen0 + ck.dscr_base;
-    uint32_t* vlen = vlen0 + ck.scr_base;
+    gptr<const uint32_t> dlen = gp(dlen0 + ck.dscr_base);
+    gptr<uint32_t> vlen = gp(vlen0 + ck.scr_base);
     (void)dsrc0;
     (void)vsrc0;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1750,7 +1732,7 @@ __device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, 
       uint32_t lv[U];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
-        if (id[u] != 0xFFFFFFFFu) lv[u] = dlen[id[u]];
+        if (id[u] != 0xFFFFFFFFu) lv[u] = ldlen ? ldlen[id[u]] : dlen[id[u]];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
         if (id[u] != 0xFFFFFFFFu) {
@@ -1768,8 +1750,14 @@ __device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, 
 // Dictionary indices of every chunk on this path (ChunkWork::lvdict), by the chunk's value type:
 // 4- / 8-byte values gathered from its PLAIN dictionary page (k_prepare checked it), byte arrays
 // as entry addresses and lengths.
+//
+// The dictionary itself (<= 2 KiB: 4- / 8-byte values) or, for byte arrays, its entries' lengths
+// (<= 512 entries) are copied into the wave's LDS words at each page change, so that the gathers
+// are LDS reads: on CDNA the vector memory counter covers loads and stores in issue order, and a
+// wave waiting for a global gather would wait for every store it issued before it as well.
 struct LvDictOut {
   static constexpr bool PIPE = false;  // (its gathers hold the registers the prefetch would take)
+  static constexpr uint32_t XW = 512;  // per-wave LDS words: the dictionary, or its entry lengths
   const uint64_t* dsrc;
   const uint32_t* dlen;
   uint64_t* vsrc;
@@ -1779,28 +1767,45 @@ struct LvDictOut {
   const uint8_t* dict;
   uint32_t ndict;
   int es;
-  __device__ void page(const ChunkWork& c, const PageWork* pages, const uint8_t* blob, int) {
+  bool lds;  // the page's dictionary (or entry lengths) is in the wave's LDS words
+  __device__ void page(const ChunkWork& c, const PageWork* pages, const uint8_t* blob, int, uint32_t* xw) {
     ck = &c;
     es = c.es;
     val_out = c.val_out;
     const PageWork& dp = pages[c.dict_page];
     dict = blob + dp.base;
     ndict = dp.num_values;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (es == 4 || es == 8) {
+      const uint32_t nw = ndict * (uint32_t)es / 4u;  // (k_prepare checked the page holds them)
+      lds = nw <= XW;
+      if (lds)
+        for (uint32_t i = lane; i < nw; i += WAVE)
+          xw[i] = (uint32_t)dict[4 * i] | ((uint32_t)dict[4 * i + 1] << 8) | ((uint32_t)dict[4 * i + 2] << 16) |
+                  ((uint32_t)dict[4 * i + 3] << 24);
+    } else {
+      lds = ndict <= XW;
+      if (lds)
+        for (uint32_t i = lane; i < ndict; i += WAVE) xw[i] = gp(dlen)[c.dscr_base + i];
+    }
+    wave_lds_sync();
   }
   __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                              const LvWin& x, uint32_t base, uint32_t endo, int, const ChunkWork* chunks,
-                             PageWork* pages) const {
+                             PageWork* pages, const uint32_t* xw) const {
     if (es == 0) {
       lv_write_badict(rl, stage, blob, blob_len, x, base, endo, *ck, pages, const_cast<ChunkWork*>(chunks), dsrc, dlen,
-                      vsrc, vlen);
+                      vsrc, vlen, lds ? xw : nullptr);
       return;
     }
     const uint64_t da = (uint64_t)(dict - blob);
     uint32_t bad;
     if (es == 8)
-      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 8) == 0, val_out);
+      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 8) == 0, lds ? xw : nullptr,
+                             gp(val_out));
     else
-      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 4) == 0, val_out);
+      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 4) == 0, lds ? xw : nullptr,
+                             gp(val_out));
     if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)x.p, ST_PANIC);
   }
 };
@@ -1914,7 +1919,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     if (endo <= base || R == 0) continue;
     const ChunkWork& ck = chunks[pw.chunk];
     lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
-                  lv_maxl(ck, sel), pages, lv_out(ck, sel));
+                  lv_maxl(ck, sel), pages, gp(lv_out(ck, sel)));
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }
@@ -1999,8 +2004,10 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
                                                      PageWork* pages, int npages, const ChunkWork* chunks,
                                                      int sel, RunTables rt, LevelTables lt, Writer wr) {
   __shared__ LeWave sm[WG / WAVE];
+  __shared__ uint32_t smx[WG / WAVE][Writer::XW];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LeWave& E = sm[wid];
+  uint32_t* xw = smx[wid];
   const uint32_t total = lt.wbase[npages];
   const uint32_t nwv = gridDim.x * (WG / WAVE), gw = blockIdx.x * (WG / WAVE) + wid;
   const uint32_t per = (total + nwv - 1u) / nwv;
@@ -2011,7 +2018,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   LvWin x;
   x.p = p;
   bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
-  if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel);
+  if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel, xw);
   LeLoad nf;  // the next window's loads, issued while the current one is written
   nf.ok = false;
   uint32_t nb0 = 0, nb1 = 0, nbk = 0;  // run bounds (wfirst) of window nbk of the page, read ahead
@@ -2023,7 +2030,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       pend = lt.wbase[p + 1];
       x.p = p;
       walked = pend > wb && rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
-      if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel);
+      if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel, xw);
       nf.ok = false;
       nbv = false;
     }
@@ -2054,7 +2061,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       lv_stage(blob, blob_len, x, E.stage, le_nch(w));  // ends with a wave LDS sync (run list too)
       const uint32_t base = E.rstart[0];
       const uint32_t endo = endn < x.s.n ? endn : x.s.n;
-      if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages);
+      if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
       wave_lds_sync();
       continue;
     }
@@ -2106,7 +2113,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     const uint32_t base = E.rstart[0];
     const uint32_t endn = E.endn;
     const uint32_t endo = endn < x.s.n ? endn : x.s.n;
-    if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages);
+    if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }

@@ -284,7 +284,7 @@ __device__ inline void tile_one(const uint8_t* __restrict__ blob, uint64_t blob_
 struct TxLevels {
   static constexpr int V = 8;
   static constexpr int PG = 2;
-  int16_t* out;  // page output base
+  gptr<int16_t> out;  // page output base
   int16_t maxl;
   bool count;
   uint32_t nonnull;
@@ -297,14 +297,14 @@ struct TxLevels {
         for (int j = 0; j < V; ++j)
           nonnull += (((m[s] >> j) & 1u) && (int16_t)v[s][j] == maxl) ? 1u : 0u;
       }
-      int16_t* o = out + g0 + (uint32_t)s * stride;
+      gptr<int16_t> o = out + g0 + (uint32_t)s * stride;
       if (m[s]) {
         uint4 pk;
         pk.x = (v[s][0] & 0xFFFFu) | (v[s][1] << 16);
         pk.y = (v[s][2] & 0xFFFFu) | (v[s][3] << 16);
         pk.z = (v[s][4] & 0xFFFFu) | (v[s][5] << 16);
         pk.w = (v[s][6] & 0xFFFFu) | (v[s][7] << 16);
-        *reinterpret_cast<uint4*>(o) = pk;
+        gst16(reinterpret_cast<gptr<uint8_t>>(o), pk);
       }
     }
   }
@@ -318,19 +318,19 @@ struct TxLevels {
 struct TxBool {
   static constexpr int V = 16;
   static constexpr int PG = 1;
-  uint8_t* out;
+  gptr<uint8_t> out;
   template <int NG>
   __device__ void put(uint32_t g0, uint32_t stride, const uint32_t (&v)[NG][V], const uint32_t (&m)[NG]) {
 #pragma unroll
     for (int s = 0; s < NG; ++s) {
-      uint8_t* o = out + g0 + (uint32_t)s * stride;
+      gptr<uint8_t> o = out + g0 + (uint32_t)s * stride;
       if (m[s]) {
         uint32_t q[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           q[k] = (v[s][4 * k] & 0xFFu) | ((v[s][4 * k + 1] & 0xFFu) << 8) |
                  ((v[s][4 * k + 2] & 0xFFu) << 16) | ((v[s][4 * k + 3] & 0xFFu) << 24);
-        *reinterpret_cast<uint4*>(o) = make_uint4(q[0], q[1], q[2], q[3]);
+        gst16(o, make_uint4(q[0], q[1], q[2], q[3]));
       }
     }
   }
@@ -352,7 +352,7 @@ struct TxDict {
   const uint8_t* dict;  // PLAIN dictionary page payload
   uint32_t ndict;
   bool aligned;         // dict payload aligned to its value size
-  uint8_t* out;         // page output base
+  gptr<uint8_t> out;    // page output base
   int32_t err;
 
   template <int NG>
@@ -382,13 +382,13 @@ struct TxDict {
         }
 #pragma unroll
       for (int s = 0; s < NG; ++s) {
-        T* o = reinterpret_cast<T*>(out) + g0 + (uint64_t)s * stride;
+        gptr<T> o = reinterpret_cast<gptr<T>>(out) + g0 + (uint64_t)s * stride;
         if (m[s]) {
           if constexpr (ES == 8)
-            *reinterpret_cast<uint4*>(o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32),
-                                                      (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
+            gst16(reinterpret_cast<gptr<uint8_t>>(o), make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32),
+                                                                 (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32)));
           else
-            *reinterpret_cast<uint4*>(o) = make_uint4(x[s][0], x[s][1], x[s][2], x[s][3]);
+            gst16(reinterpret_cast<gptr<uint8_t>>(o), make_uint4(x[s][0], x[s][1], x[s][2], x[s][3]));
         }
       }
     } else {  // 1-byte (BOOLEAN) and 12-byte (INT96) values: byte copies
@@ -402,12 +402,12 @@ struct TxDict {
             err = ST_PANIC;
             continue;
           }
-          uint8_t* o = out + ((uint64_t)g0 + (uint64_t)s * stride + (uint32_t)j) * ES;
+          gptr<uint8_t> o = out + ((uint64_t)g0 + (uint64_t)s * stride + (uint32_t)j) * ES;
           const uint8_t* p = dict + (uint64_t)idx * ES;
           if (ES == 12 && aligned) {
             const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
             const uint32_t a = q[0], b = q[1], c = q[2];
-            uint32_t* od = reinterpret_cast<uint32_t*>(o);
+            gptr<uint32_t> od = reinterpret_cast<gptr<uint32_t>>(o);
             od[0] = a;
             od[1] = b;
             od[2] = c;
@@ -423,11 +423,11 @@ struct TxDict {
       err = ST_PANIC;
       return;
     }
-    uint8_t* d = out + (uint64_t)o * ES;
+    gptr<uint8_t> d = out + (uint64_t)o * ES;
     const uint8_t* p = dict + (uint64_t)idx * ES;
     if ((ES == 4 || ES == 8) && aligned) {
-      if constexpr (ES == 8) *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(p);
-      else *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(p);
+      if constexpr (ES == 8) *reinterpret_cast<gptr<uint64_t>>(d) = *reinterpret_cast<const uint64_t*>(p);
+      else *reinterpret_cast<gptr<uint32_t>>(d) = *reinterpret_cast<const uint32_t*>(p);
     } else {
 #pragma unroll 1
       for (int k = 0; k < ES; ++k) d[k] = p[k];

@@ -39,6 +39,10 @@ hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*,
                            hipEvent_t*);
 hipError_t pqg_launch_plain(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, const uint32_t*, uint32_t,
                             uint64_t, const uint32_t*, uint32_t, hipStream_t);
+hipError_t pqg_launch_plain_spec(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
+                                 uint64_t, hipStream_t);
+hipError_t pqg_launch_plain_fix(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, uint32_t,
+                                hipStream_t);
 hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
                                uint32_t, RunTables, LevelTables, hipStream_t);
 hipError_t pqg_launch_delta_tiled(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint32_t, const uint32_t*,
@@ -63,7 +67,8 @@ constexpr int SS_DICT = 2;  // device/pqg_runs.hpp StreamSel: dictionary indices
 // general-path dictionary tiles by value size (1, 4, 8, 12) and all of them, byte-array
 // dictionary tiles off the level path, byte-array copy tiles, RLE boolean tiles, PLAIN
 // fixed-width pages (a page list) and PLAIN boolean tiles.
-enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_N };
+// TL_PSPEC: PLAIN pages of the chunks whose values are copied speculatively (ChunkWork::spec).
+enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_PSPEC, TL_N };
 
 // What the host knows of one chunk of a decode until its results are delivered.
 struct ChunkHost {
@@ -83,6 +88,7 @@ struct Slot {
   ChunkWork* h_res = nullptr;  // pinned: the chunk table copied back after the decode
   size_t res_cap = 0;
   hipEvent_t ev[10] = {};  // 0-5 stage boundaries; 6-7 / 8-9 around the def-level path / values kernel
+  hipEvent_t fork = nullptr, join = nullptr;  // the side stream's speculative PLAIN copy
   bool kl = false, kv = false;  // events 6-7 / 8-9 recorded by the last decode
   bool used = false;     // a decode was enqueued and its timings not yet harvested
   bool pending = false;  // a decode was enqueued and its results not yet delivered
@@ -136,6 +142,8 @@ struct pqg_ctx {
   int cur = 0;          // slot of the last decode
   hipStream_t stream = nullptr;
   bool timing = false;
+  bool overlap = true;  // speculative PLAIN copy on the side stream (pqg_ctx_set_overlap)
+  hipStream_t side = nullptr;  // lowest-priority stream of that copy
   uint64_t seq = 0;     // decodes issued
   int calls = 0;        // decodes issued since the last pqg_sync
   // first failure among decodes delivered at a slot's reuse, reported by the next pqg_sync
@@ -284,8 +292,17 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     delete ctx;
     return PQG_ERR_HIP;
   }
-  for (Slot& sl : ctx->slot)
+  for (Slot& sl : ctx->slot) {
     for (auto& ev : sl.ev) hipEventCreate(&ev);
+    hipEventCreateWithFlags(&sl.fork, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sl.join, hipEventDisableTiming);
+  }
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least) != hipSuccess) {
+    delete ctx;
+    return PQG_ERR_HIP;
+  }
   ctx->cur = 1;
   *out = ctx;
   return PQG_OK;
@@ -317,6 +334,12 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
       for (void* b : sl.lvbuf[k]) hipFree(b);
     }
     for (auto& ev : sl.ev) hipEventDestroy(ev);
+    hipEventDestroy(sl.fork);
+    hipEventDestroy(sl.join);
+  }
+  if (ctx->side) {
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
   }
   hipFree(ctx->sp_tiles);
   hipFree(ctx->dbgbuf);
@@ -327,6 +350,12 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
 int pqg_ctx_set_timing(pqg_ctx* ctx, int enabled) {
   if (!ctx) return PQG_ERR_INVALID;
   ctx->timing = enabled != 0;
+  return PQG_OK;
+}
+
+int pqg_ctx_set_overlap(pqg_ctx* ctx, int enabled) {
+  if (!ctx) return PQG_ERR_INVALID;
+  ctx->overlap = enabled != 0;
   return PQG_OK;
 }
 
@@ -481,7 +510,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   std::vector<uint32_t> tl[TL_N];
   std::vector<PageWork> pw(np);
   uint32_t total_tiles = 0;
-  uint64_t nwin = 0, plain_max = 0, scr = 0, dscr = 0;
+  uint64_t nwin = 0, plain_max = 0, spec_max = 0, scr = 0, dscr = 0;
   uint32_t def_w = 0, rep_w = 0;  // bit masks of the level streams' widths
   bool any_def = false, any_rep = false, any_plain = false, any_pbool = false, any_ba = false, any_dba = false;
   bool any_badict = false, ba_lv = false, any_rbool = false, fixed_gen = false;
@@ -611,12 +640,18 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
             any_pbool = true;
             list_tiles(TL_PBOOL, PQG_PLAIN);
           } else if (es > 0) {
-            any_plain = true;
+            // values of a chunk whose data pages are all PLAIN, behind def levels: copied at the
+            // offsets the value sections give, beside the level decode (checked by the scan)
+            bool only_plain = true;
+            for (int e = 0; e < 16; ++e) only_plain &= !enc[e] || e == PQG_PLAIN;
+            c.spec = ctx->overlap && es >= 4 && cp.want_def && only_plain ? 1u : 0u;
+            if (!c.spec) any_plain = true;
             for (uint32_t i = 0; i < n; ++i) {
               const PageWork& w = pw[p0 + i];
               if (w.ntiles && w.encoding == PQG_PLAIN) {
-                tl[TL_PLAIN].push_back(p0 + i);
-                if (w.nbytes > plain_max) plain_max = w.nbytes;
+                tl[c.spec ? TL_PSPEC : TL_PLAIN].push_back(p0 + i);
+                uint64_t& mx = c.spec ? spec_max : plain_max;
+                if (w.nbytes > mx) mx = w.nbytes;
               }
             }
           }
@@ -829,6 +864,15 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   hipEvent_t* ev = sl.ev;
   if (ctx->timing) hipEventRecord(ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, ini, s), "prepare");
+  const bool spec = np && ntl[TL_PSPEC];
+  if (spec) {  // fork: the speculative PLAIN copy on the side stream, beside everything below
+    HIPCHK(hipEventRecord(sl.fork, s), "event");
+    HIPCHK(hipStreamWaitEvent(ctx->side, sl.fork, 0), "stream wait");
+    HIPCHK(pqg_launch_plain_spec(b, blob_len, d_pages, ni, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], spec_max,
+                                 ctx->side),
+           "speculative plain");
+    HIPCHK(hipEventRecord(sl.join, ctx->side), "event");
+  }
   if (ctx->timing) hipEventRecord(ev[1], s);
   // the value-offset scan runs in the def stream's last kernel when no rep stream follows it
   const bool fused_scan = np && any_def && !any_rep;
@@ -898,6 +942,10 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
                                  sl.rt[K_BOOL], sl.lt(K_BOOL, 64), s),
              "rle bool");
     }
+  }
+  if (spec) {  // join, then the chunks the offset scan flagged copied again
+    HIPCHK(hipStreamWaitEvent(s, sl.join, 0), "stream wait");
+    HIPCHK(pqg_launch_plain_fix(b, blob_len, d_pages, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], s), "plain fix-up");
   }
   if (ctx->timing) hipEventRecord(ev[4], s);
   if (nc)

@@ -353,6 +353,7 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
   }
   s.ndec = s.host_col >= 0 ? (uint32_t)s.host_col : nc;
   s.blob_len = at;
+  const auto tp = std::chrono::steady_clock::now();
   // ---- payloads into pinned staging, page by page over the pool
   RCHK(s.h_blob.need(at + 64), "hipHostMalloc staging");
   RCHK(s.d_blob.need(at + 64), "hipMalloc blob");
@@ -367,6 +368,7 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
     const PagePlan& pp = c.plan[work[k].second];
     wst[k] = fill_page(pp, rgm.columns[work[k].first].codec, hb + c.base, werr[k]);
   });
+  const auto tf = std::chrono::steady_clock::now();
   for (size_t k = 0; k < work.size(); ++k)  // the lowest failing (column, page): the reference's first
     if (wst[k]) {
       const uint32_t j = work[k].first;
@@ -405,6 +407,13 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
   if (st) return rgr_fail(g, st, pqg_error_message(s.ctx));
   RCHK(hipEventRecord(s.ev_dec, g->s_dec), "event");
   if ((st = enqueue_known_d2h(g, s))) return st;
+  const auto te = std::chrono::steady_clock::now();
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  g->st.plan_ms += ms(t0, tp);
+  g->st.fill_ms += ms(tp, tf);
+  g->st.enqueue_ms += ms(t1, te);
   g->count++;
   g->st.row_groups++;
   g->st.file_bytes += file_bytes;
@@ -425,7 +434,9 @@ int pqg_rgr_wait(pqg_rgr* g, int* rg_out, int* bad_column, int* bad_page) {
   g->count--;
   g->cur = (int)(&s - g->slot);
   int call = -1, chunk = -1, page = -1;
+  const auto t0 = std::chrono::steady_clock::now();
   int st = pqg_sync_detail(s.ctx, &call, &chunk, &page);
+  const auto t1 = std::chrono::steady_clock::now();
   if (st == PQG_ERR_CAPACITY) {  // a byte-array chunk decoded to more than its bound: grow, decode again
     bool grew = false;
     RCHK(hipStreamSynchronize(g->s_d2h), "sync D2H");  // the first pass's copies land before buffers move
@@ -472,6 +483,9 @@ int pqg_rgr_wait(pqg_rgr* g, int* rg_out, int* bad_column, int* bad_page) {
     }
     RCHK(hipStreamSynchronize(g->s_d2h), "sync D2H");
   }
+  const auto t2 = std::chrono::steady_clock::now();
+  g->st.sync_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  g->st.d2h_wait_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
   for (uint32_t j = 0; j < s.ndec; ++j) {
     const pqg_output& o = s.outs[j];
     const bool ba = s.desc[j].physical_type == PQG_BYTE_ARRAY || s.desc[j].physical_type == PQG_FIXED_LEN_BYTE_ARRAY;

@@ -62,6 +62,10 @@ struct PageWork {
   uint64_t value_out;   // index of this page's first value in its chunk's value output
   uint64_t byte_out;    // BYTE_ARRAY/FLBA: first byte of this page's values in the byte output
   uint64_t nbytes_out;  // BYTE_ARRAY/FLBA: bytes this page produces
+  // ---- speculative PLAIN copy (ChunkWork::spec): the values the page's value section holds
+  // (val_bytes / es, set by k_prepare) and their chunk-exclusive prefix (k_spec_scan)
+  uint64_t spec_n;
+  uint64_t spec_out;
   // ---- host-filled
   uint32_t chunk;       // the column chunk of the batch this page belongs to (ChunkWork index)
   uint32_t pad1;
@@ -244,6 +248,8 @@ struct ChunkWork {
   uint32_t first_page;
   uint32_t npages;
   uint32_t lvdict;       // 1: its dictionary indices take the hybrid-stream (level) path
+  uint32_t spec;         // 1: its PLAIN values are copied at speculative offsets beside the level decode
+  uint32_t spec_bad;     // set by the value-offset scan when a speculative offset or count was wrong
   ChunkResult res;       // filled by the kernels, copied back after the decode
 };
 

@@ -66,13 +66,16 @@ class RgrOutput(C.Structure):
 
 class RgrStats(C.Structure):
     _fields_ = [("row_groups", C.c_uint64), ("file_bytes", C.c_uint64), ("staged_bytes", C.c_uint64),
-                ("output_bytes", C.c_uint64), ("host_ms", C.c_double)]
+                ("output_bytes", C.c_uint64), ("host_ms", C.c_double), ("plan_ms", C.c_double),
+                ("fill_ms", C.c_double), ("enqueue_ms", C.c_double), ("sync_ms", C.c_double),
+                ("d2h_wait_ms", C.c_double)]
 
 
 RGR_HOST_OUTPUT = 1
 
 EXPORTS = [
-    "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_decode_chunk", "pqg_decode_chunks",
+    "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_ctx_set_overlap", "pqg_decode_chunk",
+    "pqg_decode_chunks",
     "pqg_sync", "pqg_sync_detail",
     "pqg_get_timings", "pqg_reset_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
@@ -100,6 +103,7 @@ def lib():
         L.pqg_ctx_create.argtypes = [i32, C.POINTER(vp)]
         L.pqg_ctx_destroy.argtypes = [vp]
         L.pqg_ctx_set_timing.argtypes = [vp, i32]
+        L.pqg_ctx_set_overlap.argtypes = [vp, i32]
         L.pqg_decode_chunk.argtypes = [vp, C.POINTER(Column), vp, u64, C.POINTER(Page), C.c_uint32,
                                        C.POINTER(Output), vp]
         L.pqg_decode_chunks.argtypes = [vp, C.c_uint32, C.POINTER(Column), vp, u64, C.POINTER(C.POINTER(Page)),
@@ -196,6 +200,10 @@ class Context:
     def set_timing(self, enabled):
         """HIP events around the decode stages (pqg_get_timings); call with no decode pending."""
         lib().pqg_ctx_set_timing(self.h, 1 if enabled else 0)
+
+    def set_overlap(self, enabled):
+        """Speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap); default on."""
+        lib().pqg_ctx_set_overlap(self.h, 1 if enabled else 0)
 
     def decode_async(self, column, blob, blob_len, pages, out, stream=0, npages=None):
         """Enqueue pqg_decode_chunk. `blob` is a device pointer (int), `pages` a ctypes Page

@@ -236,3 +236,58 @@ def test_batch_reports_failing_chunk(oracle, ctx):
     # the healthy chunks were decoded all the same (their counters filled)
     assert res[0]["num_values"] == len(oracle.read_column(zoo[0][1], zoo[0][2], max_def=1)["values"])
     assert pqgpu.OK == 0
+
+
+def _plain_zoo(oracle, seed=21):
+    """Chunks whose data pages are all PLAIN behind def levels (the speculative copy's chunks),
+    one with trailing bytes after its values (the reference reads the non-null values only), one
+    whose first page holds fewer value bytes than its non-null values need (EOF)."""
+    rng = np.random.default_rng(seed)
+    i32 = lambda nn: rng.integers(-2 ** 31, 2 ** 31, nn, dtype=np.int64).astype(np.int32).tobytes()  # noqa: E731
+    i64 = lambda nn: rng.integers(-2 ** 62, 2 ** 62, nn, dtype=np.int64).tobytes()  # noqa: E731
+    f64 = lambda nn: rng.standard_normal(nn).tobytes()  # noqa: E731
+    i96 = lambda nn: rng.integers(0, 256, nn * 12, dtype=np.uint8).tobytes()  # noqa: E731
+    z = [("int32_plain", oracle.INT32, [_opt(oracle, rng, n, 0.3, i32, oracle.PLAIN) for n in (5000, 70001, 3)],
+          1, 0, -1, True),
+         ("double_plain_v2", oracle.DOUBLE, [_opt(oracle, rng, n, 0.0, f64, oracle.PLAIN, v2=True) for n in (4096, 9)],
+          1, 0, -1, True),
+         ("int96_plain", oracle.INT96, [_opt(oracle, rng, n, 0.2, i96, oracle.PLAIN) for n in (1000, 2000)],
+          1, 0, -1, True)]
+    pages = [_opt(oracle, rng, n, 0.1, i64, oracle.PLAIN) for n in (3000, 6000, 50)]
+    pages[1] = oracle.PageSpec(pages[1].page_type, pages[1].buf + b"\x07" * 21, pages[1].num_values, pages[1].encoding)
+    z.append(("int64_plain_trailing", oracle.INT64, pages, 1, 0, -1, True))
+    return z
+
+
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_speculative_plain_copy(oracle, ctx, overlap):
+    """PLAIN values behind def levels, copied beside the level decode at the value sections'
+    offsets (pqg_ctx_set_overlap 1) or after it (0): identical to the oracle, including a chunk whose
+    speculative offsets are wrong (trailing value bytes: re-copied at the true offsets)."""
+    zoo = _plain_zoo(oracle)
+    ctx.set_overlap(overlap)
+    try:
+        for order in (list(range(len(zoo))), [3, 0, 2, 1]):
+            st, res = _decode_batch(ctx, zoo, order)
+            _check_zoo(oracle, zoo, st, res, order)
+    finally:
+        ctx.set_overlap(1)
+
+
+def test_speculative_plain_copy_short_section(oracle, ctx):
+    """A PLAIN page whose value section is shorter than its non-null values: EOF on that page, the
+    same with the speculative copy as without (eof_err!, decoding.rs:138-186)."""
+    zoo = _plain_zoo(oracle, seed=22)
+    name, pt, pages, md, mr, tl, wdef = zoo[0]
+    pages = list(pages)
+    pages[1] = oracle.PageSpec(pages[1].page_type, pages[1].buf[:-9], pages[1].num_values, pages[1].encoding)
+    zoo[0] = (name, pt, pages, md, mr, tl, wdef)
+    ref = oracle.read_column(pt, pages, max_def=md)
+    assert ref["status"] != 0
+    for overlap in (1, 0):
+        ctx.set_overlap(overlap)
+        try:
+            st, res = _decode_batch(ctx, zoo)
+        finally:
+            ctx.set_overlap(1)
+        assert st[0] == ref["status"] and st[2] == 0 and st[3] == 1, (overlap, st)
