@@ -309,6 +309,31 @@ int16_t pqg_triplet_iter_rep_level(pqg_triplet_iter *it);
 int pqg_triplet_iter_is_null(pqg_triplet_iter *it);
 int pqg_triplet_iter_value(pqg_triplet_iter *it, void *out, size_t cap, size_t *len);
 
+/* ---------------------------------------------------------------- rows
+ * Record assembly into rows: RowIter / ReaderIter over the reader tree TreeBuilder builds from the
+ * file schema (record/reader.rs:38-717): optional, group, LIST (3-level and the legacy 2-level
+ * forms), MAP / MAP_KEY_VALUE and unannotated repeated fields, leaf values converted by physical and
+ * converted type (Field::convert_*, record/api.rs:449-555). Each leaf column chunk is decoded on
+ * the GPU through a column reader (pqg_column_reader_open with `ctx`) and read through its triplet
+ * iterator with `batch_size` levels per batch. row_group = -1 iterates every row group of the file
+ * (RowIter::from_file), else that one (RowIter::from_row_group). */
+typedef struct pqg_row_iter pqg_row_iter;
+int pqg_row_iter_open(pqg_file_reader *r, int row_group, pqg_ctx *ctx, size_t batch_size, pqg_row_iter **out);
+/* The same over a projection of the message's top-level fields, in the given order (fields named
+ * that the schema lacks: PQG_ERR_GENERAL, "Root schema does not contain projection"). */
+int pqg_row_iter_open_fields(pqg_file_reader *r, int row_group, pqg_ctx *ctx, size_t batch_size,
+                             const char *const *fields, uint32_t nfields, pqg_row_iter **out);
+void pqg_row_iter_close(pqg_row_iter *it);
+/* The next row, rendered into buf (NUL-terminated): format 0 = the reference's Display text
+ * (Row / Field fmt, record/api.rs:144-157, 557-666; dates and timestamps in UTC), 1 = JSON:
+ * a row is [[name, field], ...], a field null or {"Kind": value} with Kind the Field variant name
+ * (Group: fields as a row, List: [fields], Map: [[key, value], ...], Bytes: [bytes], Decimal: its
+ * text). *has_row = 0 at the end. With cap too small: PQG_ERR_CAPACITY, *len = the text's length,
+ * and the same row is returned by the next call. A failing column chunk ends the iteration with
+ * its status (the reference panics there: read_next().unwrap(), reader.rs:400-401). */
+int pqg_row_iter_next(pqg_row_iter *it, int format, char *buf, size_t cap, size_t *len, int *has_row);
+const char *pqg_row_iter_error(pqg_row_iter *it);
+
 #ifdef __cplusplus
 }
 #endif

@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWor
 //    scan; their tile-relative offsets replace them in place (32-bit: a tile's bytes come from
 //    one page, < 4 GiB); the offsets go out coalesced from LDS;
 //  - values of at most BA_SMALL bytes (the common case: short strings) are staged: per round of
-//    BA_RN values, each thread loads its BA_RV consecutive values (16 bytes each, all loads in
+//    BA_RN values, each thread loads BA_RV values (lanes on consecutive ones) (16 bytes each, all loads in
 //    flight together, no store between them to wait for) and writes their bytes into an LDS image
 //    of the round's output, aligned as the output is; the workgroup then stores the image with
 //    16-byte stores (byte stores at the round's two ends only);
@@ -651,7 +651,8 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
     uint32_t dd[BA_RV], ln[BA_RV];
 #pragma unroll
     for (uint32_t i = 0; i < BA_RV; ++i) {  // loads of the thread's values, all in flight
-      const uint32_t j = r0 + tid * BA_RV + i;
+      const uint32_t j = r0 + i * WG + tid;  // (lanes on consecutive values: their image bytes
+                                             // fall in different LDS banks)
       ln[i] = 0;
       dd[i] = 0;
       if (j < r1) {

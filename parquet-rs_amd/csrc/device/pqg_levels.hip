@@ -1563,8 +1563,8 @@ __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const u
 // run, gathers its value from the PLAIN dictionary page; groups of 16 / ES outputs, one 16-byte
 // store each (element stores for the groups shared with a neighbouring window). Returns nonzero
 // when an index is out of the dictionary (the reference panics).
-template <int ES>
-__device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+template <int ES, bool LDSD>
+__device__ __forceinline__ uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
                                          uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
                                          const uint8_t* __restrict__ dict, uint32_t ndict, bool aligned,
                                          const uint32_t* ldict, gptr<uint8_t> __restrict__ out) {
@@ -1579,7 +1579,7 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
   while (lgn * 2u <= rl.R) lgn *= 2u;
   // U groups per lane per step: their indices first, then every gather, then the stores (the
   // gathers of a step are in flight together)
-  constexpr uint32_t U = ES == 8 ? 8 : 4;
+  constexpr uint32_t U = LDSD ? 2 : (ES == 8 ? 8 : 4);  // (LDS gathers: 2 keep the emit at 80 VGPRs)
   uint32_t a = 0, bad = 0;
 #pragma unroll 1
   for (uint64_t kb = k0 + lane; kb < k1; kb += (uint64_t)WAVE * U) {
@@ -1628,7 +1628,7 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
       for (uint32_t j = 0; j < V; ++j) {
         T t = 0;
         if ((msk[u] >> j) & 1u) {
-          if (ldict) {  // the dictionary in LDS (LvDictOut::page): no global load to wait for
+          if constexpr (LDSD) {  // the dictionary in LDS (LvDictOut::page): no global load to wait for
             if constexpr (ES == 8)
               t = (uint64_t)ldict[2 * id[u][j]] | ((uint64_t)ldict[2 * id[u][j] + 1] << 32);
             else
@@ -1663,6 +1663,116 @@ __device__ inline uint32_t lv_write_dict(const LvRuns& rl, const uint32_t* stage
   return bad;
 }
 
+// lv_write_dict for windows of long runs (average >= 64 outputs, random indices give bit-packed
+// runs of 504), the dictionary in LDS: run by run, the wave's lanes take the run's whole 16-byte
+// groups, each read with one 8-byte stage load (V indices of w <= 8 bits) and V LDS gathers (RLE
+// runs: one gather, the same 16 bytes stored); no per-output run search. The groups a run
+// boundary or the window's ends cut (at most R + 1) then go one per lane, output by output.
+template <int ES>
+__device__ __forceinline__ uint32_t lv_write_dict_runs(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
+                                              uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo,
+                                              uint32_t ndict, const uint32_t* ldict, gptr<uint8_t> __restrict__ out) {
+  using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
+  constexpr uint32_t V = 16u / ES;
+  constexpr uint32_t U = 4;  // (80 VGPRs for the kernel with the U = 2 of lv_write_dict: 6 waves per SIMD)
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
+  const uint64_t go = x.s.out;
+  uint32_t bad = 0;
+  auto gather = [&](uint32_t idx) -> T {
+    if constexpr (ES == 8) return (uint64_t)ldict[2 * idx] | ((uint64_t)ldict[2 * idx + 1] << 32);
+    else return ldict[idx];
+  };
+  auto pack = [&](const T* f) -> uint4 {
+    if constexpr (ES == 8)
+      return make_uint4((uint32_t)f[0], (uint32_t)(f[0] >> 32), (uint32_t)f[1], (uint32_t)(f[1] >> 32));
+    else
+      return make_uint4(f[0], f[1], f[2], f[3]);
+  };
+#pragma unroll 1
+  for (uint32_t b = 0; b < rl.R; ++b) {  // (wave-uniform)
+    const uint32_t rs = rl.rstart[b], re = rl.rstart[b + 1], inf = rl.rinfo[b];
+    const uint32_t st = rs > base ? rs : base, en = re < endo ? re : endo;
+    if (st >= en) continue;
+    const uint64_t g0 = (go + st + V - 1) / V, g1 = (go + en) / V;  // groups inside [st, en)
+    if (g0 >= g1) continue;
+    if (inf & R_RLE) {
+      const uint32_t idx = inf & 0x7FFFFFFFu;
+      bad |= idx >= ndict ? 1u : 0u;
+      T f[V];
+#pragma unroll
+      for (uint32_t j = 0; j < V; ++j) f[j] = idx < ndict ? gather(idx) : (T)0;
+      const uint4 v = pack(f);
+      for (uint64_t k = g0 + lane; k < g1; k += WAVE) gst16(out + k * 16u, v);
+      continue;
+    }
+    const uint64_t bit0 = (uint64_t)inf * 8ull;
+#pragma unroll 1
+    for (uint64_t kb = g0 + lane; kb < g1; kb += (uint64_t)WAVE * U) {
+      T f[U][V];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint64_t k = kb + (uint64_t)u * WAVE;
+        if (k >= g1) continue;
+        const uint32_t o = (uint32_t)(k * V - go);  // page-relative first output of the group
+        const uint64_t bit = bit0 + (uint64_t)(o - rs) * w;
+        const uint64_t x8 = lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u);
+#pragma unroll
+        for (uint32_t j = 0; j < V; ++j) {
+          const uint32_t idx = (uint32_t)(x8 >> (j * w)) & wm;
+          bad |= idx >= ndict ? 1u : 0u;
+          f[u][j] = idx < ndict ? gather(idx) : (T)0;
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint64_t k = kb + (uint64_t)u * WAVE;
+        if (k < g1) gst16(out + k * 16u, pack(f[u]));
+      }
+    }
+  }
+  // cut groups: the one holding each boundary q (base, every inner run start, endo) not on a
+  // group edge; consecutive boundaries in one group take it once
+  uint32_t lgn = 1;
+  while (lgn * 2u <= rl.R) lgn *= 2u;
+  auto qpos = [&](uint32_t c) -> uint64_t {  // boundary c in global outputs (c = 0: base, R: endo)
+    const uint32_t p = c == 0 ? base : c >= rl.R ? endo : rl.rstart[c];
+    return go + (p < base ? base : p > endo ? endo : p);
+  };
+#pragma unroll 1
+  for (uint32_t c0 = 0; c0 <= rl.R; c0 += WAVE) {
+    const uint32_t c = c0 + lane;
+    if (c > rl.R) continue;
+    const uint64_t q = qpos(c);
+    if (q % V == 0) continue;
+    const uint64_t k = q / V;
+    if (c > 0) {
+      const uint64_t qp = qpos(c - 1);
+      if (qp % V != 0 && qp / V == k) continue;  // (taken by the previous boundary's lane)
+    }
+    uint32_t a = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < V; ++j) {
+      const uint64_t gl = k * V + j;
+      if (gl < go + base || gl >= go + endo) continue;
+      const uint32_t o = (uint32_t)(gl - go);
+      for (uint32_t sp = lgn; sp; sp >>= 1)
+        if (a + sp < rl.R && rl.rstart[a + sp] <= o) a += sp;
+      const uint32_t inf = rl.rinfo[a];
+      uint32_t idx;
+      if (inf & R_RLE) {
+        idx = inf & 0x7FFFFFFFu;
+      } else {
+        const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[a]) * w;
+        idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+      }
+      bad |= idx >= ndict ? 1u : 0u;
+      reinterpret_cast<gptr<T>>(out)[gl] = idx < ndict ? gather(idx) : (T)0;
+    }
+  }
+  return bad;
+}
+
 // What the walked-page emit writes: levels / booleans, or dictionary values. page() takes the
 // per-page state (the chunk's buffer and parameters) when the emit moves to another page, so
 // that a window's writes start without a dependent load.
@@ -1687,7 +1797,7 @@ struct LvLevelOut {
 // decoded): per output the entry's index, in the value-length slot (the byte-array scan and copy,
 // pqg_bytes.hip BaSrc, take the entry's address and length from there), and the page's byte total.
 // Scratch slots: the chunk's scr_base (values) and dscr_base (dictionary entries) on.
-__device__ inline void lv_write_badict(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
+__device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                                        const LvWin& x, uint32_t base, uint32_t endo, const ChunkWork& ck,
                                        PageWork* pages, ChunkWork* chunks, const uint64_t* __restrict__ dsrc0,
                                        const uint32_t* __restrict__ dlen0, uint64_t* __restrict__ vsrc0,
@@ -1768,7 +1878,7 @@ struct LvDictOut {
   uint32_t ndict;
   int es;
   bool lds;  // the page's dictionary (or entry lengths) is in the wave's LDS words
-  __device__ void page(const ChunkWork& c, const PageWork* pages, const uint8_t* blob, int, uint32_t* xw) {
+  __device__ __forceinline__ void page(const ChunkWork& c, const PageWork* pages, const uint8_t* blob, int, uint32_t* xw) {
     ck = &c;
     es = c.es;
     val_out = c.val_out;
@@ -1790,22 +1900,25 @@ struct LvDictOut {
     }
     wave_lds_sync();
   }
-  __device__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
-                             const LvWin& x, uint32_t base, uint32_t endo, int, const ChunkWork* chunks,
-                             PageWork* pages, const uint32_t* xw) const {
+  __device__ __forceinline__ void operator()(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob,
+                                             uint64_t blob_len, const LvWin& x, uint32_t base, uint32_t endo, int,
+                                             const ChunkWork* chunks, PageWork* pages, const uint32_t* xw) const {
     if (es == 0) {
       lv_write_badict(rl, stage, blob, blob_len, x, base, endo, *ck, pages, const_cast<ChunkWork*>(chunks), dsrc, dlen,
                       vsrc, vlen, lds ? xw : nullptr);
       return;
     }
-    const uint64_t da = (uint64_t)(dict - blob);
     uint32_t bad;
-    if (es == 8)
-      bad = lv_write_dict<8>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 8) == 0, lds ? xw : nullptr,
-                             gp(val_out));
-    else
-      bad = lv_write_dict<4>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, (da % 4) == 0, lds ? xw : nullptr,
-                             gp(val_out));
+    if ((uint64_t)(endo - base) >= 64ull * rl.R && x.s.w <= 8) {  // long runs: run by run
+      bad = es == 8 ? lv_write_dict_runs<8>(rl, stage, blob, blob_len, x, base, endo, ndict, xw, gp(val_out))
+                    : lv_write_dict_runs<4>(rl, stage, blob, blob_len, x, base, endo, ndict, xw, gp(val_out));
+    } else if (!lds) {  // (the host puts only dictionaries of <= 2^8 entries on this path: they fit)
+      bad = 0;
+      if ((threadIdx.x & 63u) == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)x.p, ST_INVALID_ARG);
+    } else {
+      bad = es == 8 ? lv_write_dict<8, true>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, true, xw, gp(val_out))
+                    : lv_write_dict<4, true>(rl, stage, blob, blob_len, x, base, endo, dict, ndict, true, xw, gp(val_out));
+    }
     if (__ballot(bad) && (threadIdx.x & 63u) == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)x.p, ST_PANIC);
   }
 };

@@ -136,6 +136,8 @@ void read_schema_element(Reader& r, SchemaNode& s) {
       case 4: s.name = r.binary(); break;
       case 5: s.num_children = r.i32(); break;
       case 6: s.converted_type = r.i32(); break;
+      case 7: s.scale = r.i32(); break;
+      case 8: s.precision = r.i32(); break;
       default: r.skip(t);
     }
   }

@@ -22,6 +22,7 @@ struct SchemaNode {
   int repetition = 0;       // 0 REQUIRED, 1 OPTIONAL, 2 REPEATED
   int num_children = 0;
   int converted_type = -1;
+  int scale = 0, precision = 0;  // DECIMAL
 };
 
 struct LeafColumn {

@@ -86,7 +86,8 @@ EXPORTS = [
     "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
     "pqg_space_values", "pqg_rg_ctx_create", "pqg_rg_ctx_destroy", "pqg_rg_decode", "pqg_rg_sync",
     "pqg_rg_sync_call", "pqg_rg_error_message", "pqg_rgr_open", "pqg_rgr_close", "pqg_rgr_submit",
-    "pqg_rgr_wait", "pqg_rgr_column", "pqg_rgr_get_stats", "pqg_rgr_error",
+    "pqg_rgr_wait", "pqg_rgr_column", "pqg_rgr_get_stats", "pqg_rgr_error", "pqg_row_iter_open",
+    "pqg_row_iter_open_fields", "pqg_row_iter_close", "pqg_row_iter_next", "pqg_row_iter_error",
 ]
 
 _lib = None
@@ -161,6 +162,14 @@ def lib():
         L.pqg_rgr_get_stats.argtypes = [vp, C.POINTER(RgrStats)]
         L.pqg_rgr_error.argtypes = [vp]
         L.pqg_rgr_error.restype = C.c_char_p
+        L.pqg_row_iter_open.argtypes = [vp, i32, vp, C.c_size_t, C.POINTER(vp)]
+        L.pqg_row_iter_open_fields.argtypes = [vp, i32, vp, C.c_size_t, C.POINTER(C.c_char_p), C.c_uint32,
+                                               C.POINTER(vp)]
+        L.pqg_row_iter_close.argtypes = [vp]
+        L.pqg_row_iter_close.restype = None
+        L.pqg_row_iter_next.argtypes = [vp, i32, vp, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_int)]
+        L.pqg_row_iter_error.argtypes = [vp]
+        L.pqg_row_iter_error.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -528,6 +537,54 @@ class RowGroupReader:
         s = RgrStats()
         lib().pqg_rgr_get_stats(self.h, C.byref(s))
         return {k: getattr(s, k) for k, _ in RgrStats._fields_}
+
+
+class RowIter:
+    """RowIter (record/reader.rs:588-717) over GPU-decoded column chunks: iterate to get rows as
+    parsed JSON ([[name, field], ...], fields {"Kind": value} or None) or, with display=True, the
+    reference's Display text."""
+
+    def __init__(self, reader, ctx, row_group=-1, batch_size=1024, display=False, fields=None):
+        self.reader = reader
+        self.h = C.c_void_p()
+        if fields is None:
+            st = lib().pqg_row_iter_open(reader.h, row_group, ctx.h, batch_size, C.byref(self.h))
+        else:
+            arr = (C.c_char_p * max(len(fields), 1))(*[f.encode() for f in fields])
+            st = lib().pqg_row_iter_open_fields(reader.h, row_group, ctx.h, batch_size, arr, len(fields),
+                                                C.byref(self.h))
+        if st:
+            raise PqgError(st, reader.error() if fields is not None else "pqg_row_iter_open")
+        self.fmt = 0 if display else 1
+        self.buf = C.create_string_buffer(1 << 16)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pqg_row_iter_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        import json
+        n, has = C.c_size_t(), C.c_int()
+        st = lib().pqg_row_iter_next(self.h, self.fmt, self.buf, len(self.buf), C.byref(n), C.byref(has))
+        if st == CAPACITY:
+            self.buf = C.create_string_buffer(n.value + 1)
+            st = lib().pqg_row_iter_next(self.h, self.fmt, self.buf, len(self.buf), C.byref(n), C.byref(has))
+        if st:
+            raise PqgError(st, lib().pqg_row_iter_error(self.h).decode(errors="replace"))
+        if not has.value:
+            raise StopIteration
+        text = self.buf.raw[:n.value].decode("utf-8", errors="surrogateescape")
+        return text if self.fmt == 0 else json.loads(text)
 
 
 class ColumnReader:
