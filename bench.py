@@ -269,10 +269,13 @@ def time_steps(ctx, w, stream, steps, warmup, dist=None):
     return (t1 - t0) / steps
 
 
-def time_stages(pqgpu, ctx, w, stream, n):
+def time_stages(pqgpu, ctx, w, stream, n, overlap):
     """Average stage / dominant-kernel device times over n decodes with HIP events on the decode
-    stream (the same kernel sequence as the production path)."""
+    stream. The stages are timed one after the other (pqg_ctx_set_overlap 0: the PLAIN copy after
+    the level path, not beside it on the side stream), so that each kernel's time and roofline are
+    its own; the step time (`value`) is the production path with the overlap."""
     ctx.set_timing(True)
+    ctx.set_overlap(False)
     pqgpu.lib().pqg_reset_timings(ctx.h)
     for _ in range(n):
         decode_once(ctx, w, stream)
@@ -280,6 +283,7 @@ def time_stages(pqgpu, ctx, w, stream, n):
     assert st == 0, (st, bad, ctx.error_message())
     tm = ctx.timings()
     ctx.set_timing(False)
+    ctx.set_overlap(overlap)
     return tm
 
 
@@ -420,7 +424,7 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
     w = Workload(pqgpu, args, rank, kind, p_null=p_null)
     checked = check_values(ctx, w, stream)
     per_step = max_over_ranks(time_steps(ctx, w, stream, steps, warmup, dist), dist)
-    tm = time_stages(pqgpu, ctx, w, stream, max(3, steps // 4))
+    tm = time_stages(pqgpu, ctx, w, stream, max(3, steps // 4), args.overlap)
     units = w.levels if kind == "levels" else w.values
     step_bytes = w.in_bytes + w.out_bytes
     variant = None
@@ -455,6 +459,9 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": dom,
         "roofline_stages": rl if len(rl) > 1 else None,
+        "stages_note": ("stage and kernel times from HIP events with the stages one after the other "
+                        "(pqg_ctx_set_overlap 0); ms_per_step is the production path, PLAIN copy beside "
+                        "the level decode" if kind == "levels" and args.overlap else None),
         "stages_ms": {"prepare": tm.prepare_ms, "levels": tm.levels_ms, "scan": tm.scan_ms,
                       "values": tm.values_ms, "total": tm.total_ms,
                       "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},

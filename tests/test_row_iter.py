@@ -190,8 +190,10 @@ def _plain(v):
         return [(_plain(a), _plain(b)) for a, b in x]
     if k == "Bytes":
         return bytes(x)
-    if k in ("Float", "Double"):
-        return float(x) if not isinstance(x, str) else float(x)
+    if k == "Float":  # (the f32's shortest text: back to the f32, then widened as pyarrow widens it)
+        return float(np.float32(float(x)))
+    if k == "Double":
+        return float(x)
     return x
 
 
