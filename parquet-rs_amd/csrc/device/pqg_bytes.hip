@@ -517,6 +517,18 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWor
 //  - longer values are copied value by value, 8 bytes at a time.
 __device__ inline uint32_t ba_pad(uint32_t j) { return j + (j >> 4); }
 
+// Small dictionaries of the level path's byte-array chunks take k_ba_copy_sd (below).
+constexpr uint32_t BSD_N = 1024;
+constexpr uint32_t BSD_BYTES = 12288;
+constexpr uint32_t BSD_IMG = WG * 16;  // round image (longer rounds: byte stores from LDS)
+
+__device__ inline bool ba_small_dict(const PageWork& pw, const ChunkWork& ck, const PageWork* pages) {
+  if (!(pw.encoding == E_RLE_DICTIONARY && ck.lvdict && ck.dict_page >= 0)) return false;
+  const PageWork& dp = pages[ck.dict_page];
+  return dp.num_values <= BSD_N && dp.nbytes <= BSD_BYTES;
+}
+
+
 constexpr uint32_t BA_RV = 4;                     // values per thread per staged round
 constexpr uint32_t BA_RN = BA_RV * WG;            // values per round
 constexpr uint32_t BA_SMALL = 16;                 // longest value the staged rounds take
@@ -550,7 +562,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pw, ck)) return;
+  if (!ba_page_ok(pw, ck) || ba_small_dict(pw, ck, pages)) return;  // (small dictionaries: k_ba_copy_sd)
   const uint32_t t = gt - pw.ltile0;
   const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
   const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
@@ -684,6 +696,98 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
   }
 }
 
+// k_ba_copy for the dictionary pages of the level path's chunks whose dictionary is small (at most
+// BSD_N entries in at most BSD_BYTES bytes: short categorical strings): the dictionary page's bytes
+// and its entries' offsets and lengths are staged in LDS, so a value's length and bytes cost LDS
+// reads only; the only global loads are the values' indices (coalesced, all 16 in flight at once).
+// The tile goes in rounds of WG values (lane l: value k * WG + l): a workgroup scan of the round's
+// lengths gives its offsets (stored coalesced) and its bytes are assembled in an LDS image of the
+// round's output and stored with 16-byte stores. The general kernel exits for these tiles.
+__global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
+                                                   const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                                   const uint32_t* __restrict__ tl, const uint32_t* __restrict__ vlen0,
+                                                   const uint64_t* __restrict__ dsrc0, const uint32_t* __restrict__ dlen0,
+                                                   const uint64_t* __restrict__ tsum) {
+  __shared__ __attribute__((aligned(16))) uint8_t ldict[BSD_BYTES + 16];
+  __shared__ uint32_t doff[BSD_N], dln[BSD_N];
+  __shared__ __attribute__((aligned(16))) uint8_t img[BSD_IMG + 32];
+  __shared__ uint32_t wsum[WG / 64];
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
+  const PageWork pw = pages[p];
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!ba_page_ok(pw, ck) || !ba_small_dict(pw, ck, pages)) return;
+  const uint32_t t = gt - pw.ltile0;
+  const uint64_t n = pw.nonnull, vo = pw.value_out;
+  const uint64_t t0 = (uint64_t)t * BA_T;
+  if (t0 >= n) return;
+  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
+  const uint32_t* vlen = vlen0 + ck.scr_base;
+  // the tile's indices, all loads in flight (lane l: values k * WG + l)
+  uint32_t idx[BA_VPT];
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint32_t j = k * WG + tid;
+    idx[k] = j < cnt ? vlen[vo + t0 + j] : 0u;
+  }
+  // the dictionary page and its entries into LDS
+  const PageWork& dp = pages[ck.dict_page];
+  const uint32_t nd = dp.num_values, nb = dp.nbytes;
+  for (uint32_t i = tid; i < nb; i += WG) ldict[i] = blob[dp.base + i];
+  for (uint32_t i = tid; i < nd; i += WG) {
+    doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - dp.base);
+    dln[i] = dlen0[ck.dscr_base + i];
+  }
+  __syncthreads();
+  uint64_t run = tsum[gt];  // output byte offset of the round's first value
+#pragma unroll 1
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint32_t j = k * WG + tid;
+    if (k * WG >= cnt) break;
+    const bool in = j < cnt;
+    const uint32_t ln = in ? dln[idx[k]] : 0u;
+    uint32_t incl = ln;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+      if (lane >= (uint32_t)off) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t pre = incl - ln, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WG / 64; ++w) {
+      if (w < wv) pre += wsum[w];
+      tot += wsum[w];
+    }
+    if (in) offsets[vo + t0 + j] = (int64_t)(run + pre);
+    const uint64_t gA = run, gB = run + tot;
+    const uint32_t sh = (uint32_t)(gA & 15u);
+    if (tot + 16 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is
+      const uint32_t b0 = pre + sh, so = in ? doff[idx[k]] : 0u;
+      for (uint32_t q = 0; q < ln; ++q) img[b0 + q] = ldict[so + q];
+      __syncthreads();
+      const uint64_t c0 = gA & ~15ull;
+      for (uint64_t c = c0 + (uint64_t)tid * 16u; c < gB; c += (uint64_t)WG * 16u) {
+        const uint32_t ii = (uint32_t)(c - c0);
+        if (c >= gA && c + 16 <= gB) {
+          gst16(out + c, *reinterpret_cast<const uint4*>(img + ii));
+        } else {
+          for (uint32_t q = 0; q < 16; ++q)
+            if (c + q >= gA && c + q < gB) out[c + q] = img[ii + q];
+        }
+      }
+    } else if (in) {  // long values: straight from the LDS dictionary
+      const uint32_t so = doff[idx[k]];
+      for (uint32_t q = 0; q < ln; ++q) out[gA + pre + q] = ldict[so + q];
+    }
+    run += tot;
+    __syncthreads();  // (wsum and the image are reused by the next round)
+  }
+}
+
 // DELTA_BYTE_ARRAY values (decoding.rs:788-822), one wave per page: the previous value lives
 // in LDS; value i overwrites bytes [prefix_i, prefix_i + suffix_len) of it and is then
 // streamed to the output.
@@ -765,9 +869,9 @@ hipError_t pqg_launch_badict_general(const uint8_t* blob, uint64_t blob_len, Pag
 // DELTA_BYTE_ARRAY pages, page byte offsets, then the tiled copy over the listed tiles (the tiles
 // of the byte-array pages) and the DELTA_BYTE_ARRAY rebuild.
 hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
-                            const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, uint64_t* vsrc,
-                            uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* tsum,
-                            hipStream_t s) {
+                            const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, bool has_lvdict,
+                            uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen,
+                            uint64_t* tsum, hipStream_t s) {
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
   if (ntl) {
@@ -775,8 +879,10 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
                        tsum);
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
     hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vsrc, vlen,
-                       dsrc, dlen,
-                       tsum);
+                       dsrc, dlen, tsum);
+    if (has_lvdict)
+      hipLaunchKernelGGL(k_ba_copy_sd, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vlen,
+                         dsrc, dlen, tsum);
   }
   if (has_dba)
     hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, chunks, vsrc, vlen, vpre);

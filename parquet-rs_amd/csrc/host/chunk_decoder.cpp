@@ -55,8 +55,8 @@ hipError_t pqg_launch_badict_general(const uint8_t*, uint64_t, PageWork*, int, C
                                      const uint32_t*, uint32_t, RunTables, uint64_t*, uint32_t*, uint64_t*, uint32_t*,
                                      int, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
-                            uint32_t, bool, uint64_t*, uint32_t*, uint32_t*, const uint64_t*, const uint32_t*, uint64_t*,
-                            hipStream_t);
+                            uint32_t, bool, bool, uint64_t*, uint32_t*, uint32_t*, const uint64_t*, const uint32_t*,
+                            uint64_t*, hipStream_t);
 }
 
 // Stream kinds of the hybrid-stream tables: def, rep, dictionary indices, RLE booleans.
@@ -916,7 +916,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
              "byte-array dictionary indices");
     if (any_ba) {
       if (!ctx->values_kernel) ctx->values_kernel = any_dba ? PQG_DELTA_BYTE_ARRAY : PQG_PLAIN;
-      HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba,
+      HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba, ba_lv,
                               sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, s),
              "byte arrays");
     }
