@@ -73,7 +73,7 @@ def parse(argv=None):
     ap.add_argument("--at-batch", default="step", choices=["step", "rg"],
                     help="alltypes: one pqg_decode_chunks over every chunk of the step (step) or one "
                          "pqg_rg_decode per row group on two alternating streams (rg)")
-    ap.add_argument("--overlap", type=int, default=1,
+    ap.add_argument("--overlap", type=int, default=0,
                     help="speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / partition / reduction plumbing only (gloo, no GPU, no value)")

@@ -482,40 +482,69 @@ __global__ void __launch_bounds__(WG) k_plain_copy(const uint8_t* __restrict__ b
   const uint64_t dend = dst + nbytes;
   const uint64_t c0 = dst & ~15ull;
   // PC_U chunks per lane per step (WG * 16 bytes apart: each wave-instruction stays contiguous),
-  // their loads all issued before the stores
+  // their loads all issued before the stores. A chunk's 16 source bytes start sh bytes into an
+  // aligned 16-byte source chunk (the same sh for every chunk of the page): each lane loads its
+  // aligned chunk with one 16-byte load and takes the next one from the lane above (DPP wave
+  // shift; lane 63 loads it), then v_alignbyte picks the 16 bytes.
   constexpr uint32_t PC_U = 4;
   const uint64_t stepb = (uint64_t)WG * 16ull;
-  for (uint64_t cb = c0 + (uint64_t)blockIdx.x * stepb * PC_U + threadIdx.x * 16ull; cb < dend;
-       cb += (uint64_t)gridDim.x * stepb * PC_U) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t sh = (uint32_t)((src - dst) & 15u), q4 = sh >> 2, r8 = (sh & 3u);
+  const uint64_t wbase = c0 + (uint64_t)(threadIdx.x >> 6) * 1024u;  // (wave-uniform: the loop below is too)
+  for (uint64_t cw = wbase + (uint64_t)blockIdx.x * stepb * PC_U; cw < dend; cw += (uint64_t)gridDim.x * stepb * PC_U) {
     uint4 v[PC_U];
     bool full[PC_U];
+    uint4 A[PC_U], N[PC_U];
 #pragma unroll
     for (uint32_t u = 0; u < PC_U; ++u) {
-      const uint64_t c = cb + u * stepb;
+      const uint64_t c = cw + u * stepb + lane * 16u;
       full[u] = c >= dst && c + 16 <= dend;
-      if (!full[u]) continue;
-      const uint64_t s = src + (c - dst);
-      const uint64_t sal = s & ~3ull;
-      const uint32_t sh = (uint32_t)(s - sal);
-      uint32_t w[5];
-      if (sal + 20 <= blob_len) {
-        const uint32_t* sp = reinterpret_cast<const uint32_t*>(blob + sal);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) w[k] = __builtin_nontemporal_load(sp + k);
+      const uint64_t a = src + (c - dst) - sh;  // aligned source chunk (wraps below the blob: guarded)
+      if (a + 16 <= blob_len) {
+        const pqg_u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const pqg_u32x4*>(blob + a));
+        A[u] = make_uint4(t[0], t[1], t[2], t[3]);
       } else {
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          w[k] = gbyte(blob, blob_len, sal + 4 * k) | (gbyte(blob, blob_len, sal + 4 * k + 1) << 8) |
-                 (gbyte(blob, blob_len, sal + 4 * k + 2) << 16) | (gbyte(blob, blob_len, sal + 4 * k + 3) << 24);
+        A[u] = gload_u128_tail(blob, blob_len, a);
       }
-      v[u].x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-      v[u].y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-      v[u].z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-      v[u].w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+      if (lane == 63u && sh) N[u] = a + 32 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a + 16)
+                                                       : gload_u128_tail(blob, blob_len, a + 16);
     }
 #pragma unroll
     for (uint32_t u = 0; u < PC_U; ++u) {
-      const uint64_t c = cb + u * stepb;
+      if (sh == 0) {
+        v[u] = A[u];
+        continue;
+      }
+      uint4 n;  // lane + 1's aligned chunk (DPP wave_shl:1)
+      n.x = (uint32_t)__builtin_amdgcn_update_dpp((int)N[u].x, (int)A[u].x, 0x130, 0xf, 0xf, false);
+      n.y = (uint32_t)__builtin_amdgcn_update_dpp((int)N[u].y, (int)A[u].y, 0x130, 0xf, 0xf, false);
+      n.z = (uint32_t)__builtin_amdgcn_update_dpp((int)N[u].z, (int)A[u].z, 0x130, 0xf, 0xf, false);
+      n.w = (uint32_t)__builtin_amdgcn_update_dpp((int)N[u].w, (int)A[u].w, 0x130, 0xf, 0xf, false);
+      const uint32_t w[8] = {A[u].x, A[u].y, A[u].z, A[u].w, n.x, n.y, n.z, n.w};
+      uint32_t o[4];
+      switch (q4) {  // (wave-uniform)
+        case 0:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r8);
+          break;
+        case 1:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], r8);
+          break;
+        case 2:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(w[j + 3], w[j + 2], r8);
+          break;
+        default:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(w[j + 4], w[j + 3], r8);
+          break;
+      }
+      v[u] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PC_U; ++u) {
+      const uint64_t c = cw + u * stepb + lane * 16u;
       if (full[u]) {
         gst16(out + c, v[u]);
       } else if (c < dend) {  // a chunk shared with a neighbouring page: its bytes only
@@ -676,14 +705,13 @@ hipError_t pqg_launch_plain(const uint8_t* blob, uint64_t blob_len, PageWork* pa
 // `side` (mode 1), launched after k_prepare; the re-copy of flagged chunks (mode 2) on `s` once the
 // offset scan has run there and the side stream's copy is joined.
 hipError_t pqg_launch_plain_spec(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
-                                 ChunkWork* chunks, const uint32_t* pl, uint32_t npl, uint64_t max_bytes,
+                                 ChunkWork* chunks, const uint32_t* pl, uint32_t npl, uint32_t gx,
                                  hipStream_t side) {
   hipLaunchKernelGGL(k_spec_scan, dim3(1), dim3(WG), 0, side, pages, chunks, npages);
-  // one workgroup per page: the copy holds a few workgroups per CU and leaves the rest of the
+  // gx workgroups per page: the copy holds a few workgroups per CU and leaves the rest of the
   // chip to the level decode it runs beside (a full-size grid takes every CU and the level
   // kernels wait for it)
-  (void)max_bytes;
-  hipLaunchKernelGGL(k_plain_copy, dim3(1, npl), dim3(WG), 0, side, blob, blob_len, pages, chunks, pl, 1);
+  hipLaunchKernelGGL(k_plain_copy, dim3(gx, npl), dim3(WG), 0, side, blob, blob_len, pages, chunks, pl, 1);
   return hipGetLastError();
 }
 

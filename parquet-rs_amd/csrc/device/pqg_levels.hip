@@ -1077,6 +1077,92 @@ __device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV
   wave_lds_sync();
 }
 
+// Speculative parallel walk of the chain from window position e0 over the segment tables: lane s
+// guesses the chain's first position in segment s (q; valid: one lies in the segment) by walking
+// at most LV_SPK segments — from e0 for the lanes up to LV_SPK segments past e0's, else from the
+// first byte of segment s - LV_SPK (chains entering at different positions mostly meet within a
+// few headers) — and r = its table entry, c its outputs, inc the inclusive sum of c over the
+// lanes. The guesses are checked: each one's exit is the next valid lane's guess (leaving the
+// window: there is none), for the lanes whose outputs start below lim (the walk's stop). A chain
+// that never meets the true one (payload bytes parsed in another phase) makes its lane's guess
+// wrong: then every lane walks again from the guess of the valid lane before it, up to LV_SPR
+// rounds (a wrong guess between right ones is put right by one). When the check passes, the
+// valid guesses are the chain (by induction from e0's segment, whose guess is e0), found with
+// ~LV_SPK dependent table reads instead of one per segment. Returns false if it never passes.
+constexpr uint32_t LV_SPK = 4;  // segments walked per guess
+constexpr uint32_t LV_SPR = 4;  // repair rounds
+
+__device__ inline bool lv_spec_chain(const LvWave& W, uint32_t e0, uint64_t lim, uint32_t& q, bool& valid, uint2& r,
+                                     uint64_t& inc) {
+  const uint32_t lane = threadIdx.x & 63u, lo = lane * LV_SEG;
+  q = lane <= e0 / LV_SEG + LV_SPK ? e0 : lo - LV_SPK * LV_SEG;
+#pragma unroll 1
+  for (uint32_t round = 0;; ++round) {
+#pragma unroll
+    for (uint32_t it = 0; it < LV_SPK; ++it)
+      if (q < lo) q = W.JC[(q % LV_SEG) * WAVE + q / LV_SEG].x & 0xFFFFu;  // (exits and codes >= LV_WIN stop)
+    valid = q >= lo && q < lo + LV_SEG;
+    r = valid ? W.JC[(q - lo) * WAVE + lane] : make_uint2(LV_J_END, 0u);
+    const uint64_t vm = __ballot(valid);
+    const uint64_t after = lane == 63u ? 0ull : vm & (~0ull << (lane + 1u));
+    const uint32_t nxt = after ? (uint32_t)__builtin_ctzll(after) : 64u;
+    const uint32_t gn = (uint32_t)__shfl((int)q, (int)(nxt & 63u), 64);
+    const uint32_t xq = r.x & 0xFFFFu;
+    const bool okl = xq < LV_WIN ? nxt < 64u && gn == xq : nxt == 64u;
+    const uint32_t c = valid ? r.y : 0u;
+    inc = wave_incl_scan_cnt(c);
+    if (!__any(valid && inc - c < lim && inc < lim && !okl)) return true;
+    if (round == LV_SPR) return false;
+    // repair: from the guess of the valid lane before this one (e0 for the lanes before any)
+    const uint64_t before = vm & ((1ull << lane) - 1ull);
+    const int pv = before ? 63 - __builtin_clzll(before) : 0;
+    const uint32_t gp = (uint32_t)__shfl((int)q, pv, 64);
+    q = before ? gp : e0;
+  }
+}
+
+// A wave's contiguous range [g0, g1) of the dense pages' windows (wbase2): the page is found once
+// and then advanced with the window, its stream parsed once per page (a grid-stride loop paid a
+// binary search and the page's dependent loads per window).
+struct LvDense {
+  uint32_t g0, g1, pb, pend, wb;
+  bool ok;
+  __device__ inline void page(const uint8_t* blob, const PageWork* pages, const ChunkWork* chunks, int sel,
+                              const RunTables& rt, const LevelTables& lt, LvWin& x) {
+    pend = lt.wbase2[x.p + 1];
+    wb = lt.wbase[x.p];
+    ok = pend > pb && rt.pflag[x.p] == PF_PAGE && lv_stream(blob, pages[x.p], sel, chunks, x.s);
+  }
+  __device__ inline bool begin(const uint8_t* blob, const PageWork* pages, int npages, const ChunkWork* chunks, int sel,
+                               const RunTables& rt, const LevelTables& lt, LvWin& x) {
+    const uint32_t total = lt.wbase2[npages];
+    const uint32_t nwv = gridDim.x * (WG / WAVE), gw = blockIdx.x * (WG / WAVE) + rfl(threadIdx.x >> 6);
+    const uint32_t per = (total + nwv - 1u) / nwv;
+    g0 = gw * per;
+    g1 = min(total, g0 + per);
+    if (g0 >= g1) return false;
+    x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g0);
+    pb = lt.wbase2[x.p];
+    page(blob, pages, chunks, sel, rt, lt, x);
+    return true;
+  }
+  // window g2 (>= the last one asked): x.p / x.k / x.s set; false for a page off the window path
+  __device__ inline bool at(const uint8_t* blob, const PageWork* pages, const ChunkWork* chunks, int sel,
+                            const RunTables& rt, const LevelTables& lt, LvWin& x, uint32_t& g2) {
+    while (g2 >= pend) {
+      ++x.p;
+      pb = pend;
+      page(blob, pages, chunks, sel, rt, lt, x);
+    }
+    if (!ok) {
+      g2 = pend - 1u;
+      return false;
+    }
+    x.k = g2 - pb;
+    return true;
+  }
+};
+
 // ------------------------------------------------------------------------------ k_lv_win
 // Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -1085,14 +1171,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ LvSmem sm;
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
-  const uint32_t total = lt.wbase2[npages];
-  for (uint32_t g2 = blockIdx.x * (WG / WAVE) + wid; g2 < total; g2 += gridDim.x * (WG / WAVE)) {
-    LvWin x;
-    x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
-    const PageWork& pw = pages[x.p];
-    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, chunks, x.s)) continue;
-    x.k = g2 - lt.wbase2[x.p];
-    const uint32_t g = lt.wbase[x.p] + x.k;
+  LvDense D;
+  LvWin x;
+  if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
+  for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
+    if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
+    const uint32_t g = D.wb + x.k;
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w;
     lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
@@ -1103,14 +1187,46 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       uint32_t pc[LV_SEG], pv[LV_SEG], bpm;
       lv_seg_build(W, x, pc, pv, bpm);
       uint32_t e = lane, hs = 0, c = 0;
+      // the chain from position 0, speculatively (lv_spec_chain); each entry's chain is then
+      // followed only until it meets it, the rest from the chain's per-segment suffix sums
+      uint32_t q;
+      bool valid;
+      uint2 r;
+      uint64_t ci;
+      const bool spec = lv_spec_chain(W, 0u, ~0ull, q, valid, r, ci);
+      uint32_t* sp = W.stage;  // (staged bytes no longer needed): chain position, header and output suffixes
+      uint32_t exitc = LV_J_END;
+      if (spec) {
+        const uint32_t h = valid ? (uint32_t)__builtin_popcount(r.x >> 16) : 0u, cc = valid ? r.y : 0u;
+        const uint32_t hi = wave_incl_scan_u32(h);
+        const uint32_t htot = (uint32_t)__shfl((int)hi, 63, 64);
+        const uint64_t ctot = __shfl(ci, 63, 64);
+        const uint64_t vm = __ballot(valid);
+        exitc = (uint32_t)__shfl((int)(r.x & 0xFFFFu), 63 - __builtin_clzll(vm), 64);  // (lane 0 is valid)
+        const uint64_t cs = ctot - ci + cc;
+        sp[lane] = valid ? q : LV_NONE;
+        sp[64 + lane] = htot - hi + h;
+        sp[128 + lane] = cs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cs;
+        wave_lds_sync();
+      }
 #pragma unroll 1
       while (__any(e < LV_WIN)) {
         if (e < LV_WIN) {
-          const uint2 r = W.JC[(e % LV_SEG) * WAVE + e / LV_SEG];
-          hs += (uint32_t)__builtin_popcount(r.x >> 16);
-          const uint32_t s2 = c + r.y;
+          const uint32_t sg = e / LV_SEG;
+          uint32_t dh, dc;
+          if (spec && sp[sg] == e) {  // on the chain from 0: its rest
+            dh = sp[64 + sg];
+            dc = sp[128 + sg];
+            e = exitc;
+          } else {
+            const uint2 t = W.JC[(e % LV_SEG) * WAVE + sg];
+            dh = (uint32_t)__builtin_popcount(t.x >> 16);
+            dc = t.y;
+            e = t.x & 0xFFFFu;
+          }
+          hs += dh;
+          const uint32_t s2 = c + dc;
           c = s2 < c ? 0xFFFFFFFFu : s2;
-          e = r.x & 0xFFFFu;
         }
       }
       tab[lane] = make_uint2(e | (min(hs, 0xFFFFu) << 16), c);
@@ -1932,14 +2048,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   __shared__ LvSmem sm;
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   LvWave& W = sm.wv[wid];
-  const uint32_t total = lt.wbase2[npages];
-  for (uint32_t g2 = blockIdx.x * (WG / WAVE) + wid; g2 < total; g2 += gridDim.x * (WG / WAVE)) {
-    LvWin x;
-    x.p = lv_page_of(lt.wbase2, (uint32_t)npages, g2);
+  LvDense D;
+  LvWin x;
+  if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
+  for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
+    if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
     const PageWork& pw = pages[x.p];
-    if (rt.pflag[x.p] != PF_PAGE || !lv_stream(blob, pw, sel, chunks, x.s)) continue;
-    x.k = g2 - lt.wbase2[x.p];
-    const uint2 wi = lt.win[lt.wbase[x.p] + x.k];
+    const uint2 wi = lt.win[D.wb + x.k];
     if (wi.x == LV_NONE) continue;  // no true header in this window
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen, n = x.s.n;
@@ -1986,6 +2101,24 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       const uint64_t lim = (uint64_t)n - base;
       uint32_t e = e0, mym = 0;
       uint64_t acc = 0, myacc = 0;
+      {  // speculatively in parallel (lv_spec_chain): the segments the walk visits are the chain's
+         // segments before the one whose outputs reach lim
+        uint32_t q;
+        bool valid;
+        uint2 r;
+        uint64_t inc;
+        if (lv_spec_chain(W, e0, lim, q, valid, r, inc)) {
+          const uint64_t P = inc - (valid ? r.y : 0u);
+          const bool vis = valid && P < lim;
+          mym = vis ? r.x >> 16 : 0u;
+          myacc = P;
+          const uint64_t vsm = __ballot(vis);
+          const int last = vsm ? 63 - __builtin_clzll(vsm) : 0;
+          acc = vsm ? __shfl(inc, last, 64) : 0ull;
+          e = vsm ? (uint32_t)__shfl((int)(r.x & 0xFFFFu), last, 64) : LV_WIN;
+          e = e < LV_WIN ? LV_WIN : e;  // (a chain past lim: not walked on; e matters only below lim)
+        }
+      }
 #pragma unroll 1
       while (e < LV_WIN) {
         const uint32_t sg = e / SEG;
@@ -2046,6 +2179,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
 // the previous window's stores.
 constexpr uint32_t LE_RPL = (LW_RPW + 1 + WAVE - 1) / WAVE;  // record registers per lane (5)
 constexpr uint32_t LE_SPL = (LE_STG / 16 + WAVE - 1) / WAVE;  // stage registers per lane (3)
+constexpr uint32_t LE_SMAX = 16;                              // waves per window at most
+constexpr uint32_t LE_SLICE = 16384;                          // outputs per slice at least
 
 struct LeWave {
   uint32_t stage[LE_STG / 4];
@@ -2123,12 +2258,31 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   uint32_t* xw = smx[wid];
   const uint32_t total = lt.wbase[npages];
   const uint32_t nwv = gridDim.x * (WG / WAVE), gw = blockIdx.x * (WG / WAVE) + wid;
-  const uint32_t per = (total + nwv - 1u) / nwv;
-  const uint32_t g0 = gw * per, g1 = min(total, g0 + per);
+  // fewer windows than waves (short streams of long runs: 2^20 levels in one RLE run per page):
+  // S waves per window, each writing a slice of its outputs; else contiguous window ranges
+  const uint32_t S = total && total < nwv ? min(nwv / total, LE_SMAX) : 1u, slice = gw % S;
+  const uint32_t per = S > 1 ? 1u : (total + nwv - 1u) / nwv;
+  const uint32_t g0 = S > 1 ? gw / S : gw * per, g1 = min(total, g0 + per);
   if (g0 >= g1) return;
   uint32_t p = lv_page_of(lt.wbase, (uint32_t)npages, g0);
   uint32_t wb = lt.wbase[p], pend = lt.wbase[p + 1];
   LvWin x;
+  // outputs [base, endo) of a window -> this wave's slice, its inner bounds on 64-output edges of
+  // the chunk's buffer (whole 16-byte stores on both sides)
+  auto cut = [&](uint32_t& base, uint32_t& endo) {
+    if (S == 1) return;
+    const uint64_t lo = x.s.out + base, T = endo - base;
+    const uint32_t Se = (uint32_t)min((uint64_t)S, (T + LE_SLICE - 1) / LE_SLICE);  // slices of >= LE_SLICE outputs
+    auto bnd = [&](uint32_t i) -> uint32_t {
+      if (i == 0) return base;
+      if (i >= Se) return endo;
+      const uint64_t a = (lo + T * i / Se) & ~63ull;
+      return a <= lo ? base : (uint32_t)(a - x.s.out);
+    };
+    const uint32_t b0 = bnd(slice), b1 = bnd(slice + 1);
+    base = b0;
+    endo = b1;
+  };
   x.p = p;
   bool walked = rt.pflag[p] == PF_WALK && lv_stream(blob, pages[p], sel, chunks, x.s);
   if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel, xw);
@@ -2172,8 +2326,9 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       }
       x.W0 = x.k * LV_WIN;
       lv_stage(blob, blob_len, x, E.stage, le_nch(w));  // ends with a wave LDS sync (run list too)
-      const uint32_t base = E.rstart[0];
-      const uint32_t endo = endn < x.s.n ? endn : x.s.n;
+      uint32_t base = E.rstart[0];
+      uint32_t endo = endn < x.s.n ? endn : x.s.n;
+      if (endo > base) cut(base, endo);
       if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
       wave_lds_sync();
       continue;
@@ -2223,9 +2378,10 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       x.sb = (uint32_t)(x.s.S + x.W0 - A);
       x.cap = le_nch(w) * 16u;
     }
-    const uint32_t base = E.rstart[0];
+    uint32_t base = E.rstart[0];
     const uint32_t endn = E.endn;
-    const uint32_t endo = endn < x.s.n ? endn : x.s.n;
+    uint32_t endo = endn < x.s.n ? endn : x.s.n;
+    if (endo > base) cut(base, endo);
     if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }

@@ -40,7 +40,7 @@ hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*,
 hipError_t pqg_launch_plain(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, const uint32_t*, uint32_t,
                             uint64_t, const uint32_t*, uint32_t, hipStream_t);
 hipError_t pqg_launch_plain_spec(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
-                                 uint64_t, hipStream_t);
+                                 uint32_t, hipStream_t);
 hipError_t pqg_launch_plain_fix(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, uint32_t,
                                 hipStream_t);
 hipError_t pqg_launch_rle_bool(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
@@ -142,7 +142,7 @@ struct pqg_ctx {
   int cur = 0;          // slot of the last decode
   hipStream_t stream = nullptr;
   bool timing = false;
-  bool overlap = true;  // speculative PLAIN copy on the side stream (pqg_ctx_set_overlap)
+  int overlap = 0;  // speculative PLAIN copy on the side stream (pqg_ctx_set_overlap): its workgroups per page
   hipStream_t side = nullptr;  // lowest-priority stream of that copy
   uint64_t seq = 0;     // decodes issued
   int calls = 0;        // decodes issued since the last pqg_sync
@@ -355,7 +355,7 @@ int pqg_ctx_set_timing(pqg_ctx* ctx, int enabled) {
 
 int pqg_ctx_set_overlap(pqg_ctx* ctx, int enabled) {
   if (!ctx) return PQG_ERR_INVALID;
-  ctx->overlap = enabled != 0;
+  ctx->overlap = enabled < 0 ? 0 : enabled;
   return PQG_OK;
 }
 
@@ -868,7 +868,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   if (spec) {  // fork: the speculative PLAIN copy on the side stream, beside everything below
     HIPCHK(hipEventRecord(sl.fork, s), "event");
     HIPCHK(hipStreamWaitEvent(ctx->side, sl.fork, 0), "stream wait");
-    HIPCHK(pqg_launch_plain_spec(b, blob_len, d_pages, ni, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], spec_max,
+    HIPCHK(pqg_launch_plain_spec(b, blob_len, d_pages, ni, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], (uint32_t)ctx->overlap,
                                  ctx->side),
            "speculative plain");
     HIPCHK(hipEventRecord(sl.join, ctx->side), "event");

@@ -211,8 +211,9 @@ class Context:
         lib().pqg_ctx_set_timing(self.h, 1 if enabled else 0)
 
     def set_overlap(self, enabled):
-        """Speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap); default on."""
-        lib().pqg_ctx_set_overlap(self.h, 1 if enabled else 0)
+        """Speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap): 0 off (default), n > 0 on with
+        n workgroups per page."""
+        lib().pqg_ctx_set_overlap(self.h, int(enabled))
 
     def decode_async(self, column, blob, blob_len, pages, out, stream=0, npages=None):
         """Enqueue pqg_decode_chunk. `blob` is a device pointer (int), `pages` a ctypes Page
