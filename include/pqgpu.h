@@ -140,9 +140,10 @@ int pqg_ctx_set_timing(pqg_ctx *ctx, int enabled);
  * (a page's value section holds exactly its non-null values in every file the reference writes);
  * the value-offset scan checks every such page and the chunks where a count or offset differs are
  * copied again at the true offsets. enabled = 0 copies after the levels only (the default: the
- * copy and the level kernels share HBM, and measured on MI355X the side copy pays off only for
- * sparse def streams, p_null 0.5: 1.72 -> 1.63 ms, and costs 0.1-0.35 ms otherwise); enabled = n
- * > 0 runs the side copy with n workgroups per page. */
+ * copy and the level kernels share HBM; measured on MI355X the side copy pays off only for sparse
+ * def streams); 1 forks the side copy right after the page preparation, one workgroup per page
+ * (p_null 0.5: 1.72 -> 1.63 ms, but p_null 0: 1.96 -> 2.3-2.6 ms); 2 forks it after the def
+ * levels' front end, beside their emit, on a full grid. */
 int pqg_ctx_set_overlap(pqg_ctx *ctx, int enabled);
 
 /* Enqueue the decode of one column chunk on `stream` (asynchronous). `blob` is a device

@@ -606,7 +606,7 @@ extern "C" {
 
 hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                          int sel, uint32_t widths, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* vsrc,
-                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s);
+                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s, hipEvent_t front = nullptr);
 
 hipError_t pqg_launch_prepare(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                               ChunkWork* chunks, uint32_t* tile_page, PrepInit ini, hipStream_t s) {
@@ -637,14 +637,14 @@ hipError_t pqg_launch_page_counts(PageWork* pages, int npages, ChunkWork* chunks
 // (levels + per-page non-null counts, pqg_levels.hip), then the general hybrid decoder for the
 // streams it hands back (one workgroup per handed-back page; the others exit at once). `widths`:
 // bit mask of the streams' bit widths (1 << w). scan: the value-offset scan runs in that last
-// kernel's last workgroup.
+// kernel's last workgroup. front: recorded after the front end (plan .. compact), when given.
 hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                              int which, uint32_t widths, const uint32_t* tile_page, RunTables rt, LevelTables lt,
-                             hipStream_t s, hipEvent_t* kev, int scan) {
+                             hipStream_t s, hipEvent_t* kev, int scan, hipEvent_t front) {
   const int sel = which ? SS_REP : SS_DEF;
   if (kev) (void)hipEventRecord(kev[0], s);
   hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, chunks, sel, widths, nullptr, nullptr, nullptr, nullptr,
-                               rt, lt, s);
+                               rt, lt, s, front);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, sel, rt,
                      lt.ctr + 1, scan);

@@ -1163,6 +1163,41 @@ struct LvDense {
   }
 };
 
+// The next window's staged bytes, loaded into registers while the current window is processed
+// (window kernels: one global round trip per window otherwise stands between two windows).
+struct LvPf {
+  uint4 a, b;
+  uint64_t A;
+  uint32_t p, k;
+  bool ok;
+  __device__ inline void issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x, uint32_t k2) {
+    const uint32_t lane = threadIdx.x & 63u;
+    A = (x.s.S + (uint64_t)k2 * LV_WIN) & ~15ull;
+    const uint64_t a0 = A + lane * 16u, a1 = A + (WAVE + lane) * 16u;
+    a = a0 + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a0) : gload_u128_tail(blob, blob_len, a0);
+    b = lane + WAVE < LV_STG_CH ? (a1 + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a1)
+                                                       : gload_u128_tail(blob, blob_len, a1))
+                                : make_uint4(0u, 0u, 0u, 0u);
+    p = x.p;
+    k = k2;
+    ok = true;
+  }
+  // window x's stage: from the registers when they hold it, else loaded now
+  __device__ inline void stage(const uint8_t* __restrict__ blob, uint64_t blob_len, LvWin& x, uint32_t* st) {
+    if (!(ok && p == x.p && k == x.k)) {
+      lv_stage(blob, blob_len, x, st, LV_STG_CH);
+      return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    x.sb = (uint32_t)(x.s.S + x.W0 - A);
+    x.cap = LV_STG_CH * 16u;
+    reinterpret_cast<uint4*>(st)[lane] = a;
+    if (lane + WAVE < LV_STG_CH) reinterpret_cast<uint4*>(st)[WAVE + lane] = b;
+    ok = false;
+    wave_lds_sync();
+  }
+};
+
 // ------------------------------------------------------------------------------ k_lv_win
 // Window path: windows g2 of the dense pages (wbase2); g = the page's window in wbase terms.
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_lv_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -1173,13 +1208,16 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   LvWave& W = sm.wv[wid];
   LvDense D;
   LvWin x;
+  LvPf pf;
+  pf.ok = false;
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
     const uint32_t g = D.wb + x.k;
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w;
-    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
+    pf.stage(blob, blob_len, x, W.stage);
+    if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1);
     // table of the entry offsets: (exit offset from W0 or terminal code | headers << 16, outputs)
     const uint32_t ent = lv_ent(w);
     uint2* tab = lt.tab + (uint64_t)g * lt.tstride;
@@ -2050,6 +2088,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   LvWave& W = sm.wv[wid];
   LvDense D;
   LvWin x;
+  LvPf pf;
+  pf.ok = false;
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
@@ -2060,7 +2100,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen, n = x.s.n;
     const uint32_t e0 = wi.x & 0xFFFFu, nh = wi.x >> 16;  // entry, true headers (saturated)
     const uint32_t base = wi.y;
-    lv_stage(blob, blob_len, x, W.stage, LV_STG_CH);
+    pf.stage(blob, blob_len, x, W.stage);
+    if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1);
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
@@ -2139,17 +2180,20 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
       uint32_t k = rb;
       uint64_t oa = (uint64_t)base + myacc;
-#pragma unroll
-      for (uint32_t t = 0; t < SEG; ++t) {
-        if ((mym >> t) & 1u) {
-          const bool bp = (bpm >> t) & 1u;
-          const uint32_t v = pv[t];
-          W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
-          W.runs.rinfo[k] = bp ? v : (R_RLE | v);
-          bad |= !lv_run_ok(bp, v, pc[t], oa, n, slen, w);
-          ++k;
-          oa += pc[t];
-        }
+      // the segment's true headers parsed again from the stage (keeping the segment build's 32
+      // per-position registers live through the walk spilled them)
+      const uint32_t i0 = lane * SEG;
+#pragma unroll 1
+      for (uint32_t m = mym; m; m &= m - 1u) {
+        const uint32_t t = (uint32_t)__builtin_ctz(m);
+        uint32_t nx, c, v;
+        bool bp;
+        lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (a true header: parses)
+        W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
+        W.runs.rinfo[k] = bp ? v : (R_RLE | v);
+        bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
+        ++k;
+        oa += c;
       }
       R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
       T = acc;
@@ -2410,10 +2454,11 @@ extern "C" {
 // (scratch dsrc/dlen -> vsrc/vlen). widths: bit mask (1 << w) of the level streams' bit widths.
 hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                          int sel, uint32_t widths, const uint64_t* dsrc, const uint32_t* dlen, uint64_t* vsrc,
-                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s) {
+                         uint32_t* vlen, RunTables rt, LevelTables lt, hipStream_t s, hipEvent_t front) {
   if (npages <= 0) return hipSuccess;
   const uint32_t wgrid = 256u * 8u;
   lv_front(blob, blob_len, pages, npages, chunks, sel, rt, lt, wgrid, s);
+  if (front) (void)hipEventRecord(front, s);
   if (sel == SS_DICT) {  // (dense dictionary streams went to the general decoder)
     hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks,
                        sel, rt, lt, LvDictOut{dsrc, dlen, vsrc, vlen});

@@ -30,10 +30,10 @@ extern "C" {
 hipError_t pqg_launch_prepare(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, uint32_t*, PrepInit, hipStream_t);
 hipError_t pqg_launch_run_index(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, RunTables, hipStream_t);
 hipError_t pqg_launch_levels(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, uint32_t, const uint32_t*,
-                             RunTables, LevelTables, hipStream_t, hipEvent_t*, int);
+                             RunTables, LevelTables, hipStream_t, hipEvent_t*, int, hipEvent_t);
 hipError_t pqg_launch_scan(PageWork*, int, ChunkWork*, hipStream_t);
 hipError_t pqg_launch_lv(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, uint32_t, const uint64_t*,
-                         const uint32_t*, uint64_t*, uint32_t*, RunTables, LevelTables, hipStream_t);
+                         const uint32_t*, uint64_t*, uint32_t*, RunTables, LevelTables, hipStream_t, hipEvent_t = nullptr);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
                            const uint32_t* const*, const uint32_t*, const uint32_t*, uint32_t, RunTables, hipStream_t,
                            hipEvent_t*);
@@ -142,7 +142,7 @@ struct pqg_ctx {
   int cur = 0;          // slot of the last decode
   hipStream_t stream = nullptr;
   bool timing = false;
-  int overlap = 0;  // speculative PLAIN copy on the side stream (pqg_ctx_set_overlap): its workgroups per page
+  int overlap = 0;  // speculative PLAIN copy on the side stream (pqg_ctx_set_overlap): 0 off, 1 early, 2 late
   hipStream_t side = nullptr;  // lowest-priority stream of that copy
   uint64_t seq = 0;     // decodes issued
   int calls = 0;        // decodes issued since the last pqg_sync
@@ -355,7 +355,7 @@ int pqg_ctx_set_timing(pqg_ctx* ctx, int enabled) {
 
 int pqg_ctx_set_overlap(pqg_ctx* ctx, int enabled) {
   if (!ctx) return PQG_ERR_INVALID;
-  ctx->overlap = enabled < 0 ? 0 : enabled;
+  ctx->overlap = enabled < 0 ? 0 : enabled > 2 ? 2 : enabled;
   return PQG_OK;
 }
 
@@ -865,26 +865,38 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   if (ctx->timing) hipEventRecord(ev[0], s);
   if (np) HIPCHK(pqg_launch_prepare(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, ini, s), "prepare");
   const bool spec = np && ntl[TL_PSPEC];
-  if (spec) {  // fork: the speculative PLAIN copy on the side stream, beside everything below
-    HIPCHK(hipEventRecord(sl.fork, s), "event");
+  // fork: the speculative PLAIN copy on the side stream, beside everything below (overlap 1:
+  // right after k_prepare, one workgroup per page; 2: after the def levels' front end, beside
+  // their emit, a full grid)
+  auto fork_spec = [&](uint32_t gx) -> int {
     HIPCHK(hipStreamWaitEvent(ctx->side, sl.fork, 0), "stream wait");
-    HIPCHK(pqg_launch_plain_spec(b, blob_len, d_pages, ni, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], (uint32_t)ctx->overlap,
-                                 ctx->side),
+    HIPCHK(pqg_launch_plain_spec(b, blob_len, d_pages, ni, d_chunks, tlp[TL_PSPEC], ntl[TL_PSPEC], gx, ctx->side),
            "speculative plain");
     HIPCHK(hipEventRecord(sl.join, ctx->side), "event");
+    return PQG_OK;
+  };
+  const bool late_fork = spec && ctx->overlap == 2 && any_def;
+  if (spec && !late_fork) {
+    HIPCHK(hipEventRecord(sl.fork, s), "event");
+    if (const int e = fork_spec(1u)) return e;
   }
   if (ctx->timing) hipEventRecord(ev[1], s);
   // the value-offset scan runs in the def stream's last kernel when no rep stream follows it
   const bool fused_scan = np && any_def && !any_rep;
   if (np && any_def) {
     HIPCHK(pqg_launch_levels(b, blob_len, d_pages, ni, d_chunks, 0, def_w, sl.tile_page, sl.rt[K_DEF],
-                             sl.lt(K_DEF, tstride[K_DEF]), s, ctx->timing ? &ev[6] : nullptr, fused_scan ? 1 : 0),
+                             sl.lt(K_DEF, tstride[K_DEF]), s, ctx->timing ? &ev[6] : nullptr, fused_scan ? 1 : 0,
+                             late_fork ? sl.fork : nullptr),
            "def levels");
+    if (late_fork) {
+      const uint64_t gx = (spec_max + 64ull * 256ull - 1) / (64ull * 256ull) + 1;  // 4 x 16 bytes per lane
+      if (const int e = fork_spec((uint32_t)(gx > 4096 ? 4096 : gx))) return e;
+    }
     sl.kl = ctx->timing;
   }
   if (np && any_rep)
     HIPCHK(pqg_launch_levels(b, blob_len, d_pages, ni, d_chunks, 1, rep_w, sl.tile_page, sl.rt[K_REP],
-                             sl.lt(K_REP, tstride[K_REP]), s, nullptr, 0),
+                             sl.lt(K_REP, tstride[K_REP]), s, nullptr, 0, nullptr),
            "rep levels");
   if (ctx->timing) hipEventRecord(ev[2], s);
   if (np && !fused_scan) HIPCHK(pqg_launch_scan(d_pages, ni, d_chunks, s), "scan");

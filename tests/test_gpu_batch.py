@@ -259,11 +259,12 @@ def _plain_zoo(oracle, seed=21):
     return z
 
 
-@pytest.mark.parametrize("overlap", [1, 0])
+@pytest.mark.parametrize("overlap", [2, 1, 0])
 def test_speculative_plain_copy(oracle, ctx, overlap):
     """PLAIN values behind def levels, copied beside the level decode at the value sections'
-    offsets (pqg_ctx_set_overlap 1) or after it (0): identical to the oracle, including a chunk whose
-    speculative offsets are wrong (trailing value bytes: re-copied at the true offsets)."""
+    offsets (pqg_ctx_set_overlap 1: from the start, 2: beside the emit) or after it (0): identical
+    to the oracle, including a chunk whose speculative offsets are wrong (trailing value bytes:
+    re-copied at the true offsets)."""
     zoo = _plain_zoo(oracle)
     ctx.set_overlap(overlap)
     try:
@@ -271,7 +272,7 @@ def test_speculative_plain_copy(oracle, ctx, overlap):
             st, res = _decode_batch(ctx, zoo, order)
             _check_zoo(oracle, zoo, st, res, order)
     finally:
-        ctx.set_overlap(1)
+        ctx.set_overlap(0)
 
 
 def test_speculative_plain_copy_short_section(oracle, ctx):
@@ -284,10 +285,10 @@ def test_speculative_plain_copy_short_section(oracle, ctx):
     zoo[0] = (name, pt, pages, md, mr, tl, wdef)
     ref = oracle.read_column(pt, pages, max_def=md)
     assert ref["status"] != 0
-    for overlap in (1, 0):
+    for overlap in (2, 1, 0):
         ctx.set_overlap(overlap)
         try:
             st, res = _decode_batch(ctx, zoo)
         finally:
-            ctx.set_overlap(1)
+            ctx.set_overlap(0)
         assert st[0] == ref["status"] and st[2] == 0 and st[3] == 1, (overlap, st)
