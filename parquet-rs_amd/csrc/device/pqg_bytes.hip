@@ -196,7 +196,21 @@ __global__ void __launch_bounds__(WG) k_ba_dict_prep(const uint8_t* __restrict__
   } else {
     st = plain_ba_walk(sm, blob, blob_len, S, dp.nbytes, n, dsrc, dlen);
   }
-  if (st && threadIdx.x == 0) report(pages, chunks, dict_page, st);
+  // a dictionary that fails to decode: every entry empty, so that the data pages' kernels, which
+  // run before the chunk's error is read, never follow an entry the walk did not write (the
+  // reference stops at this page, configure_dictionary: column/reader.rs:463-481)
+  __shared__ int32_t st_s;
+  if (threadIdx.x == 0) st_s = 0;
+  __syncthreads();
+  if (st) st_s = st;
+  __syncthreads();
+  if (st_s) {
+    for (uint64_t i = threadIdx.x; i < n; i += WG) {
+      dsrc[i] = S;
+      dlen[i] = 0;
+    }
+    if (threadIdx.x == 0) report(pages, chunks, dict_page, st_s);
+  }
 }
 
 struct BaDictEmit {

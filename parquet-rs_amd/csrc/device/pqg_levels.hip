@@ -1089,7 +1089,10 @@ __device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV
 // rounds (a wrong guess between right ones is put right by one). When the check passes, the
 // valid guesses are the chain (by induction from e0's segment, whose guess is e0), found with
 // ~LV_SPK dependent table reads instead of one per segment. Returns false if it never passes.
-constexpr uint32_t LV_SPK = 4;  // segments walked per guess
+#ifndef PQG_LV_SPK
+#define PQG_LV_SPK 4
+#endif
+constexpr uint32_t LV_SPK = PQG_LV_SPK;  // segments walked per guess
 constexpr uint32_t LV_SPR = 4;  // repair rounds
 
 __device__ inline bool lv_spec_chain(const LvWave& W, uint32_t e0, uint64_t lim, uint32_t& q, bool& valid, uint2& r,
@@ -1121,17 +1124,32 @@ __device__ inline bool lv_spec_chain(const LvWave& W, uint32_t e0, uint64_t lim,
   }
 }
 
+// Output buffer of stream `sel` of a chunk: def / rep levels, RLE booleans.
+__device__ inline uint8_t* lv_out(const ChunkWork& ck, int sel) {
+  return sel == SS_DEF ? (uint8_t*)ck.def_out : sel == SS_REP ? (uint8_t*)ck.rep_out : ck.val_out;
+}
+
+// Max level of stream `sel` (the def count's test, column/reader.rs:212-226).
+__device__ inline uint32_t lv_maxl(const ChunkWork& ck, int sel) {
+  return sel == SS_DEF ? (uint32_t)ck.cp.max_def : sel == SS_REP ? (uint32_t)ck.cp.max_rep : 1u;
+}
+
 // A wave's contiguous range [g0, g1) of the dense pages' windows (wbase2): the page is found once
 // and then advanced with the window, its stream parsed once per page (a grid-stride loop paid a
 // binary search and the page's dependent loads per window).
 struct LvDense {
   uint32_t g0, g1, pb, pend, wb;
   bool ok;
+  uint8_t* out;   // the page's output buffer and max level (k_lv_emit), read once per page: a load
+  uint32_t maxl;  // issued after a window's stores waits for them to complete (one vmcnt)
   __device__ inline void page(const uint8_t* blob, const PageWork* pages, const ChunkWork* chunks, int sel,
                               const RunTables& rt, const LevelTables& lt, LvWin& x) {
     pend = lt.wbase2[x.p + 1];
     wb = lt.wbase[x.p];
     ok = pend > pb && rt.pflag[x.p] == PF_PAGE && lv_stream(blob, pages[x.p], sel, chunks, x.s);
+    const ChunkWork& ck = chunks[pages[x.p].chunk];
+    out = lv_out(ck, sel);
+    maxl = lv_maxl(ck, sel);
   }
   __device__ inline bool begin(const uint8_t* blob, const PageWork* pages, int npages, const ChunkWork* chunks, int sel,
                                const RunTables& rt, const LevelTables& lt, LvWin& x) {
@@ -1167,10 +1185,13 @@ struct LvDense {
 // (window kernels: one global round trip per window otherwise stands between two windows).
 struct LvPf {
   uint4 a, b;
+  uint2 wi;  // k_lv_emit: the window's stitch result (lt.win), with its bytes
   uint64_t A;
   uint32_t p, k;
   bool ok;
-  __device__ inline void issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x, uint32_t k2) {
+  __device__ inline void issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x, uint32_t k2,
+                               const uint2* wsrc = nullptr) {
+    if (wsrc) wi = wsrc[k2];
     const uint32_t lane = threadIdx.x & 63u;
     A = (x.s.S + (uint64_t)k2 * LV_WIN) & ~15ull;
     const uint64_t a0 = A + lane * 16u, a1 = A + (WAVE + lane) * 16u;
@@ -1706,16 +1727,6 @@ __device__ inline uint32_t lv_write_wide(const LvRuns& rl, const uint32_t* stage
   return cnt;
 }
 
-// Output buffer of stream `sel` of a chunk: def / rep levels, RLE booleans.
-__device__ inline uint8_t* lv_out(const ChunkWork& ck, int sel) {
-  return sel == SS_DEF ? (uint8_t*)ck.def_out : sel == SS_REP ? (uint8_t*)ck.rep_out : ck.val_out;
-}
-
-// Max level of stream `sel` (the def count's test, column/reader.rs:212-226).
-__device__ inline uint32_t lv_maxl(const ChunkWork& ck, int sel) {
-  return sel == SS_DEF ? (uint32_t)ck.cp.max_def : sel == SS_REP ? (uint32_t)ck.cp.max_rep : 1u;
-}
-
 // Outputs of one window from its run list (into out, the page's chunk buffer), and the def count.
 template <int OUT>
 __device__ inline void lv_write(const LvRuns& rl, const uint32_t* stage, const uint8_t* __restrict__ blob,
@@ -2110,15 +2121,18 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
-    const PageWork& pw = pages[x.p];
-    const uint2 wi = lt.win[D.wb + x.k];
-    if (wi.x == LV_NONE) continue;  // no true header in this window
+    const uint2 wi = pf.ok && pf.p == x.p && pf.k == x.k ? pf.wi : lt.win[D.wb + x.k];
+    if (wi.x == LV_NONE) {  // no true header in this window
+      pf.ok = false;
+      if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1, lt.win + D.wb);
+      continue;
+    }
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen, n = x.s.n;
     const uint32_t e0 = wi.x & 0xFFFFu, nh = wi.x >> 16;  // entry, true headers (saturated)
     const uint32_t base = wi.y;
     pf.stage(blob, blob_len, x, W.stage);
-    if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1);
+    if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1, lt.win + D.wb);
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
@@ -2224,9 +2238,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (endo <= base || R == 0) continue;
-    const ChunkWork& ck = chunks[pw.chunk];
     lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
-                  lv_maxl(ck, sel), pages, gp(lv_out(ck, sel)));
+                  D.maxl, pages, gp(D.out));
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
 }

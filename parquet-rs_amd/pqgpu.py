@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpqgpu.so")
+# PQG_LIBDIR selects an experiment build (Makefile VARIANT=...) for A/B timing; default lib/
+LIB_PATH = os.path.join(_HERE, os.environ.get("PQG_LIBDIR", "lib"), "libpqgpu.so")
 
 OK, GENERAL, NYI, EOF, PANIC, HANG, CAPACITY, INVALID, HIP = range(9)
 STATUS_NAMES = ["OK", "General", "NYI", "EOF", "Panic", "Hang", "Capacity", "Invalid", "HIP"]
