@@ -1,7 +1,7 @@
 // copy_ceiling.hip — the achievable HBM copy rate on this device, for bench.py's roofline
 // context (measurement tooling; not part of the decode library). A 16-byte-per-lane
 // grid-stride copy (the MI355X_MICROARCH.md "float4 copy" shape), plain and non-temporal
-// variants; the faster one is reported.
+// variants at three grid sizes; the fastest is reported.
 #pragma clang diagnostic ignored "-Wunused-result"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -47,8 +47,12 @@ double pqg_copy_ceiling_gbs(uint64_t bytes, int iters) {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   double best = 0;
-  const unsigned grid = 256 * 16;
-  for (int nt = 0; nt < 2; ++nt) {
+  // grids of 16, 64 and 256 workgroups per CU (tools/ubench/copy_sweep.hip: the largest grids
+  // copy fastest on MI355X, 5.8-6.0 TB/s with non-temporal loads and stores)
+  const unsigned grids[3] = {256 * 16, 256 * 64, 256 * 256};
+  for (int v = 0; v < 6 && best >= 0; ++v) {
+    const int nt = v & 1;
+    const unsigned grid = grids[v >> 1];
     for (int w = 0; w < 2; ++w) {
       if (nt) hipLaunchKernelGGL(k_copy16<true>, dim3(grid), dim3(256), 0, 0, a, b, n16);
       else hipLaunchKernelGGL(k_copy16<false>, dim3(grid), dim3(256), 0, 0, a, b, n16);
