@@ -2256,12 +2256,23 @@ constexpr uint32_t LE_SPL = (LE_STG / 16 + WAVE - 1) / WAVE;  // stage registers
 constexpr uint32_t LE_SMAX = 16;                              // waves per window at most
 constexpr uint32_t LE_SLICE = 16384;                          // outputs per slice at least
 
-struct LeWave {
-  uint32_t stage[LE_STG / 4];
+// The unpipelined writers (dictionary values) take up to LE_UNIT consecutive windows of a page as
+// one unit (their run records are contiguous, at most LW_RPW runs in all): one chain of dependent
+// loads (bounds, records, payload) per unit instead of per window.
+#ifndef PQG_LE_UNIT
+#define PQG_LE_UNIT 2
+#endif
+constexpr uint32_t LE_UNIT = PQG_LE_UNIT;
+constexpr uint32_t LE_STG_U = LE_UNIT * LV_WIN + 64 * 16 + 64;
+
+template <uint32_t STG>
+struct LeWaveT {
+  uint32_t stage[STG / 4];
   uint32_t rstart[LW_RPW + 1];
   uint32_t rinfo[LW_RPW];
   uint32_t endn;
 };
+using LeWave = LeWaveT<LE_STG>;
 
 // One window's loads in flight: its run records [fr, fr + R] and staged payload.
 struct LeLoad {
@@ -2271,9 +2282,9 @@ struct LeLoad {
   bool ok;  // loads issued (a window of the same walked page with runs, R <= LW_RPW)
 };
 
-__device__ inline uint32_t le_nch(uint32_t w) {
-  const uint32_t n = (LV_WIN + 16u + 64u * w + 16u) / 16u + 1u;
-  return n > LE_STG / 16 ? LE_STG / 16 : n;
+__device__ inline uint32_t le_nch(uint32_t w, uint32_t nwin = 1, uint32_t stg = LE_STG) {
+  const uint32_t n = (nwin * LV_WIN + 16u + 64u * w + 16u) / 16u + 1u;
+  return n > stg / 16 ? stg / 16 : n;
 }
 
 __device__ inline void le_issue(const uint8_t* __restrict__ blob, uint64_t blob_len, const uint2* rc, uint32_t R,
@@ -2299,7 +2310,8 @@ __device__ inline void le_issue(const uint8_t* __restrict__ blob, uint64_t blob_
   f.ok = true;
 }
 
-__device__ inline void le_install(const LeLoad& f, LeWave& E) {
+template <class WaveT>
+__device__ inline void le_install(const LeLoad& f, WaveT& E) {
   const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
   for (uint32_t j = 0; j < LE_RPL; ++j) {
@@ -2325,10 +2337,11 @@ template <class Writer>
 __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                      PageWork* pages, int npages, const ChunkWork* chunks,
                                                      int sel, RunTables rt, LevelTables lt, Writer wr) {
-  __shared__ LeWave sm[WG / WAVE];
+  using WaveT = LeWaveT<Writer::PIPE ? LE_STG : LE_STG_U>;
+  __shared__ WaveT sm[WG / WAVE];
   __shared__ uint32_t smx[WG / WAVE][Writer::XW];
   const uint32_t wid = rfl(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  LeWave& E = sm[wid];
+  WaveT& E = sm[wid];
   uint32_t* xw = smx[wid];
   const uint32_t total = lt.wbase[npages];
   const uint32_t nwv = gridDim.x * (WG / WAVE), gw = blockIdx.x * (WG / WAVE) + wid;
@@ -2383,8 +2396,16 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     const uint32_t* wf = lt.wfirst + wb + p;
     const uint2* recp = lt.rec + (uint64_t)LW_REC * (wb + 2ull * p);
     const uint32_t w = (uint32_t)x.s.w;
-    if constexpr (!Writer::PIPE) {  // one window at a time: records and payload straight to LDS
-      const uint32_t fr = wf[x.k], fe = wf[x.k + 1];
+    if constexpr (!Writer::PIPE) {  // a unit of windows at a time: records and payload straight to LDS
+      // the unit: windows [x.k, x.k + nu) of this page with at most LW_RPW runs in all (lane i
+      // reads the run bound of window x.k + i)
+      const uint32_t lim = S > 1 ? 1u : min(LE_UNIT, min(g1, pend) - g);
+      const uint32_t fi = lane <= lim ? wf[x.k + lane] : 0u;
+      const uint32_t fr = rfl(fi);
+      const uint64_t fit = __ballot(lane >= 1 && lane <= lim && fi - fr <= LW_RPW);
+      const uint32_t nu = fit & 2ull ? (uint32_t)__builtin_ctzll(~(fit >> 1)) : 1u;  // leading windows that fit
+      const uint32_t fe = (uint32_t)__shfl((int)fi, (int)nu, 64);
+      g += nu - 1u;  // (the loop's ++g moves past the unit)
       if (fr == fe) continue;
       const uint32_t R = fe - fr;
       if (R > LW_RPW) {
@@ -2399,7 +2420,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
         E.rinfo[i] = r.y;
       }
       x.W0 = x.k * LV_WIN;
-      lv_stage(blob, blob_len, x, E.stage, le_nch(w));  // ends with a wave LDS sync (run list too)
+      lv_stage(blob, blob_len, x, E.stage, le_nch(w, nu, LE_STG_U));  // ends with a wave LDS sync (run list too)
       uint32_t base = E.rstart[0];
       uint32_t endo = endn < x.s.n ? endn : x.s.n;
       if (endo > base) cut(base, endo);

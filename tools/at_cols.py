@@ -23,7 +23,7 @@ def main():
     import pqgtools
     import bench
     args = bench.parse(["--config", "alltypes", "--rowgroups", "1", "--rg-rows", str(a.rg_rows)])
-    w = bench.AlltypesWorkload(pqgpu, args, 0)
+    w = bench.AlltypesWorkload(pqgpu, args, 0, 1)
     ctx = pqgpu.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
