@@ -308,33 +308,37 @@ __device__ inline bool lv_nodict(const PageWork* pages, const ChunkWork& ck, int
 
 __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
                                                 const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
-  lv_scan_windows(npages, lt.wbase, [&](int p) -> uint32_t {
+  // one thread per page: flag, window and segment counts (into wbase / sbase, scanned in place
+  // by the last workgroup; a single workgroup paid the pages' dependent loads four at a time)
+  const int p = (int)(blockIdx.x * WG + threadIdx.x);
+  if (p < npages) {
     const PageWork& pw = pages[p];
     const ChunkWork& ck = chunks[pw.chunk];
     const bool nodict = lv_nodict(pages, ck, sel);
     Stream s;
-    uint32_t flag = 0, nw = 0;
+    uint32_t flag = 0, nw = 0, ns = 0;
     if (get_stream(blob, pw, sel, ck.cp, s) && (sel != SS_DICT || ck.lvdict)) {
       if (!nodict && lv_stream(blob, pw, sel, chunks, s) && (s.n == 0 || s.slen > 0)) {
         flag = PF_PAGE;
         nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
         if (sel == SS_DEF) pages[p].nonnull = 0;
+        if (!lt.dense[p] && s.n && s.slen) {
+          const uint32_t sw = lw_segw((uint32_t)s.w);
+          ns = ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
+        }
       } else {
         flag = PF_BAIL;
         atomicAdd(rt.nfall, 1u);
       }
     }
     rt.pflag[p] = flag;
-    return nw;
-  });
-  lv_scan_windows(npages, lt.sbase, [&](int p) -> uint32_t {
-    Stream s;
-    if (lv_nodict(pages, chunks[pages[p].chunk], sel) || lt.dense[p] || !lv_stream(blob, pages[p], sel, chunks, s) ||
-        !s.n || !s.slen)
-      return 0u;
-    const uint32_t sw = lw_segw((uint32_t)s.w);
-    return ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
-  });
+    lt.wbase[p] = nw;
+    lt.sbase[p] = ns;
+  }
+  if (last_workgroup(lt.ctr + 2)) {
+    lv_scan_windows(npages, lt.wbase, [&](int q) -> uint32_t { return lt.wbase[q]; });
+    lv_scan_windows(npages, lt.sbase, [&](int q) -> uint32_t { return lt.sbase[q]; });
+  }
 }
 
 // One workgroup: windows of the pages the walker left to the window path (wbase2).
@@ -2489,7 +2493,7 @@ static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, in
   if (sel == SS_BOOL)  // (def / rep: k_prepare probed them; dictionary indices: cleared there)
     hipLaunchKernelGGL(k_lv_probe, dim3((npages + WG / WAVE - 1) / (WG / WAVE)), dim3(WG), 0, s, blob, blob_len,
                        pages, npages, chunks, sel, lt);
-  hipLaunchKernelGGL(k_lv_plan, dim3(1), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
+  hipLaunchKernelGGL(k_lv_plan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segscan, dim3(npages), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);

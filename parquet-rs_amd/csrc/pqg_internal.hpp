@@ -204,7 +204,7 @@ struct LevelTables {
   uint32_t* dense;   // [pages] 1: the stream's first 64 headers lie within 1 KiB (k_lv_probe): the
                      // window path takes it without a segment walk
   uint32_t* ctr;     // [16] last-workgroup tickets (zero between launches): [0] k_lv_segscan,
-                     // [1] k_lv_fallback
+                     // [1] k_lv_fallback, [2] k_lv_plan
   uint32_t tstride;  // tab entries per window: lv_ent of the widest stream of the decode (the
                      // streams of a batch's chunks may differ in bit width)
 };
