@@ -65,10 +65,13 @@ def _check(oracle, ctx, specs, max_def=1):
     return got, ref
 
 
-@pytest.mark.parametrize("p_null", [0.5, 0.1, 0.05, 0.0])
+@pytest.mark.parametrize("p_null", [0.5, 0.3, 0.2, 0.1, 0.05, 0.0])
 def test_headline_pages_full_size(oracle, ctx, p_null):
     """Six 2^20-level pages and a ragged seventh, written by the bench's generator at the bench's
-    seed, against the oracle: every level and every value."""
+    seed, against the oracle: every level and every value. p_null 0.2-0.3: dense windows whose
+    speculative chain walk needs several repair rounds or falls back to the serial walk (payload
+    bytes parsed out of phase for a whole window); p_null 0: one RLE run per page, its outputs
+    written by 16 waves per window in slices."""
     n = 6 * PAGE + 12345
     host, pages, info = _gen_levels_plain(n, p_null, 0x5EED0002 + int(p_null * 1000))
     assert info.npages == 7
