@@ -553,7 +553,10 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     cp.want_rep = col->max_rep > 0 && out->rep_levels;
     // byte-array entries (address + length per value) take every index width; 4- / 8-byte values
     // up to 8 bits (wider: a large dictionary, gathered faster by the tiled expand)
-    cp.dict_maxw = is_ba ? 16u : 8u;
+#ifndef PQG_DICT_MAXW
+#define PQG_DICT_MAXW 8u
+#endif
+    cp.dict_maxw = is_ba ? 16u : PQG_DICT_MAXW;
     cp.debug = dbg_env;
     c.def_out = out->def_levels;
     c.rep_out = out->rep_levels;
