@@ -2053,7 +2053,10 @@ __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t
 // wave waiting for a global gather would wait for every store it issued before it as well.
 struct LvDictOut {
   static constexpr bool PIPE = false;  // (its gathers hold the registers the prefetch would take: measured slower, 1.61 -> 1.68 ms)
-  static constexpr uint32_t XW = 512;  // per-wave LDS words: the dictionary, or its entry lengths
+#ifndef PQG_DICT_XW
+#define PQG_DICT_XW 512
+#endif
+  static constexpr uint32_t XW = PQG_DICT_XW;  // per-wave LDS words: the dictionary, or its entry lengths
   const uint64_t* dsrc;
   const uint32_t* dlen;
   uint64_t* vsrc;
