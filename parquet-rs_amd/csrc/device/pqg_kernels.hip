@@ -246,12 +246,11 @@ struct LevelsPageMaker {
 
 __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                         PageWork* pages, ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
-                                        int sel, RunTables rt) {
+                                        int sel, RunTables rt, int p) {
   __shared__ IndexSmem ism;
   __shared__ TileSmem sm;
   __shared__ int32_t st_s;
   __shared__ uint64_t red[WG / 64];
-  const int p = blockIdx.x;
   if (rt.pflag[p] != PF_BAIL) return;
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
@@ -284,14 +283,21 @@ __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64
 
 __device__ inline void scan_values(PageWork* pages, ChunkWork* chunks, int npages);
 
+constexpr int LF_GRID = 256;  // k_lv_fallback workgroups at most
+
 // scan != 0 (a def stream, no rep stream after it): the grid's last workgroup also runs
 // k_scan_values (the non-null counts are final), one launch fewer per decode.
 __global__ void __launch_bounds__(WG) k_lv_fallback(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                     PageWork* pages, ChunkWork* chunks,
                                                     const uint32_t* __restrict__ tile_page, int sel, RunTables rt,
-                                                    uint32_t* ctr, int scan) {
-  lv_fallback_page(blob, blob_len, pages, chunks, tile_page, sel, rt);
-  if (scan && last_workgroup(ctr)) scan_values(pages, chunks, (int)gridDim.x);
+                                                    uint32_t* ctr, int scan, int npages) {
+  // a grid of at most LF_GRID workgroups strides over the pages (handed-back pages are rare: a
+  // workgroup per page made the launch itself cost ~10 us more)
+  for (int p = (int)blockIdx.x; p < npages; p += (int)gridDim.x) {
+    lv_fallback_page(blob, blob_len, pages, chunks, tile_page, sel, rt, p);
+    __syncthreads();  // (the page's shared state before the next page's)
+  }
+  if (scan && last_workgroup(ctr)) scan_values(pages, chunks, npages);
 }
 
 // Tile expand of RLE_DICTIONARY indices with the dictionary gather: the tile's page names its
@@ -646,8 +652,8 @@ hipError_t pqg_launch_levels(const uint8_t* blob, uint64_t blob_len, PageWork* p
   hipError_t e = pqg_launch_lv(blob, blob_len, pages, npages, chunks, sel, widths, nullptr, nullptr, nullptr, nullptr,
                                rt, lt, s, front);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lv_fallback, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, sel, rt,
-                     lt.ctr + 1, scan);
+  hipLaunchKernelGGL(k_lv_fallback, dim3(npages < LF_GRID ? npages : LF_GRID), dim3(WG), 0, s, blob, blob_len, pages,
+                     chunks, tile_page, sel, rt, lt.ctr + 1, scan, npages);
   if (kev) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();
 }
