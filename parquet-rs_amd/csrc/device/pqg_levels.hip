@@ -845,12 +845,13 @@ __device__ inline uint32_t lv_segscan_serial(LvSeg* seg, const uint2* srec, uint
 }
 
 __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
-                                       int npages, const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
+                                       int npages, const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt,
+                                       uint32_t p) {
   __shared__ uint64_t wout[WG / WAVE];
   __shared__ uint32_t wrun[WG / WAVE], wlast[WG / WAVE], wmin[WG / WAVE];
   __shared__ uint64_t c_out;
   __shared__ uint32_t c_run, c_pos, J_s, broken_s, verdict_s;
-  const uint32_t p = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+  const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
   if (p >= (uint32_t)npages || rt.pflag[p] != PF_PAGE) return;
   Stream s;
   if (!lv_stream(blob, pages[p], sel, chunks, s)) return;
@@ -979,7 +980,10 @@ __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const P
 __global__ void __launch_bounds__(WG) k_lv_segscan(const uint8_t* __restrict__ blob, const PageWork* __restrict__ pages,
                                                    int npages, const ChunkWork* chunks, int sel, RunTables rt,
                                                    LevelTables lt) {
-  lv_segscan_page(blob, pages, npages, chunks, sel, rt, lt);
+  for (uint32_t p = blockIdx.x; p < (uint32_t)npages; p += gridDim.x) {
+    lv_segscan_page(blob, pages, npages, chunks, sel, rt, lt, p);
+    __syncthreads();  // (the page's shared state before the next page's)
+  }
   if (last_workgroup(lt.ctr + 0)) lv_plan2_scan(npages, rt, lt);
 }
 
@@ -2499,7 +2503,11 @@ static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, in
   hipLaunchKernelGGL(k_lv_plan, dim3((npages + WG - 1) / WG), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_bound, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_segwalk, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
-  hipLaunchKernelGGL(k_lv_segscan, dim3(npages), dim3(WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);
+#ifndef PQG_SS_GRID
+#define PQG_SS_GRID 512
+#endif
+  hipLaunchKernelGGL(k_lv_segscan, dim3(npages < PQG_SS_GRID ? npages : PQG_SS_GRID), dim3(WG), 0, s, blob, pages, npages,
+                     chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_lv_compact, dim3(wgrid), dim3(WG), 0, s, npages, rt, lt);
 }
 
