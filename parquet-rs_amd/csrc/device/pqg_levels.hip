@@ -2264,7 +2264,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
 // the previous window's stores.
 constexpr uint32_t LE_RPL = (LW_RPW + 1 + WAVE - 1) / WAVE;  // record registers per lane (5)
 constexpr uint32_t LE_SPL = (LE_STG / 16 + WAVE - 1) / WAVE;  // stage registers per lane (3)
-constexpr uint32_t LE_SMAX = 16;                              // waves per window at most
+#ifndef PQG_EW_GRIDX
+#define PQG_EW_GRIDX 1
+#endif
+#ifndef PQG_LE_SMAX
+#define PQG_LE_SMAX 16
+#endif
+constexpr uint32_t LE_SMAX = PQG_LE_SMAX;                     // waves per window at most
 constexpr uint32_t LE_SLICE = 16384;                          // outputs per slice at least
 
 // The unpipelined writers (dictionary values) take up to LE_UNIT consecutive windows of a page as
@@ -2545,7 +2551,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
                        chunks, sel, rt, lt, LvLevelOut<1>{});
   } else {
     hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
-    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
+    hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid * PQG_EW_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages,
                        chunks, sel, rt, lt, LvLevelOut<2>{});
   }
   return hipGetLastError();
