@@ -193,10 +193,9 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
   if (!valid_chunk(r, rg, col) || !ctx || !out) return PQG_ERR_INVALID;
   *out = nullptr;
   ChunkPages* c = get_chunk(r, rg, col);
-  if (c->status) {
-    r->err = c->err;
-    return c->status;
-  }
+  // a header / decompression failure on page k: the pages before it are decoded and served, the
+  // batch that reaches page k returns its status (read_new_page -> get_next_page, column/reader.rs:269-275)
+  const int host_st = c->status;
   std::unique_ptr<pqg_column_reader> cr(new pqg_column_reader());
   const LeafColumn& l = r->meta.leaves[col];
   cr->col.physical_type = l.physical_type;
@@ -211,6 +210,13 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
     if (p.page_type == PQG_PAGE_DATA || p.page_type == PQG_PAGE_DATA_V2) cr->total_levels += p.num_values;
   }
   const uint64_t n = cr->total_levels;
+  if (host_st && c->pages.empty()) {  // nothing before the failure: the first batch fails
+    cr->status = host_st;
+    cr->err = c->err;
+    cr->bad_level = 0;
+    *out = cr.release();
+    return PQG_OK;
+  }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   if (!r->staging || r->staging->device != dev) {
@@ -298,6 +304,10 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
   if (st != PQG_OK) {
     cr->bad_level = (bad >= 0 && bad < (int)page_start.size()) ? page_start[bad] : 0;
     // a bad dictionary page (or any failure before the first data page) fails the first batch
+  } else if (host_st) {  // every page before the host failure decoded: it fails the batch after them
+    cr->status = host_st;
+    cr->err = c->err;
+    cr->bad_level = n;
   }
   *out = cr.release();
   return PQG_OK;
@@ -317,8 +327,9 @@ int pqg_column_reader_read_batch(pqg_column_reader* cr, size_t batch_size, int16
   if (cr->col.max_def > 0 && !def) return PQG_ERR_INVALID;
   uint64_t left = cr->total_levels - cr->L;
   uint64_t nlev = batch_size < left ? batch_size : left;
+  // (a failure after the last decoded page fails the call that finds no levels left)
+  if (cr->status != PQG_OK && cr->L + (nlev ? nlev : 1) > cr->bad_level) return cr->status;
   if (nlev == 0) return PQG_OK;
-  if (cr->status != PQG_OK && cr->L + nlev > cr->bad_level) return cr->status;
   uint64_t nval = nlev;
   if (use_def) {
     nval = 0;

@@ -509,6 +509,7 @@ int decompress(int codec, const uint8_t* in, uint64_t in_len, uint8_t* out, uint
 
 int plan_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMeta& cc,
                      std::vector<PagePlan>& plan, uint64_t& blob_len, std::string& err) {
+  blob_len = 64;
   // get_column_page_reader, file/reader.rs:314-330
   int64_t start = cc.has_dict_offset ? cc.dictionary_page_offset : cc.data_page_offset;
   int64_t len = cc.total_compressed_size;
@@ -519,6 +520,8 @@ int plan_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
   const uint8_t* p = file + start;
   uint64_t avail = (uint64_t)len, pos = 0, at = 0;
   int64_t seen = 0;
+  // on a failure `plan` keeps the pages before it (their payloads can still be filled and decoded,
+  // so that a failure on an earlier page is reported first, as the reference's page-by-page reads do)
   // SerializedPageReader::get_next_page, file/reader.rs:420-522
   while (seen < cc.num_values) {
     PageHeaderInfo h;
@@ -580,6 +583,7 @@ int plan_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
     }
     plan.push_back(pp);
     at = (at + out_len + 63) & ~63ull;
+    blob_len = at + 64;
   }
   blob_len = at + 64;  // tail slack
   return PQG_OK;
@@ -598,15 +602,18 @@ int read_chunk_pages(const uint8_t* file, uint64_t file_len, const ColumnChunkMe
                      std::vector<uint8_t>& blob, std::vector<pqg_page>& pages, std::string& err) {
   std::vector<PagePlan> plan;
   uint64_t len = 0;
-  int st = plan_chunk_pages(file, file_len, cc, plan, len, err);
-  if (st) return st;
+  std::string herr;
+  const int hst = plan_chunk_pages(file, file_len, cc, plan, len, herr);
+  // the pages before a header failure are read first: a decompression failure on one of them is
+  // the reference's first error (get_next_page reads and decompresses page by page)
   blob.assign(len, 0);
   for (const PagePlan& pp : plan) {
-    st = fill_page(pp, cc.codec, blob.data(), err);
+    const int st = fill_page(pp, cc.codec, blob.data(), err);
     if (st) return st;
     pages.push_back(pp.page);
   }
-  return PQG_OK;
+  if (hst) err = herr;
+  return hst;
 }
 
 }  // namespace pqg

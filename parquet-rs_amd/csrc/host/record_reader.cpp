@@ -470,6 +470,7 @@ Field read_field(Node& n) {  // Reader::read_field (reader.rs:397-472)
 // ---------------------------------------------------------------- rendering
 std::string fmt_float(double v, bool is_f32) {  // api.rs:570-583: {:E} outside [1e-15, 1e19], else {:?}
   char b[64];
+  if (v != v) return "NaN";  // both range tests fail: {:?} prints any NaN as "NaN"
   if (v > 1e19 || v < 1e-15) {
     auto res = is_f32 ? std::to_chars(b, b + sizeof(b), (float)v, std::chars_format::scientific)
                       : std::to_chars(b, b + sizeof(b), v, std::chars_format::scientific);

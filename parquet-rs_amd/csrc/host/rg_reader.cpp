@@ -131,6 +131,8 @@ struct Col {
 struct Slot {
   int rg = -1;
   pqg_ctx* ctx = nullptr;  // one decode in flight per slot, so each is synced on its own
+  hipStream_t s_d2h = nullptr;  // the slot's own D2H copies: waiting for them never waits for the
+                                // next row group's decode (its copies are on another slot's stream)
   hipEvent_t ev_h2d = nullptr, ev_dec = nullptr;
   Buf h_blob, d_blob;
   uint64_t blob_len = 0;
@@ -152,7 +154,7 @@ struct pqg_rgr {
   int device = 0;
   int flags = 0;
   Pool* pool = nullptr;
-  hipStream_t s_h2d = nullptr, s_dec = nullptr, s_d2h = nullptr;
+  hipStream_t s_h2d = nullptr, s_dec = nullptr;
   Slot slot[3];
   int head = 0, count = 0, cur = -1;
   pqg_rgr_stats st{};
@@ -212,11 +214,11 @@ int pqg_rgr_open(pqg_file_reader* r, int device, int host_threads, int flags, pq
   };
   if (hipSetDevice(device) != hipSuccess) return bail(PQG_ERR_HIP);
   if (hipStreamCreateWithFlags(&g->s_h2d, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&g->s_d2h, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) != hipSuccess)
     return bail(PQG_ERR_HIP);
   for (Slot& s : g->slot) {
     if (pqg_ctx_create(device, &s.ctx) != PQG_OK) return bail(PQG_ERR_HIP);
+    if (hipStreamCreateWithFlags(&s.s_d2h, hipStreamNonBlocking) != hipSuccess) return bail(PQG_ERR_HIP);
     if (hipEventCreateWithFlags(&s.ev_h2d, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s.ev_dec, hipEventDisableTiming) != hipSuccess)
       return bail(PQG_ERR_HIP);
@@ -231,8 +233,11 @@ int pqg_rgr_close(pqg_rgr* g) {
   if (!g) return PQG_OK;
   if (g->s_dec) hipStreamSynchronize(g->s_dec);
   if (g->s_h2d) hipStreamSynchronize(g->s_h2d);
-  if (g->s_d2h) hipStreamSynchronize(g->s_d2h);
   for (Slot& s : g->slot) {
+    if (s.s_d2h) {
+      hipStreamSynchronize(s.s_d2h);
+      hipStreamDestroy(s.s_d2h);
+    }
     if (s.ctx) pqg_ctx_destroy(s.ctx);
     if (s.ev_h2d) hipEventDestroy(s.ev_h2d);
     if (s.ev_dec) hipEventDestroy(s.ev_dec);
@@ -246,7 +251,6 @@ int pqg_rgr_close(pqg_rgr* g) {
   }
   if (g->s_h2d) hipStreamDestroy(g->s_h2d);
   if (g->s_dec) hipStreamDestroy(g->s_dec);
-  if (g->s_d2h) hipStreamDestroy(g->s_d2h);
   delete g->pool;
   delete g;
   return PQG_OK;
@@ -258,19 +262,19 @@ const char* pqg_rgr_error(pqg_rgr* g) { return g ? g->err.c_str() : "null reader
 // slot), byte-array offsets (up to every level slot + 1).
 static int enqueue_known_d2h(pqg_rgr* g, Slot& s) {
   if (!(g->flags & PQG_RGR_HOST_OUTPUT)) return PQG_OK;
-  RCHK(hipStreamWaitEvent(g->s_d2h, s.ev_dec, 0), "wait decode");
+  RCHK(hipStreamWaitEvent(s.s_d2h, s.ev_dec, 0), "wait decode");
   for (uint32_t j = 0; j < s.ndec; ++j) {
     Col& c = s.cols[j];
     const pqg_column& d = s.desc[j];
     const bool ba = d.physical_type == PQG_BYTE_ARRAY || d.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
     const uint64_t n = c.levels;
     if (!n) continue;
-    if (d.max_def > 0) RCHK(hipMemcpyAsync(c.hst[O_DEF].p, c.dev[O_DEF].p, n * 2, hipMemcpyDeviceToHost, g->s_d2h), "D2H def");
-    if (d.max_rep > 0) RCHK(hipMemcpyAsync(c.hst[O_REP].p, c.dev[O_REP].p, n * 2, hipMemcpyDeviceToHost, g->s_d2h), "D2H rep");
+    if (d.max_def > 0) RCHK(hipMemcpyAsync(c.hst[O_DEF].p, c.dev[O_DEF].p, n * 2, hipMemcpyDeviceToHost, s.s_d2h), "D2H def");
+    if (d.max_rep > 0) RCHK(hipMemcpyAsync(c.hst[O_REP].p, c.dev[O_REP].p, n * 2, hipMemcpyDeviceToHost, s.s_d2h), "D2H rep");
     if (ba) {
-      RCHK(hipMemcpyAsync(c.hst[O_OFF].p, c.dev[O_OFF].p, (n + 1) * 8, hipMemcpyDeviceToHost, g->s_d2h), "D2H offsets");
+      RCHK(hipMemcpyAsync(c.hst[O_OFF].p, c.dev[O_OFF].p, (n + 1) * 8, hipMemcpyDeviceToHost, s.s_d2h), "D2H offsets");
     } else {
-      RCHK(hipMemcpyAsync(c.hst[O_VAL].p, c.dev[O_VAL].p, c.vcap, hipMemcpyDeviceToHost, g->s_d2h), "D2H values");
+      RCHK(hipMemcpyAsync(c.hst[O_VAL].p, c.dev[O_VAL].p, c.vcap, hipMemcpyDeviceToHost, s.s_d2h), "D2H values");
     }
   }
   return PQG_OK;
@@ -340,10 +344,9 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
     c.len = 0;
     if (s.host_col >= 0) continue;
     c.host_st = plan_chunk_pages(r->data, r->len, rgm.columns[j], c.plan, c.len, c.host_err);
-    if (c.host_st) {
-      c.host_page = (int)c.plan.size();
+    if (c.host_st) {  // the pages before the failing header are still filled and decoded: a failure
+      c.host_page = (int)c.plan.size();  // on one of them is reported first
       s.host_col = (int)j;
-      continue;
     }
     c.base = at;
     at = (at + c.len + 255) & ~255ull;
@@ -351,7 +354,8 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
     for (const PagePlan& pp : c.plan)
       if (pp.page.page_type == PQG_PAGE_DATA || pp.page.page_type == PQG_PAGE_DATA_V2) c.levels += pp.page.num_values;
   }
-  s.ndec = s.host_col >= 0 ? (uint32_t)s.host_col : nc;
+  // columns handed to the decode: up to a failing column, which takes the pages before its failure
+  s.ndec = s.host_col < 0 ? nc : (uint32_t)s.host_col + (s.cols[s.host_col].plan.empty() ? 0u : 1u);
   s.blob_len = at;
   const auto tp = std::chrono::steady_clock::now();
   // ---- payloads into pinned staging, page by page over the pool
@@ -371,13 +375,17 @@ int pqg_rgr_submit(pqg_rgr* g, int rg) {
   const auto tf = std::chrono::steady_clock::now();
   for (size_t k = 0; k < work.size(); ++k)  // the lowest failing (column, page): the reference's first
     if (wst[k]) {
-      const uint32_t j = work[k].first;
+      const uint32_t j = work[k].first, i = work[k].second;
       Col& c = s.cols[j];
       c.host_st = wst[k];
-      c.host_page = (int)work[k].second;
+      c.host_page = (int)i;
       c.host_err = werr[k];
       s.host_col = (int)j;
-      s.ndec = j;
+      c.plan.resize(i);  // the pages before it are decoded (a decode failure there comes first)
+      c.levels = 0;
+      for (const PagePlan& pp : c.plan)
+        if (pp.page.page_type == PQG_PAGE_DATA || pp.page.page_type == PQG_PAGE_DATA_V2) c.levels += pp.page.num_values;
+      s.ndec = j + (i ? 1u : 0u);
       break;
     }
   // ---- tables and outputs
@@ -439,7 +447,7 @@ int pqg_rgr_wait(pqg_rgr* g, int* rg_out, int* bad_column, int* bad_page) {
   const auto t1 = std::chrono::steady_clock::now();
   if (st == PQG_ERR_CAPACITY) {  // a byte-array chunk decoded to more than its bound: grow, decode again
     bool grew = false;
-    RCHK(hipStreamSynchronize(g->s_d2h), "sync D2H");  // the first pass's copies land before buffers move
+    RCHK(hipStreamSynchronize(s.s_d2h), "sync D2H");  // the first pass's copies land before buffers move
     for (uint32_t j = 0; j < s.ndec; ++j)
       if (s.outs[j].num_bytes > s.cols[j].vcap) {
         s.cols[j].vcap = s.outs[j].num_bytes;
@@ -479,9 +487,9 @@ int pqg_rgr_wait(pqg_rgr* g, int* rg_out, int* bad_column, int* bad_page) {
       Col& c = s.cols[j];
       const bool ba = d.physical_type == PQG_BYTE_ARRAY || d.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
       const uint64_t nb = s.outs[j].num_bytes < c.vcap ? s.outs[j].num_bytes : c.vcap;
-      if (ba && nb) RCHK(hipMemcpyAsync(c.hst[O_VAL].p, c.dev[O_VAL].p, nb, hipMemcpyDeviceToHost, g->s_d2h), "D2H bytes");
+      if (ba && nb) RCHK(hipMemcpyAsync(c.hst[O_VAL].p, c.dev[O_VAL].p, nb, hipMemcpyDeviceToHost, s.s_d2h), "D2H bytes");
     }
-    RCHK(hipStreamSynchronize(g->s_d2h), "sync D2H");
+    RCHK(hipStreamSynchronize(s.s_d2h), "sync D2H");
   }
   const auto t2 = std::chrono::steady_clock::now();
   g->st.sync_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();

@@ -212,8 +212,9 @@ class Context:
         lib().pqg_ctx_set_timing(self.h, 1 if enabled else 0)
 
     def set_overlap(self, enabled):
-        """Speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap): 0 off (default), n > 0 on with
-        n workgroups per page."""
+        """Speculative PLAIN copy beside the level decode (pqg_ctx_set_overlap), a mode: 0 off (default),
+        1 early fork (one workgroup per page on a side stream), 2 late fork (full grid); values above 2
+        are taken as 2."""
         lib().pqg_ctx_set_overlap(self.h, int(enabled))
 
     def decode_async(self, column, blob, blob_len, pages, out, stream=0, npages=None):

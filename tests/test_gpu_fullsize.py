@@ -80,6 +80,40 @@ def test_headline_pages_full_size(oracle, ctx, p_null):
     _check(oracle, ctx, _specs(oracle, host, pages, info.npages))
 
 
+def test_dictionary_pages_bench_shape(oracle, ctx):
+    """Config 3's page shape (bench.py `dict`): a 65 536-entry INT64 dictionary page and 2^20-index
+    data pages of bit width 16, written by the bench's own generator (pqg_gen_dict_int64: reference
+    DictEncoder + RleEncoder, rle.rs:152-316), four full pages and a ragged fifth, against the
+    oracle's read_batch (get_batch_with_dict, rle.rs:437-487; DictDecoder, decoding.rs:282-309):
+    every value. This is the general decoder's full-page path (k_run_index's 64-run fast-forward,
+    k_tile_desc, 256 k_texpand_dict tiles per page)."""
+    import ctypes as C
+
+    import pqgpu
+    L = pqgtools.lib()
+    n = 4 * PAGE + 54321
+    info = pqgtools.WorkloadInfo()
+    seed = 0x5EED0003
+    assert L.pqg_gen_dict_int64(n, 65536, PAGE, seed, 8, None, 0, None, 0, C.byref(info)) == 0
+    host = np.zeros(info.blob_len + 64, np.uint8)
+    pages = (pqgpu.Page * info.npages)()
+    assert L.pqg_gen_dict_int64(n, 65536, PAGE, seed, 8, host.ctypes.data_as(C.c_void_p), info.blob_len, pages,
+                                info.npages, C.byref(info)) == 0
+    assert info.npages == 6 and pages[0].page_type == oracle.PAGE_DICTIONARY and pages[0].num_values == 65536
+    assert host[pages[1].offset] == 16  # the data page's bit width byte
+    specs = _specs(oracle, host, pages, info.npages)
+    ref = oracle.read_column(oracle.INT64, specs, batch_size=1024)
+    got = pqgpu.decode_column(ctx, pqgpu.INT64, specs)
+    assert ref["status"] == 0, ref["message"]
+    assert got["status"] == 0, got["message"]
+    assert got["num_values"] == n == len(ref["values"])
+    np.testing.assert_array_equal(got["values"], ref["values"])
+    # and the generator's own truth for the ragged last page
+    last = np.zeros(pages[5].num_values, np.int64)
+    L.pqg_truth_dict_int64(n, 65536, PAGE, seed, 4, last.ctypes.data)
+    np.testing.assert_array_equal(got["values"][4 * PAGE:], last)
+
+
 # ------------------------------------------------------------------------------ crafted streams
 # A one-bit level stream of the writer's full bit-packed runs (header 0x7F: 63 groups, 504 levels,
 # 64 bytes apart), whose payload bytes are chosen so that chains entering a window on payload

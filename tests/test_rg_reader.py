@@ -168,3 +168,94 @@ def test_corrupt_page_fails_at_its_column(tmp_path):
             _check_row_group(rd, g)
     rd.close()
     r.close()
+
+
+def _damaged_file(tmp_path, payload_page=None, header_page=None, col=10, rg=1):
+    """The alltypes file (SNAPPY) with page `payload_page` of (rg, col) given a garbled compressed
+    payload and/or page `header_page`'s header overwritten. timestamp_col holds three pages at
+    ROWS rows: its dictionary page, a dictionary-encoded page, the PLAIN fallback page."""
+    import _pagewalk
+    pq = pytest.importorskip("pyarrow.parquet")
+    path = str(tmp_path / f"bad_{payload_page}_{header_page}.parquet")
+    pqgtools.write_alltypes_file(path, ROWS, GROUPS, row0=ROW0, p_null=P_NULL, seed=SEED, codec=1, threads=8)
+    cc = pq.ParquetFile(path).metadata.row_group(rg).column(col)
+    start = cc.dictionary_page_offset if cc.has_dictionary_page else cc.data_page_offset
+    data = bytearray(open(path, "rb").read())
+    pages = _pagewalk.chunk_pages(data, start, cc.total_compressed_size)
+    assert len(pages) == 3
+    if payload_page is not None:
+        _, at, n, _ = pages[payload_page]
+        for k in range(4):  # the snappy preamble (uncompressed length): the page fails to decompress
+            data[at + k] = 0xFF
+    if header_page is not None:
+        at = pages[header_page][0]
+        for k in range(6):
+            data[at + k] = 0xFF
+    open(path, "wb").write(bytes(data))
+    return path
+
+
+def test_decompression_failure_before_a_bad_header_is_reported_first(tmp_path):
+    """Pages are read in order (SerializedPageReader::get_next_page reads and decompresses one page
+    before parsing the next header, file/reader.rs:420-461): a garbled payload on page 1 is the
+    chunk's error even though page 2's header is damaged too."""
+    import pqgpu
+    both = pqgpu.FileReader(_damaged_file(tmp_path, payload_page=1, header_page=2))
+    one = pqgpu.FileReader(_damaged_file(tmp_path, payload_page=1))
+    hdr = pqgpu.FileReader(_damaged_file(tmp_path, header_page=2))
+    errs = []
+    for r in (both, one, hdr):
+        with pytest.raises(pqgpu.PqgError) as e:
+            r.chunk_pages(1, 10)
+        errs.append((e.value.status, str(e.value)))
+    assert errs[0] == errs[1] and errs[0] != errs[2], errs
+    for r in (both, one, hdr):
+        r.close()
+
+
+@pytest.mark.gpu
+def test_row_group_reader_reports_the_earliest_host_failure(tmp_path):
+    """pqg_rgr: a damaged payload on page 1 and a damaged header on page 2 of timestamp_col report
+    page 1; a damaged header alone reports page 2 after the pages before it decoded."""
+    import pqgpu
+    for payload, header, want in ((1, 2, 1), (None, 2, 2)):
+        r = pqgpu.FileReader(_damaged_file(tmp_path, payload_page=payload, header_page=header))
+        rd = pqgpu.RowGroupReader(r)
+        rd.submit(1)
+        st, rg, col, page = rd.wait()
+        assert st != 0 and (rg, col, page) == (1, 10, want), (st, rg, col, page, rd.error())
+        assert all(rd.column(j)[0] == 0 for j in range(10))
+        assert rd.column(10)[0] != 0
+        rd.close()
+        r.close()
+
+
+@pytest.mark.gpu
+def test_column_reader_serves_the_pages_before_a_bad_header(tmp_path):
+    """read_batch over a chunk whose third page header is damaged: the levels and values of the
+    pages before it come back as decoded, the batch that reaches the damaged page fails
+    (read_new_page -> get_next_page, column/reader.rs:269-275)."""
+    import pqgpu
+    r = pqgpu.FileReader(_damaged_file(tmp_path, header_page=2))
+    ctx = pqgpu.Context(0)
+    cr = r.column_reader(1, 10, ctx)
+    lv, vals, _ = _truth(1, 10)
+    good = pqgpu.FileReader(_damaged_file(tmp_path))  # the same file undamaged: page 1's level count
+    _, hp, n = good.chunk_pages(1, 10)
+    n1 = hp[1].num_values
+    got_d, got_v = [], []
+    with pytest.raises(pqgpu.PqgError):
+        while True:
+            v, d, _, _, _ = cr.read_batch(1000)
+            got_d.append(d)
+            got_v.append(v)
+            assert len(d) == 1000 or sum(map(len, got_d)) == n1
+    d = np.concatenate(got_d)
+    assert len(d) == n1
+    np.testing.assert_array_equal(d, lv[:n1])
+    nv = int(np.count_nonzero(lv[:n1]))
+    assert np.concatenate(got_v).tobytes() == vals[:12 * nv].tobytes()
+    cr.close()
+    ctx.close()
+    good.close()
+    r.close()

@@ -270,3 +270,22 @@ def test_rows_display_text(ctx):
     assert list(it) == [exp]
     it.close()
     r.close()
+
+
+def test_rows_display_float_specials(ctx, tmp_path):
+    """Display of FLOAT / DOUBLE fields outside the fixed-notation range (record/api.rs:570-583):
+    {:E} above 1e19 and below 1e-15 (zero and negatives included), {:?} otherwise; a NaN fails
+    both range tests and prints as Rust's {:?} does, "NaN"."""
+    pa = pytest.importorskip("pyarrow")
+    pq = pytest.importorskip("pyarrow.parquet")
+    import pqgpu
+    vals = [float("nan"), 1.5, 0.0, -2.0, float("inf"), 3e20]
+    path = str(tmp_path / "floats.parquet")
+    pq.write_table(pa.table({"f": pa.array(vals, pa.float32()), "d": pa.array(vals, pa.float64())}), path,
+                   use_dictionary=False, compression="NONE")
+    r = pqgpu.FileReader(path)
+    it = pqgpu.RowIter(r, ctx, display=True)
+    txt = ["NaN", "1.5", "0E0", "-2E0", "inf", "3E20"]
+    assert list(it) == ["{f: %s, d: %s}" % (t, t) for t in txt]
+    it.close()
+    r.close()
