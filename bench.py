@@ -58,7 +58,13 @@ def parse(argv=None):
     ap.add_argument("--delta-bits", type=int, default=16)
     ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--mini-blocks", type=int, default=4)
-    ap.add_argument("--variants", type=int, default=1, help="also time the p_null 0.5 / 0.1 variants")
+    ap.add_argument("--variants", type=int, default=1,
+                    help="also time the p_null 0.5 / 0.1 variants (config 2) and the writer-default DELTA "
+                         "block shape, 128 values in 4 mini-blocks of 32 (config 4, encoding.rs:508-509)")
+    ap.add_argument("--split", default="auto", choices=["auto", "weak", "strong"],
+                    help="configs 2-4 over N ranks: weak = every rank decodes its own 1e9-value stream; "
+                         "strong = the ranks split one 1e9-value stream into contiguous page ranges "
+                         "(SURVEY 8(e)); auto = weak, plus a strong-scaling line per config when N > 1")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--pcie", type=int, default=1, help="also time the host-to-host (PCIe) rate")
     ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline budget of the headline")
@@ -80,7 +86,7 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-from sharding import max_over_ranks, row_groups_for_rank, shard_seed  # noqa: E402
+from sharding import max_over_ranks, pages_for_rank, row_groups_for_rank, shard_seed  # noqa: E402
 
 
 def _free_port():
@@ -133,7 +139,7 @@ class Workload:
     """Synthetic pages generated on the host by the reference-identical writers of
     libpqgtools.so (tools/gen) and uploaded once to HBM."""
 
-    def __init__(self, pqgpu, args, rank, kind, p_null=None):
+    def __init__(self, pqgpu, args, rank, kind, p_null=None, block=None, world=1, strong=False):
         import torch
         import pqgtools
         L = pqgtools.lib()
@@ -144,23 +150,32 @@ class Workload:
         self.p_null = p_null
         self.page_values = args.page_values
         self.dict_size, self.delta_bits = args.dict_size, args.delta_bits
+        self.block = block or (args.block_size, args.mini_blocks)
         th = host_threads(args.threads)[0]
+        # weak: this rank's own stream (seeded per rank), every page of it; strong: pages
+        # [first, first + count) of the one stream every rank shares (rank 0's seed)
+        srank = 0 if strong else rank
+        npages_all = (n + args.page_values - 1) // args.page_values
+        self.first, cnt = pages_for_rank(npages_all, world, rank) if strong else (0, npages_all)
+        self.strong = strong
+        first = self.first
         if kind == "levels":
-            self.seed = shard_seed(args.seed + 2, rank)
-            gen = lambda blob, cap, pages, pcap: L.pqg_gen_levels_plain(
-                n, p_null, args.page_values, self.seed, th, blob, cap, pages, pcap, C.byref(info))
+            self.seed = shard_seed(args.seed + 2, srank)
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_levels_plain_pages(
+                n, p_null, args.page_values, self.seed, first, cnt, th, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT32, -1, 1, 0)
             self.es = 4
         elif kind == "dict":
-            self.seed = shard_seed(args.seed + 3, rank)
-            gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64(
-                n, args.dict_size, args.page_values, self.seed, th, blob, cap, pages, pcap, C.byref(info))
+            self.seed = shard_seed(args.seed + 3, srank)
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_dict_int64_pages(
+                n, args.dict_size, args.page_values, self.seed, first, cnt, th, blob, cap, pages, pcap,
+                C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
         else:
-            self.seed = shard_seed(args.seed + 4, rank)
-            gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64(
-                n, args.delta_bits, args.page_values, args.block_size, args.mini_blocks, self.seed,
+            self.seed = shard_seed(args.seed + 4, srank)
+            gen = lambda blob, cap, pages, pcap: L.pqg_gen_delta_int64_pages(
+                n, args.delta_bits, args.page_values, self.block[0], self.block[1], self.seed, first, cnt,
                 th, blob, cap, pages, pcap, C.byref(info))
             self.col = pqgpu.Column(pqgpu.INT64, -1, 0, 0)
             self.es = 8
@@ -224,10 +239,11 @@ def check_values(ctx, w, stream):
     for k in sorted({0, ndata // 2, ndata - 1}):
         cnt = w.pages[first + k].num_values
         lo = k * w.page_values  # every page but the last holds page_values levels/values
+        gk = w.first + k        # the page's index in the stream (strong scaling: this rank's range)
         if w.kind == "levels":
             lv = np.zeros(cnt, np.int16)
             vals = np.zeros(cnt, np.int32)
-            nn = L.pqg_truth_levels_plain(w.n, w.p_null, w.page_values, w.seed, k, lv.ctypes.data, vals.ctypes.data)
+            nn = L.pqg_truth_levels_plain(w.n, w.p_null, w.page_values, w.seed, gk, lv.ctypes.data, vals.ctypes.data)
             got_lv = w.d_def[lo:lo + cnt].cpu().numpy()
             assert np.array_equal(got_lv, lv), f"def levels of page {k} differ from the generator"
             voff = int((w.d_def[:lo] == 1).sum().item())
@@ -236,9 +252,9 @@ def check_values(ctx, w, stream):
         else:
             vals = np.zeros(cnt, np.int64)
             if w.kind == "dict":
-                L.pqg_truth_dict_int64(w.n, w.dict_size, w.page_values, w.seed, k, vals.ctypes.data)
+                L.pqg_truth_dict_int64(w.n, w.dict_size, w.page_values, w.seed, gk, vals.ctypes.data)
             else:
-                L.pqg_truth_delta_int64(w.n, w.delta_bits, w.page_values, w.seed, k, vals.ctypes.data)
+                L.pqg_truth_delta_int64(w.n, w.delta_bits, w.page_values, w.seed, gk, vals.ctypes.data)
             got_v = w.d_val[8 * lo:8 * (lo + cnt)].cpu().numpy().view(np.int64)
             assert np.array_equal(got_v, vals), f"values of page {k} differ from the generator"
         checked += 1
@@ -415,48 +431,62 @@ LEVEL_NOTE = ("HIP events around pqg_launch_levels: the def-level kernel chain (
 
 
 def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, steps=None, warmup=None,
-              cpu_seconds=None, extras=True):
+              cpu_seconds=None, extras=True, block=None, variant=None, strong=False):
     """One of configs[1..3]: generate, check, time (production path), stage times, roofline, and
-    on rank 0 of a 1-GPU run the PCIe-inclusive rate and the CPU baseline."""
+    on rank 0 of a 1-GPU run the PCIe-inclusive rate and the CPU baseline. strong: the ranks split
+    one stream into contiguous page ranges (value = the stream's units / the slowest rank's time)."""
     import torch
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
-    w = Workload(pqgpu, args, rank, kind, p_null=p_null)
+    w = Workload(pqgpu, args, rank, kind, p_null=p_null, block=block, world=world, strong=strong)
     checked = check_values(ctx, w, stream)
     per_step = max_over_ranks(time_steps(ctx, w, stream, steps, warmup, dist), dist)
     tm = time_stages(pqgpu, ctx, w, stream, max(3, steps // 4), args.overlap)
     units = w.levels if kind == "levels" else w.values
     step_bytes = w.in_bytes + w.out_bytes
-    variant = None
     if kind == "levels":
         lev_b = w.level_bytes_in + 2 * w.levels   # level stream in + int16 levels out
         val_b = 2 * w.values * w.es               # PLAIN values in + out
         variant = f"p{int(round(p_null * 100)):02d}"
-        stages = [("level path", tm.levels_kernel_ms, lev_b), ("k_plain_copy", tm.values_kernel_ms, val_b)]
+        stages = [("level path", tm.levels_kernel_ms, lev_b, w.level_bytes_in),
+                  ("k_plain_copy", tm.values_kernel_ms, val_b, w.values * w.es)]
     elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
-        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
+        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
     else:                  # deltas in + values out
-        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes)]
+        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
+        if tuple(w.block) != (512, 4):
+            variant = f"b{w.block[0]}x{w.block[1]}"
     rl = []
-    for name, ms, nb in stages:
+    for name, ms, nb, nin in stages:
         tr, src = pmc_traffic(kind, name, variant)
-        rl.append(roofline(name, ms, nb, tr, src, LEVEL_NOTE if name == "level path" else None))
+        r = roofline(name, ms, nb, tr, src, LEVEL_NOTE if name == "level path" else None)
+        r["read_bytes_per_launch"] = nin
+        r["read_gbs"] = nin / (ms * 1e-3) / 1e9 if ms else None  # SURVEY 8(d): In / time
+        rl.append(r)
     dom = max(rl, key=lambda r: r["avg_ms"] or 0)
+    # the stream each rank decodes: its own (weak) or its page range of the shared one (strong)
+    job_units = (w.n if strong else units * world)
     res = {
-        "value": units * world / per_step,
+        "value": job_units / per_step,
         "unit": "levels/s" if kind == "levels" else "values/s",
         "ms_per_step": per_step * 1e3,
         "gbps": step_bytes / per_step / 1e9 * world,
+        # SURVEY 8(d): read-only rate (encoded page bytes / step time) and the reference bench's
+        # unit, encoded MB/s (benches/decoding.rs:111 sets Throughput::Bytes of the encoded buffer)
+        "read_gbps": w.in_bytes / per_step / 1e9 * world,
+        "encoded_mb_per_s": w.in_bytes / per_step / 1e6 * world,
         "config": {"workload": {"levels": "configs[1]: RLE/bit-packed def levels (max_def 1) + PLAIN INT32",
                                 "dict": "configs[2]: RLE_DICTIONARY INT64, 64K dictionary",
                                 "delta": "configs[3]: DELTA_BINARY_PACKED INT64"}[kind],
                    "levels_per_gpu": w.levels, "values_per_gpu": w.values,
                    "pages_per_gpu": w.npages, "page_values": args.page_values,
                    "p_null": w.p_null, "in_bytes_per_gpu": w.in_bytes, "out_bytes_per_gpu": w.out_bytes,
-                   "block_size": args.block_size if kind == "delta" else None,
-                   "mini_blocks": args.mini_blocks if kind == "delta" else None,
+                   "block_size": w.block[0] if kind == "delta" else None,
+                   "mini_blocks": w.block[1] if kind == "delta" else None,
+                   "values_per_mini_block": w.block[0] // w.block[1] if kind == "delta" else None,
                    "gen_seconds": round(w.gen_s, 1),
-                   "parallelism": f"row-group partitions x{world}, no collective"},
+                   "parallelism": (f"one stream split into contiguous page ranges x{world}, no collective"
+                                   if strong else f"row-group partitions x{world}, no collective")},
         "roofline": dom,
         "roofline_stages": rl if len(rl) > 1 else None,
         "stages_note": ("stage and kernel times from HIP events with the stages one after the other "
@@ -467,6 +497,16 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
                       "levels_kernel": tm.levels_kernel_ms, "values_kernel": tm.values_kernel_ms},
         "value_check": checked,
     }
+    if strong:  # the job's bytes (sum of the ranks' shares) over the slowest rank's time
+        tot = [float(w.in_bytes), float(w.out_bytes)]
+        if dist is not None:
+            t = torch.tensor(tot, dtype=torch.float64)
+            dist.all_reduce(t)
+            tot = [float(x) for x in t]
+        res["gbps"] = (tot[0] + tot[1]) / per_step / 1e9
+        res["read_gbps"] = tot[0] / per_step / 1e9
+        res["encoded_mb_per_s"] = tot[0] / per_step / 1e6
+        res["config"]["first_page"] = w.first
     if extras and rank == 0 and world == 1:
         if args.pcie:
             res["pcie_inclusive"] = pcie_inclusive(ctx, w, stream)
@@ -853,30 +893,52 @@ def main(argv=None):
     import pqgpu
     stream = torch.cuda.current_stream().cuda_stream
     head = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if args.split == "strong" else "weak", "vs_baseline": None,
             "data": "synthetic pages from reference-identical writers (SplitMix64 seeded)"}
     sub = {}
     kinds = ["levels", "dict", "delta", "alltypes"] if args.config == "all" else [args.config]
     ctx = pqgpu.Context(torch.cuda.current_device())
     ctx.set_overlap(args.overlap)
     short_steps = max(5, args.steps // 2)
+    strong = args.split == "strong"
+
+    def brief(r, key):
+        return {key: r["value"], "ms_per_step": r["ms_per_step"], "gbps": r["gbps"], "read_gbps": r["read_gbps"],
+                "encoded_mb_per_s": r["encoded_mb_per_s"], "values_per_gpu": r["config"]["values_per_gpu"],
+                "config": {k: r["config"][k] for k in ("block_size", "mini_blocks", "values_per_mini_block",
+                                                       "pages_per_gpu", "parallelism") if k in r["config"]},
+                "roofline": r["roofline"], "roofline_stages": r["roofline_stages"], "stages_ms": r["stages_ms"],
+                "value_check": r["value_check"]}
+
     for kind in kinds:
         if kind == "alltypes":
             sub[kind] = run_alltypes(pqgpu, args, world, rank, dist, stream)
-        elif kind == "levels":
-            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "levels", p_null=args.p_null)
+            continue
+        unit_key = "levels_per_s" if kind == "levels" else "values_per_s"
+        if kind == "levels":
+            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "levels", p_null=args.p_null,
+                                  strong=strong)
             if args.variants:
                 var = {}
                 for p in (0.5, 0.1):
                     r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "levels", p_null=p,
-                                  steps=short_steps, warmup=2, extras=False)
-                    var[f"p_null={p}"] = {"levels_per_s": r["value"], "ms_per_step": r["ms_per_step"],
-                                          "gbps": r["gbps"], "values_per_gpu": r["config"]["values_per_gpu"],
-                                          "roofline": r["roofline"], "roofline_stages": r["roofline_stages"],
-                                          "stages_ms": r["stages_ms"], "value_check": r["value_check"]}
+                                  steps=short_steps, warmup=2, extras=False, strong=strong)
+                    var[f"p_null={p}"] = brief(r, unit_key)
                 sub[kind]["variants"] = var
         else:
-            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, cpu_seconds=6.0)
+            sub[kind] = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, cpu_seconds=6.0, strong=strong)
+            if kind == "delta" and args.variants:
+                # the reference writer's default block (DeltaBitPackEncoder: 128 values, 4 mini-blocks
+                # of 32, encoding.rs:508-509): the shape real parquet-rs files carry
+                r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "delta", steps=short_steps, warmup=2,
+                              extras=False, block=(128, 4), strong=strong)
+                sub[kind]["variants"] = {"block128_4x32": brief(r, unit_key)}
+        if args.split == "auto" and world > 1:
+            # strong scaling alongside: the ranks split one 1e9-value stream into page ranges
+            r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind,
+                          p_null=args.p_null if kind == "levels" else None, steps=short_steps, warmup=2,
+                          extras=False, strong=True)
+            sub[kind]["strong_scaling"] = dict(brief(r, unit_key), scaling="strong")
     ctx.close()
     top = kinds[0]
     result = dict(head)

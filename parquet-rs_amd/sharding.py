@@ -1,4 +1,4 @@
-"""Row-group partitioning across GPUs (one process per GPU, weak scaling).
+"""Row-group and page-range partitioning across GPUs (one process per GPU).
 
 parquet-rs reads row groups independently (file/reader.rs:252-260 hands each RowGroupReader
 its own file handle), so the multi-GPU layout is a partition of row groups over ranks with no
@@ -25,6 +25,18 @@ def row_groups_for_rank(sizes, world, rank):
         bounds.append(n)
     bounds.append(n)
     return list(range(bounds[rank], bounds[rank + 1]))
+
+
+def pages_for_rank(npages, world, rank):
+    """Contiguous page range [first, first + count) of one column-chunk stream for `rank` (strong
+    scaling: N ranks split the same stream; pages are independent decode units once the dictionary
+    page is replicated, and DELTA state resets per page, decoding.rs:501-533). Ranks differ by at
+    most one page."""
+    if world <= 1:
+        return 0, npages
+    q, r = divmod(npages, world)
+    first = rank * q + min(rank, r)
+    return first, q + (1 if rank < r else 0)
 
 
 def shard_seed(base, rank):

@@ -216,3 +216,109 @@ def test_gpu_page_shards_concatenate_to_whole(kind):
         ctx.close()
     assert b"".join(p[0] for p in parts) == whole[0]
     assert b"".join(p[1] for p in parts) == whole[1]
+
+
+# ---- strong scaling: N ranks split ONE stream into contiguous page ranges
+
+
+def test_page_ranges_cover_the_stream_once():
+    for npages in (1, 2, 7, 954):
+        for world in (1, 2, 3, 8):
+            rs = [sharding.pages_for_rank(npages, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert sum(c for _, c in rs) == npages and max(c for _, c in rs) - min(c for _, c in rs) <= 1
+
+
+STREAM_N, STREAM_PV = 5 * 65536 + 777, 65536  # six pages, the last ragged
+
+
+def _stream_pages(kind, first, count):
+    """Pages [first, first + count) of one config-2/3/4 stream from the bench's page-range
+    generators (the dictionary page first for config 3)."""
+    import ctypes as C
+
+    import numpy as np
+    import pqgpu
+    import pqgtools
+    L = pqgtools.lib()
+    info = pqgtools.WorkloadInfo()
+    if kind == "levels":
+        gen = lambda b, cap, pg, pc: L.pqg_gen_levels_plain_pages(STREAM_N, 0.1, STREAM_PV, 0x5EED0002, first, count,
+                                                                  2, b, cap, pg, pc, C.byref(info))
+    elif kind == "dict":
+        gen = lambda b, cap, pg, pc: L.pqg_gen_dict_int64_pages(STREAM_N, 65536, STREAM_PV, 0x5EED0003, first, count,
+                                                                2, b, cap, pg, pc, C.byref(info))
+    else:
+        gen = lambda b, cap, pg, pc: L.pqg_gen_delta_int64_pages(STREAM_N, 16, STREAM_PV, 128, 4, 0x5EED0004, first,
+                                                                 count, 2, b, cap, pg, pc, C.byref(info))
+    assert gen(None, 0, None, 0) == 0
+    host = np.zeros(info.blob_len + 64, np.uint8)
+    pages = (pqgpu.Page * info.npages)()
+    assert gen(host.ctypes.data_as(C.c_void_p), info.blob_len, pages, info.npages) == 0
+    return host, pages, info
+
+
+def _stream_decode_oracle(kind, first, count):
+    import pyoracle
+    host, pages, info = _stream_pages(kind, first, count)
+    specs = [pyoracle.PageSpec(p.page_type, host[p.offset:p.offset + p.nbytes].tobytes(), p.num_values, p.encoding,
+                               p.def_encoding, p.rep_encoding) for p in (pages[i] for i in range(info.npages))]
+    ptype = {"levels": pyoracle.INT32, "dict": pyoracle.INT64, "delta": pyoracle.INT64}[kind]
+    r = pyoracle.read_column(ptype, specs, max_def=1 if kind == "levels" else 0)
+    assert r["status"] == 0, r["message"]
+    return (r["def"].tobytes() if kind == "levels" else b""), r["values"].tobytes()
+
+
+def _stream_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    sys.path.insert(0, os.path.join(root, "tools", "gen"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        npages = (STREAM_N + STREAM_PV - 1) // STREAM_PV
+        first, count = sharding.pages_for_rank(npages, world, rank)
+        mine = {k: _stream_decode_oracle(k, first, count) for k in ("levels", "dict", "delta")}
+        allp = [None] * world
+        dist.all_gather_object(allp, (first, count, mine))
+        q.put((rank, allp))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_gloo_world2_stream_split_concatenates_to_whole():
+    """bench.py --split strong: each of 2 ranks generates and decodes its contiguous page range of
+    one stream (configs 2-4, the dictionary page replicated); the ranks' outputs in rank order are
+    the single-rank decode of the whole stream, byte for byte."""
+    world = 2
+    port = 33500 + os.getpid() % 2000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(world)]
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    _, allp = res[0]
+    assert [a[0] for a in allp] == [0, allp[0][1]]
+    npages = (STREAM_N + STREAM_PV - 1) // STREAM_PV
+    for kind in ("levels", "dict", "delta"):
+        whole = _stream_decode_oracle(kind, 0, npages)
+        assert b"".join(a[2][kind][0] for a in allp) == whole[0], kind
+        assert b"".join(a[2][kind][1] for a in allp) == whole[1], kind
+
+
+def test_page_range_generator_is_the_whole_streams_pages():
+    """A page range from the generator holds exactly those pages of the whole stream."""
+    for kind in ("levels", "dict", "delta"):
+        hw, pw, iw = _stream_pages(kind, 0, 6)
+        hr, pr, ir = _stream_pages(kind, 2, 3)
+        d = 1 if kind == "dict" else 0
+        for i in range(ir.npages - d):
+            a, b = pr[d + i], pw[d + 2 + i]
+            assert (a.num_values, a.nbytes) == (b.num_values, b.nbytes)
+            assert hr[a.offset:a.offset + a.nbytes].tobytes() == hw[b.offset:b.offset + b.nbytes].tobytes()

@@ -18,6 +18,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -339,29 +340,35 @@ static uint64_t levels_page(uint64_t n, double p_null, uint32_t page_levels, uin
   return nn;
 }
 
-int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
-                         int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
-                         uint32_t pages_cap, pqg_workload_info* info) {
+// Pages [first, first + count) of the config-2 stream (a rank's contiguous share of one stream:
+// page p's content depends on the seed and p alone).
+int pqg_gen_levels_plain_pages(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed, uint32_t first,
+                               uint32_t count, int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                               uint32_t pages_cap, pqg_workload_info* info) {
   if (!info || page_levels == 0) return PQG_ERR_INVALID;
-  const uint32_t np = (uint32_t)((n + page_levels - 1) / page_levels);
+  const uint32_t all = (uint32_t)((n + page_levels - 1) / page_levels);
+  if (first > all || count > all - first) return PQG_ERR_INVALID;
+  const uint32_t np = count;
   const uint64_t slot = align64(4 + rle_bound(1, page_levels) + 4ull * page_levels);
   info->npages = np;
   info->blob_len = slot * np;
-  info->total_levels = n;
+  info->total_levels = 0;
+  for (uint32_t p = first; p < first + np; ++p) info->total_levels += std::min<uint64_t>(page_levels, n - (uint64_t)p * page_levels);
   info->total_values = 0;
   if (!blob) return PQG_OK;
   if (blob_cap < slot * np || pages_cap < np) return PQG_ERR_CAPACITY;
   std::vector<uint64_t> nonnull(np);
-  parallel_pages(np, threads, [&](uint32_t p) {
-    uint8_t* out = blob + (uint64_t)p * slot;
+  parallel_pages(np, threads, [&](uint32_t q) {
+    const uint32_t p = first + q;
+    uint8_t* out = blob + (uint64_t)q * slot;
     std::vector<int16_t> lv;
     std::vector<int32_t> vals(page_levels);
     const uint64_t nn = levels_page(n, p_null, page_levels, seed, p, lv, vals.data());
     const uint64_t cnt = lv.size();
     uint64_t ll = pqg_encode_levels_v1(lv.data(), cnt, 1, out, slot - 4 * cnt);
     memcpy(out + ll, vals.data(), 4 * nn);
-    pqg_page& pg = pages[p];
-    pg.offset = (uint64_t)p * slot;
+    pqg_page& pg = pages[q];
+    pg.offset = (uint64_t)q * slot;
     pg.nbytes = (uint32_t)(ll + 4 * nn);
     pg.num_values = (uint32_t)cnt;
     pg.page_type = PQG_PAGE_DATA;
@@ -369,10 +376,18 @@ int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64
     pg.def_encoding = PQG_RLE;
     pg.rep_encoding = PQG_BIT_PACKED;
     pg.def_len = pg.rep_len = 0;
-    nonnull[p] = nn;
+    nonnull[q] = nn;
   });
   for (uint64_t x : nonnull) info->total_values += x;
   return PQG_OK;
+}
+
+int pqg_gen_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
+                         int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                         uint32_t pages_cap, pqg_workload_info* info) {
+  if (page_levels == 0) return PQG_ERR_INVALID;
+  return pqg_gen_levels_plain_pages(n, p_null, page_levels, seed, 0, (uint32_t)((n + page_levels - 1) / page_levels),
+                                    threads, blob, blob_cap, pages, pages_cap, info);
 }
 
 uint64_t pqg_truth_levels_plain(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
@@ -401,32 +416,44 @@ static void dict_page_indices(uint64_t n, uint32_t dict_size, uint32_t page_valu
   for (uint64_t i = 0; i < cnt; ++i) idx[i] = (uint32_t)((splitmix64(s) >> 32) * dict_size >> 32);
 }
 
-int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
-                       int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
-                       uint32_t pages_cap, pqg_workload_info* info) {
+// The dictionary page and data pages [first, first + count) of the config-3 stream.
+int pqg_gen_dict_int64_pages(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed, uint32_t first,
+                             uint32_t count, int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                             uint32_t pages_cap, pqg_workload_info* info) {
   if (!info || page_values == 0 || dict_size == 0) return PQG_ERR_INVALID;
-  const uint32_t ndata = (uint32_t)((n + page_values - 1) / page_values);
+  const uint32_t all = (uint32_t)((n + page_values - 1) / page_values);
+  if (first > all || count > all - first) return PQG_ERR_INVALID;
+  const uint32_t ndata = count;
   const int bw = dict_size == 1 ? 1 : log2_ceil(dict_size);  // encoding.rs:325-334
   const uint64_t dslot = align64(8ull * dict_size);
   const uint64_t slot = align64(1 + rle_bound(bw, page_values));
   info->npages = ndata + 1;
   info->blob_len = dslot + slot * ndata;
-  info->total_levels = n;
-  info->total_values = n;
+  info->total_levels = 0;
+  for (uint32_t p = first; p < first + ndata; ++p) info->total_levels += std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+  info->total_values = info->total_levels;
   if (!blob) return PQG_OK;
   if (blob_cap < info->blob_len || pages_cap < ndata + 1) return PQG_ERR_CAPACITY;
   dict_values(dict_size, seed, blob);
   pages[0] = pqg_page{0, 8u * dict_size, dict_size, PQG_PAGE_DICTIONARY, PQG_PLAIN_DICTIONARY,
                       PQG_RLE, PQG_RLE, 0, 0};
-  parallel_pages(ndata, threads, [&](uint32_t p) {
-    uint8_t* out = blob + dslot + (uint64_t)p * slot;
+  parallel_pages(ndata, threads, [&](uint32_t q) {
+    uint8_t* out = blob + dslot + (uint64_t)q * slot;
     std::vector<uint32_t> idx;
-    dict_page_indices(n, dict_size, page_values, seed, p, idx);
+    dict_page_indices(n, dict_size, page_values, seed, first + q, idx);
     uint64_t l = pqg_encode_dict_indices(idx.data(), idx.size(), bw, out, slot);
-    pages[p + 1] = pqg_page{dslot + (uint64_t)p * slot, (uint32_t)l, (uint32_t)idx.size(), PQG_PAGE_DATA,
+    pages[q + 1] = pqg_page{dslot + (uint64_t)q * slot, (uint32_t)l, (uint32_t)idx.size(), PQG_PAGE_DATA,
                             PQG_PLAIN_DICTIONARY, PQG_RLE, PQG_BIT_PACKED, 0, 0};
   });
   return PQG_OK;
+}
+
+int pqg_gen_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                       int threads, uint8_t* blob, uint64_t blob_cap, pqg_page* pages,
+                       uint32_t pages_cap, pqg_workload_info* info) {
+  if (page_values == 0) return PQG_ERR_INVALID;
+  return pqg_gen_dict_int64_pages(n, dict_size, page_values, seed, 0, (uint32_t)((n + page_values - 1) / page_values),
+                                  threads, blob, blob_cap, pages, pages_cap, info);
 }
 
 uint64_t pqg_truth_dict_int64(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
@@ -455,31 +482,44 @@ static void delta_page_values(uint64_t n, int delta_bits, uint32_t page_values, 
   }
 }
 
-int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
-                        int mini_blocks, uint64_t seed, int threads, uint8_t* blob,
-                        uint64_t blob_cap, pqg_page* pages, uint32_t pages_cap,
-                        pqg_workload_info* info) {
+// Pages [first, first + count) of the config-4 stream.
+int pqg_gen_delta_int64_pages(uint64_t n, int delta_bits, uint32_t page_values, int block_size, int mini_blocks,
+                              uint64_t seed, uint32_t first, uint32_t count, int threads, uint8_t* blob,
+                              uint64_t blob_cap, pqg_page* pages, uint32_t pages_cap, pqg_workload_info* info) {
   if (!info || page_values == 0 || delta_bits < 1 || delta_bits > 63) return PQG_ERR_INVALID;
-  const uint32_t np = (uint32_t)((n + page_values - 1) / page_values);
+  const uint32_t all = (uint32_t)((n + page_values - 1) / page_values);
+  if (first > all || count > all - first) return PQG_ERR_INVALID;
+  const uint32_t np = count;
   const uint64_t blocks = (page_values + block_size - 1) / block_size + 1;
   const uint64_t slot = align64(64 + 8ull * page_values + blocks * (10 + mini_blocks) + 8ull * block_size);
   info->npages = np;
   info->blob_len = slot * np;
-  info->total_levels = n;
-  info->total_values = n;
+  info->total_levels = 0;
+  for (uint32_t p = first; p < first + np; ++p) info->total_levels += std::min<uint64_t>(page_values, n - (uint64_t)p * page_values);
+  info->total_values = info->total_levels;
   if (!blob) return PQG_OK;
   if (blob_cap < info->blob_len || pages_cap < np) return PQG_ERR_CAPACITY;
-  int rc = PQG_OK;
-  parallel_pages(np, threads, [&](uint32_t p) {
+  std::atomic<int> rc{PQG_OK};
+  parallel_pages(np, threads, [&](uint32_t q) {
     std::vector<int64_t> v;
-    delta_page_values(n, delta_bits, page_values, seed, p, v);
-    uint8_t* out = blob + (uint64_t)p * slot;
+    delta_page_values(n, delta_bits, page_values, seed, first + q, v);
+    uint8_t* out = blob + (uint64_t)q * slot;
     uint64_t l = delta_encode(v.data(), v.size(), block_size, mini_blocks, out, slot);
     if (!l) rc = PQG_ERR_CAPACITY;
-    pages[p] = pqg_page{(uint64_t)p * slot, (uint32_t)l, (uint32_t)v.size(), PQG_PAGE_DATA,
+    pages[q] = pqg_page{(uint64_t)q * slot, (uint32_t)l, (uint32_t)v.size(), PQG_PAGE_DATA,
                         PQG_DELTA_BINARY_PACKED, PQG_RLE, PQG_BIT_PACKED, 0, 0};
   });
   return rc;
+}
+
+int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
+                        int mini_blocks, uint64_t seed, int threads, uint8_t* blob,
+                        uint64_t blob_cap, pqg_page* pages, uint32_t pages_cap,
+                        pqg_workload_info* info) {
+  if (page_values == 0) return PQG_ERR_INVALID;
+  return pqg_gen_delta_int64_pages(n, delta_bits, page_values, block_size, mini_blocks, seed, 0,
+                                   (uint32_t)((n + page_values - 1) / page_values), threads, blob, blob_cap, pages,
+                                   pages_cap, info);
 }
 
 uint64_t pqg_truth_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, uint64_t seed,

@@ -52,6 +52,21 @@ int pqg_gen_delta_int64(uint64_t n, int delta_bits, uint32_t page_values, int bl
                         uint64_t blob_cap, pqg_page *pages, uint32_t pages_cap,
                         pqg_workload_info *info);
 
+/* The same streams, pages [first, first + count) only (config 3: with the dictionary page first):
+ * a rank's contiguous share of one stream, byte-identical to those pages of the whole. */
+int pqg_gen_levels_plain_pages(uint64_t n, double p_null, uint32_t page_levels, uint64_t seed,
+                               uint32_t first, uint32_t count, int threads, uint8_t *blob,
+                               uint64_t blob_cap, pqg_page *pages, uint32_t pages_cap,
+                               pqg_workload_info *info);
+int pqg_gen_dict_int64_pages(uint64_t n, uint32_t dict_size, uint32_t page_values, uint64_t seed,
+                             uint32_t first, uint32_t count, int threads, uint8_t *blob,
+                             uint64_t blob_cap, pqg_page *pages, uint32_t pages_cap,
+                             pqg_workload_info *info);
+int pqg_gen_delta_int64_pages(uint64_t n, int delta_bits, uint32_t page_values, int block_size,
+                              int mini_blocks, uint64_t seed, uint32_t first, uint32_t count,
+                              int threads, uint8_t *blob, uint64_t blob_cap, pqg_page *pages,
+                              uint32_t pages_cap, pqg_workload_info *info);
+
 /* Config 5: one row group (`rows` rows from global row `row0`) of the alltypes_plain schema (11
  * OPTIONAL columns: id INT32, bool_col BOOLEAN, tinyint/smallint/int INT32, bigint INT64, float,
  * double, date_string / string BYTE_ARRAY, timestamp INT96), written with the reference writer's

@@ -12,7 +12,8 @@ EXPORTS = ["pqg_encode_rle", "pqg_encode_levels_v1", "pqg_encode_delta", "pqg_en
            "pqg_gen_levels_plain", "pqg_gen_dict_int64", "pqg_gen_delta_int64",
            "pqg_truth_levels_plain", "pqg_truth_dict_int64", "pqg_truth_delta_int64",
            "pqg_gen_alltypes", "pqg_alltypes_copy", "pqg_alltypes_free", "pqg_truth_alltypes",
-           "pqg_write_alltypes_file"]
+           "pqg_write_alltypes_file", "pqg_gen_levels_plain_pages", "pqg_gen_dict_int64_pages",
+           "pqg_gen_delta_int64_pages"]
 
 # alltypes_plain schema (data/alltypes_plain.parquet): 11 OPTIONAL leaves, physical types
 ALLTYPES = [("id", 1), ("bool_col", 0), ("tinyint_col", 1), ("smallint_col", 1), ("int_col", 1),
@@ -53,6 +54,12 @@ def lib():
                                          C.POINTER(WorkloadInfo)]
         L.pqg_gen_delta_int64.argtypes = [u64, i32, u32, i32, i32, u64, i32, vp, u64,
                                           C.POINTER(Page), u32, C.POINTER(WorkloadInfo)]
+        L.pqg_gen_levels_plain_pages.argtypes = [u64, C.c_double, u32, u64, u32, u32, i32, vp, u64,
+                                                 C.POINTER(Page), u32, C.POINTER(WorkloadInfo)]
+        L.pqg_gen_dict_int64_pages.argtypes = [u64, u32, u32, u64, u32, u32, i32, vp, u64, C.POINTER(Page), u32,
+                                               C.POINTER(WorkloadInfo)]
+        L.pqg_gen_delta_int64_pages.argtypes = [u64, i32, u32, i32, i32, u64, u32, u32, i32, vp, u64,
+                                                C.POINTER(Page), u32, C.POINTER(WorkloadInfo)]
         L.pqg_truth_levels_plain.argtypes = [u64, C.c_double, u32, u64, u32, vp, vp]
         L.pqg_truth_levels_plain.restype = u64
         L.pqg_truth_dict_int64.argtypes = [u64, u32, u32, u64, u32, vp]
