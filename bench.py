@@ -378,6 +378,7 @@ def pcie_inclusive(ctx, w, stream, iters=3):
 
 
 LEVEL_PATH = ("k_lv_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
+DELTA_STAGE = ("k_delta_",)  # k_delta_hdr, k_delta_lb, k_delta_page, the tiled path's kernels
 
 
 def pmc_traffic(kind, kernel, variant=None):
@@ -397,8 +398,9 @@ def pmc_traffic(kind, kernel, variant=None):
         except (OSError, ValueError, KeyError):
             continue
         names = {k.replace("pqg::", ""): e for k, e in ks.items() if "traffic_bytes" in e}
-        if kernel == "level path":
-            tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(LEVEL_PATH)]
+        if kernel in ("level path", "DELTA stage"):  # a chain of kernels timed as one: their sum
+            pre = LEVEL_PATH if kernel == "level path" else DELTA_STAGE
+            tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(pre)]
             if tot:
                 return sum(tot), os.path.relpath(path, ROOT)
             continue
@@ -452,8 +454,9 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
                   ("k_plain_copy", tm.values_kernel_ms, val_b, w.values * w.es)]
     elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
         stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
-    else:                  # deltas in + values out
-        stages = [("k_delta_page<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
+    else:                  # deltas in + values out (HIP events around the DELTA kernels: header pass,
+        # look-back tile kernel, and the page pass / tiled path for pages those leave)
+        stages = [("DELTA stage", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
         if tuple(w.block) != (512, 4):
             variant = f"b{w.block[0]}x{w.block[1]}"
     rl = []

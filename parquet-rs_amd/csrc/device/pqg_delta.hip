@@ -26,6 +26,7 @@ namespace pqg {
 
 // DeltaPage::tiled values set by k_delta_page (0 / 1 are the tiled path's own)
 constexpr uint32_t DP_DONE = 2u, DP_FALLBACK = 3u;
+constexpr uint32_t DP_LB = 4u;  // k_delta_lb decodes the page (k_delta_hdr found its tile starts)
 
 __device__ inline uint32_t rfl32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   const uint32_t lane = threadIdx.x & 63;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
-  if (dt.page[p].tiled == DP_DONE) return;  // decoded by k_delta_page
+  if (dt.page[p].tiled == DP_DONE || dt.page[p].tiled == DP_LB) return;  // decoded by k_delta_page / k_delta_lb
   DeltaPage info{0, 0, 0, 0, 0};
   if (pw.status != 0) {
     if (lane == 0) dt.page[p] = info;
@@ -569,193 +570,384 @@ __global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__
 // that needs more reloads the full window). Anything else (an error the reference reports, a header or payload outside the
 // staged window, more than 8 mini-blocks, mini-blocks of a size not a multiple of 16, blocks
 // not dividing 4096) marks the page DP_FALLBACK for the tiled path, which reports errors exactly.
-constexpr int DPG_STAGE = 12288;
-constexpr int DPG_CH = DPG_STAGE / 16 / WG;  // 16-byte loads per thread per tile
-constexpr uint32_t DPG_T = 4096;             // deltas per tile
-constexpr int DPG_NB = 32;                   // blocks per tile (blocks of >= 128 values)
+#ifndef PQG_DPG_NT
+#define PQG_DPG_NT 256
+#endif
+constexpr int DPG_NT = PQG_DPG_NT;  // threads per page workgroup (tile = DPG_NT * DPT deltas)
 
+template <int NT>
+struct DpgShape {
+  static constexpr uint32_t T = NT * DPT;               // deltas per tile
+  static constexpr int STAGE = (int)T * 3;              // staged stream bytes per tile (w <= 23 fits)
+  static constexpr int CH = STAGE / 16 / NT;            // 16-byte loads per thread per tile
+  static constexpr int NB = (int)T / 128;               // blocks per tile at most (blocks of >= 128 values)
+  static constexpr int NW = NT / 64;                    // waves
+  static_assert(NB <= 64, "one lane per block header");
+  static_assert(CH * 16 * NT == STAGE, "whole loads");
+};
+
+template <int NT>
 struct DeltaPageSmem {
+  using S = DpgShape<NT>;
   union {
-    uint32_t stage[(DPG_STAGE + 64) / 4];
-    uint4 stq[(DPG_STAGE + 64) / 16];
+    uint32_t stage[(S::STAGE + 64) / 4];
+    uint4 stq[(S::STAGE + 64) / 16];
   };
-  uint64_t mind[DPG_NB];
-  uint32_t pos[DPG_NB];
-  uint32_t mboff[DPG_NB][8];
-  uint32_t mbw[DPG_NB][8];
-  uint64_t wsum[WG / 64];
+  uint64_t mind[S::NB];
+  uint32_t pos[S::NB];
+  uint32_t mboff[S::NB][8];
+  uint32_t mbw[S::NB][8];
+  uint64_t wsum[S::NW];
   uint32_t ctl[4];  // 0: fallback, 1: header of the next tile's first block, 2: window too short
 };
 
-template <int ES>
-__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG) k_delta_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
+// Block header at stream offset hp (stage-relative rel) as the chain needs it: its byte length
+// up to the payload's end (hop). ok: the 8-byte window holds the varint's end; in: inside the
+// stage (rel + 24 <= lim).
+__device__ inline uint32_t dpg_hop(const uint32_t* stage, uint32_t rel, uint32_t nmb32, uint32_t vpmb32, bool& ok) {
+  const uint64_t lo8 = lload_u64(stage, rel);
+  const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+  ok = t8 != 0;
+  const uint32_t vl = ok ? ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u : 8u;
+  const uint64_t wy = lload_u64(stage, rel + vl);
+  const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
+  const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+  const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+  const uint64_t h = (uint64_t)vl + nmb32 + (uint64_t)(vpmb32 >> 3) * sumw;
+  return h > 0x0FFFFFFFull ? 0x0FFFFFFFu : (uint32_t)h;
+}
+
+// The stream header of a DELTA page as k_delta_page / k_delta_hdr take it (decoding.rs:501-533):
+// false for anything they leave to the tiled path (which reports the reference's errors).
+struct DpgHead {
+  uint32_t q;          // stream offset of the first block header
+  uint32_t nmb, vpmb;  // mini-blocks per block, values per mini-block
+  uint32_t need;       // deltas (values - 1)
+  uint64_t first;      // first value
+};
+
+template <uint32_t TT>
+__device__ inline bool dpg_head(const uint8_t* sp, uint32_t slen, uint64_t n, DpgHead& h) {
+  uint64_t block_size, nmb, total, fz;
+  uint32_t q = 0;
+  int l;
+  if ((l = g_vlq(sp, q, slen, block_size)) <= 0) return false;
+  q += l;
+  if ((l = g_vlq(sp, q, slen, nmb)) <= 0) return false;
+  q += l;
+  if ((l = g_vlq(sp, q, slen, total)) <= 0) return false;
+  q += l;
+  if ((l = g_vlq(sp, q, slen, fz)) <= 0) return false;
+  q += l;
+  if ((int64_t)nmb <= 0 || nmb > 8) return false;
+  const uint64_t vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
+  if (vpmb % 16 != 0 || vpmb == 0 || vpmb * nmb < 128 || TT % (vpmb * nmb) != 0) return false;
+  if (total < n || n > 0x7FFFFFFFull || slen >= (1u << 28)) return false;
+  h.q = q;
+  h.nmb = (uint32_t)nmb;
+  h.vpmb = (uint32_t)vpmb;
+  h.need = n > 0 ? (uint32_t)n - 1u : 0u;
+  h.first = (uint64_t)unzigzag(fz);
+  return true;
+}
+
+// Wave 0 (all 64 lanes): the block headers of the tile whose first header is at stream offset
+// hdr, staged from stream offset sb (win bytes of the STG staged), found by a speculative scan:
+// lane j guesses block j's header offset (hdr + j * hguess), parses its length there, and the
+// exclusive scan of those lengths gives the next guesses; the prefix of lanes whose guess equals
+// the scan is exact and grows by at least one lane per round, so at most nb + 1 rounds (blocks of
+// one length, the writer's fixed widths, take one or two). Then lane j parses block j's header
+// (min delta, widths: the checks of k_delta_index) into sm. fb: a header the tiled path must
+// take; shortwin: a header or payload past the win staged bytes (stage the full window); hp: the
+// offset past the tile's last block (the next tile's first header).
+template <int NT, int ES>
+__device__ inline void dpg_headers(DeltaPageSmem<NT>& sm, uint32_t hdr, uint32_t hguess, uint32_t sb, uint32_t win,
+                                   uint32_t slen, uint32_t nb, uint32_t b0, uint32_t need, uint32_t nmb32,
+                                   uint32_t vpmb32, bool& fb, bool& shortwin, uint32_t& hp) {
+  constexpr int STG = DpgShape<NT>::STAGE;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t vpb = vpmb32 * nmb32;
+  const uint32_t wmax = ES == 4 ? 32u : 64u;
+  uint32_t P = hdr + lane * hguess;
+  fb = true;  // (stays set if the scan never settles)
+  shortwin = false;
+  hp = hdr;
+#pragma unroll 1
+  for (uint32_t round = 0; round <= nb; ++round) {
+    const uint32_t rel = P - sb;
+    const bool act = lane < nb;
+    const bool inw = P < slen && rel + 24u <= (uint32_t)STG;  // parseable from the stage
+    const bool inwin = rel + 24u <= win;                       // staged for this tile
+    bool okv = false;
+    uint32_t h = 0;
+    if (act && inw && inwin) h = dpg_hop(sm.stage, rel, nmb32, vpmb32, okv);
+    const bool good = act && inw && inwin && okv;
+    const uint32_t incl = wave_scan_incl_u32(good ? h : 0u);
+    const uint64_t Q64 = (uint64_t)hdr + (incl - (good ? h : 0u));
+    const uint32_t Q = Q64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)Q64;
+    const uint64_t diff = __ballot(act && Q != P);
+    const uint32_t m = diff ? (uint32_t)__builtin_ctzll(diff) : nb;  // lanes [0, m) exact
+    const uint64_t badm = __ballot(act && lane < m && !good);  // an exact lane that cannot be taken
+    if (badm) {
+      const uint32_t f = (uint32_t)__builtin_ctzll(badm);
+      const bool f_inw = __shfl((int)(inw ? 1 : 0), (int)f, 64) != 0;
+      const bool f_win = __shfl((int)(inwin ? 1 : 0), (int)f, 64) != 0;
+      // past the bytes staged for this tile: stage the full window; past the stream or the
+      // stage, or a varint without its end in 8 bytes: the tiled path
+      shortwin = f_inw && !f_win;
+      fb = !shortwin;
+      return;
+    }
+    if (m >= nb) {  // every block's offset exact: the chain ends past the last one
+      const uint32_t e = (uint32_t)__shfl((int)incl, (int)(nb - 1u), 64);
+      const uint64_t he = (uint64_t)hdr + e;
+      hp = he > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)he;
+      fb = false;
+      break;
+    }
+    P = Q;
+  }
+  bool lfb = false;
+  if (lane < nb) {
+    const uint32_t pos = P, rel = pos - sb, b = b0 + lane;
+    const uint64_t lo8 = lload_u64(sm.stage, rel), hi8 = lload_u64(sm.stage, rel + 8);
+    const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+    const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;  // t8 != 0 (the scan)
+    uint64_t y = lo8 & 0x7F7F7F7F7F7F7F7Full;
+    if (vl < 8) y &= (1ull << (8 * vl)) - 1ull;
+    y = (y & 0x007F007F007F007Full) | ((y & 0x7F007F007F007F00ull) >> 1);
+    y = (y & 0x00003FFF00003FFFull) | ((y & 0x3FFF00003FFF0000ull) >> 2);
+    const uint64_t zz = (y & 0x000000000FFFFFFFull) | ((y & 0x0FFFFFFF00000000ull) >> 4);
+    if ((uint64_t)pos + vl + nmb32 > slen) lfb = true;
+    const uint32_t payload = pos + vl + nmb32;
+    const uint32_t left = need - b * vpb;
+    const uint32_t inblk = left < vpb ? left : vpb;
+    const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
+    const uint32_t sh = vl * 8u;  // widths: bytes [vl, vl + nmb) of the 16-byte window
+    const uint64_t wv = sh < 64 ? ((lo8 >> sh) | (sh ? hi8 << (64 - sh) : 0ull)) : hi8;
+    uint32_t boff = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 8; ++m) {
+      const uint32_t wdt = m < nmb32 ? (uint32_t)((wv >> (8 * m)) & 0xFFu) : 0u;
+      if (m < nmb32 && m < mneed && (wdt > wmax || (uint64_t)payload + boff + (vpmb32 * wdt) / 8 > slen)) lfb = true;
+      sm.mbw[lane][m] = wdt;
+      sm.mboff[lane][m] = boff;
+      boff += m < nmb32 ? (vpmb32 * wdt) / 8 : 0u;
+    }
+    sm.pos[lane] = payload;
+    sm.mind[lane] = (uint64_t)unzigzag(zz);
+  }
+  fb = __ballot(lfb) != 0;
+  // the tile's payload must be staged too (its last block's end is the next tile's header)
+  if (!fb && hp - sb > win) shortwin = true;
+}
+
+// Every thread: its DPT deltas of the tile [D0, D1) (min delta + packed value; from the stage when
+// inside the win staged bytes, else global loads); returns their sum.
+template <int NT>
+__device__ inline uint64_t dpg_unpack(const DeltaPageSmem<NT>& sm, const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                      uint64_t S, uint32_t sb, uint32_t win, uint32_t D0, uint32_t D1, uint32_t nmb32,
+                                      uint32_t vpmb32, uint64_t (&x)[DPT]) {
+  const uint32_t vpb = vpmb32 * nmb32;
+  const uint32_t lim = win * 8u;  // staged bits
+  const uint32_t r0 = (uint32_t)threadIdx.x * DPT;  // tile-relative first delta
+  uint64_t s = 0;
+  if (D0 + r0 < D1) {
+    const uint32_t bi = r0 / vpb, m = (r0 - bi * vpb) / vpmb32, kk = r0 - bi * vpb - m * vpmb32;
+    const uint32_t wdt = sm.mbw[bi][m];
+    const uint64_t mn = sm.mind[bi];
+    const uint32_t base = (sm.pos[bi] + sm.mboff[bi][m] - sb) * 8u + kk * wdt;  // bit offset in the window
+    const uint32_t cnt = D1 - D0 - r0 < (uint32_t)DPT ? D1 - D0 - r0 : (uint32_t)DPT;
+    const uint32_t wm = wdt >= 32 ? 0xFFFFFFFFu : (1u << wdt) - 1u;
+    if (wdt <= 32 && base + DPT * wdt <= lim) {
+#pragma unroll
+      for (int j = 0; j < DPT; ++j) {
+        const uint32_t bit = base + (uint32_t)j * wdt;
+        const uint32_t wi = bit >> 5;
+        const uint32_t r = __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
+        x[j] = (uint32_t)j < cnt ? mn + r : 0ull;
+        s += x[j];
+      }
+    } else {  // outside the window or wider than 32 bits: global reads
+#pragma unroll
+      for (int j = 0; j < DPT; ++j) {
+        uint64_t v = 0;
+        if ((uint32_t)j < cnt) {
+          const uint64_t gb = ((uint64_t)sm.pos[bi] + sm.mboff[bi][m]) * 8ull + (uint64_t)(kk + j) * wdt;
+          const uint64_t abs = S + (gb >> 3);
+          const uint32_t sh = (uint32_t)(gb & 7);
+          uint64_t r = gload_u64(blob, blob_len, abs) >> sh;
+          if (wdt + sh > 64) r |= gload_u64(blob, blob_len, abs + 8) << (64 - sh);
+          v = mn + (wdt >= 64 ? r : (r & ((1ull << wdt) - 1ull)));
+        }
+        x[j] = v;
+        s += v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) x[j] = 0;
+  }
+  return s;
+}
+
+// The tile's values (deltas [D0, D0 + cnt) -> values [D0 + 1, ...)) from registers through the
+// stage buffer: WR waves' values per round, 16-byte stores of contiguous output per instruction.
+template <int ES, int NT>
+__device__ inline void dpg_store(DeltaPageSmem<NT>& sm, const uint64_t (&val)[DPT], gptr<uint8_t> tb, uint32_t cnt) {
+  using SH = DpgShape<NT>;
+  const int tid = threadIdx.x;
+  constexpr uint32_t CPT = DPT * ES / 16;                   // 16-byte chunks per thread
+  constexpr uint32_t WB = 64u * DPT * ES;                   // bytes of one wave's values
+  constexpr uint32_t WPR0 = (uint32_t)SH::STAGE / WB;       // waves whose values fit the stage
+  constexpr uint32_t WPR = WPR0 >= 8 ? 8 : WPR0 >= 4 ? 4 : WPR0 >= 2 ? 2 : 1;
+  constexpr uint32_t NR = (uint32_t)SH::NW / (WPR < (uint32_t)SH::NW ? WPR : (uint32_t)SH::NW);  // rounds
+  constexpr uint32_t WR = (uint32_t)SH::NW / NR;            // waves per round
+  constexpr uint32_t QV = WR * 64u * DPT;                   // values per round
+  constexpr uint32_t NCH = QV * ES / 16;                    // chunks per round
+#pragma unroll 1
+  for (uint32_t qq = 0; qq < NR; ++qq) {
+    if ((uint32_t)(tid >> 6) / WR == qq) {
+      const uint32_t tl = (uint32_t)tid - qq * WR * 64u;
+#pragma unroll
+      for (uint32_t c = 0; c < CPT; ++c) {
+        uint4 v4;
+        if (ES == 8)
+          v4 = make_uint4((uint32_t)val[2 * c], (uint32_t)(val[2 * c] >> 32), (uint32_t)val[2 * c + 1],
+                          (uint32_t)(val[2 * c + 1] >> 32));
+        else
+          v4 = make_uint4((uint32_t)val[4 * c], (uint32_t)val[4 * c + 1], (uint32_t)val[4 * c + 2],
+                          (uint32_t)val[4 * c + 3]);
+        const uint32_t ci = tl * CPT + c;
+        sm.stq[ci ^ (tl & 7u)] = v4;  // xor swizzle against bank conflicts
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < (NCH + NT - 1) / NT; ++r) {
+      const uint32_t ci = (uint32_t)tid + r * NT;
+      if (ci < NCH) {
+        const uint4 v4 = sm.stq[ci ^ ((ci / CPT) & 7u)];
+        const uint32_t v0 = qq * QV + ci * (16 / ES);
+        gptr<uint8_t> dst = tb + (uint64_t)v0 * ES;
+        if (v0 + 16 / ES <= cnt) {
+          gst16(dst, v4);
+        } else if (v0 < cnt) {
+          const uint32_t qa[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (uint32_t e = 0; e < 16 / ES; ++e) {
+            if (v0 + e >= cnt) break;
+            if (ES == 8) reinterpret_cast<gptr<uint64_t>>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
+            else reinterpret_cast<gptr<uint32_t>>(dst)[e] = qa[e];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Workgroup scan of the threads' delta sums: acc = the value before this thread's first delta
+// (carry + the deltas of the threads before it); returns the tile's sum.
+template <int NT>
+__device__ inline uint64_t dpg_scan(DeltaPageSmem<NT>& sm, uint64_t s, uint64_t carry, uint64_t& acc) {
+  const int tid = threadIdx.x;
+  uint64_t incl = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y2 = __shfl_up(incl, off, 64);
+    if ((tid & 63) >= off) incl += y2;
+  }
+  if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+  __syncthreads();
+  acc = carry + incl - s;
+  uint64_t tot = 0;
+#pragma unroll
+  for (int wv = 0; wv < DpgShape<NT>::NW; ++wv) {
+    if (wv < (tid >> 6)) acc += sm.wsum[wv];
+    tot += sm.wsum[wv];
+  }
+  return tot;
+}
+
+template <int ES, int NT>
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT) k_delta_page(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                    PageWork* pages, const ChunkWork* chunks, DeltaTables dt) {
-  __shared__ DeltaPageSmem sm;
+  using SH = DpgShape<NT>;
+  constexpr uint32_t TT = SH::T;
+  constexpr int STG = SH::STAGE;
+  __shared__ DeltaPageSmem<NT> sm;
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
+  if (dt.page[p].tiled == DP_LB) return;  // decoded by k_delta_lb
   const gptr<uint8_t> __restrict__ out = gp(chunks[pw.chunk].val_out);
   DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
-  if (pw.status != 0) {
-    if (tid == 0) {
-      dt.page[p] = info;
-      atomicAdd(dt.nfall, 1u);
-    }
-    return;
-  }
   const uint64_t S = pw.base + pw.val_off;
   const uint32_t slen = pw.val_bytes;
-  const uint8_t* sp = blob + S;
-  uint64_t block_size, nmb, total, fz;
-  uint32_t q = 0;
-  bool bad = false;
-  int l;
-  if ((l = g_vlq(sp, q, slen, block_size)) <= 0) bad = true;
-  q += l > 0 ? l : 0;
-  if (!bad && (l = g_vlq(sp, q, slen, nmb)) <= 0) bad = true;
-  q += l > 0 ? l : 0;
-  if (!bad && (l = g_vlq(sp, q, slen, total)) <= 0) bad = true;
-  q += l > 0 ? l : 0;
-  if (!bad && (l = g_vlq(sp, q, slen, fz)) <= 0) bad = true;
-  q += l > 0 ? l : 0;
-  const uint64_t n = pw.nonnull;
-  uint64_t vpmb = 0;
-  if (!bad) {
-    if ((int64_t)nmb <= 0 || nmb > 8) bad = true;
-    else {
-      vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
-      if (vpmb % 16 != 0 || vpmb == 0 || vpmb * nmb < 128 || DPG_T % (vpmb * nmb) != 0) bad = true;
-    }
-  }
-  if (!bad && (total < n || n > 0x7FFFFFFFull || slen >= (1u << 28))) bad = true;
-  if (bad) {
+  DpgHead hd;
+  if (pw.status != 0 || !dpg_head<TT>(blob + S, slen, pw.nonnull, hd)) {
     if (tid == 0) {
       dt.page[p] = info;
       atomicAdd(dt.nfall, 1u);
     }
     return;
   }
-  const uint32_t nmb32 = (uint32_t)nmb, vpmb32 = (uint32_t)vpmb, vpb = vpmb32 * nmb32;
-  const uint32_t nn = (uint32_t)n;
-  const uint32_t need = nn > 0 ? nn - 1 : 0u;  // deltas
-  const uint32_t wmax = ES == 4 ? 32u : 64u;
-  const uint64_t first = (uint64_t)unzigzag(fz);
+  const uint32_t nmb32 = hd.nmb, vpmb32 = hd.vpmb, vpb = vpmb32 * nmb32, need = hd.need;
   const gptr<uint8_t> ob = out + pw.value_out * (uint64_t)ES;
-  if (tid == 0 && nn > 0) {  // value 0
-    if (ES == 8) *reinterpret_cast<gptr<uint64_t>>(ob) = first;
-    else *reinterpret_cast<gptr<uint32_t>>(ob) = (uint32_t)first;
+  if (tid == 0 && pw.nonnull > 0) {  // value 0
+    if (ES == 8) *reinterpret_cast<gptr<uint64_t>>(ob) = hd.first;
+    else *reinterpret_cast<gptr<uint32_t>>(ob) = (uint32_t)hd.first;
   }
-  uint4 pv[DPG_CH];
-  uint64_t SB = (S + q) & ~15ull;  // stage base of the current tile (absolute)
-  uint32_t win = DPG_STAGE;        // bytes staged for the current tile
+  uint4 pv[SH::CH];
+  uint64_t SB = (S + hd.q) & ~15ull;  // stage base of the current tile (absolute)
+  uint32_t win = STG;                 // bytes staged for the current tile
   auto issue = [&](uint64_t base, uint32_t nbytes) {
-    const bool fast = base + DPG_STAGE <= blob_len;
+    const bool fast = base + STG <= blob_len;
 #pragma unroll
-    for (int c = 0; c < DPG_CH; ++c) {
-      const uint32_t off = (uint32_t)(tid + c * WG) * 16u;
+    for (int c = 0; c < SH::CH; ++c) {
+      const uint32_t off = (uint32_t)(tid + c * NT) * 16u;
       const uint64_t a = base + off;
       pv[c] = off >= nbytes ? make_uint4(0u, 0u, 0u, 0u)
               : fast        ? *reinterpret_cast<const uint4*>(blob + a)
                             : gload_u128_tail(blob, blob_len, a);
     }
   };
-  const uint32_t ntl = (need + DPG_T - 1) / DPG_T;
+  const uint32_t ntl = (need + TT - 1) / TT;
   if (ntl) issue(SB, win);
-  uint32_t hdr = q;        // header of the current tile's first block (stream offset)
-  uint64_t carry = first;  // value before the tile's first delta
+  uint32_t hdr = hd.q;        // header of the current tile's first block (stream offset)
+  uint64_t carry = hd.first;  // value before the tile's first delta
+  uint32_t hguess = 0;        // block length guess for the header scan (the last tile's average)
   for (uint32_t k = 0; k < ntl; ++k) {
-    const uint32_t D0 = k * DPG_T;
-    const uint32_t D1 = D0 + DPG_T < need ? D0 + DPG_T : need;
+    const uint32_t D0 = k * TT;
+    const uint32_t D1 = D0 + TT < need ? D0 + TT : need;
     const uint32_t nb = (D1 - D0 + vpb - 1) / vpb;  // blocks of the tile
   restage:
-    // ---- install the staged bytes
 #pragma unroll
-    for (int c = 0; c < DPG_CH; ++c) sm.stq[tid + c * WG] = pv[c];
-    if (tid < 16) sm.stage[DPG_STAGE / 4 + tid] = 0;
+    for (int c = 0; c < SH::CH; ++c) sm.stq[tid + c * NT] = pv[c];
+    if (tid < 16) sm.stage[STG / 4 + tid] = 0;
     __syncthreads();
     const uint32_t sb = (uint32_t)(SB - S);  // stream offset of staged byte 0 (mod 2^32)
-    // ---- wave 0: block header chain, then one block header per lane
     if (tid < 64) {
-      const uint32_t lane = (uint32_t)tid;
-      uint32_t hp = hdr, posv = 0;
-      bool fb = false;
-      bool shortwin = false;
-      for (uint32_t j = 0; j < nb; ++j) {
-        const uint32_t rel = hp - sb;
-        if (hp >= slen || rel + 24u > (uint32_t)DPG_STAGE) {
-          fb = true;
-          break;
-        }
-        if (rel + 24u > win) {  // past the bytes staged for this tile: stage the full window
-          shortwin = true;
-          break;
-        }
-        posv = lane == j ? hp : posv;
-        const uint64_t lo8 = lload_u64(sm.stage, rel);
-        const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
-        if (!t8) {
-          fb = true;
-          break;
-        }
-        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
-        const uint64_t wy = lload_u64(sm.stage, rel + vl);
-        const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
-        const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
-        const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
-        const uint64_t nx = (uint64_t)hp + vl + nmb32 + (uint64_t)(vpmb32 >> 3) * sumw;
-        hp = nx > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)nx;
-      }
-      bool lfb = false;
-      if (!fb && !shortwin && lane < nb) {
-        const uint32_t pos = posv, rel = pos - sb, b = D0 / vpb + lane;
-        const uint64_t lo8 = lload_u64(sm.stage, rel), hi8 = lload_u64(sm.stage, rel + 8);
-        const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
-        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;  // t8 != 0 (chain above)
-        uint64_t y = lo8 & 0x7F7F7F7F7F7F7F7Full;
-        if (vl < 8) y &= (1ull << (8 * vl)) - 1ull;
-        y = (y & 0x007F007F007F007Full) | ((y & 0x7F007F007F007F00ull) >> 1);
-        y = (y & 0x00003FFF00003FFFull) | ((y & 0x3FFF00003FFF0000ull) >> 2);
-        const uint64_t zz = (y & 0x000000000FFFFFFFull) | ((y & 0x0FFFFFFF00000000ull) >> 4);
-        if ((uint64_t)pos + vl + nmb32 > slen) lfb = true;
-        const uint32_t payload = pos + vl + nmb32;
-        if (rel + 24u > win) shortwin = true;
-        const uint32_t left = need - b * vpb;
-        const uint32_t inblk = left < vpb ? left : vpb;
-        const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
-        const uint32_t sh = vl * 8u;  // widths: bytes [vl, vl + nmb) of the 16-byte window
-        const uint64_t wv = sh < 64 ? ((lo8 >> sh) | (sh ? hi8 << (64 - sh) : 0ull)) : hi8;
-        uint32_t boff = 0;
-#pragma unroll
-        for (uint32_t m = 0; m < 8; ++m) {
-          const uint32_t wdt = m < nmb32 ? (uint32_t)((wv >> (8 * m)) & 0xFFu) : 0u;
-          if (m < nmb32 && m < mneed &&
-              (wdt > wmax || (uint64_t)payload + boff + (vpmb32 * wdt) / 8 > slen)) lfb = true;
-          sm.mbw[lane][m] = wdt;
-          sm.mboff[lane][m] = boff;
-          boff += m < nmb32 ? (vpmb32 * wdt) / 8 : 0u;
-        }
-        sm.pos[lane] = payload;
-        sm.mind[lane] = (uint64_t)unzigzag(zz);
-      }
-      fb = fb || __ballot(lfb) != 0;
-      // the tile's payload must be staged too (its last block's end is the next tile's header)
-      if (!fb && (hp - sb > win || __ballot(shortwin))) shortwin = true;
-      if (lane == 0) {
+      bool fb, shortwin;
+      uint32_t hp;
+      dpg_headers<NT, ES>(sm, hdr, hguess, sb, win, slen, nb, D0 / vpb, need, nmb32, vpmb32, fb, shortwin, hp);
+      if (tid == 0) {
         sm.ctl[0] = fb ? 1u : 0u;
         sm.ctl[1] = hp;
         sm.ctl[2] = shortwin ? 1u : 0u;
       }
     }
     __syncthreads();
-    if (sm.ctl[2] && !sm.ctl[0] && win < (uint32_t)DPG_STAGE) {  // stage the full window and redo
-      win = DPG_STAGE;
+    if (sm.ctl[2] && !sm.ctl[0] && win < (uint32_t)STG) {  // stage the full window and redo
+      win = STG;
       issue(SB, win);
       __syncthreads();  // every read of the stage is done before the reinstall
       goto restage;
     }
-    if (sm.ctl[0]) {  // leave the page to the tiled path
+    if (sm.ctl[0]) {  // leave the page to the tiled path (a payload past a full window: global reads)
       if (tid == 0) {
         dt.page[p] = info;
         atomicAdd(dt.nfall, 1u);
@@ -763,124 +955,369 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(WG)
       return;
     }
     const uint32_t span = sm.ctl[1] - hdr;  // this tile's bytes: the next tile likely needs as many
+    hguess = nb ? span / nb : 0u;
     hdr = sm.ctl[1];
     const uint64_t SBn = (S + hdr) & ~15ull;
-    const uint32_t winn = min((uint32_t)DPG_STAGE, (span + span / 8u + 256u + 15u) & ~15u);
+    const uint32_t winn = min((uint32_t)STG, (span + span / 8u + 256u + 15u) & ~15u);
     if (k + 1 < ntl) issue(SBn, winn);
-    // ---- 16 deltas of one mini-block per thread
-    const uint32_t lim = win * 8u;  // staged bits
-    const uint32_t r0 = (uint32_t)tid * DPT;  // tile-relative first delta
     uint64_t x[DPT];
-    uint64_t s = 0;
-    if (D0 + r0 < D1) {
-      const uint32_t bi = r0 / vpb, m = (r0 - bi * vpb) / vpmb32, kk = r0 - bi * vpb - m * vpmb32;
-      const uint32_t wdt = sm.mbw[bi][m];
-      const uint64_t mn = sm.mind[bi];
-      const uint32_t base = (sm.pos[bi] + sm.mboff[bi][m] - sb) * 8u + kk * wdt;  // bit offset in the window
-      const uint32_t cnt = D1 - D0 - r0 < (uint32_t)DPT ? D1 - D0 - r0 : (uint32_t)DPT;
-      const uint32_t wm = wdt >= 32 ? 0xFFFFFFFFu : (1u << wdt) - 1u;
-      if (wdt <= 32 && base + DPT * wdt <= lim) {
-#pragma unroll
-        for (int j = 0; j < DPT; ++j) {
-          const uint32_t bit = base + (uint32_t)j * wdt;
-          const uint32_t wi = bit >> 5;
-          const uint32_t r = __builtin_amdgcn_alignbit(sm.stage[wi + 1], sm.stage[wi], bit & 31u) & wm;
-          x[j] = (uint32_t)j < cnt ? mn + r : 0ull;
-          s += x[j];
-        }
-      } else {  // outside the window or wider than 32 bits: global reads
-#pragma unroll
-        for (int j = 0; j < DPT; ++j) {
-          uint64_t v = 0;
-          if ((uint32_t)j < cnt) {
-            const uint64_t gb = ((uint64_t)sm.pos[bi] + sm.mboff[bi][m]) * 8ull + (uint64_t)(kk + j) * wdt;
-            const uint64_t abs = S + (gb >> 3);
-            const uint32_t sh = (uint32_t)(gb & 7);
-            uint64_t r = gload_u64(blob, blob_len, abs) >> sh;
-            if (wdt + sh > 64) r |= gload_u64(blob, blob_len, abs + 8) << (64 - sh);
-            v = mn + (wdt >= 64 ? r : (r & ((1ull << wdt) - 1ull)));
-          }
-          x[j] = v;
-          s += v;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < DPT; ++j) x[j] = 0;
-    }
-    // ---- workgroup scan; the barrier also ends every read of the stage and the tables
-    uint64_t incl = s;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint64_t y2 = __shfl_up(incl, off, 64);
-      if ((tid & 63) >= off) incl += y2;
-    }
-    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
-    __syncthreads();
-    uint64_t acc = carry + incl - s;
-    for (int wv = 0; wv < (tid >> 6); ++wv) acc += sm.wsum[wv];
-    carry += sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+    const uint64_t s = dpg_unpack<NT>(sm, blob, blob_len, S, sb, win, D0, D1, nmb32, vpmb32, x);
+    uint64_t acc;
+    carry += dpg_scan<NT>(sm, s, carry, acc);  // (the barrier also ends every read of the stage)
     uint64_t val[DPT];
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       acc += x[j];
       val[j] = acc;
     }
-    // ---- stores through the stage buffer: quarter qq = wave qq's values [1024 qq, + 1024)
-    const uint32_t cnt = D1 - D0;
-    const gptr<uint8_t> tb = ob + (uint64_t)(D0 + 1) * ES;
-    constexpr uint32_t CPT = DPT * ES / 16;  // 16-byte chunks per thread
-    constexpr uint32_t QV = DPG_T / 4;       // values per quarter
-    constexpr uint32_t NCH = QV * ES / 16;   // chunks per quarter
-#pragma unroll 1
-    for (int qq = 0; qq < 4; ++qq) {
-      if ((tid >> 6) == qq) {
-        const uint32_t tl = (uint32_t)tid & 63u;
-#pragma unroll
-        for (uint32_t c = 0; c < CPT; ++c) {
-          uint4 v4;
-          if (ES == 8)
-            v4 = make_uint4((uint32_t)val[2 * c], (uint32_t)(val[2 * c] >> 32), (uint32_t)val[2 * c + 1],
-                            (uint32_t)(val[2 * c + 1] >> 32));
-          else
-            v4 = make_uint4((uint32_t)val[4 * c], (uint32_t)val[4 * c + 1], (uint32_t)val[4 * c + 2],
-                            (uint32_t)val[4 * c + 3]);
-          const uint32_t ci = tl * CPT + c;
-          sm.stq[ci ^ (tl & 7u)] = v4;  // xor swizzle against bank conflicts
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t r = 0; r < (NCH + WG - 1) / WG; ++r) {
-        const uint32_t ci = (uint32_t)tid + r * WG;
-        if (ci < NCH) {
-          const uint4 v4 = sm.stq[ci ^ ((ci / CPT) & 7u)];
-          const uint32_t v0 = (uint32_t)qq * QV + ci * (16 / ES);
-          gptr<uint8_t> dst = tb + (uint64_t)v0 * ES;
-          if (v0 + 16 / ES <= cnt) {
-            gst16(dst, v4);
-          } else if (v0 < cnt) {
-            const uint32_t qa[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-            for (uint32_t e = 0; e < 16 / ES; ++e) {
-              if (v0 + e >= cnt) break;
-              if (ES == 8) reinterpret_cast<gptr<uint64_t>>(dst)[e] = (uint64_t)qa[2 * e] | ((uint64_t)qa[2 * e + 1] << 32);
-              else reinterpret_cast<gptr<uint32_t>>(dst)[e] = qa[e];
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
+    dpg_store<ES, NT>(sm, val, ob + (uint64_t)(D0 + 1) * ES, D1 - D0);
     SB = SBn;
     win = winn;
   }
   if (tid == 0) {
-    info.first = first;
+    info.first = hd.first;
     info.vpmb = vpmb32;
     info.nmb = nmb32;
     info.tiled = DP_DONE;
     dt.page[p] = info;
+  }
+}
+
+// ============================================================================ look-back path
+//
+// Config 4 at more than one workgroup per page (a page's tiles are independent once each knows
+// where its first block header is and the running value before it):
+//   k_delta_hdr  one workgroup per page finds the stream offset of every tile's first block header
+//                (dt.tstart) by a speculative scan over global memory: thread j guesses block j's
+//                header offset from the average block length so far, parses the header there (16
+//                bytes), and the workgroup's exclusive scan of those lengths checks the guesses;
+//                the exact prefix is kept and the next round starts after it (blocks of one length,
+//                the writer's fixed widths: 256 blocks per round). It checks every block header
+//                as k_delta_page does; a page it cannot take (an error, a header form the page pass
+//                refuses, blocks of irregular lengths) stays with k_delta_page.
+//   k_delta_lb   a resident grid walks the tiles of every such page round-robin (tile t by
+//                workgroup t mod G): stage, block headers, unpack and sum the tile's deltas, then a
+//                decoupled look-back over the page's earlier tiles gives the running value
+//                (value i = first + sum of deltas d < i, wrapping: decoding.rs:560-566), then scan
+//                and store. Tile sums travel as 8-byte {epoch tag, 32-bit half} granules written by
+//                one agent-scope store each and polled by agent-scope loads (MI355X_MICROARCH.md,
+//                inter-workgroup visibility, R2), so no fence; a tile waits only for tiles of the
+//                same or an earlier round of the round-robin, all resident, so the waits end; every
+//                spin is bounded (a timeout reports ST_GENERAL for the page).
+constexpr int DLB_NT = 256;
+using DlbShape = DpgShape<DLB_NT>;
+static_assert(DlbShape::T == DELTA_TILE, "look-back tiles are the page table's tiles");
+
+#define DLB_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+typedef __attribute__((address_space(1))) unsigned long long dlb_gu64;
+typedef __attribute__((address_space(1))) unsigned int dlb_gu32;
+
+template <int ES>
+__global__ void __launch_bounds__(WG) k_delta_hdr(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                  PageWork* pages, const ChunkWork* chunks, DeltaTables dt) {
+  __shared__ uint32_t wtot[WG / 64], wfirst[WG / 64], wbad[WG / 64];
+  __shared__ uint32_t ts_s[WG + 1];  // start of the tile of each block of the round (LDS: tstart is global)
+  const int p = blockIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  if (p == 0 && tid < 8) dt.ticket[tid] = 0;  // k_delta_lb's per-XCD tile counters (read after this launch)
+  const PageWork& pw = pages[p];
+  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
+  if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
+  DeltaPage info{0, 0, 0, 0, 0};  // (tiled 0: k_delta_page decides)
+  const uint64_t S = pw.base + pw.val_off;
+  const uint32_t slen = pw.val_bytes;
+  DpgHead hd;
+  if (pw.status != 0 || !dpg_head<DELTA_TILE>(blob + S, slen, pw.nonnull, hd) || hd.need == 0) {
+    if (tid == 0) dt.page[p] = info;
+    return;
+  }
+  const uint32_t nmb32 = hd.nmb, vpmb32 = hd.vpmb, vpb = vpmb32 * nmb32, need = hd.need;
+  const uint32_t wmax = ES == 4 ? 32u : 64u;
+  const uint32_t nblocks = (need + vpb - 1) / vpb, bpt = DELTA_TILE / vpb;
+  uint32_t* tstart = dt.tstart + pw.ltile0;
+  uint32_t cur = hd.q, b = 0, H = 0, slow = 0;
+  bool ok_page = true;
+  if (tid == 0) ts_s[WG] = cur;
+#pragma unroll 1
+  while (b < nblocks) {
+    const uint32_t j = tid;
+    const bool act = b + j < nblocks;
+    const uint64_t P64 = (uint64_t)cur + (uint64_t)j * H;
+    const uint32_t P = P64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)P64;
+    bool good = false;
+    uint32_t h = 0;
+    if (act && P < slen) {
+      const uint64_t lo8 = gload_u64(blob, blob_len, S + P), hi8 = gload_u64(blob, blob_len, S + P + 8);
+      const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+      if (t8) {
+        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
+        const uint32_t sh = vl * 8u;
+        const uint64_t wv = sh < 64 ? ((lo8 >> sh) | (hi8 << (64 - sh))) : hi8;
+        const uint32_t payload = P + vl + nmb32;
+        const uint32_t bb = b + j;
+        const uint32_t left = need - bb * vpb;
+        const uint32_t inblk = left < vpb ? left : vpb;
+        const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
+        uint64_t boff = 0;
+        bool chk = (uint64_t)P + vl + nmb32 <= slen;
+#pragma unroll
+        for (uint32_t m = 0; m < 8; ++m) {
+          const uint32_t wdt = m < nmb32 ? (uint32_t)((wv >> (8 * m)) & 0xFFu) : 0u;
+          if (m < nmb32 && m < mneed && (wdt > wmax || (uint64_t)payload + boff + (vpmb32 * wdt) / 8 > slen)) chk = false;
+          boff += m < nmb32 ? (vpmb32 * wdt) / 8 : 0u;
+        }
+        const uint64_t hh = (uint64_t)vl + nmb32 + boff;
+        good = chk && hh < 0x0FFFFFFFull;
+        h = good ? (uint32_t)hh : 0u;
+      }
+    }
+    // workgroup exclusive scan of the lengths: the chain's offsets if every guess before is right
+    const uint32_t incl = wave_scan_incl_u32(h);
+    if (lane == 63) wtot[wid] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WG / 64; ++w) {
+      before += w < wid ? wtot[w] : 0u;
+      total += wtot[w];
+    }
+    const uint64_t Q64 = (uint64_t)cur + before + incl - h;
+    const bool mism = act && Q64 != (uint64_t)P;
+    // first mismatching thread, and the first thread that cannot be taken (in thread order)
+    const uint64_t mm = __ballot(mism), bm = __ballot(act && !good);
+    if (lane == 0) {
+      wfirst[wid] = mm ? wid * 64u + (uint32_t)__builtin_ctzll(mm) : 0xFFFFFFFFu;
+      wbad[wid] = bm ? wid * 64u + (uint32_t)__builtin_ctzll(bm) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t m = 0xFFFFFFFFu, f = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t w = 0; w < WG / 64; ++w) {
+      m = min(m, wfirst[w]);
+      f = min(f, wbad[w]);
+    }
+    const uint32_t nact = min((uint32_t)WG, nblocks - b);
+    if (m > nact) m = nact;  // lanes [0, m) exact
+    if (f < m) {  // an exact block the page pass would refuse: k_delta_page takes the page
+      ok_page = false;
+      break;
+    }
+    // tile starts among the exact blocks; every block header of a tile must lie within the
+    // stage k_delta_lb loads from the tile's start (wider tiles stay with the page pass)
+    if (j < m && (b + j) % bpt == 0) {
+      tstart[(b + j) / bpt] = P;
+      ts_s[j] = P;
+    }
+    __syncthreads();
+    bool fits = true;
+    if (j < m) {
+      const uint32_t r = (b + j) % bpt;  // the block's place in its tile
+      const uint32_t ts = j >= r ? ts_s[j - r] : ts_s[WG];  // (ts_s[WG]: the last tile start of earlier rounds)
+      fits = (uint64_t)P - ts + 24u <= (uint64_t)DlbShape::STAGE;
+    }
+    if (__syncthreads_or(!fits)) {
+      ok_page = false;
+      break;
+    }
+    if (j == 0) {  // the tile start the next round's first blocks belong to
+      uint32_t last = ts_s[WG];
+      for (uint32_t k = 0; k < m; ++k)
+        if ((b + k) % bpt == 0) last = ts_s[k];
+      ts_s[WG] = last;
+    }
+    // next round: after the exact prefix (block b + m's offset is the scan at thread m)
+    uint32_t nc;
+    if (m >= nact) {
+      const uint64_t e = (uint64_t)cur + total;
+      nc = e > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)e;
+    } else {
+      __shared__ uint32_t nc_s;
+      if (j == m) nc_s = (uint32_t)(Q64 > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : Q64);
+      __syncthreads();
+      nc = nc_s;
+    }
+    H = m ? (nc - cur) / m : H;
+    cur = nc;
+    b += m;
+    if (m < 32u && b < nblocks && ++slow > 4u) {  // irregular block lengths: the page pass walks them
+      ok_page = false;
+      break;
+    }
+    __syncthreads();  // (wtot / wfirst are rewritten by the next round)
+  }
+  if (tid == 0) {
+    if (ok_page) {
+      info.first = hd.first;
+      info.vpmb = vpmb32;
+      info.nmb = nmb32;
+      info.tiled = DP_LB;
+      info.pad = H;  // the average block length: k_delta_lb's header scan guess
+    }
+    dt.page[p] = info;
+  }
+}
+
+// Tile t's sum granules (lo, hi), read once: the kind (1 aggregate, 2 inclusive) when both carry
+// this call's tag with the same kind, else 0 (not yet published, or half rewritten).
+__device__ inline uint32_t dlb_peek(const DeltaTables& dt, uint32_t t, uint32_t epoch, uint64_t& v) {
+  dlb_gu64* g = (dlb_gu64*)(dt.lb + 2ull * t);
+  const uint64_t lo = __hip_atomic_load(g, DLB_RLX), hi = __hip_atomic_load(g + 1, DLB_RLX);
+  const uint32_t tl = (uint32_t)(lo >> 32), th = (uint32_t)(hi >> 32);
+  if (tl == th && (tl >> 2) == epoch && (tl & 3u)) {
+    v = (lo & 0xFFFFFFFFull) | (hi << 32);
+    return tl & 3u;
+  }
+  return 0u;
+}
+
+__device__ inline void dlb_write(const DeltaTables& dt, uint32_t t, uint32_t epoch, uint32_t kind, uint64_t v) {
+  dlb_gu64* g = (dlb_gu64*)(dt.lb + 2ull * t);
+  const uint64_t tag = (uint64_t)((epoch << 2) | kind) << 32;
+  __hip_atomic_store(g, tag | (v & 0xFFFFFFFFull), DLB_RLX);
+  __hip_atomic_store(g + 1, tag | (v >> 32), DLB_RLX);
+}
+
+template <int ES>
+__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(DLB_NT) k_delta_lb(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     PageWork* pages, const ChunkWork* chunks,
+                                                     const uint32_t* __restrict__ tile_page, uint32_t ntiles,
+                                                     DeltaTables dt) {
+  using SH = DlbShape;
+  constexpr uint32_t TT = SH::T;
+  constexpr int STG = SH::STAGE;
+  __shared__ DeltaPageSmem<DLB_NT> sm;
+  __shared__ uint64_t carry_s;
+  __shared__ uint32_t fail_s, tk_s;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t epoch = dt.epoch;
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7u;
+#pragma unroll 1
+  for (;;) {
+    // the next tile: tile k * 8 + c is the k-th ticket of counter c; a workgroup draws from its own
+    // XCD's counter, then (that one drained) from the others. Each counter hands out its tiles in
+    // order, so the lowest unfinished tile is always handed out or held by a running workgroup
+    // whose look-back finds its predecessors finished: the waits end.
+    if (tid == 0) {
+      uint32_t tt = 0xFFFFFFFFu;
+      for (uint32_t r = 0; r < 8u && tt == 0xFFFFFFFFu; ++r) {
+        const uint32_t c = (xcc + r) & 7u;
+        if (__hip_atomic_load((dlb_gu32*)&dt.ticket[c], DLB_RLX) * 8ull + c >= ntiles) continue;
+        const uint32_t k = __hip_atomic_fetch_add((dlb_gu32*)&dt.ticket[c], 1u, DLB_RLX);
+        if ((uint64_t)k * 8u + c < ntiles) tt = k * 8u + c;
+      }
+      tk_s = tt;
+    }
+    __syncthreads();
+    const uint32_t t = tk_s;
+    __syncthreads();  // (tk_s is rewritten for the next tile)
+    if (t == 0xFFFFFFFFu) break;
+    const uint32_t p = tile_page[t];
+    const PageWork& pw = pages[p];
+    if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) continue;
+    if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) continue;
+    const DeltaPage dp = dt.page[p];
+    if (dp.tiled != DP_LB) continue;
+    const uint32_t i = t - pw.ltile0;
+    const uint32_t need = (uint32_t)pw.nonnull - 1u, D0 = i * TT;
+    if (D0 >= need) continue;
+    const uint32_t D1 = D0 + TT < need ? D0 + TT : need;
+    const uint32_t vpb = dp.vpmb * dp.nmb, nb = (D1 - D0 + vpb - 1) / vpb;
+    const uint64_t S = pw.base + pw.val_off;
+    const uint32_t slen = pw.val_bytes;
+    const uint32_t hdr = dt.tstart[t];
+    const uint64_t SB = (S + hdr) & ~15ull;
+    const uint32_t sb = (uint32_t)(SB - S);
+    {
+      const bool fast = SB + STG <= blob_len;
+#pragma unroll
+      for (int c = 0; c < SH::CH; ++c) {
+        const uint64_t a = SB + (uint32_t)(tid + c * DLB_NT) * 16u;
+        sm.stq[tid + c * DLB_NT] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
+      }
+      if (tid < 16) sm.stage[STG / 4 + tid] = 0;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      bool fb, shortwin;
+      uint32_t hp;
+      // (k_delta_hdr checked these headers; the block length guess from the page's average)
+      dpg_headers<DLB_NT, ES>(sm, hdr, dp.pad, sb, STG, slen, nb, D0 / vpb, need, dp.nmb, dp.vpmb, fb, shortwin, hp);
+      if (tid == 0) fail_s = fb ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool failed = fail_s != 0;  // (k_delta_hdr checked these headers: never, short of a bug)
+    uint64_t x[DPT];
+    uint64_t sx = 0;
+    if (!failed) {
+      sx = dpg_unpack<DLB_NT>(sm, blob, blob_len, S, sb, STG, D0, D1, dp.nmb, dp.vpmb, x);
+    } else {
+#pragma unroll
+      for (int j2 = 0; j2 < DPT; ++j2) x[j2] = 0;
+    }
+    uint64_t acc;
+    const uint64_t T = dpg_scan<DLB_NT>(sm, sx, 0ull, acc);  // acc: within the tile
+    // ---- publish the tile's sum, look back for the running value before it
+    if (tid < 64) {
+      uint64_t carry = dp.first;
+      bool bad = failed;
+      if (i > 0) {
+        if (lane == 0) dlb_write(dt, t, epoch, 1u, T);
+        // lane l reads tile j - l: the nearest inclusive value and the aggregates after it (a
+        // tile not yet published: read again); the page's tile 0 publishes an inclusive value
+        uint64_t sum = 0;
+        uint32_t j = t - 1, spins = 0;
+        while (true) {
+          const bool in = lane <= j - pw.ltile0;
+          uint64_t v = 0;
+          const uint32_t k = in ? dlb_peek(dt, j - lane, epoch, v) : 0u;
+          const uint64_t notr = __ballot(in && k == 0u), incm = __ballot(in && k == 2u);
+          const uint32_t f = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;   // nearest inclusive
+          const uint32_t r = notr ? (uint32_t)__builtin_ctzll(notr) : 64u;   // nearest unpublished
+          if (f < r || (r == 64u && incm == 0ull && __ballot(in) == ~0ull)) {
+            uint64_t add = (in && lane <= f) ? v : 0ull;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, 64);
+            sum += add;
+            if (f < 64u) break;
+            j -= 64u;  // 64 aggregates: further back
+            continue;
+          }
+          if (++spins > (1u << 22)) {  // bounded: a look-back that never ends reports the page
+            bad = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        carry = sum;
+      }
+      if (lane == 0) {
+        dlb_write(dt, t, epoch, 2u, carry + T);
+        carry_s = carry;
+        fail_s = bad ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+    if (fail_s) {
+      if (tid == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)p, ST_GENERAL);
+      __syncthreads();
+      continue;
+    }
+    const uint64_t carry = carry_s;
+    const gptr<uint8_t> ob = gp(chunks[pw.chunk].val_out) + pw.value_out * (uint64_t)ES;
+    if (i == 0 && tid == 0) {  // value 0
+      if (ES == 8) *reinterpret_cast<gptr<uint64_t>>(ob) = dp.first;
+      else *reinterpret_cast<gptr<uint32_t>>(ob) = (uint32_t)dp.first;
+    }
+    uint64_t val[DPT];
+    acc += carry;
+#pragma unroll
+    for (int j2 = 0; j2 < DPT; ++j2) {
+      acc += x[j2];
+      val[j2] = acc;
+    }
+    dpg_store<ES, DLB_NT>(sm, val, ob + (uint64_t)(D0 + 1) * ES, D1 - D0);
   }
 }
 
@@ -905,9 +1342,15 @@ __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ b
 // at once when it left none (dt.nfall), then the per-page stream decoder for what those refuse.
 template <int ES>
 static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
-                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, hipStream_t s, hipEvent_t* kev) {
+                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, hipStream_t s, hipEvent_t* kev,
+                        uint32_t lb_grid) {
   if (kev) (void)hipEventRecord(kev[0], s);
-  hipLaunchKernelGGL(k_delta_page<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, dt);
+  if (lb_grid) {
+    hipLaunchKernelGGL(k_delta_hdr<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, dt);
+    hipLaunchKernelGGL(k_delta_lb<ES>, dim3(lb_grid), dim3(DLB_NT), 0, s, blob, blob_len, pages, chunks, tile_page,
+                       ntiles, dt);
+  }
+  hipLaunchKernelGGL((k_delta_page<ES, DPG_NT>), dim3(npages), dim3(DPG_NT), 0, s, blob, blob_len, pages, chunks, dt);
   if (kev) (void)hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, chunks, dt);
   if (ntiles) {
@@ -920,11 +1363,37 @@ static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
 }
 
 // es_mask: bit mask of the DELTA_BINARY_PACKED chunks' value sizes (4: INT32, 8: INT64).
+// Workgroups of k_delta_lb<ES> that fit the device at once (it walks the tiles by tickets: the
+// grid is for occupancy, not for correctness).
+template <int ES>
+static uint32_t delta_lb_grid(uint32_t ntiles) {
+#ifndef PQG_DELTA_LB
+#define PQG_DELTA_LB 1
+#endif
+  if (!PQG_DELTA_LB || ntiles == 0) return 0;
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  int g = dev >= 0 && dev < 64 ? cached[dev] : 0;
+  if (!g) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_delta_lb<ES>, DLB_NT, 0) != hipSuccess || per <= 0) per = 4;
+    g = cus * per;
+    if (dev >= 0 && dev < 64) cached[dev] = g;
+  }
+  return (uint32_t)g < ntiles ? (uint32_t)g : ntiles;
+}
+
+// es_mask: bit mask of the DELTA_BINARY_PACKED chunks' value sizes (4: INT32, 8: INT64).
 extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                                              ChunkWork* chunks, uint32_t ntiles, const uint32_t* tile_page,
                                              DeltaTables dt, uint32_t es_mask, hipStream_t s, hipEvent_t* kev) {
-  if (es_mask & 8u) delta_tiled<8>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, kev);
-  if (es_mask & 4u) delta_tiled<4>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, (es_mask & 8u) ? nullptr : kev);
+  if (es_mask & 8u)
+    delta_tiled<8>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, kev, delta_lb_grid<8>(ntiles));
+  if (es_mask & 4u)
+    delta_tiled<4>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, (es_mask & 8u) ? nullptr : kev,
+                   delta_lb_grid<4>(ntiles));
   return hipGetLastError();
 }
 

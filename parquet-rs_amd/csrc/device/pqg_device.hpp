@@ -86,6 +86,17 @@ __device__ inline void seg_scan_pages(const PageWork* pages, const ChunkWork* ch
   }
 }
 
+// Inclusive scan over the wave's 64 lanes (DPP row shifts and row broadcasts, no LDS).
+__device__ inline uint32_t wave_scan_incl_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 // Little-endian byte load from global memory, guarded by the blob size.
 __device__ inline uint32_t gbyte(const uint8_t* blob, uint64_t blob_len, uint64_t a) {
   return a < blob_len ? blob[a] : 0u;

@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(64) k_prepare(const uint8_t* __restrict__ blob
     prepare_page(blob, blob_len, pages, p, chunks, pw_s);
     if (p == 0)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 8; ++i)
         if (ini.word[i]) *ini.word[i] = ini.val[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i)

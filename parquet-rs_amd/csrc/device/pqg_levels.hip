@@ -118,6 +118,18 @@ __device__ inline uint64_t wave_incl_scan_cnt(uint32_t c) {
   return ic;
 }
 
+// The same for 64-bit counts.
+__device__ inline uint64_t wave_incl_scan_cnt64(uint64_t c) {
+  if (!__ballot(c >= (1ull << 25))) return wave_incl_scan_u32((uint32_t)c);
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t b = __shfl_up(c, d, 64);
+    if (lane >= (uint32_t)d) c += b;
+  }
+  return c;
+}
+
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS accesses have completed
   __builtin_amdgcn_wave_barrier();
@@ -1253,26 +1265,24 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     if (w == 1) {  // 64 entry offsets: lane e follows entry e across the segments
       uint32_t pc[LV_SEG], pv[LV_SEG], bpm;
       lv_seg_build(W, x, pc, pv, bpm);
-      uint32_t e = lane, hs = 0, c = 0;
+      uint32_t e = lane, c = 0, me = 0xFFFFu;
       // the chain from position 0, speculatively (lv_spec_chain); each entry's chain is then
-      // followed only until it meets it, the rest from the chain's per-segment suffix sums
+      // followed only until it meets it (me: where), the rest from the chain's per-segment suffix
+      // sums
       uint32_t q;
       bool valid;
       uint2 r;
       uint64_t ci;
       const bool spec = lv_spec_chain(W, 0u, ~0ull, q, valid, r, ci);
-      uint32_t* sp = W.stage;  // (staged bytes no longer needed): chain position, header and output suffixes
+      uint32_t* sp = W.stage;  // (staged bytes no longer needed): chain position, output suffixes
       uint32_t exitc = LV_J_END;
       if (spec) {
-        const uint32_t h = valid ? (uint32_t)__builtin_popcount(r.x >> 16) : 0u, cc = valid ? r.y : 0u;
-        const uint32_t hi = wave_incl_scan_u32(h);
-        const uint32_t htot = (uint32_t)__shfl((int)hi, 63, 64);
+        const uint32_t cc = valid ? r.y : 0u;
         const uint64_t ctot = __shfl(ci, 63, 64);
         const uint64_t vm = __ballot(valid);
         exitc = (uint32_t)__shfl((int)(r.x & 0xFFFFu), 63 - __builtin_clzll(vm), 64);  // (lane 0 is valid)
         const uint64_t cs = ctot - ci + cc;
         sp[lane] = valid ? q : LV_NONE;
-        sp[64 + lane] = htot - hi + h;
         sp[128 + lane] = cs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cs;
         wave_lds_sync();
       }
@@ -1280,23 +1290,61 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       while (__any(e < LV_WIN)) {
         if (e < LV_WIN) {
           const uint32_t sg = e / LV_SEG;
-          uint32_t dh, dc;
+          uint32_t dc;
           if (spec && sp[sg] == e) {  // on the chain from 0: its rest
-            dh = sp[64 + sg];
+            me = me == 0xFFFFu ? e : me;
             dc = sp[128 + sg];
             e = exitc;
           } else {
             const uint2 t = W.JC[(e % LV_SEG) * WAVE + sg];
-            dh = (uint32_t)__builtin_popcount(t.x >> 16);
             dc = t.y;
             e = t.x & 0xFFFFu;
           }
-          hs += dh;
           const uint32_t s2 = c + dc;
           c = s2 < c ? 0xFFFFFFFFu : s2;
         }
       }
-      tab[lane] = make_uint2(e | (min(hs, 0xFFFFu) << 16), c);
+      // the reference chain of the window's emit (k_lv_emit: the true chain's headers are its
+      // headers from where the true entry's chain meets it, and the few before): the chain most
+      // entries leave the window by (the chain from 0 when entry 0 is one of them), so that the
+      // true entry, whichever it is, almost always meets it inside the window
+      uint32_t bx = 0, bn = 0, bl = 0;
+      for (uint64_t rem = ~0ull; rem;) {
+        const uint32_t ld = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t xv = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)ld);
+        const uint64_t m = __ballot(e == xv);
+        const uint32_t nm = (uint32_t)__builtin_popcountll(m);
+        if (nm > bn) {
+          bn = nm;
+          bx = xv;
+          bl = ld;
+        }
+        rem &= ~m;
+      }
+      uint16_t ref = (uint16_t)(spec && valid ? (r.x >> 16) : 0u);
+      const uint32_t e0x = (uint32_t)__builtin_amdgcn_readlane((int)e, 0);
+      if (!spec) me = 0xFFFFu;
+      if (spec && e0x != bx) {  // another chain leaves by the majority exit: it is the reference
+        wave_lds_sync();  // (every read of sp is done)
+        me = 0xFFFFu;
+        ref = 0;
+        if (lv_spec_chain(W, bl, ~0ull, q, valid, r, ci)) {
+          sp[lane] = valid ? q : LV_NONE;
+          ref = (uint16_t)(valid ? (r.x >> 16) : 0u);
+          wave_lds_sync();
+          uint32_t f = lane;
+#pragma unroll 1
+          while (__any(f < LV_WIN && me == 0xFFFFu)) {
+            if (f < LV_WIN && me == 0xFFFFu) {
+              const uint32_t sg = f / LV_SEG;
+              if (sp[sg] == f) me = f;
+              else f = W.JC[(f % LV_SEG) * WAVE + sg].x & 0xFFFFu;
+            }
+          }
+        }
+      }
+      lt.bmp[(uint64_t)g * WAVE + lane] = ref;
+      tab[lane] = make_uint2(e | (me << 16), c);
       wave_lds_sync();  // the next window's stage and table
       continue;
     }
@@ -2140,14 +2188,79 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     }
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w, vb = (w + 7u) >> 3, slen = x.s.slen, n = x.s.n;
-    const uint32_t e0 = wi.x & 0xFFFFu, nh = wi.x >> 16;  // entry, true headers (saturated)
+    // entry; bit width 1: where the entry's chain meets the window's reference chain (0xFFFF:
+    // not inside the window), else the true headers (saturated)
+    const uint32_t e0 = wi.x & 0xFFFFu, nh = wi.x >> 16;
     const uint32_t base = wi.y;
+    // bit width 1, the entry's chain meets the reference chain: that chain's headers (k_lv_win's
+    // bitmap, one 16-bit mask per segment) from the meeting point on
+    const bool viaref = w == 1 && nh != 0xFFFFu;
+    const uint32_t refm = viaref ? (uint32_t)lt.bmp[(uint64_t)(D.wb + x.k) * WAVE + lane] : 0u;
     pf.stage(blob, blob_len, x, W.stage);
     if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1, lt.win + D.wb);
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
-    if (nh <= LV_SERIAL) {
+    if (viaref) {
+      constexpr uint32_t SEG = LV_SEG;
+      const uint32_t me = nh, i0 = lane * SEG;
+      // the entry's own headers before the meeting point: one lane, serially, into a short list
+      uint32_t* pre = W.runs.rinfo;  // (the run list is written after these are read)
+      if (lane == 0) {
+        uint32_t qq = e0, np = 0;
+        while (qq < me && np < 64u) {
+          uint32_t nx, c, v;
+          bool bp;
+          if (!lv_parse4(W.stage, qq + x.sb, x.W0 + qq, slen, w, vb, nx, c, v, bp)) break;
+          pre[np++] = qq;
+          qq = nx - x.W0;
+        }
+        pre[64] = qq == me ? np : 0xFFFFFFFFu;  // (the walk must land on the meeting point)
+      }
+      wave_lds_sync();
+      const uint32_t np = pre[64];
+      uint32_t mym = i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0));
+      for (uint32_t k = 0; k < np && np != 0xFFFFFFFFu; ++k) {
+        const uint32_t qq = pre[k];
+        if (qq >= i0 && qq < i0 + SEG) mym |= 1u << (qq - i0);
+      }
+      // outputs of this segment's true headers, then their place: a lane scan
+      uint64_t so = 0;
+#pragma unroll 1
+      for (uint32_t m = mym; m; m &= m - 1u) {
+        const uint32_t t = (uint32_t)__builtin_ctz(m);
+        uint32_t nx, c, v;
+        bool bp;
+        lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (chain headers parse)
+        so += c;
+      }
+      const uint64_t si = wave_incl_scan_cnt64(so);
+      const uint64_t tot = __shfl(si, 63, 64);
+      bad = __ballot(np == 0xFFFFFFFFu) != 0;
+      wave_lds_sync();  // (the prefix list is read)
+      if (!bad) {
+        const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
+        const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
+        uint32_t k = rb;
+        uint64_t oa = (uint64_t)base + (si - so);
+#pragma unroll 1
+        for (uint32_t m = mym; m; m &= m - 1u) {
+          const uint32_t t = (uint32_t)__builtin_ctz(m);
+          uint32_t nx, c, v;
+          bool bp;
+          lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);
+          W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
+          W.runs.rinfo[k] = bp ? v : (R_RLE | v);
+          bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
+          ++k;
+          oa += c;
+        }
+        R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
+        T = tot;
+      } else {  // (the entry's chain did not land on the meeting point: a table k_lv_win made wrong)
+        bad = true;
+      }
+    } else if (w != 1 && nh <= LV_SERIAL) {
       // sparse window: one lane follows the chain from the entry
       if (lane == 0) {
         uint32_t q = x.W0 + e0, nr = 0;

@@ -112,8 +112,9 @@ struct Slot {
   size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
+  uint32_t dt_epoch = 0;  // look-back tag of the last decode (DeltaTables::epoch)
   // level path (pqg_levels.hip): buffers of LevelTables per stream kind, grown on demand
-  static constexpr int LV_BUFS = 13;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr
+  static constexpr int LV_BUFS = 14;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr, bmp
   void* lvbuf[K_N][LV_BUFS] = {};
   size_t lvcap[K_N][LV_BUFS] = {};
   LevelTables lt(int k, uint32_t tstride) const {
@@ -131,6 +132,7 @@ struct Slot {
     t.spos = (uint32_t*)lvbuf[k][10];
     t.dense = (uint32_t*)lvbuf[k][11];
     t.ctr = (uint32_t*)lvbuf[k][12];
+    t.bmp = (uint16_t*)lvbuf[k][13];
     t.tstride = tstride;
     return t;
   }
@@ -330,6 +332,9 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dt.inc);
     hipFree(sl.dt.flag);
     hipFree(sl.dt.nfall);
+    hipFree(sl.dt.tstart);
+    hipFree(sl.dt.lb);
+    hipFree(sl.dt.ticket);
     for (int k = 0; k < K_N; ++k) {
       for (void* b : sl.lvbuf[k]) hipFree(b);
     }
@@ -807,9 +812,9 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     const size_t need[Slot::LV_BUFS] = {(size_t)np + 1, (size_t)np + 1, nwin + np + 1,
                                         64 * (nwin + 2 * (size_t)np) + 1, (nwin + 1) * ent, nwin + 1,
                                         (size_t)np + 1, nseg, nseg, nseg * LW_SCAP, nseg * LW_SCAP,
-                                        (size_t)np + 1, 16};
+                                        (size_t)np + 1, 16, (nwin + 1) * 64};
     const size_t elem[Slot::LV_BUFS] = {4, 4, 4, sizeof(uint2), sizeof(uint2), sizeof(uint2),
-                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4, 4};
+                                        4, 4, sizeof(LvSeg), sizeof(uint2), 4, 4, 4, 2};
     const bool fresh_ctr = sl.lvbuf[k][12] == nullptr;
     for (int bb = 0; bb < Slot::LV_BUFS; ++bb)
       if ((st = grow(ctx, &sl.lvbuf[k][bb], &sl.lvcap[k][bb], need[bb], elem[bb], "hipMalloc level tables"))) return st;
@@ -835,6 +840,9 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       hipFree(sl.dt.inc);
       hipFree(sl.dt.flag);
       hipFree(sl.dt.nfall);
+      hipFree(sl.dt.tstart);
+      hipFree(sl.dt.lb);
+      hipFree(sl.dt.ticket);
       sl.dt = DeltaTables{};
       sl.dt_tcap = sl.dt_pcap = 0;
       const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
@@ -844,12 +852,22 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
       HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
       HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
+      HIPCHK(hipMalloc(&sl.dt.tstart, tc * sizeof(uint32_t)), "hipMalloc delta tile starts");
+      HIPCHK(hipMalloc(&sl.dt.lb, tc * 2 * sizeof(uint64_t)), "hipMalloc delta look-back granules");
+      HIPCHK(hipMalloc(&sl.dt.ticket, 8 * sizeof(uint32_t)), "hipMalloc delta tickets");
+      // granule tags must never match a later decode's epoch by accident: zeroed once here
+      HIPCHK(hipMemsetAsync(sl.dt.lb, 0, tc * 2 * sizeof(uint64_t), s), "memset delta granules");
       sl.dt_tcap = tc;
       sl.dt_pcap = pc;
     }
     ini.word[nw_] = sl.dt.nfall;
     ini.val[nw_++] = 0u;
     sl.dt.dbg = (dbg_env & 32) ? ctx->dbgbuf : nullptr;
+    if (++sl.dt_epoch >= (1u << 30)) {  // (tags of 2^30 decodes ago: zero the granules again)
+      HIPCHK(hipMemsetAsync(sl.dt.lb, 0, sl.dt_tcap * 2 * sizeof(uint64_t), s), "memset delta granules");
+      sl.dt_epoch = 1;
+    }
+    sl.dt.epoch = sl.dt_epoch;
   }
   ini.dense_def = need_lv[K_DEF] ? sl.lt(K_DEF, 0).dense : nullptr;
   ini.dense_rep = need_lv[K_REP] ? sl.lt(K_REP, 0).dense : nullptr;

@@ -76,8 +76,8 @@ struct PageWork {
 // launches): counters to a value, per-page flag arrays to 0, and the dictionary page check of
 // fixed-width dictionaries (dict_es: value size, 0 = none; decoding.rs:282-288, :145-147).
 struct PrepInit {
-  uint32_t* word[4];
-  uint32_t val[4];
+  uint32_t* word[8];
+  uint32_t val[8];
   uint32_t* pzero[3];
   // level-path density probe (LevelTables::dense) of the def / rep streams, run by k_prepare's
   // wave right after it locates them; dense_zero: a stream kind's array cleared instead
@@ -165,6 +165,10 @@ struct DeltaTables {
   uint32_t* flag;     // [tiles] epoch * 4 + {1 aggregate, 2 inclusive}
   uint64_t* dbg;      // diagnostics: per-page phase cycles of k_delta_page (PQG_DEBUG bit 5)
   uint32_t* nfall;    // pages k_delta_page left to the tiled path (0: its tile kernels exit at once)
+  uint32_t* tstart;   // [tiles] stream offset of the tile's first block header (k_delta_hdr)
+  uint64_t* lb;       // [2 * tiles] look-back granules {tag, 32-bit half} of the tile sums (k_delta_lb)
+  uint32_t* ticket;   // [8] k_delta_lb's per-XCD tile counters (zeroed by k_delta_hdr)
+  uint32_t epoch;     // this decode's look-back tag (never 0; the granules are zeroed at allocation)
 };
 
 // Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
@@ -201,6 +205,8 @@ struct LevelTables {
   uint2* rec;        // [64 * (windows + 2 * pages)] walked pages' runs: (first output, info)
   uint2* tab;        // [windows * tstride] per window and entry offset: (exit offset, outputs)
   uint2* win;        // [windows] (true entry offset | LV_NONE, first output) (k_lv_stitch)
+  uint16_t* bmp;     // [windows * 64] bit width 1: per segment of 16 bytes, the headers of the
+                     // window's reference chain (k_lv_win), for k_lv_emit
   uint32_t* dense;   // [pages] 1: the stream's first 64 headers lie within 1 KiB (k_lv_probe): the
                      // window path takes it without a segment walk
   uint32_t* ctr;     // [16] last-workgroup tickets (zero between launches): [0] k_lv_segscan,

@@ -345,3 +345,38 @@ def test_dense_level_windows_with_long_runs(oracle, ctx, long_run):
         vals = rng.integers(-2 ** 31, 2 ** 31, size=nn, dtype=np.int64).astype(np.int32)
         pages.append(oracle.PageSpec(oracle.PAGE_DATA, lev + vals.tobytes(), n, oracle.PLAIN))
     _same(oracle, ctx, oracle.INT32, pages, max_def=1)
+
+
+@pytest.mark.parametrize("shape", [(512, 4), (128, 4)])
+@pytest.mark.parametrize("ptype", ["INT32", "INT64"])
+def test_delta_bench_pages_lookback(oracle, ctx, ptype, shape):
+    """Config 4's pages at the bench shape and at the reference writer's default (128 / 4 x 32,
+    encoding.rs:508-509), several pages of 2^20 values and a ragged one, from the bench's own
+    generator: every tile of every page goes through the header pass (k_delta_hdr) and the
+    look-back tile kernel (k_delta_lb), whose running values chain across 256 tiles per page."""
+    import ctypes as C
+
+    import pqgpu
+    import pqgtools
+    L = pqgtools.lib()
+    info = pqgtools.WorkloadInfo()
+    n, page = 3 * (1 << 20) + 77_777, 1 << 20
+    bits = 16 if ptype == "INT64" else 12
+    assert L.pqg_gen_delta_int64(n, bits, page, shape[0], shape[1], 0x5EED0004, 8, None, 0, None, 0, C.byref(info)) == 0
+    host = np.zeros(info.blob_len + 64, np.uint8)
+    pages = (pqgpu.Page * info.npages)()
+    assert L.pqg_gen_delta_int64(n, bits, page, shape[0], shape[1], 0x5EED0004, 8, host.ctypes.data_as(C.c_void_p),
+                                 info.blob_len, pages, info.npages, C.byref(info)) == 0
+    specs = [oracle.PageSpec(p.page_type, host[p.offset:p.offset + p.nbytes].tobytes(), p.num_values, p.encoding)
+             for p in (pages[i] for i in range(info.npages))]
+    t = getattr(oracle, ptype)
+    if ptype == "INT32":  # the generator writes INT64 pages: re-encode the same values as INT32
+        vals = oracle.read_column(oracle.INT64, specs)["values"].astype(np.int32)
+        specs, o = [], 0
+        for i in range(info.npages):
+            k = pages[i].num_values
+            specs.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_encode(t, vals[o:o + k], *shape), k,
+                                         oracle.DELTA_BINARY_PACKED))
+            o += k
+    got, ref = _same(oracle, ctx, t, specs)
+    assert got["num_values"] == n
