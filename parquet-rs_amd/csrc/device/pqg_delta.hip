@@ -885,6 +885,13 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
   if (dt.page[p].tiled == DP_LB) return;  // decoded by k_delta_lb
   const gptr<uint8_t> __restrict__ out = gp(chunks[pw.chunk].val_out);
   DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
+#ifdef PQG_DPG_OFF  // (experiment builds: every page to the tiled path)
+  if (tid == 0) {
+    dt.page[p] = info;
+    atomicAdd(dt.nfall, 1u);
+  }
+  return;
+#endif
   const uint64_t S = pw.base + pw.val_off;
   const uint32_t slen = pw.val_bytes;
   DpgHead hd;
@@ -1264,31 +1271,48 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(DLB
       bool bad = failed;
       if (i > 0) {
         if (lane == 0) dlb_write(dt, t, epoch, 1u, T);
-        // lane l reads tile j - l: the nearest inclusive value and the aggregates after it (a
-        // tile not yet published: read again); the page's tile 0 publishes an inclusive value
+        // the tile before (j): one lane polls its granules until published (polls are kept to one
+        // word pair per waiting workgroup: many pollers cut the chip's bandwidth); an aggregate
+        // sends the wave over the 63 tiles before it in one pass, up to the nearest inclusive
+        // value, or up to the nearest tile not yet published, which is polled next
         uint64_t sum = 0;
-        uint32_t j = t - 1, spins = 0;
+        uint32_t j = t - 1;
+#pragma unroll 1
         while (true) {
-          const bool in = lane <= j - pw.ltile0;
-          uint64_t v = 0;
-          const uint32_t k = in ? dlb_peek(dt, j - lane, epoch, v) : 0u;
-          const uint64_t notr = __ballot(in && k == 0u), incm = __ballot(in && k == 2u);
-          const uint32_t f = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;   // nearest inclusive
-          const uint32_t r = notr ? (uint32_t)__builtin_ctzll(notr) : 64u;   // nearest unpublished
-          if (f < r || (r == 64u && incm == 0ull && __ballot(in) == ~0ull)) {
-            uint64_t add = (in && lane <= f) ? v : 0ull;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, 64);
-            sum += add;
-            if (f < 64u) break;
-            j -= 64u;  // 64 aggregates: further back
-            continue;
+          uint64_t v0 = 0;
+          uint32_t k0 = 0;
+          if (lane == 0) {
+            for (uint32_t spins = 0; spins < (1u << 20); ++spins) {
+              if ((k0 = dlb_peek(dt, j, epoch, v0)) != 0u) break;
+              __builtin_amdgcn_s_sleep(8);
+            }
           }
-          if (++spins > (1u << 22)) {  // bounded: a look-back that never ends reports the page
+          k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+          v0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0);
+          if (k0 == 0u) {  // bounded: a look-back that never ends reports the page
             bad = true;
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          sum += v0;
+          if (k0 == 2u) break;
+          const bool in = lane >= 1u && lane <= j - pw.ltile0;
+          uint64_t v = 0;
+          const uint32_t k = in ? dlb_peek(dt, j - lane, epoch, v) : 0u;
+          const uint64_t notr = __ballot(in && k == 0u), incm = __ballot(in && k == 2u);
+          const uint32_t f = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;  // nearest inclusive
+          const uint32_t r = notr ? (uint32_t)__builtin_ctzll(notr) : 64u;  // nearest unpublished
+          const uint32_t upto = f < r ? f : r - 1u;  // lanes [1, upto] are summed
+          uint64_t add = (in && lane <= upto) ? v : 0ull;
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, 64);
+          sum += add;
+          if (f < r) break;
+          if (r == 64u && __ballot(in) != (~0ull << 1)) {  // (the page's tile 0 is inclusive: never)
+            bad = true;
+            break;
+          }
+          j -= r;  // the nearest unpublished tile (or, all 63 aggregates, the one past them)
         }
         carry = sum;
       }

@@ -2663,7 +2663,11 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
     hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<1>>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages,
                        chunks, sel, rt, lt, LvLevelOut<1>{});
   } else {
-    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+#ifndef PQG_LE_GRIDX
+#define PQG_LE_GRIDX 1
+#endif
+    hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid * PQG_LE_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel,
+                       rt, lt);
     hipLaunchKernelGGL(k_lv_emit_walk<LvLevelOut<2>>, dim3(wgrid * PQG_EW_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages,
                        chunks, sel, rt, lt, LvLevelOut<2>{});
   }
