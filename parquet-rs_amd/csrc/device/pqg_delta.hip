@@ -26,7 +26,6 @@ namespace pqg {
 
 // DeltaPage::tiled values set by k_delta_page (0 / 1 are the tiled path's own)
 constexpr uint32_t DP_DONE = 2u, DP_FALLBACK = 3u;
-constexpr uint32_t DP_LB = 4u;  // k_delta_lb decodes the page (k_delta_hdr found its tile starts)
 
 __device__ inline uint32_t rfl32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
@@ -53,7 +52,7 @@ __global__ void __launch_bounds__(64) k_delta_index(const uint8_t* __restrict__ 
   const uint32_t lane = threadIdx.x & 63;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
-  if (dt.page[p].tiled == DP_DONE || dt.page[p].tiled == DP_LB) return;  // decoded by k_delta_page / k_delta_lb
+  if (dt.page[p].tiled == DP_DONE) return;  // decoded by k_delta_page
   DeltaPage info{0, 0, 0, 0, 0};
   if (pw.status != 0) {
     if (lane == 0) dt.page[p] = info;
@@ -556,20 +555,23 @@ __global__ void __launch_bounds__(WG) k_delta_expand(const uint8_t* __restrict__
 
 // ============================================================================ page pass
 //
-// k_delta_page: one 256-thread workgroup per page decodes the page's whole value stream tile by
-// tile, carrying the running value in registers, so no index pass, tile sums, tile scan or
-// cross-workgroup wait is needed. Tiles are 4096 deltas (value i = first + sum of deltas d < i,
-// decoding.rs:560-566; the tile of deltas [D0, D1) yields values [D0 + 1, D1 + 1)), and blocks
-// must divide the tile, so a block never spans two tiles. Per tile: wave 0 follows the block
-// header chain (one 8-byte LDS read per block for the varint length, one for the widths) and
-// then parses each block's header on its own lane (the checks of k_delta_index); every thread
-// unpacks 16 deltas of one mini-block (hoisted parameters, 32-bit bit offsets, one funnel shift
-// per delta), the workgroup scans, adds the carry and stores through an LDS transpose (quarters
-// of 1024 values). The next tile's bytes are loaded into registers
-// while the current tile is expanded, as many as the current tile spanned plus a margin (a tile
-// that needs more reloads the full window). Anything else (an error the reference reports, a header or payload outside the
-// staged window, more than 8 mini-blocks, mini-blocks of a size not a multiple of 16, blocks
-// not dividing 4096) marks the page DP_FALLBACK for the tiled path, which reports errors exactly.
+// k_delta_page: one workgroup per page (DPG_NT threads) decodes the page's whole value stream tile
+// by tile, carrying the running value in registers, so no index pass, tile sums, tile scan or
+// cross-workgroup wait is needed. Tiles are DPG_NT * 16 deltas (value i = first + sum of deltas
+// d < i, decoding.rs:560-566; the tile of deltas [D0, D1) yields values [D0 + 1, D1 + 1)), and
+// blocks must divide the tile, so a block never spans two tiles. Per tile: wave 0 finds the
+// tile's block headers by a speculative scan (dpg_headers: lane j guesses block j's offset from
+// the previous tile's average block length, the wave's exclusive scan of the lengths parsed there
+// checks the guesses, an exact prefix grows each round: one or two rounds for the writer's
+// blocks, 512-value or 128-value alike, instead of a serial walk of 8 or 32 headers) and parses
+// each block's header on its own lane (the checks of k_delta_index); every thread unpacks 16
+// deltas of one mini-block (hoisted parameters, 32-bit bit offsets, one funnel shift per delta),
+// the workgroup scans, adds the carry and stores through an LDS transpose (a wave's values per
+// round). The next tile's bytes are loaded into registers while the current tile is expanded, as
+// many as the current tile spanned plus a margin (a tile that needs more reloads the full window).
+// Anything else (an error the reference reports, a header outside the staged window, more than 8
+// mini-blocks, mini-blocks of a size not a multiple of 16, blocks not dividing the tile) marks the
+// page DP_FALLBACK for the tiled path, which reports errors exactly.
 #ifndef PQG_DPG_NT
 #define PQG_DPG_NT 256
 #endif
@@ -882,7 +884,6 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
   const PageWork& pw = pages[p];
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
   if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
-  if (dt.page[p].tiled == DP_LB) return;  // decoded by k_delta_lb
   const gptr<uint8_t> __restrict__ out = gp(chunks[pw.chunk].val_out);
   DeltaPage info{0, 0, DP_FALLBACK, 0, 0};
 #ifdef PQG_DPG_OFF  // (experiment builds: every page to the tiled path)
@@ -990,361 +991,6 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
   }
 }
 
-// ============================================================================ look-back path
-//
-// Config 4 at more than one workgroup per page (a page's tiles are independent once each knows
-// where its first block header is and the running value before it):
-//   k_delta_hdr  one workgroup per page finds the stream offset of every tile's first block header
-//                (dt.tstart) by a speculative scan over global memory: thread j guesses block j's
-//                header offset from the average block length so far, parses the header there (16
-//                bytes), and the workgroup's exclusive scan of those lengths checks the guesses;
-//                the exact prefix is kept and the next round starts after it (blocks of one length,
-//                the writer's fixed widths: 256 blocks per round). It checks every block header
-//                as k_delta_page does; a page it cannot take (an error, a header form the page pass
-//                refuses, blocks of irregular lengths) stays with k_delta_page.
-//   k_delta_lb   a resident grid walks the tiles of every such page round-robin (tile t by
-//                workgroup t mod G): stage, block headers, unpack and sum the tile's deltas, then a
-//                decoupled look-back over the page's earlier tiles gives the running value
-//                (value i = first + sum of deltas d < i, wrapping: decoding.rs:560-566), then scan
-//                and store. Tile sums travel as 8-byte {epoch tag, 32-bit half} granules written by
-//                one agent-scope store each and polled by agent-scope loads (MI355X_MICROARCH.md,
-//                inter-workgroup visibility, R2), so no fence; a tile waits only for tiles of the
-//                same or an earlier round of the round-robin, all resident, so the waits end; every
-//                spin is bounded (a timeout reports ST_GENERAL for the page).
-constexpr int DLB_NT = 256;
-using DlbShape = DpgShape<DLB_NT>;
-static_assert(DlbShape::T == DELTA_TILE, "look-back tiles are the page table's tiles");
-
-#define DLB_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
-typedef __attribute__((address_space(1))) unsigned long long dlb_gu64;
-typedef __attribute__((address_space(1))) unsigned int dlb_gu32;
-
-template <int ES>
-__global__ void __launch_bounds__(WG) k_delta_hdr(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                  PageWork* pages, const ChunkWork* chunks, DeltaTables dt) {
-  __shared__ uint32_t wtot[WG / 64], wfirst[WG / 64], wbad[WG / 64];
-  __shared__ uint32_t ts_s[WG + 1];  // start of the tile of each block of the round (LDS: tstart is global)
-  const int p = blockIdx.x;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  if (p == 0 && tid < 8) dt.ticket[tid] = 0;  // k_delta_lb's per-XCD tile counters (read after this launch)
-  const PageWork& pw = pages[p];
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) return;
-  DeltaPage info{0, 0, 0, 0, 0};  // (tiled 0: k_delta_page decides)
-  const uint64_t S = pw.base + pw.val_off;
-  const uint32_t slen = pw.val_bytes;
-  DpgHead hd;
-  if (pw.status != 0 || !dpg_head<DELTA_TILE>(blob + S, slen, pw.nonnull, hd) || hd.need == 0) {
-    if (tid == 0) dt.page[p] = info;
-    return;
-  }
-  const uint32_t nmb32 = hd.nmb, vpmb32 = hd.vpmb, vpb = vpmb32 * nmb32, need = hd.need;
-  const uint32_t wmax = ES == 4 ? 32u : 64u;
-  const uint32_t nblocks = (need + vpb - 1) / vpb, bpt = DELTA_TILE / vpb;
-  uint32_t* tstart = dt.tstart + pw.ltile0;
-  uint32_t cur = hd.q, b = 0, H = 0, slow = 0;
-  bool ok_page = true;
-  if (tid == 0) ts_s[WG] = cur;
-#pragma unroll 1
-  while (b < nblocks) {
-    const uint32_t j = tid;
-    const bool act = b + j < nblocks;
-    const uint64_t P64 = (uint64_t)cur + (uint64_t)j * H;
-    const uint32_t P = P64 > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)P64;
-    bool good = false;
-    uint32_t h = 0;
-    if (act && P < slen) {
-      const uint64_t lo8 = gload_u64(blob, blob_len, S + P), hi8 = gload_u64(blob, blob_len, S + P + 8);
-      const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
-      if (t8) {
-        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
-        const uint32_t sh = vl * 8u;
-        const uint64_t wv = sh < 64 ? ((lo8 >> sh) | (hi8 << (64 - sh))) : hi8;
-        const uint32_t payload = P + vl + nmb32;
-        const uint32_t bb = b + j;
-        const uint32_t left = need - bb * vpb;
-        const uint32_t inblk = left < vpb ? left : vpb;
-        const uint32_t mneed = (inblk + vpmb32 - 1) / vpmb32;
-        uint64_t boff = 0;
-        bool chk = (uint64_t)P + vl + nmb32 <= slen;
-#pragma unroll
-        for (uint32_t m = 0; m < 8; ++m) {
-          const uint32_t wdt = m < nmb32 ? (uint32_t)((wv >> (8 * m)) & 0xFFu) : 0u;
-          if (m < nmb32 && m < mneed && (wdt > wmax || (uint64_t)payload + boff + (vpmb32 * wdt) / 8 > slen)) chk = false;
-          boff += m < nmb32 ? (vpmb32 * wdt) / 8 : 0u;
-        }
-        const uint64_t hh = (uint64_t)vl + nmb32 + boff;
-        good = chk && hh < 0x0FFFFFFFull;
-        h = good ? (uint32_t)hh : 0u;
-      }
-    }
-    // workgroup exclusive scan of the lengths: the chain's offsets if every guess before is right
-    const uint32_t incl = wave_scan_incl_u32(h);
-    if (lane == 63) wtot[wid] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < WG / 64; ++w) {
-      before += w < wid ? wtot[w] : 0u;
-      total += wtot[w];
-    }
-    const uint64_t Q64 = (uint64_t)cur + before + incl - h;
-    const bool mism = act && Q64 != (uint64_t)P;
-    // first mismatching thread, and the first thread that cannot be taken (in thread order)
-    const uint64_t mm = __ballot(mism), bm = __ballot(act && !good);
-    if (lane == 0) {
-      wfirst[wid] = mm ? wid * 64u + (uint32_t)__builtin_ctzll(mm) : 0xFFFFFFFFu;
-      wbad[wid] = bm ? wid * 64u + (uint32_t)__builtin_ctzll(bm) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    uint32_t m = 0xFFFFFFFFu, f = 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t w = 0; w < WG / 64; ++w) {
-      m = min(m, wfirst[w]);
-      f = min(f, wbad[w]);
-    }
-    const uint32_t nact = min((uint32_t)WG, nblocks - b);
-    if (m > nact) m = nact;  // lanes [0, m) exact
-    if (f < m) {  // an exact block the page pass would refuse: k_delta_page takes the page
-      ok_page = false;
-      break;
-    }
-    // tile starts among the exact blocks; every block header of a tile must lie within the
-    // stage k_delta_lb loads from the tile's start (wider tiles stay with the page pass)
-    if (j < m && (b + j) % bpt == 0) {
-      tstart[(b + j) / bpt] = P;
-      ts_s[j] = P;
-    }
-    __syncthreads();
-    bool fits = true;
-    if (j < m) {
-      const uint32_t r = (b + j) % bpt;  // the block's place in its tile
-      const uint32_t ts = j >= r ? ts_s[j - r] : ts_s[WG];  // (ts_s[WG]: the last tile start of earlier rounds)
-      fits = (uint64_t)P - ts + 24u <= (uint64_t)DlbShape::STAGE;
-    }
-    if (__syncthreads_or(!fits)) {
-      ok_page = false;
-      break;
-    }
-    if (j == 0) {  // the tile start the next round's first blocks belong to
-      uint32_t last = ts_s[WG];
-      for (uint32_t k = 0; k < m; ++k)
-        if ((b + k) % bpt == 0) last = ts_s[k];
-      ts_s[WG] = last;
-    }
-    // next round: after the exact prefix (block b + m's offset is the scan at thread m)
-    uint32_t nc;
-    if (m >= nact) {
-      const uint64_t e = (uint64_t)cur + total;
-      nc = e > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)e;
-    } else {
-      __shared__ uint32_t nc_s;
-      if (j == m) nc_s = (uint32_t)(Q64 > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : Q64);
-      __syncthreads();
-      nc = nc_s;
-    }
-    H = m ? (nc - cur) / m : H;
-    cur = nc;
-    b += m;
-    if (m < 32u && b < nblocks && ++slow > 4u) {  // irregular block lengths: the page pass walks them
-      ok_page = false;
-      break;
-    }
-    __syncthreads();  // (wtot / wfirst are rewritten by the next round)
-  }
-  if (tid == 0) {
-    if (ok_page) {
-      info.first = hd.first;
-      info.vpmb = vpmb32;
-      info.nmb = nmb32;
-      info.tiled = DP_LB;
-      info.pad = H;  // the average block length: k_delta_lb's header scan guess
-    }
-    dt.page[p] = info;
-  }
-}
-
-// Tile t's sum granules (lo, hi), read once: the kind (1 aggregate, 2 inclusive) when both carry
-// this call's tag with the same kind, else 0 (not yet published, or half rewritten).
-__device__ inline uint32_t dlb_peek(const DeltaTables& dt, uint32_t t, uint32_t epoch, uint64_t& v) {
-  dlb_gu64* g = (dlb_gu64*)(dt.lb + 2ull * t);
-  const uint64_t lo = __hip_atomic_load(g, DLB_RLX), hi = __hip_atomic_load(g + 1, DLB_RLX);
-  const uint32_t tl = (uint32_t)(lo >> 32), th = (uint32_t)(hi >> 32);
-  if (tl == th && (tl >> 2) == epoch && (tl & 3u)) {
-    v = (lo & 0xFFFFFFFFull) | (hi << 32);
-    return tl & 3u;
-  }
-  return 0u;
-}
-
-__device__ inline void dlb_write(const DeltaTables& dt, uint32_t t, uint32_t epoch, uint32_t kind, uint64_t v) {
-  dlb_gu64* g = (dlb_gu64*)(dt.lb + 2ull * t);
-  const uint64_t tag = (uint64_t)((epoch << 2) | kind) << 32;
-  __hip_atomic_store(g, tag | (v & 0xFFFFFFFFull), DLB_RLX);
-  __hip_atomic_store(g + 1, tag | (v >> 32), DLB_RLX);
-}
-
-template <int ES>
-__global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(DLB_NT) k_delta_lb(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     PageWork* pages, const ChunkWork* chunks,
-                                                     const uint32_t* __restrict__ tile_page, uint32_t ntiles,
-                                                     DeltaTables dt) {
-  using SH = DlbShape;
-  constexpr uint32_t TT = SH::T;
-  constexpr int STG = SH::STAGE;
-  __shared__ DeltaPageSmem<DLB_NT> sm;
-  __shared__ uint64_t carry_s;
-  __shared__ uint32_t fail_s, tk_s;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t epoch = dt.epoch;
-  uint32_t xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  xcc &= 7u;
-#pragma unroll 1
-  for (;;) {
-    // the next tile: tile k * 8 + c is the k-th ticket of counter c; a workgroup draws from its own
-    // XCD's counter, then (that one drained) from the others. Each counter hands out its tiles in
-    // order, so the lowest unfinished tile is always handed out or held by a running workgroup
-    // whose look-back finds its predecessors finished: the waits end.
-    if (tid == 0) {
-      uint32_t tt = 0xFFFFFFFFu;
-      for (uint32_t r = 0; r < 8u && tt == 0xFFFFFFFFu; ++r) {
-        const uint32_t c = (xcc + r) & 7u;
-        if (__hip_atomic_load((dlb_gu32*)&dt.ticket[c], DLB_RLX) * 8ull + c >= ntiles) continue;
-        const uint32_t k = __hip_atomic_fetch_add((dlb_gu32*)&dt.ticket[c], 1u, DLB_RLX);
-        if ((uint64_t)k * 8u + c < ntiles) tt = k * 8u + c;
-      }
-      tk_s = tt;
-    }
-    __syncthreads();
-    const uint32_t t = tk_s;
-    __syncthreads();  // (tk_s is rewritten for the next tile)
-    if (t == 0xFFFFFFFFu) break;
-    const uint32_t p = tile_page[t];
-    const PageWork& pw = pages[p];
-    if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) continue;
-    if (pw.encoding != E_DELTA_BINARY_PACKED || chunks[pw.chunk].es != ES) continue;
-    const DeltaPage dp = dt.page[p];
-    if (dp.tiled != DP_LB) continue;
-    const uint32_t i = t - pw.ltile0;
-    const uint32_t need = (uint32_t)pw.nonnull - 1u, D0 = i * TT;
-    if (D0 >= need) continue;
-    const uint32_t D1 = D0 + TT < need ? D0 + TT : need;
-    const uint32_t vpb = dp.vpmb * dp.nmb, nb = (D1 - D0 + vpb - 1) / vpb;
-    const uint64_t S = pw.base + pw.val_off;
-    const uint32_t slen = pw.val_bytes;
-    const uint32_t hdr = dt.tstart[t];
-    const uint64_t SB = (S + hdr) & ~15ull;
-    const uint32_t sb = (uint32_t)(SB - S);
-    {
-      const bool fast = SB + STG <= blob_len;
-#pragma unroll
-      for (int c = 0; c < SH::CH; ++c) {
-        const uint64_t a = SB + (uint32_t)(tid + c * DLB_NT) * 16u;
-        sm.stq[tid + c * DLB_NT] = fast ? *reinterpret_cast<const uint4*>(blob + a) : gload_u128_tail(blob, blob_len, a);
-      }
-      if (tid < 16) sm.stage[STG / 4 + tid] = 0;
-    }
-    __syncthreads();
-    if (tid < 64) {
-      bool fb, shortwin;
-      uint32_t hp;
-      // (k_delta_hdr checked these headers; the block length guess from the page's average)
-      dpg_headers<DLB_NT, ES>(sm, hdr, dp.pad, sb, STG, slen, nb, D0 / vpb, need, dp.nmb, dp.vpmb, fb, shortwin, hp);
-      if (tid == 0) fail_s = fb ? 1u : 0u;
-    }
-    __syncthreads();
-    const bool failed = fail_s != 0;  // (k_delta_hdr checked these headers: never, short of a bug)
-    uint64_t x[DPT];
-    uint64_t sx = 0;
-    if (!failed) {
-      sx = dpg_unpack<DLB_NT>(sm, blob, blob_len, S, sb, STG, D0, D1, dp.nmb, dp.vpmb, x);
-    } else {
-#pragma unroll
-      for (int j2 = 0; j2 < DPT; ++j2) x[j2] = 0;
-    }
-    uint64_t acc;
-    const uint64_t T = dpg_scan<DLB_NT>(sm, sx, 0ull, acc);  // acc: within the tile
-    // ---- publish the tile's sum, look back for the running value before it
-    if (tid < 64) {
-      uint64_t carry = dp.first;
-      bool bad = failed;
-      if (i > 0) {
-        if (lane == 0) dlb_write(dt, t, epoch, 1u, T);
-        // the tile before (j): one lane polls its granules until published (polls are kept to one
-        // word pair per waiting workgroup: many pollers cut the chip's bandwidth); an aggregate
-        // sends the wave over the 63 tiles before it in one pass, up to the nearest inclusive
-        // value, or up to the nearest tile not yet published, which is polled next
-        uint64_t sum = 0;
-        uint32_t j = t - 1;
-#pragma unroll 1
-        while (true) {
-          uint64_t v0 = 0;
-          uint32_t k0 = 0;
-          if (lane == 0) {
-            for (uint32_t spins = 0; spins < (1u << 20); ++spins) {
-              if ((k0 = dlb_peek(dt, j, epoch, v0)) != 0u) break;
-              __builtin_amdgcn_s_sleep(8);
-            }
-          }
-          k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
-          v0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32) |
-               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0);
-          if (k0 == 0u) {  // bounded: a look-back that never ends reports the page
-            bad = true;
-            break;
-          }
-          sum += v0;
-          if (k0 == 2u) break;
-          const bool in = lane >= 1u && lane <= j - pw.ltile0;
-          uint64_t v = 0;
-          const uint32_t k = in ? dlb_peek(dt, j - lane, epoch, v) : 0u;
-          const uint64_t notr = __ballot(in && k == 0u), incm = __ballot(in && k == 2u);
-          const uint32_t f = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;  // nearest inclusive
-          const uint32_t r = notr ? (uint32_t)__builtin_ctzll(notr) : 64u;  // nearest unpublished
-          const uint32_t upto = f < r ? f : r - 1u;  // lanes [1, upto] are summed
-          uint64_t add = (in && lane <= upto) ? v : 0ull;
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, 64);
-          sum += add;
-          if (f < r) break;
-          if (r == 64u && __ballot(in) != (~0ull << 1)) {  // (the page's tile 0 is inclusive: never)
-            bad = true;
-            break;
-          }
-          j -= r;  // the nearest unpublished tile (or, all 63 aggregates, the one past them)
-        }
-        carry = sum;
-      }
-      if (lane == 0) {
-        dlb_write(dt, t, epoch, 2u, carry + T);
-        carry_s = carry;
-        fail_s = bad ? 1u : 0u;
-      }
-    }
-    __syncthreads();
-    if (fail_s) {
-      if (tid == 0) report(pages, const_cast<ChunkWork*>(chunks), (int)p, ST_GENERAL);
-      __syncthreads();
-      continue;
-    }
-    const uint64_t carry = carry_s;
-    const gptr<uint8_t> ob = gp(chunks[pw.chunk].val_out) + pw.value_out * (uint64_t)ES;
-    if (i == 0 && tid == 0) {  // value 0
-      if (ES == 8) *reinterpret_cast<gptr<uint64_t>>(ob) = dp.first;
-      else *reinterpret_cast<gptr<uint32_t>>(ob) = (uint32_t)dp.first;
-    }
-    uint64_t val[DPT];
-    acc += carry;
-#pragma unroll
-    for (int j2 = 0; j2 < DPT; ++j2) {
-      acc += x[j2];
-      val[j2] = acc;
-    }
-    dpg_store<ES, DLB_NT>(sm, val, ob + (uint64_t)(D0 + 1) * ES, D1 - D0);
-  }
-}
-
 // Per-page fallback for pages the tiled path does not take (k_delta with a page filter).
 template <int ES>
 __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -1366,14 +1012,8 @@ __global__ void __launch_bounds__(WG) k_delta_rest(const uint8_t* __restrict__ b
 // at once when it left none (dt.nfall), then the per-page stream decoder for what those refuse.
 template <int ES>
 static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
-                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, hipStream_t s, hipEvent_t* kev,
-                        uint32_t lb_grid) {
+                        uint32_t ntiles, const uint32_t* tile_page, DeltaTables dt, hipStream_t s, hipEvent_t* kev) {
   if (kev) (void)hipEventRecord(kev[0], s);
-  if (lb_grid) {
-    hipLaunchKernelGGL(k_delta_hdr<ES>, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, dt);
-    hipLaunchKernelGGL(k_delta_lb<ES>, dim3(lb_grid), dim3(DLB_NT), 0, s, blob, blob_len, pages, chunks, tile_page,
-                       ntiles, dt);
-  }
   hipLaunchKernelGGL((k_delta_page<ES, DPG_NT>), dim3(npages), dim3(DPG_NT), 0, s, blob, blob_len, pages, chunks, dt);
   if (kev) (void)hipEventRecord(kev[1], s);
   hipLaunchKernelGGL(k_delta_index<ES>, dim3(npages), dim3(64), 0, s, blob, blob_len, pages, chunks, dt);
@@ -1387,37 +1027,11 @@ static void delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages,
 }
 
 // es_mask: bit mask of the DELTA_BINARY_PACKED chunks' value sizes (4: INT32, 8: INT64).
-// Workgroups of k_delta_lb<ES> that fit the device at once (it walks the tiles by tickets: the
-// grid is for occupancy, not for correctness).
-template <int ES>
-static uint32_t delta_lb_grid(uint32_t ntiles) {
-#ifndef PQG_DELTA_LB
-#define PQG_DELTA_LB 1
-#endif
-  if (!PQG_DELTA_LB || ntiles == 0) return 0;
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  int g = dev >= 0 && dev < 64 ? cached[dev] : 0;
-  if (!g) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_delta_lb<ES>, DLB_NT, 0) != hipSuccess || per <= 0) per = 4;
-    g = cus * per;
-    if (dev >= 0 && dev < 64) cached[dev] = g;
-  }
-  return (uint32_t)g < ntiles ? (uint32_t)g : ntiles;
-}
-
-// es_mask: bit mask of the DELTA_BINARY_PACKED chunks' value sizes (4: INT32, 8: INT64).
 extern "C" hipError_t pqg_launch_delta_tiled(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages,
                                              ChunkWork* chunks, uint32_t ntiles, const uint32_t* tile_page,
                                              DeltaTables dt, uint32_t es_mask, hipStream_t s, hipEvent_t* kev) {
-  if (es_mask & 8u)
-    delta_tiled<8>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, kev, delta_lb_grid<8>(ntiles));
-  if (es_mask & 4u)
-    delta_tiled<4>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, (es_mask & 8u) ? nullptr : kev,
-                   delta_lb_grid<4>(ntiles));
+  if (es_mask & 8u) delta_tiled<8>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, kev);
+  if (es_mask & 4u) delta_tiled<4>(blob, blob_len, pages, npages, chunks, ntiles, tile_page, dt, s, (es_mask & 8u) ? nullptr : kev);
   return hipGetLastError();
 }
 

@@ -2178,7 +2178,24 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   LvPf pf;
   pf.ok = false;
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 256): per wave s_memtime cycles in the window's staging wait,
+  // run placement and output writes, and the windows written
+  const bool stamps = (chunks[0].cp.debug & 256) && chunks[0].cp.dbgbuf;
+  uint64_t ts0 = 0, tacc[3] = {0, 0, 0}, tn = 0;
+#define LE_STAMP(k)                                   \
+  if (stamps) {                                       \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+    tacc[k] += t1 - ts0;                              \
+    ts0 = t1;                                         \
+  }
+#else
+#define LE_STAMP(k)
+#endif
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
+#ifdef PQG_DIAG
+    if (stamps) ts0 = __builtin_amdgcn_s_memtime();
+#endif
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
     const uint2 wi = pf.ok && pf.p == x.p && pf.k == x.k ? pf.wi : lt.win[D.wb + x.k];
     if (wi.x == LV_NONE) {  // no true header in this window
@@ -2198,6 +2215,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     const uint32_t refm = viaref ? (uint32_t)lt.bmp[(uint64_t)(D.wb + x.k) * WAVE + lane] : 0u;
     pf.stage(blob, blob_len, x, W.stage);
     if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1, lt.win + D.wb);
+#ifdef PQG_DIAG
+    if (stamps && viaref) asm volatile("" ::"v"(refm));  // (the bitmap's load has landed)
+#endif
+    LE_STAMP(0)
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
@@ -2362,10 +2383,26 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (endo <= base || R == 0) continue;
+    LE_STAMP(1)
     lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
                   D.maxl, pages, gp(D.out));
     wave_lds_sync();  // the run list and stage are refilled by the next window
+    LE_STAMP(2)
+#ifdef PQG_DIAG
+    ++tn;
+#endif
   }
+#ifdef PQG_DIAG
+  if (stamps && lane == 0) {
+    const uint32_t gw = blockIdx.x * (WG / WAVE) + wid;
+    uint64_t* d = chunks[0].cp.dbgbuf + 4ull * gw;
+    d[0] = tacc[0];
+    d[1] = tacc[1];
+    d[2] = tacc[2];
+    d[3] = tn;
+  }
+#endif
+#undef LE_STAMP
 }
 
 // ------------------------------------------------------------------------------ k_lv_emit_walk
@@ -2650,7 +2687,11 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
     return hipGetLastError();
   }
   // (k_lv_plan2's scan ran in k_lv_segscan's last workgroup)
-  hipLaunchKernelGGL(k_lv_win, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+#ifndef PQG_LW_GRIDX
+#define PQG_LW_GRIDX 1
+#endif
+  hipLaunchKernelGGL(k_lv_win, dim3(wgrid * PQG_LW_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt,
+                     lt);
   // window tables of 64 / 128 entry offsets (bit width 1 / 2) take the readlane walks
   if (widths & 2u)
     hipLaunchKernelGGL(k_lv_stitch<1>, dim3(npages), dim3(SC_WG), 0, s, blob, pages, npages, chunks, sel, rt, lt);

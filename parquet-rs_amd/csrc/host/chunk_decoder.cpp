@@ -112,7 +112,6 @@ struct Slot {
   size_t pfcap = 0;      // pages the rt[].pflag arrays hold
   DeltaTables dt = {};   // DELTA_BINARY_PACKED tiled path
   size_t dt_tcap = 0, dt_pcap = 0;
-  uint32_t dt_epoch = 0;  // look-back tag of the last decode (DeltaTables::epoch)
   // level path (pqg_levels.hip): buffers of LevelTables per stream kind, grown on demand
   static constexpr int LV_BUFS = 14;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr, bmp
   void* lvbuf[K_N][LV_BUFS] = {};
@@ -332,9 +331,6 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dt.inc);
     hipFree(sl.dt.flag);
     hipFree(sl.dt.nfall);
-    hipFree(sl.dt.tstart);
-    hipFree(sl.dt.lb);
-    hipFree(sl.dt.ticket);
     for (int k = 0; k < K_N; ++k) {
       for (void* b : sl.lvbuf[k]) hipFree(b);
     }
@@ -685,10 +681,11 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     p0 += n;
   }
 #ifdef PQG_DIAG
-  if (dbg_env & (16 | 32 | 64 | 128)) {
+  if (dbg_env & (16 | 32 | 64 | 128 | 256)) {
     size_t need = (size_t)(total_tiles * 4 > (uint64_t)np * 2 ? total_tiles * 4 : (uint64_t)np * 2) * 16;
     if (need < (size_t)np * 64) need = (size_t)np * 64;
     if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + np + 1) * 32;  // per level-stream segment
+    if (dbg_env & 256) need = (size_t)2048 * 64 * 4 * 32;                 // per wave of k_lv_emit (grids <= 64 x)
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
@@ -840,9 +837,6 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       hipFree(sl.dt.inc);
       hipFree(sl.dt.flag);
       hipFree(sl.dt.nfall);
-      hipFree(sl.dt.tstart);
-      hipFree(sl.dt.lb);
-      hipFree(sl.dt.ticket);
       sl.dt = DeltaTables{};
       sl.dt_tcap = sl.dt_pcap = 0;
       const size_t tc = sl.tcap, pc = (size_t)np < 1024 ? 1024 : np;
@@ -852,22 +846,13 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       HIPCHK(hipMalloc(&sl.dt.inc, tc * sizeof(uint64_t)), "hipMalloc delta inc");
       HIPCHK(hipMalloc(&sl.dt.flag, tc * sizeof(uint32_t)), "hipMalloc delta flags");
       HIPCHK(hipMalloc(&sl.dt.nfall, sizeof(uint32_t)), "hipMalloc delta fallback count");
-      HIPCHK(hipMalloc(&sl.dt.tstart, tc * sizeof(uint32_t)), "hipMalloc delta tile starts");
-      HIPCHK(hipMalloc(&sl.dt.lb, tc * 2 * sizeof(uint64_t)), "hipMalloc delta look-back granules");
-      HIPCHK(hipMalloc(&sl.dt.ticket, 8 * sizeof(uint32_t)), "hipMalloc delta tickets");
-      // granule tags must never match a later decode's epoch by accident: zeroed once here
-      HIPCHK(hipMemsetAsync(sl.dt.lb, 0, tc * 2 * sizeof(uint64_t), s), "memset delta granules");
       sl.dt_tcap = tc;
       sl.dt_pcap = pc;
     }
     ini.word[nw_] = sl.dt.nfall;
     ini.val[nw_++] = 0u;
     sl.dt.dbg = (dbg_env & 32) ? ctx->dbgbuf : nullptr;
-    if (++sl.dt_epoch >= (1u << 30)) {  // (tags of 2^30 decodes ago: zero the granules again)
-      HIPCHK(hipMemsetAsync(sl.dt.lb, 0, sl.dt_tcap * 2 * sizeof(uint64_t), s), "memset delta granules");
-      sl.dt_epoch = 1;
-    }
-    sl.dt.epoch = sl.dt_epoch;
+
   }
   ini.dense_def = need_lv[K_DEF] ? sl.lt(K_DEF, 0).dense : nullptr;
   ini.dense_rep = need_lv[K_REP] ? sl.lt(K_REP, 0).dense : nullptr;

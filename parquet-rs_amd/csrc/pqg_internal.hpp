@@ -165,10 +165,6 @@ struct DeltaTables {
   uint32_t* flag;     // [tiles] epoch * 4 + {1 aggregate, 2 inclusive}
   uint64_t* dbg;      // diagnostics: per-page phase cycles of k_delta_page (PQG_DEBUG bit 5)
   uint32_t* nfall;    // pages k_delta_page left to the tiled path (0: its tile kernels exit at once)
-  uint32_t* tstart;   // [tiles] stream offset of the tile's first block header (k_delta_hdr)
-  uint64_t* lb;       // [2 * tiles] look-back granules {tag, 32-bit half} of the tile sums (k_delta_lb)
-  uint32_t* ticket;   // [8] k_delta_lb's per-XCD tile counters (zeroed by k_delta_hdr)
-  uint32_t epoch;     // this decode's look-back tag (never 0; the granules are zeroed at allocation)
 };
 
 // Level-path tables (device/pqg_levels.hip), per stream kind (def, rep, RLE booleans).
