@@ -588,12 +588,20 @@ struct DpgShape {
   static_assert(CH * 16 * NT == STAGE, "whole loads");
 };
 
+// The stage doubles as the store transpose buffer; with PQG_DPG_OBUF it holds a whole tile of
+// 8-byte values (one store round: every wave's values at once; the per-page grid leaves LDS to
+// spare), else as many waves' values as the stream stage holds (measured on config 4: one store
+// round 2.48 ms per step, the stage-sized rounds 2.38 ms -- off by default).
+#ifndef PQG_DPG_OBUF
+#define PQG_DPG_OBUF 0
+#endif
 template <int NT>
 struct DeltaPageSmem {
   using S = DpgShape<NT>;
+  static constexpr int OB = PQG_DPG_OBUF && (int)S::T * 8 > S::STAGE ? (int)S::T * 8 : S::STAGE;
   union {
     uint32_t stage[(S::STAGE + 64) / 4];
-    uint4 stq[(S::STAGE + 64) / 16];
+    uint4 stq[(OB + 64) / 16];
   };
   uint64_t mind[S::NB];
   uint32_t pos[S::NB];
@@ -801,7 +809,7 @@ __device__ inline void dpg_store(DeltaPageSmem<NT>& sm, const uint64_t (&val)[DP
   const int tid = threadIdx.x;
   constexpr uint32_t CPT = DPT * ES / 16;                   // 16-byte chunks per thread
   constexpr uint32_t WB = 64u * DPT * ES;                   // bytes of one wave's values
-  constexpr uint32_t WPR0 = (uint32_t)SH::STAGE / WB;       // waves whose values fit the stage
+  constexpr uint32_t WPR0 = (uint32_t)DeltaPageSmem<NT>::OB / WB;  // waves whose values fit the buffer
   constexpr uint32_t WPR = WPR0 >= 8 ? 8 : WPR0 >= 4 ? 4 : WPR0 >= 2 ? 2 : 1;
   constexpr uint32_t NR = (uint32_t)SH::NW / (WPR < (uint32_t)SH::NW ? WPR : (uint32_t)SH::NW);  // rounds
   constexpr uint32_t WR = (uint32_t)SH::NW / NR;            // waves per round
@@ -825,7 +833,7 @@ __device__ inline void dpg_store(DeltaPageSmem<NT>& sm, const uint64_t (&val)[DP
       }
     }
     __syncthreads();
-#pragma unroll
+#pragma unroll 2
     for (uint32_t r = 0; r < (NCH + NT - 1) / NT; ++r) {
       const uint32_t ci = (uint32_t)tid + r * NT;
       if (ci < NCH) {

@@ -52,6 +52,33 @@ __global__ __launch_bounds__(256) void k_gather_lds(const uint64_t* __restrict__
   }
 }
 
+// Partially LDS-resident dictionary: entries [0, S) in LDS (up to 19456 x 8 B = 152 KiB, one
+// workgroup of NT threads per CU), the rest gathered from global memory (L2); persistent over
+// tiles of NT * 2 * NG outputs.
+template <int NG, int NT>
+__global__ __launch_bounds__(NT) void k_gather_slab(const uint64_t* __restrict__ dict, uint32_t dmask, uint32_t S,
+                                                    uint64_t* __restrict__ out, uint64_t n) {
+  __shared__ uint64_t sd[19456];
+  for (uint32_t i = threadIdx.x; i < S; i += NT) sd[i] = dict[i];
+  __syncthreads();
+  const uint64_t per = (uint64_t)NT * 2 * NG;
+  for (uint64_t base = (uint64_t)blockIdx.x * per; base < n; base += (uint64_t)gridDim.x * per) {
+    uint64_t x[NG][2];
+#pragma unroll
+    for (int s = 0; s < NG; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint64_t o = base + (uint64_t)s * NT * 2 + threadIdx.x * 2 + j;
+        const uint32_t idx = hsh((uint32_t)o) & dmask;
+        x[s][j] = idx < S ? sd[idx] : dict[idx];
+      }
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      uint64_t o = base + (uint64_t)s * NT * 2 + threadIdx.x * 2;
+      if (o < n) *reinterpret_cast<uint4*>(out + o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32), (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
+    }
+  }
+}
 
 // load flavours for the L2-served gather: 0 plain, 1 nontemporal, 2 agent-scope relaxed atomic (sc1)
 template <int NG, int MODE>
@@ -117,6 +144,16 @@ int main() {
   run("gather D=65536 NG=4", [&] { k_gather<4><<<tiles8 * 2, 256>>>(dict, 65535, out, n); });
   run("gather D=65536 NG=16", [&] { k_gather<16><<<tiles8 / 2 + 1, 256>>>(dict, 65535, out, n); });
   run("gather D=65536 nt", [&] { k_gather_m<8, 1><<<tiles8, 256>>>(dict, 65535, out, n); });
+  int cus = 256;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  for (uint32_t S : {0u, 8192u, 16384u, 19456u}) {
+    char nm[64];
+    snprintf(nm, 64, "slab S=%u NT=1024 NG=4", S);
+    run(nm, [&] { k_gather_slab<4, 1024><<<cus, 1024>>>(dict, 65535, S, out, n); });
+    snprintf(nm, 64, "slab S=%u NT=512 NG=8", S);
+    run(nm, [&] { k_gather_slab<8, 512><<<cus, 512>>>(dict, 65535, S, out, n); });
+  }
+  run("slab S=4096 D=4096 (all LDS)", [&] { k_gather_slab<4, 1024><<<cus, 1024>>>(dict, 4095, 4096, out, n); });
   run("gather D=65536 sc1", [&] { k_gather_m<8, 2><<<tiles8, 256>>>(dict, 65535, out, n); });
   run("gather4 D=65536 (1e9 x 4B)", [&] { k_gather4<4><<<tiles8, 256>>>((const uint32_t*)dict, 65535, (uint32_t*)out, n); });
   run("gather4 D=131072 (1e9 x 4B)", [&] { k_gather4<4><<<tiles8, 256>>>((const uint32_t*)dict, 131071, (uint32_t*)out, n); });
