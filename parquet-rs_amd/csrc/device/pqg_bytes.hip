@@ -182,9 +182,16 @@ __global__ void __launch_bounds__(WG) k_ba_dict_prep(const uint8_t* __restrict__
   uint64_t* dsrc = dsrc0 + ck.dscr_base;
   uint32_t* dlen = dlen0 + ck.dscr_base;
   const PageWork dp = pages[dict_page];
-  if (dp.status != 0) return;
   const uint64_t n = dp.num_values;
   const uint64_t S = dp.base;
+  if (dp.status != 0) {  // (failed before: every entry empty, as below -- the scratch is not cleared
+                         // between decodes, and the data pages' kernels still read it)
+    for (uint64_t i = threadIdx.x; i < n; i += WG) {
+      dsrc[i] = S;
+      dlen[i] = 0;
+    }
+    return;
+  }
   int32_t st = 0;
   if (type_length > 0) {  // FLBA
     if (n * (uint64_t)type_length > dp.nbytes) st = ST_EOF;

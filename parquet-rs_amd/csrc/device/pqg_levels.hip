@@ -1711,6 +1711,110 @@ __device__ inline uint32_t lv_write1(const LvRuns& rl, const uint32_t* stage, co
   return cnt;
 }
 
+// Bit width 1, a dense window whose true headers are known per segment (lane l: the mask mym of
+// positions [16 l, 16 l + 16), its first output oa): the lane parses its own headers once and ORs
+// their bits into a bitmap of the window's outputs in LDS (the jump table's space: 32-output
+// words aligned on the global output index; a word two lanes share is merged by the OR), then
+// the wave stores the bitmap expanded, one contiguous KiB per store instruction. The run list
+// (lv_write1: a binary search and a walk over the runs per word) is not built at all. Taken when
+// the words fit and no lane generates more than LV_BM_SPAN outputs (a long RLE run: word by
+// word on one lane); returns false, nothing stored, at a run the window path does not take.
+constexpr uint32_t LV_BM_WORDS = LV_WIN * 2;  // bitmap words (the jump table's 8 KiB)
+constexpr uint32_t LV_BM_SPAN = 2048;         // outputs one lane generates at most
+#ifndef PQG_LV_BM
+#define PQG_LV_BM 1  // (0: every dense window through the run list, for A/B runs)
+#endif
+
+__device__ inline bool lv_bm_fits(const LvWin& x, uint32_t base, uint64_t endo, uint64_t span) {
+  if (!PQG_LV_BM) return false;
+  const uint64_t lo = x.s.out + base, hi = x.s.out + endo;
+  return !__ballot(span > LV_BM_SPAN) && ((hi - (lo & ~31ull) + 31u) >> 5) <= LV_BM_WORDS;
+}
+
+template <int OUT>
+__device__ inline bool lv_bitmap1(LvWave& W, const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x,
+                                  uint32_t mym, uint64_t oa, uint32_t base, uint32_t endo, uint32_t n, int sel,
+                                  PageWork* pages, gptr<uint8_t> __restrict__ out) {
+  constexpr uint32_t V = 16u / OUT;  // outputs per 16-byte chunk
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t slen = x.s.slen, i0 = lane * LV_SEG;
+  const uint64_t go = x.s.out, lo = go + base, hi = go + endo;
+  const uint64_t A0 = lo & ~31ull;
+  const uint32_t nw = (uint32_t)((hi - A0 + 31u) >> 5);
+  uint32_t* bm = reinterpret_cast<uint32_t*>(W.JC);
+  wave_lds_sync();  // (the jump table / prefix list is read)
+  for (uint32_t i = lane; i < nw; i += WAVE) bm[i] = 0u;
+  wave_lds_sync();
+  bool bad = false;
+  uint32_t cw = 0xFFFFFFFFu, cb = 0, cnt = 0;
+#pragma unroll 1
+  for (uint32_t m = mym; m; m &= m - 1u) {
+    const uint32_t t = (uint32_t)__builtin_ctz(m);
+    uint32_t nx, c, v;
+    bool bp;
+    lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, 1u, 1u, nx, c, v, bp);  // (a true header: parses)
+    bad |= !lv_run_ok(bp, v, c, oa, n, slen, 1u);
+    const uint64_t e = oa + c < endo ? oa + c : (uint64_t)endo;
+#pragma unroll 1
+    for (uint64_t q = oa; q < e;) {
+      const uint64_t g = go + q;
+      const uint32_t wi = (uint32_t)((g - A0) >> 5), bpos = (uint32_t)g & 31u;
+      const uint32_t take = e - q < 32u - bpos ? (uint32_t)(e - q) : 32u - bpos;
+      const uint32_t mk = take >= 32u ? 0xFFFFFFFFu : (1u << take) - 1u;
+      uint32_t bits;
+      if (bp) {
+        const uint64_t bit = (uint64_t)v * 8ull + (q - oa);
+        bits = (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & mk;
+      } else {
+        bits = (v & 1u) ? mk : 0u;
+      }
+      if (wi != cw) {
+        if (cb) atomicOr(&bm[cw], cb);
+        cnt += (uint32_t)__builtin_popcount(cb);
+        cw = wi;
+        cb = 0;
+      }
+      cb |= bits << bpos;
+      q += take;
+    }
+    oa += c;
+  }
+  if (cb) atomicOr(&bm[cw], cb);
+  cnt += (uint32_t)__builtin_popcount(cb);
+  if (__ballot(bad)) return false;
+  wave_lds_sync();
+  // chunks [c0, c1) lie inside [lo, hi); chunk ka (holding lo) and kb (holding hi - 1) may not
+  const uint32_t ra = (uint32_t)(lo - A0), rb = (uint32_t)(hi - A0);
+  const uint32_t c0 = (ra + V - 1u) / V, c1 = rb / V, ka = ra / V, kb = (rb - 1u) / V;
+#pragma unroll 2
+  for (uint32_t k = c0 + lane; k < c1; k += WAVE) {
+    const uint32_t cbits = (bm[k * V / 32u] >> ((k * V) & 31u)) & (V == 32u ? 0xFFFFFFFFu : (1u << V) - 1u);
+    uint32_t d[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t)
+      d[t] = OUT == 2 ? (((cbits >> (2u * t)) & 3u) * 0x8001u) & 0x10001u
+                      : (((cbits >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
+    gst16(out + (A0 + (uint64_t)k * V) * OUT, make_uint4(d[0], d[1], d[2], d[3]));
+  }
+  const bool ea = lane == 0 && c0 > ka, eb = lane == 1 && c1 <= kb && !(kb == ka && c0 > ka);
+  if (ea || eb) {
+    const uint32_t kk = ea ? ka : kb;
+    for (uint32_t j = 0; j < V; ++j) {
+      const uint32_t r = kk * V + j;
+      if (r >= ra && r < rb) {
+        const uint32_t b = (bm[r >> 5] >> (r & 31u)) & 1u;
+        if (OUT == 2) reinterpret_cast<gptr<int16_t>>(out)[A0 + r] = (int16_t)b;
+        else out[A0 + r] = (uint8_t)b;
+      }
+    }
+  }
+  if (sel == SS_DEF) {
+    cnt = wave_sum_u32_(cnt);
+    if (lane == 0 && cnt) atomicAdd((unsigned long long*)&pages[x.p].nonnull, (unsigned long long)cnt);
+  }
+  return true;
+}
+
 // Wider levels: groups of G outputs (one 16-byte store), each from the runs covering it.
 // Returns this lane's count of outputs == maxl.
 template <int OUT>
@@ -2222,6 +2326,11 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     uint32_t R = 0;  // runs placed (wave-uniform)
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
+    // bit width 1: this segment's true headers and first output (window-relative); bm: written
+    // from those by lv_bitmap1, no run list placed (wave-uniform)
+    uint32_t mym = 0;
+    uint64_t myacc = 0;
+    bool bm = false;
     if (viaref) {
       constexpr uint32_t SEG = LV_SEG;
       const uint32_t me = nh, i0 = lane * SEG;
@@ -2240,7 +2349,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       }
       wave_lds_sync();
       const uint32_t np = pre[64];
-      uint32_t mym = i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0));
+      mym = i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0));
       for (uint32_t k = 0; k < np && np != 0xFFFFFFFFu; ++k) {
         const uint32_t qq = pre[k];
         if (qq >= i0 && qq < i0 + SEG) mym |= 1u << (qq - i0);
@@ -2258,8 +2367,11 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       const uint64_t si = wave_incl_scan_cnt64(so);
       const uint64_t tot = __shfl(si, 63, 64);
       bad = __ballot(np == 0xFFFFFFFFu) != 0;
+      myacc = si - so;
+      T = tot;
+      bm = !bad && lv_bm_fits(x, base, (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n, so);
       wave_lds_sync();  // (the prefix list is read)
-      if (!bad) {
+      if (!bad && !bm) {
         const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
         const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
         uint32_t k = rb;
@@ -2277,9 +2389,6 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
           oa += c;
         }
         R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
-        T = tot;
-      } else {  // (the entry's chain did not land on the meeting point: a table k_lv_win made wrong)
-        bad = true;
       }
     } else if (w != 1 && nh <= LV_SERIAL) {
       // sparse window: one lane follows the chain from the entry
@@ -2316,8 +2425,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       lv_seg_build(W, x, pc, pv, bpm);
       // the walk from the entry (wave-uniform): segment s's true headers and first output
       const uint64_t lim = (uint64_t)n - base;
-      uint32_t e = e0, mym = 0;
-      uint64_t acc = 0, myacc = 0;
+      uint32_t e = e0, mys = 0;
+      uint64_t acc = 0;
       {  // speculatively in parallel (lv_spec_chain): the segments the walk visits are the chain's
          // segments before the one whose outputs reach lim
         uint32_t q;
@@ -2329,6 +2438,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
           const bool vis = valid && P < lim;
           mym = vis ? r.x >> 16 : 0u;
           myacc = P;
+          mys = vis ? r.y : 0u;
           const uint64_t vsm = __ballot(vis);
           const int last = vsm ? 63 - __builtin_clzll(vsm) : 0;
           acc = vsm ? __shfl(inc, last, 64) : 0ull;
@@ -2344,6 +2454,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
         if (lane == sg) {
           mym = rx >> 16;
           myacc = acc;
+          mys = ry;
         }
         acc += ry;
         if (acc >= lim) break;
@@ -2351,42 +2462,52 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       }
       // a dead header, or the stream's end, before n outputs
       bad = acc < lim && (e == LV_J_DEAD || e == LV_J_END);
-      wave_lds_sync();  // the table's space now holds the run list
-      const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
-      const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
-      uint32_t k = rb;
-      uint64_t oa = (uint64_t)base + myacc;
-      // the segment's true headers parsed again from the stage (keeping the segment build's 32
-      // per-position registers live through the walk spilled them)
-      const uint32_t i0 = lane * SEG;
-#pragma unroll 1
-      for (uint32_t m = mym; m; m &= m - 1u) {
-        const uint32_t t = (uint32_t)__builtin_ctz(m);
-        uint32_t nx, c, v;
-        bool bp;
-        lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (a true header: parses)
-        W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
-        W.runs.rinfo[k] = bp ? v : (R_RLE | v);
-        bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
-        ++k;
-        oa += c;
-      }
-      R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
       T = acc;
+      bm = w == 1 && !__ballot(bad) && lv_bm_fits(x, base, (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n, mys);
+      wave_lds_sync();  // the table's space now holds the run list
+      if (!bm) {
+        const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
+        const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
+        uint32_t k = rb;
+        uint64_t oa = (uint64_t)base + myacc;
+        // the segment's true headers parsed again from the stage (keeping the segment build's 32
+        // per-position registers live through the walk spilled them)
+        const uint32_t i0 = lane * SEG;
+  #pragma unroll 1
+        for (uint32_t m = mym; m; m &= m - 1u) {
+          const uint32_t t = (uint32_t)__builtin_ctz(m);
+          uint32_t nx, c, v;
+          bool bp;
+          lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (a true header: parses)
+          W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
+          W.runs.rinfo[k] = bp ? v : (R_RLE | v);
+          bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
+          ++k;
+          oa += c;
+        }
+        R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
+      }
     }
     if (__ballot(bad)) {
       if (lane == 0) lv_bail(rt, x.p, PF_PAGE);
       continue;
     }
-    if (lane == 0) W.runs.rstart[R] = 0xFFFFFFFFu;
-    wave_lds_sync();
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
-    if (endo <= base || R == 0) continue;
-    LE_STAMP(1)
-    lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
-                  D.maxl, pages, gp(D.out));
-    wave_lds_sync();  // the run list and stage are refilled by the next window
+    if (bm) {
+      LE_STAMP(1)
+      if (endo > base && !lv_bitmap1<OUT>(W, blob, blob_len, x, mym, (uint64_t)base + myacc, base, (uint32_t)endo, n,
+                                          sel, pages, gp(D.out)) && lane == 0)
+        lv_bail(rt, x.p, PF_PAGE);
+    } else {
+      if (lane == 0) W.runs.rstart[R] = 0xFFFFFFFFu;
+      wave_lds_sync();
+      if (endo <= base || R == 0) continue;
+      LE_STAMP(1)
+      lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
+                    D.maxl, pages, gp(D.out));
+    }
+    wave_lds_sync();  // the run list / bitmap and stage are refilled by the next window
     LE_STAMP(2)
 #ifdef PQG_DIAG
     ++tn;
