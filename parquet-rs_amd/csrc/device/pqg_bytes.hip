@@ -470,12 +470,23 @@ struct BaSrc {
   const uint64_t* dsrc;
   const uint32_t* dlen;
   bool via_dict;
-  __device__ BaSrc(const ChunkWork& ck, const PageWork& pw, const uint64_t* vsrc0, const uint32_t* vlen0,
-                   const uint64_t* dsrc0, const uint32_t* dlen0)
+  uint32_t nd;  // dictionary entries: an index slot the level path did not write (a failed page's:
+                // the kernels run before the status is read; the scratch is not cleared) is empty
+  __device__ BaSrc(const ChunkWork& ck, const PageWork& pw, const PageWork* pages, const uint64_t* vsrc0,
+                   const uint32_t* vlen0, const uint64_t* dsrc0, const uint32_t* dlen0)
       : vsrc(vsrc0 + ck.scr_base), vlen(vlen0 + ck.scr_base), dsrc(dsrc0 + ck.dscr_base),
-        dlen(dlen0 + ck.dscr_base), via_dict(pw.encoding == E_RLE_DICTIONARY && ck.lvdict) {}
-  __device__ uint32_t len(uint64_t k) const { return via_dict ? dlen[vlen[k]] : vlen[k]; }
-  __device__ uint64_t src(uint64_t k) const { return via_dict ? dsrc[vlen[k]] : vsrc[k]; }
+        dlen(dlen0 + ck.dscr_base), via_dict(pw.encoding == E_RLE_DICTIONARY && ck.lvdict),
+        nd(via_dict && ck.dict_page >= 0 ? pages[ck.dict_page].num_values : 0u) {}
+  __device__ uint32_t len(uint64_t k) const {
+    if (!via_dict) return vlen[k];
+    const uint32_t i = vlen[k];
+    return i < nd ? dlen[i] : 0u;
+  }
+  __device__ uint64_t src(uint64_t k) const {
+    if (!via_dict) return vsrc[k];
+    const uint32_t i = vlen[k];
+    return i < nd ? dsrc[i] : 0u;
+  }
 };
 
 // Per listed tile (gt, global) of a byte-array page: the tile's byte count into tsum[gt] (the
@@ -491,7 +502,7 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pw, ck)) return;
   const uint32_t t = gt - pw.ltile0;
-  const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
+  const BaSrc bs(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
   uint64_t s = 0;
@@ -585,7 +596,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pw, ck) || ba_small_dict(pw, ck, pages)) return;  // (small dictionaries: k_ba_copy_sd)
   const uint32_t t = gt - pw.ltile0;
-  const BaSrc bs(ck, pw, vsrc0, vlen0, dsrc0, dlen0);
+  const BaSrc bs(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
   const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
   const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
   const uint64_t n = pw.nonnull, vo = pw.value_out;
@@ -767,7 +778,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   for (uint32_t k = 0; k < BA_VPT; ++k) {
     const uint32_t j = k * WG + tid;
     if (k * WG >= cnt) break;
-    const bool in = j < cnt;
+    const bool vj = j < cnt, in = vj && idx[k] < nd;  // (an index slot not written: empty, as BaSrc)
     const uint32_t ln = in ? dln[idx[k]] : 0u;
     uint32_t incl = ln;
 #pragma unroll
@@ -783,7 +794,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
       if (w < wv) pre += wsum[w];
       tot += wsum[w];
     }
-    if (in) offsets[vo + t0 + j] = (int64_t)(run + pre);
+    if (vj) offsets[vo + t0 + j] = (int64_t)(run + pre);
     const uint64_t gA = run, gB = run + tot;
     const uint32_t sh = (uint32_t)(gA & 15u);
     if (tot + 16 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is

@@ -331,6 +331,163 @@ __global__ void __launch_bounds__(WG) k_texpand_dict(const uint8_t* __restrict__
   tile_one(blob, blob_len, rt.desc, tl[blockIdx.x], rt.runs, sm, mk);
 }
 
+// ---- dictionaries of at most 65536 entries of 4 or 8 bytes, too large for the level path's
+// LDS copy. A random gather served from L2 costs one L2 request per value, and the request rate,
+// not HBM, bounds it (k_texpand_dict<8> at 64K entries: 4.45 ms for 1e9 values). Instead the
+// tile expand keeps each tile's indices (16-bit, one RUN_TILE slot per listed tile), and
+// k_dict_win streams the dictionary through LDS in 128 KiB windows: a workgroup of 1024 threads
+// takes 8 tiles (32 values per thread, in registers), fills window after window of their
+// dictionary by LDS-DMA (no registers held by the fill) and gathers the indices that fall in
+// each; L2 serves whole lines of the dictionary (D x ES bytes per 32768 values) instead of one
+// request per value (tools/ubench/win_ubench.hip: 2.7 ms against 4.5 ms for the L2 gather).
+struct DictIdxMaker {
+  PageWork* pages;
+  ChunkWork* chunks;
+  uint16_t* idx;  // the list's slots
+  __device__ TxDictIdx make(const QDesc& d) {
+    if (!d.qhi) return TxDictIdx{gptr<uint16_t>(nullptr), 0u, 0u, 0};
+    const ChunkWork& ck = chunks[pages[d.page].chunk];
+    return TxDictIdx{gp(idx) + (uint64_t)blockIdx.x * RUN_TILE, d.qlo, pages[ck.dict_page].num_values, 0};
+  }
+  __device__ void done(const QDesc& d, uint32_t, TxDictIdx& em) {
+    const uint64_t bad = __ballot(em.err != 0);
+    if (bad && (threadIdx.x & 63) == 0) report(pages, chunks, (int)d.page, ST_PANIC);
+  }
+};
+
+__global__ void __launch_bounds__(WG) k_texpand_didx(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     const uint32_t* __restrict__ tl, PageWork* pages,
+                                                     ChunkWork* chunks, RunTables rt, uint16_t* idx) {
+  __shared__ TileSmem sm;
+  if (*rt.nfall == 0) return;
+  DictIdxMaker mk{pages, chunks, idx};
+  tile_one(blob, blob_len, rt.desc, tl[blockIdx.x], rt.runs, sm, mk);
+}
+
+constexpr int DW_NT = 1024;                         // k_dict_win threads
+constexpr int DW_TPW = DW_NT / 128;                 // tiles per workgroup (128 threads x 32 values)
+constexpr uint32_t DW_BYTES = 128u << 10;           // window bytes
+constexpr uint32_t DW_LDS = DW_BYTES + 1024u;       // + the shift of an unaligned dictionary
+constexpr uint32_t DW_CH = DW_LDS / 16u;            // 16-byte LDS-DMA chunks per fill
+constexpr int DW_F = (int)((DW_CH + DW_NT - 1) / DW_NT);
+
+template <int ES>
+__global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                    const uint32_t* __restrict__ tl, uint32_t ntl,
+                                                    const PageWork* __restrict__ pages,
+                                                    const ChunkWork* __restrict__ chunks, RunTables rt,
+                                                    const uint16_t* __restrict__ idx) {
+  using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
+  constexpr uint32_t WIN = DW_BYTES / ES;  // entries per window
+  __shared__ uint4 win[DW_CH + 1];         // (+1: the unaligned reads' third word)
+  __shared__ int32_t dkey[DW_TPW];
+  if (*rt.nfall == 0) return;
+  const uint32_t tid = threadIdx.x, q = tid >> 7, lt = tid & 127u;
+  const uint32_t p = blockIdx.x * DW_TPW + q;
+  uint32_t qlo = 0, qhi = 0;
+  uint64_t obase = 0;
+  int32_t key = -1;
+  if (p < ntl) {
+    const QDesc& d = rt.desc[tl[p]];
+    qhi = d.qhi;
+    if (qhi) {
+      qlo = d.qlo;
+      const ChunkWork& ck = chunks[pages[d.page].chunk];
+      key = ck.dict_page;
+      obase = reinterpret_cast<uint64_t>(ck.val_out) + (d.out + qlo) * (uint64_t)ES;
+    }
+  }
+  if (lt == 0) dkey[q] = key;
+  // the thread's 32 values: 16 pairs, pair s at tile outputs qlo + 2 (128 s + lt) + {0, 1} (each
+  // store instruction of a wave one contiguous run of 64 pairs); rem: the tile's outputs from the
+  // thread's first pair on
+  const int32_t rem = (int32_t)(qhi - qlo) - (int32_t)(2u * lt);
+  const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + (uint64_t)p * RUN_TILE) + lt;
+  uint32_t ix[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) ix[s] = s * 256 < rem ? ip[s * 128] : 0u;
+  T x[16][2];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) x[s][0] = x[s][1] = 0;
+  __syncthreads();
+  for (int qq = 0; qq < DW_TPW; ++qq) {  // each distinct dictionary of the 8 tiles (uniform)
+    const int32_t kq = dkey[qq];
+    bool seen = kq < 0;
+    for (int r = 0; r < qq; ++r) seen |= dkey[r] == kq;
+    if (seen) continue;
+    const uint64_t dbase = pages[kq].base;
+    const uint32_t D = pages[kq].num_values;
+    const bool mine = key == kq;
+    for (uint32_t w0 = 0; w0 < D; w0 += WIN) {
+      const uint64_t a = dbase + (uint64_t)w0 * ES, a0 = a & ~15ull;
+      const uint32_t sh = (uint32_t)(a - a0);  // the window's first entry lands at LDS byte sh
+      const uint32_t nb = sh + (D - w0 < WIN ? D - w0 : WIN) * (uint32_t)ES;
+      __syncthreads();  // (the previous window's gathers are done)
+      // chunks c < lim: inside the window's bytes and the blob
+      const uint64_t bl = blob_len > a0 ? (blob_len - a0) / 16u : 0u;
+      const uint32_t lim = (uint32_t)min(min((uint64_t)DW_CH, (uint64_t)(nb + 15u) / 16u), bl);
+      const uint8_t* src = blob + a0 + (uint64_t)tid * 16u;
+#pragma unroll 1  // (unrolled, the fill's addresses and M0 values took registers the values need)
+      for (int f = 0; f < DW_F; ++f) {
+        const uint32_t c = (uint32_t)f * DW_NT + tid;
+        if (c < lim)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(src + (uint64_t)f * DW_NT * 16u),
+              (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)win +
+                                                         ((uint32_t)f * DW_NT + (tid & ~63u)) * 16u),
+              16, 0, 0);
+      }
+      __syncthreads();  // (vmcnt(0): the window has landed)
+      if (sh) {  // a dictionary at an odd offset: the window moved down by sh bytes, in place
+        const uint32_t k0 = sh >> 2, bs = sh & 3u;
+#pragma unroll 1
+        for (int f = 0; f < DW_F; ++f) {
+          const uint32_t c = (uint32_t)f * DW_NT + tid;
+          const uint32_t cc = c < DW_CH ? c : DW_CH - 1u;  // (LDS reads in bounds; results unused)
+          const uint4 a4 = win[cc], b4 = win[cc + 1];
+          const uint32_t v0 = a4.x, v1 = a4.y, v2 = a4.z, v3 = a4.w, v4 = b4.x, v5 = b4.y, v6 = b4.z, v7 = b4.w;
+          __syncthreads();  // (every chunk read before any is rewritten)
+          if (c < lim) {
+            // words k0 .. k0 + 4 of the 8 hold the chunk's 16 bytes from byte sh on
+            const uint32_t w0_ = k0 == 0 ? v0 : k0 == 1 ? v1 : k0 == 2 ? v2 : v3;
+            const uint32_t w1_ = k0 == 0 ? v1 : k0 == 1 ? v2 : k0 == 2 ? v3 : v4;
+            const uint32_t w2_ = k0 == 0 ? v2 : k0 == 1 ? v3 : k0 == 2 ? v4 : v5;
+            const uint32_t w3_ = k0 == 0 ? v3 : k0 == 1 ? v4 : k0 == 2 ? v5 : v6;
+            const uint32_t w4_ = k0 == 0 ? v4 : k0 == 1 ? v5 : k0 == 2 ? v6 : v7;
+            win[c] = bs ? make_uint4(__builtin_amdgcn_alignbyte(w1_, w0_, bs), __builtin_amdgcn_alignbyte(w2_, w1_, bs),
+                                     __builtin_amdgcn_alignbyte(w3_, w2_, bs), __builtin_amdgcn_alignbyte(w4_, w3_, bs))
+                        : make_uint4(w0_, w1_, w2_, w3_);
+          }
+          __syncthreads();
+        }
+      }
+      if (mine) {
+        const T* wt = reinterpret_cast<const T*>(win);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t r = (j ? ix[s] >> 16 : ix[s] & 0xFFFFu) - w0;
+            if (r < WIN) x[s][j] = wt[r];
+          }
+      }
+    }
+  }
+  gptr<uint8_t> o = reinterpret_cast<gptr<uint8_t>>(obase) + (uint64_t)lt * 2u * ES;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    gptr<uint8_t> os = o + s * 256 * ES;
+    if (s * 256 + 2 <= rem) {
+      if constexpr (ES == 8)
+        gst16(os, make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32), (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32)));
+      else
+        *reinterpret_cast<gptr<uint64_t>>(os) = (uint64_t)x[s][0] | ((uint64_t)x[s][1] << 32);
+    } else if (s * 256 < rem) {
+      *reinterpret_cast<gptr<T>>(os) = x[s][0];
+    }
+  }
+}
+
 // Dictionary index streams the level path handed back, when they are expected to be rare (the
 // dictionary's index width is within the level path's limit): one workgroup per page of a chunk
 // of ES-byte values, index walk then the page's tiles with the gather, as k_lv_fallback does for
@@ -676,7 +833,8 @@ hipError_t pqg_launch_scan(PageWork* pages, int npages, ChunkWork* chunks, hipSt
 // pass (pqg_launch_run_index with SS_DICT) having run before.
 hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                            const uint32_t* tile_page, uint32_t lv_es, const uint32_t* const* tl,
-                           const uint32_t* ntl, const uint32_t* tl_all, uint32_t ntl_all, RunTables rt,
+                           const uint32_t* ntl, const uint32_t* tl_all, uint32_t ntl_all,
+                           const uint32_t* const* wl, const uint32_t* wn, uint16_t* didx, RunTables rt,
                            hipStream_t s, hipEvent_t* kev) {
   // (the dictionary pages' checks ran in k_prepare)
   if (kev) (void)hipEventRecord(kev[0], s);
@@ -691,6 +849,18 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
     if (ntl[1]) hipLaunchKernelGGL((k_texpand_dict<4>), dim3(ntl[1]), dim3(WG), 0, s, blob, blob_len, tl[1], pages, chunks, rt);
     if (ntl[2]) hipLaunchKernelGGL((k_texpand_dict<8>), dim3(ntl[2]), dim3(WG), 0, s, blob, blob_len, tl[2], pages, chunks, rt);
     if (ntl[3]) hipLaunchKernelGGL((k_texpand_dict<12>), dim3(ntl[3]), dim3(WG), 0, s, blob, blob_len, tl[3], pages, chunks, rt);
+    // windowed gathers (wl[0] / wl[1]: tiles of 4- / 8-byte values, slots of didx in that order)
+    uint16_t* slot = didx;
+    for (int k = 0; k < 2; ++k) {
+      if (!wn[k]) continue;
+      hipLaunchKernelGGL(k_texpand_didx, dim3(wn[k]), dim3(WG), 0, s, blob, blob_len, wl[k], pages, chunks, rt, slot);
+      const dim3 g((wn[k] + DW_TPW - 1) / DW_TPW);
+      if (k == 0)
+        hipLaunchKernelGGL((k_dict_win<4>), g, dim3(DW_NT), 0, s, blob, blob_len, wl[k], wn[k], pages, chunks, rt, slot);
+      else
+        hipLaunchKernelGGL((k_dict_win<8>), g, dim3(DW_NT), 0, s, blob, blob_len, wl[k], wn[k], pages, chunks, rt, slot);
+      slot += (uint64_t)wn[k] * RUN_TILE;
+    }
   }
   if (kev) (void)hipEventRecord(kev[1], s);
   return hipGetLastError();

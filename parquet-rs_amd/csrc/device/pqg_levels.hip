@@ -236,6 +236,18 @@ __device__ inline bool lv_stream(const uint8_t* blob, const PageWork& pw, int se
 __device__ inline void lv_bail(RunTables& rt, uint32_t p, uint32_t from) {
   if (atomicCAS(&rt.pflag[p], from, PF_BAIL) == from) atomicAdd(rt.nfall, 1u);
 }
+// The same, recording in diagnostic builds where (lt.bail, PQG_DEBUG 512): 1 segment scan,
+// 2 stitch, 4 emit: a chain walk or run check, 5 emit: a run of the bitmap writes, 6 / 7
+// walked-page emit.
+#ifdef PQG_DIAG
+#define LV_BAIL(rt, lt, p, from, site)                               \
+  do {                                                               \
+    if ((lt).bail) atomicCAS(&(lt).bail[p], 0u, (uint32_t)(site));  \
+    lv_bail(rt, p, from);                                            \
+  } while (0)
+#else
+#define LV_BAIL(rt, lt, p, from, site) lv_bail(rt, p, from)
+#endif
 
 // Own positions' first hop (window-relative next offset, terminal codes >= LV_WIN) and output
 // count. Position i = j * 64 + lane.
@@ -980,7 +992,7 @@ __device__ inline void lv_segscan_page(const uint8_t* __restrict__ blob, const P
     if (verdict == 1 && sel == SS_DICT) verdict = 2;  // no window path for dictionary indices
     verdict_s = verdict;
     if (verdict == 0) rt.pflag[p] = PF_WALK;
-    else if (verdict == 2) lv_bail(rt, p, PF_PAGE);
+    else if (verdict == 2) LV_BAIL(rt, lt, p, PF_PAGE, 1);
   }
   __syncthreads();
   if (verdict_s != 0)
@@ -1586,7 +1598,7 @@ __global__ void __launch_bounds__(SC_WG) k_lv_stitch(const uint8_t* __restrict__
   if (tid == 0) {
     bool ok = ok_s != 0;
     if (serial_s) ok = lv_stitch_serial(tab, win, nw, ent, ts, n, slen);
-    if (!ok) lv_bail(rt, p, PF_PAGE);
+    if (!ok) LV_BAIL(rt, lt, p, PF_PAGE, 2);
   }
 }
 
@@ -1731,22 +1743,34 @@ __device__ inline bool lv_bm_fits(const LvWin& x, uint32_t base, uint64_t endo, 
   return !__ballot(span > LV_BM_SPAN) && ((hi - (lo & ~31ull) + 31u) >> 5) <= LV_BM_WORDS;
 }
 
-template <int OUT>
-__device__ inline bool lv_bitmap1(LvWave& W, const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x,
-                                  uint32_t mym, uint64_t oa, uint32_t base, uint32_t endo, uint32_t n, int sel,
-                                  PageWork* pages, gptr<uint8_t> __restrict__ out) {
-  constexpr uint32_t V = 16u / OUT;  // outputs per 16-byte chunk
+// The window's bitmap: outputs [lo, hi) of the page at bits (global output - A0) of words
+// bm[0, nw), A0 = lo rounded down to 32.
+struct LvBm {
+  uint64_t A0;
+  uint32_t ra, rb, nw;  // [lo, hi) - A0; words
+  __device__ LvBm(const LvWin& x, uint32_t base, uint32_t endo) {
+    const uint64_t lo = x.s.out + base;
+    A0 = lo & ~31ull;
+    ra = (uint32_t)(lo - A0);
+    rb = ra + (endo - base);
+    nw = (rb + 31u) >> 5;
+  }
+};
+
+// Generation: each lane ORs its own runs' bits (outputs from oa, page-relative) into the bitmap.
+// Returns the lane's count of 1s, or 0xFFFFFFFF for the whole wave at a run the window path does
+// not take.
+__device__ inline uint32_t lv_bm_gen(LvWave& W, const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x,
+                                     const LvBm& B, uint32_t mym, uint64_t oa, uint32_t n) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t slen = x.s.slen, i0 = lane * LV_SEG;
-  const uint64_t go = x.s.out, lo = go + base, hi = go + endo;
-  const uint64_t A0 = lo & ~31ull;
-  const uint32_t nw = (uint32_t)((hi - A0 + 31u) >> 5);
   uint32_t* bm = reinterpret_cast<uint32_t*>(W.JC);
   wave_lds_sync();  // (the jump table / prefix list is read)
-  for (uint32_t i = lane; i < nw; i += WAVE) bm[i] = 0u;
+  for (uint32_t i = lane; i < B.nw; i += WAVE) bm[i] = 0u;
   wave_lds_sync();
   bool bad = false;
   uint32_t cw = 0xFFFFFFFFu, cb = 0, cnt = 0;
+  uint32_t rs = B.ra + (uint32_t)(oa - (B.A0 + B.ra - x.s.out));  // the lane's first output, bitmap-relative
 #pragma unroll 1
   for (uint32_t m = mym; m; m &= m - 1u) {
     const uint32_t t = (uint32_t)__builtin_ctz(m);
@@ -1754,17 +1778,16 @@ __device__ inline bool lv_bitmap1(LvWave& W, const uint8_t* __restrict__ blob, u
     bool bp;
     lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, 1u, 1u, nx, c, v, bp);  // (a true header: parses)
     bad |= !lv_run_ok(bp, v, c, oa, n, slen, 1u);
-    const uint64_t e = oa + c < endo ? oa + c : (uint64_t)endo;
+    const uint32_t e = (uint64_t)rs + c < B.rb ? rs + c : B.rb;
 #pragma unroll 1
-    for (uint64_t q = oa; q < e;) {
-      const uint64_t g = go + q;
-      const uint32_t wi = (uint32_t)((g - A0) >> 5), bpos = (uint32_t)g & 31u;
-      const uint32_t take = e - q < 32u - bpos ? (uint32_t)(e - q) : 32u - bpos;
+    for (uint32_t q = rs; q < e;) {
+      const uint32_t wi = q >> 5, bpos = q & 31u;
+      const uint32_t take = e - q < 32u - bpos ? e - q : 32u - bpos;
       const uint32_t mk = take >= 32u ? 0xFFFFFFFFu : (1u << take) - 1u;
       uint32_t bits;
       if (bp) {
-        const uint64_t bit = (uint64_t)v * 8ull + (q - oa);
-        bits = (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & mk;
+        const uint32_t d = q - rs;
+        bits = (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x, v + (d >> 3)) >> (d & 7u)) & mk;
       } else {
         bits = (v & 1u) ? mk : 0u;
       }
@@ -1778,33 +1801,44 @@ __device__ inline bool lv_bitmap1(LvWave& W, const uint8_t* __restrict__ blob, u
       q += take;
     }
     oa += c;
+    rs = (uint64_t)rs + c < B.rb ? rs + c : B.rb;
   }
   if (cb) atomicOr(&bm[cw], cb);
   cnt += (uint32_t)__builtin_popcount(cb);
-  if (__ballot(bad)) return false;
+  return __ballot(bad) ? 0xFFFFFFFFu : cnt;
+}
+
+// Stores: the bitmap expanded, one contiguous KiB per store instruction (chunks shared with a
+// neighbouring window element by element), and the page's def count.
+template <int OUT>
+__device__ inline void lv_bm_store(LvWave& W, const LvWin& x, const LvBm& B, uint32_t cnt, int sel, PageWork* pages,
+                                   gptr<uint8_t> __restrict__ out) {
+  constexpr uint32_t V = 16u / OUT;  // outputs per 16-byte chunk
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t* bm = reinterpret_cast<const uint32_t*>(W.JC);
   wave_lds_sync();
-  // chunks [c0, c1) lie inside [lo, hi); chunk ka (holding lo) and kb (holding hi - 1) may not
-  const uint32_t ra = (uint32_t)(lo - A0), rb = (uint32_t)(hi - A0);
-  const uint32_t c0 = (ra + V - 1u) / V, c1 = rb / V, ka = ra / V, kb = (rb - 1u) / V;
+  gptr<uint8_t> ob = out + B.A0 * OUT;
+  // chunks [c0, c1) lie inside [ra, rb); chunk ka (holding ra) and kb (holding rb - 1) may not
+  const uint32_t c0 = (B.ra + V - 1u) / V, c1 = B.rb / V, ka = B.ra / V, kb = (B.rb - 1u) / V;
 #pragma unroll 2
   for (uint32_t k = c0 + lane; k < c1; k += WAVE) {
-    const uint32_t cbits = (bm[k * V / 32u] >> ((k * V) & 31u)) & (V == 32u ? 0xFFFFFFFFu : (1u << V) - 1u);
+    const uint32_t cbits = (bm[k * V / 32u] >> ((k * V) & 31u)) & ((1u << V) - 1u);
     uint32_t d[4];
 #pragma unroll
     for (uint32_t t = 0; t < 4; ++t)
       d[t] = OUT == 2 ? (((cbits >> (2u * t)) & 3u) * 0x8001u) & 0x10001u
                       : (((cbits >> (4u * t)) & 15u) * 0x204081u) & 0x01010101u;
-    gst16(out + (A0 + (uint64_t)k * V) * OUT, make_uint4(d[0], d[1], d[2], d[3]));
+    gst16(ob + k * 16u, make_uint4(d[0], d[1], d[2], d[3]));
   }
   const bool ea = lane == 0 && c0 > ka, eb = lane == 1 && c1 <= kb && !(kb == ka && c0 > ka);
   if (ea || eb) {
     const uint32_t kk = ea ? ka : kb;
     for (uint32_t j = 0; j < V; ++j) {
       const uint32_t r = kk * V + j;
-      if (r >= ra && r < rb) {
+      if (r >= B.ra && r < B.rb) {
         const uint32_t b = (bm[r >> 5] >> (r & 31u)) & 1u;
-        if (OUT == 2) reinterpret_cast<gptr<int16_t>>(out)[A0 + r] = (int16_t)b;
-        else out[A0 + r] = (uint8_t)b;
+        if (OUT == 2) reinterpret_cast<gptr<int16_t>>(ob)[r] = (int16_t)b;
+        else ob[r] = (uint8_t)b;
       }
     }
   }
@@ -1812,7 +1846,6 @@ __device__ inline bool lv_bitmap1(LvWave& W, const uint8_t* __restrict__ blob, u
     cnt = wave_sum_u32_(cnt);
     if (lane == 0 && cnt) atomicAdd((unsigned long long*)&pages[x.p].nonnull, (unsigned long long)cnt);
   }
-  return true;
 }
 
 // Wider levels: groups of G outputs (one 16-byte store), each from the runs covering it.
@@ -2284,9 +2317,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
 #ifdef PQG_DIAG
   // diagnostics (PQG_DEBUG bit 256): per wave s_memtime cycles in the window's staging wait,
-  // run placement and output writes, and the windows written
+  // chain / run placement, bitmap generation and output stores, and the windows written
   const bool stamps = (chunks[0].cp.debug & 256) && chunks[0].cp.dbgbuf;
-  uint64_t ts0 = 0, tacc[3] = {0, 0, 0}, tn = 0;
+  uint64_t ts0 = 0, tacc[4] = {0, 0, 0, 0}, tn = 0, tmiss = 0;
 #define LE_STAMP(k)                                   \
   if (stamps) {                                       \
     const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
@@ -2327,69 +2360,74 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     uint64_t T = 0;  // outputs of those runs (wave-uniform)
     bool bad = false;
     // bit width 1: this segment's true headers and first output (window-relative); bm: written
-    // from those by lv_bitmap1, no run list placed (wave-uniform)
+    // from those by lv_bm_gen / lv_bm_store, no run list placed (wave-uniform)
     uint32_t mym = 0;
     uint64_t myacc = 0;
     bool bm = false;
+    bool placed = false;  // (wave-uniform) the window's true headers found
     if (viaref) {
       constexpr uint32_t SEG = LV_SEG;
       const uint32_t me = nh, i0 = lane * SEG;
-      // the entry's own headers before the meeting point: one lane, serially, into a short list
-      uint32_t* pre = W.runs.rinfo;  // (the run list is written after these are read)
+      // the entry's own headers before the meeting point: one lane, serially, as a mask per
+      // segment (pm[s]); pm[64]: the walk landed on the meeting point
+      uint32_t* pm = W.runs.rinfo;  // (the run list is written after these are read)
+      pm[lane] = 0u;
+      wave_lds_sync();
       if (lane == 0) {
-        uint32_t qq = e0, np = 0;
-        while (qq < me && np < 64u) {
+        uint32_t qq = e0;
+        while (qq < me) {  // (every hop advances: at most LV_WIN + 64 of them)
           uint32_t nx, c, v;
           bool bp;
           if (!lv_parse4(W.stage, qq + x.sb, x.W0 + qq, slen, w, vb, nx, c, v, bp)) break;
-          pre[np++] = qq;
+          pm[qq / SEG] |= 1u << (qq % SEG);
           qq = nx - x.W0;
         }
-        pre[64] = qq == me ? np : 0xFFFFFFFFu;  // (the walk must land on the meeting point)
+        pm[64] = qq == me ? 1u : 0u;
       }
       wave_lds_sync();
-      const uint32_t np = pre[64];
-      mym = i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0));
-      for (uint32_t k = 0; k < np && np != 0xFFFFFFFFu; ++k) {
-        const uint32_t qq = pre[k];
-        if (qq >= i0 && qq < i0 + SEG) mym |= 1u << (qq - i0);
-      }
-      // outputs of this segment's true headers, then their place: a lane scan
-      uint64_t so = 0;
-#pragma unroll 1
-      for (uint32_t m = mym; m; m &= m - 1u) {
-        const uint32_t t = (uint32_t)__builtin_ctz(m);
-        uint32_t nx, c, v;
-        bool bp;
-        lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (chain headers parse)
-        so += c;
-      }
-      const uint64_t si = wave_incl_scan_cnt64(so);
-      const uint64_t tot = __shfl(si, 63, 64);
-      bad = __ballot(np == 0xFFFFFFFFu) != 0;
-      myacc = si - so;
-      T = tot;
-      bm = !bad && lv_bm_fits(x, base, (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n, so);
-      wave_lds_sync();  // (the prefix list is read)
-      if (!bad && !bm) {
-        const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
-        const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
-        uint32_t k = rb;
-        uint64_t oa = (uint64_t)base + (si - so);
+      if (pm[64]) {  // (else a table k_lv_win made wrong: the window takes the chain walk below)
+        placed = true;
+        mym = (i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0))) | pm[lane];
+        // outputs of this segment's true headers, then their place: a lane scan
+        uint64_t so = 0;
 #pragma unroll 1
         for (uint32_t m = mym; m; m &= m - 1u) {
           const uint32_t t = (uint32_t)__builtin_ctz(m);
           uint32_t nx, c, v;
           bool bp;
-          lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);
-          W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
-          W.runs.rinfo[k] = bp ? v : (R_RLE | v);
-          bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
-          ++k;
-          oa += c;
+          lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (chain headers parse)
+          so += c;
         }
-        R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
+        const uint64_t si = wave_incl_scan_cnt64(so);
+        myacc = si - so;
+        T = __shfl(si, 63, 64);
+        bm = lv_bm_fits(x, base, (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n, so);
+        wave_lds_sync();  // (the prefix masks are read)
+        if (!bm) {
+          const uint32_t nh_l = (uint32_t)__builtin_popcount(mym);
+          const uint32_t rb = wave_incl_scan_u32(nh_l) - nh_l;
+          uint32_t k = rb;
+          uint64_t oa = (uint64_t)base + myacc;
+#pragma unroll 1
+          for (uint32_t m = mym; m; m &= m - 1u) {
+            const uint32_t t = (uint32_t)__builtin_ctz(m);
+            uint32_t nx, c, v;
+            bool bp;
+            lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);
+            W.runs.rstart[k] = oa < 0xFFFFFFFFull ? (uint32_t)oa : 0xFFFFFFFFu;
+            W.runs.rinfo[k] = bp ? v : (R_RLE | v);
+            bad |= !lv_run_ok(bp, v, c, oa, n, slen, w);
+            ++k;
+            oa += c;
+          }
+          R = (uint32_t)__shfl((int)(rb + nh_l), 63, 64);
+        }
+      } else {
+        wave_lds_sync();
       }
+    }
+    if (placed) {
+      // (the true headers came from the reference chain)
     } else if (w != 1 && nh <= LV_SERIAL) {
       // sparse window: one lane follows the chain from the entry
       if (lane == 0) {
@@ -2489,38 +2527,56 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       }
     }
     if (__ballot(bad)) {
-      if (lane == 0) lv_bail(rt, x.p, PF_PAGE);
+      if (lane == 0) LV_BAIL(rt, lt, x.p, PF_PAGE, 4);
+#ifdef PQG_DIAG
+      // (the first failing window of the page: its index + 1, stitch entry, first output)
+      if (lt.bail && lane == 0 && atomicCAS(&lt.bail[npages + 4 * x.p], 0u, x.k + 1u) == 0u) {
+        lt.bail[npages + 4 * x.p + 1] = wi.x;
+        lt.bail[npages + 4 * x.p + 2] = wi.y;
+      }
+#endif
       continue;
     }
     // outputs [base, min(base + T, n)) of the page
     const uint64_t endo = (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n;
     if (bm) {
       LE_STAMP(1)
-      if (endo > base && !lv_bitmap1<OUT>(W, blob, blob_len, x, mym, (uint64_t)base + myacc, base, (uint32_t)endo, n,
-                                          sel, pages, gp(D.out)) && lane == 0)
-        lv_bail(rt, x.p, PF_PAGE);
+      if (endo > base) {
+        const LvBm B(x, base, (uint32_t)endo);
+        const uint32_t cnt = lv_bm_gen(W, blob, blob_len, x, B, mym, (uint64_t)base + myacc, n);
+        LE_STAMP(2)
+        if (cnt == 0xFFFFFFFFu) {
+          if (lane == 0) LV_BAIL(rt, lt, x.p, PF_PAGE, 5);
+        } else {
+          lv_bm_store<OUT>(W, x, B, cnt, sel, pages, gp(D.out));
+        }
+      }
     } else {
       if (lane == 0) W.runs.rstart[R] = 0xFFFFFFFFu;
       wave_lds_sync();
       if (endo <= base || R == 0) continue;
       LE_STAMP(1)
+      LE_STAMP(2)
       lv_write<OUT>(LvRuns{W.runs.rstart, W.runs.rinfo, R}, W.stage, blob, blob_len, x, base, (uint32_t)endo, sel,
                     D.maxl, pages, gp(D.out));
     }
     wave_lds_sync();  // the run list / bitmap and stage are refilled by the next window
-    LE_STAMP(2)
+    LE_STAMP(3)
 #ifdef PQG_DIAG
-    ++tn;
+    tn += 1ull | (viaref ? 1ull << 20 : 0ull) | (bm ? 1ull << 40 : 0ull);  // windows | via the reference | bitmap
+    tmiss += viaref && !placed ? 1u : 0u;  // the entry's chain missed the meeting point
 #endif
   }
 #ifdef PQG_DIAG
   if (stamps && lane == 0) {
     const uint32_t gw = blockIdx.x * (WG / WAVE) + wid;
-    uint64_t* d = chunks[0].cp.dbgbuf + 4ull * gw;
+    uint64_t* d = chunks[0].cp.dbgbuf + 8ull * gw;
     d[0] = tacc[0];
     d[1] = tacc[1];
     d[2] = tacc[2];
-    d[3] = tn;
+    d[3] = tacc[3];
+    d[4] = tn;
+    d[5] = tmiss;
   }
 #endif
 #undef LE_STAMP
@@ -2697,7 +2753,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       if (fr == fe) continue;
       const uint32_t R = fe - fr;
       if (R > LW_RPW) {
-        if (lane == 0) lv_bail(rt, p, PF_WALK);
+        if (lane == 0) LV_BAIL(rt, lt, p, PF_WALK, 6);
         continue;
       }
       const uint2* rc = recp + fr;
@@ -2725,7 +2781,7 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
       if (fr == fe) continue;  // no header starts in this window
       R = fe - fr;
       if (R > LW_RPW) {  // more runs than the run list holds (not from the walker's span rule)
-        if (lane == 0) lv_bail(rt, p, PF_WALK);
+        if (lane == 0) LV_BAIL(rt, lt, p, PF_WALK, 7);
         continue;
       }
       le_issue(blob, blob_len, recp + fr, R, x.s.S, x.k, w, nf);

@@ -435,4 +435,42 @@ struct TxDict {
   }
 };
 
+// The same indices kept, not gathered: 16-bit entries into the tile's slot of an index buffer
+// (outputs [lo, lo + RUN_TILE) of the tile; dictionaries of at most 65536 entries), for
+// k_dict_win's gather through LDS windows. The range check (the reference's panic) stays here.
+struct TxDictIdx {
+  static constexpr int V = 8;  // one 16-byte store of indices per group
+  static constexpr int PG = 2;
+  gptr<uint16_t> slot;
+  uint32_t lo;
+  uint32_t ndict;
+  int32_t err;
+
+  template <int NG>
+  __device__ void put(uint32_t g0, uint32_t stride, const uint32_t (&v)[NG][V], const uint32_t (&m)[NG]) {
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const bool want = (m[s] >> j) & 1u;
+        err |= (want && v[s][j] >= ndict) ? ST_PANIC : 0;
+        pk[j >> 1] |= (v[s][j] & 0xFFFFu) << (16 * (j & 1));
+      }
+      const uint32_t g = g0 + (uint32_t)s * stride - lo;
+      if (m[s] == 0xFFu) {
+        gst16(reinterpret_cast<gptr<uint8_t>>(slot + g), make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      } else if (m[s]) {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if ((m[s] >> j) & 1u) slot[g + j] = (uint16_t)v[s][j];
+      }
+    }
+  }
+  __device__ void put1(uint32_t o, uint32_t idx) {
+    if (idx >= ndict) err = ST_PANIC;
+    slot[o - lo] = (uint16_t)idx;
+  }
+};
+
 }  // namespace pqg

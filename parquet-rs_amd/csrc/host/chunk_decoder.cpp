@@ -35,8 +35,8 @@ hipError_t pqg_launch_scan(PageWork*, int, ChunkWork*, hipStream_t);
 hipError_t pqg_launch_lv(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, int, uint32_t, const uint64_t*,
                          const uint32_t*, uint64_t*, uint32_t*, RunTables, LevelTables, hipStream_t, hipEvent_t = nullptr);
 hipError_t pqg_launch_dict(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
-                           const uint32_t* const*, const uint32_t*, const uint32_t*, uint32_t, RunTables, hipStream_t,
-                           hipEvent_t*);
+                           const uint32_t* const*, const uint32_t*, const uint32_t*, uint32_t, const uint32_t* const*,
+                           const uint32_t*, uint16_t*, RunTables, hipStream_t, hipEvent_t*);
 hipError_t pqg_launch_plain(const uint8_t*, uint64_t, PageWork*, ChunkWork*, const uint32_t*, const uint32_t*, uint32_t,
                             uint64_t, const uint32_t*, uint32_t, hipStream_t);
 hipError_t pqg_launch_plain_spec(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, uint32_t,
@@ -68,7 +68,14 @@ constexpr int SS_DICT = 2;  // device/pqg_runs.hpp StreamSel: dictionary indices
 // dictionary tiles off the level path, byte-array copy tiles, RLE boolean tiles, PLAIN
 // fixed-width pages (a page list) and PLAIN boolean tiles.
 // TL_PSPEC: PLAIN pages of the chunks whose values are copied speculatively (ChunkWork::spec).
-enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_PSPEC, TL_N };
+// TL_W4 / TL_W8: general-path dictionary tiles of 4- / 8-byte values whose dictionary has at most
+// DW_MAXD entries (indices to a buffer, then the gather through LDS windows: k_dict_win).
+enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_PSPEC, TL_W4, TL_W8,
+       TL_N };
+#ifndef PQG_DWIN
+#define PQG_DWIN 1  // (0: every general-path dictionary gather served from L2, for A/B runs)
+#endif
+constexpr uint32_t DW_MAXD = 65536;  // 16-bit indices
 
 // What the host knows of one chunk of a decode until its results are delivered.
 struct ChunkHost {
@@ -105,6 +112,8 @@ struct Slot {
   uint32_t* dlen = nullptr;
   size_t dcap = 0;
   uint64_t* tsum = nullptr;  // byte-array copy: per tile, bytes then start
+  uint16_t* didx = nullptr;  // TL_W4 / TL_W8 tiles: RUN_TILE dictionary indices each
+  size_t didx_cap = 0;
   // hybrid-stream expand tiles: tile -> page map and the index-pass tables per stream kind
   uint32_t* tile_page = nullptr;
   RunTables rt[K_N] = {};
@@ -116,6 +125,7 @@ struct Slot {
   static constexpr int LV_BUFS = 14;  // wbase, wbase2, wfirst, rec, tab, win, sbase, bexit, seg, srec, spos, dense, ctr, bmp
   void* lvbuf[K_N][LV_BUFS] = {};
   size_t lvcap[K_N][LV_BUFS] = {};
+  uint32_t* bail = nullptr;  // PQG_DIAG, PQG_DEBUG 512: LevelTables::bail of the def stream
   LevelTables lt(int k, uint32_t tstride) const {
     LevelTables t{};
     t.wbase = (uint32_t*)lvbuf[k][0];
@@ -133,6 +143,7 @@ struct Slot {
     t.ctr = (uint32_t*)lvbuf[k][12];
     t.bmp = (uint16_t*)lvbuf[k][13];
     t.tstride = tstride;
+    t.bail = k == K_DEF ? bail : nullptr;
     return t;
   }
 };
@@ -323,6 +334,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.tsum);
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
+    hipFree(sl.didx);
     hipFree(sl.tile_page);
     for (RunTables& t : sl.rt) free_run_tables(t);
     hipFree(sl.dt.page);
@@ -666,7 +678,10 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
             lv_es |= (uint32_t)es;
           } else {
             fixed_gen = true;
-            list_tiles(es == 1 ? TL_D1 : es == 4 ? TL_D4 : es == 8 ? TL_D8 : TL_D12, PQG_RLE_DICTIONARY);
+            const bool win = PQG_DWIN && (es == 4 || es == 8) && dict_page >= 0 && ndict <= DW_MAXD;
+            list_tiles(win ? (es == 4 ? TL_W4 : TL_W8)
+                           : es == 1 ? TL_D1 : es == 4 ? TL_D4 : es == 8 ? TL_D8 : TL_D12,
+                       PQG_RLE_DICTIONARY);
             list_tiles(TL_DALL, PQG_RLE_DICTIONARY);
           }
         }
@@ -681,11 +696,12 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     p0 += n;
   }
 #ifdef PQG_DIAG
-  if (dbg_env & (16 | 32 | 64 | 128 | 256)) {
+  if (dbg_env & (16 | 32 | 64 | 128 | 256 | 512)) {
     size_t need = (size_t)(total_tiles * 4 > (uint64_t)np * 2 ? total_tiles * 4 : (uint64_t)np * 2) * 16;
     if (need < (size_t)np * 64) need = (size_t)np * 64;
     if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + np + 1) * 32;  // per level-stream segment
     if (dbg_env & 256) need = (size_t)2048 * 64 * 4 * 32;                 // per wave of k_lv_emit (grids <= 64 x)
+    if (dbg_env & 512) need = (size_t)np * 20 + 64;  // per page: its hand-back site, then the failing window
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
       ctx->dbgbuf = nullptr;
@@ -693,6 +709,11 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       ctx->dbg_cap = need;
     }
     ctx->dbg_n = (dbg_env & 32) ? np : total_tiles * 4;
+    sl.bail = nullptr;
+    if (dbg_env & 512) {
+      sl.bail = (uint32_t*)ctx->dbgbuf;
+      HIPCHK(hipMemsetAsync(sl.bail, 0, (size_t)np * 20, s), "memset bail sites");
+    }
     for (ChunkWork& c : cw) c.cp.dbgbuf = ctx->dbgbuf;
   }
 #endif
@@ -754,6 +775,11 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       sl.dlen = nullptr;
       HIPCHK(hipMalloc(&sl.dlen, sl.dcap * 4), "hipMalloc dlen");
     }
+  }
+  if (ntl[TL_W4] + ntl[TL_W8]) {
+    const int st = grow(ctx, (void**)&sl.didx, &sl.didx_cap, (size_t)(ntl[TL_W4] + ntl[TL_W8]) * RUN_TILE, 2,
+                        "hipMalloc dictionary indices");
+    if (st) return st;
   }
   // expand-tile bookkeeping (tile -> page, byte-array tile sums, index tables per stream kind)
   if ((size_t)total_tiles + 1 > sl.tcap) {
@@ -923,8 +949,10 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       ctx->values_kernel = PQG_RLE_DICTIONARY;
       const uint32_t* dl[4] = {tlp[TL_D1], tlp[TL_D4], tlp[TL_D8], tlp[TL_D12]};
       const uint32_t dn[4] = {ntl[TL_D1], ntl[TL_D4], ntl[TL_D8], ntl[TL_D12]};
+      const uint32_t* wl[2] = {tlp[TL_W4], tlp[TL_W8]};
+      const uint32_t wn[2] = {ntl[TL_W4], ntl[TL_W8]};
       HIPCHK(pqg_launch_dict(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, lv_es, dl, dn, tlp[TL_DALL],
-                             ntl[TL_DALL], rd, s, ctx->timing ? &ev[8] : nullptr),
+                             ntl[TL_DALL], wl, wn, sl.didx, rd, s, ctx->timing ? &ev[8] : nullptr),
              "dict");
       sl.kv = ctx->timing;
     }

@@ -209,6 +209,7 @@ struct LevelTables {
                      // [1] k_lv_fallback, [2] k_lv_plan
   uint32_t tstride;  // tab entries per window: lv_ent of the widest stream of the decode (the
                      // streams of a batch's chunks may differ in bit width)
+  uint32_t* bail;    // PQG_DIAG builds, PQG_DEBUG 512: per page, where the level path handed it back
 };
 
 // RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window

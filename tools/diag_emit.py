@@ -1,5 +1,6 @@
 """Diagnostics: where k_lv_emit's waves spend their cycles (PQG_DIAG build, PQG_DEBUG=256):
-per window, the staging wait, run placement and output writes (s_memtime stamps).
+per window, the staging wait, chain / run placement, bitmap generation and output stores
+(s_memtime stamps).
 
     make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=256 python tools/diag_emit.py --p-null 0.1
 """
@@ -36,13 +37,19 @@ def main():
         st, bad = ctx.sync()
         assert st == 0, (st, bad)
     n = 2048 * 64
-    buf = np.zeros(4 * n, np.uint64)
+    buf = np.zeros(8 * n, np.uint64)
     assert L.pqg_debug_read(ctx.h, buf.ctypes.data, buf.size) == 0
-    d = buf.reshape(n, 4).astype(np.float64)
-    d = d[d[:, 3] > 0]
-    tot = d[:, 3].sum()
-    print(f"waves {len(d)} windows {tot:.0f}")
-    for k, name in enumerate(("stage wait", "placement", "writes")):
+    raw = buf.reshape(n, 8)[:, :6]
+    raw = raw[raw[:, 4] > 0]
+    cnt = raw[:, 4]
+    miss = raw[:, 5].sum()
+    via, bmw = ((cnt >> 20) & 0xFFFFF).sum(), (cnt >> 40).sum()
+    d = raw.astype(np.float64)
+    d[:, 4] = (cnt & 0xFFFFF).astype(np.float64)
+    tot = d[:, 4].sum()
+    print(f"waves {len(d)} windows {tot:.0f}: via the reference chain {via / tot:.3f} (missed {miss / tot:.5f}), "
+          f"bitmap writes {bmw / tot:.3f}")
+    for k, name in enumerate(("stage wait", "placement", "bitmap gen", "stores")):
         print(f"  {name:11s} {d[:, k].sum() / tot:9.0f} cycles per window (wave mean {d[:, k].mean():10.0f})")
     print("levels_kernel_ms", ctx.timings().levels_kernel_ms)
 
