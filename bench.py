@@ -378,7 +378,10 @@ def pcie_inclusive(ctx, w, stream, iters=3):
 
 
 LEVEL_PATH = ("k_lv_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
-DELTA_STAGE = ("k_delta_",)  # k_delta_hdr, k_delta_lb, k_delta_page, the tiled path's kernels
+DELTA_STAGE = ("k_delta_",)  # k_delta_page, the tiled path's kernels
+# the dictionary values: tile descriptors, the tile expand (16-bit indices kept, or gathered from
+# L2) and the windowed gather (k_dict_win)
+DICT_STAGE = ("k_tile_desc", "k_texpand_d", "k_dict_win")
 
 
 def pmc_traffic(kind, kernel, variant=None):
@@ -398,8 +401,8 @@ def pmc_traffic(kind, kernel, variant=None):
         except (OSError, ValueError, KeyError):
             continue
         names = {k.replace("pqg::", ""): e for k, e in ks.items() if "traffic_bytes" in e}
-        if kernel in ("level path", "DELTA stage"):  # a chain of kernels timed as one: their sum
-            pre = LEVEL_PATH if kernel == "level path" else DELTA_STAGE
+        if kernel in ("level path", "DELTA stage", "dictionary stage"):  # kernels timed as one: their sum
+            pre = {"level path": LEVEL_PATH, "DELTA stage": DELTA_STAGE, "dictionary stage": DICT_STAGE}[kernel]
             tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(pre)]
             if tot:
                 return sum(tot), os.path.relpath(path, ROOT)
@@ -452,10 +455,12 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
         variant = f"p{int(round(p_null * 100)):02d}"
         stages = [("level path", tm.levels_kernel_ms, lev_b, w.level_bytes_in),
                   ("k_plain_copy", tm.values_kernel_ms, val_b, w.values * w.es)]
-    elif kind == "dict":   # indices in + values out (+ the L2-resident dictionary, 0.5 MiB)
-        stages = [("k_texpand_dict<8>", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
-    else:                  # deltas in + values out (HIP events around the DELTA kernels: header pass,
-        # look-back tile kernel, and the page pass / tiled path for pages those leave)
+    elif kind == "dict":   # indices in + values out (HIP events around the dictionary kernels: the
+        # tile expand keeping 16-bit indices and the windowed gather; their index round trip and
+        # the dictionary windows are traffic above these algorithmic bytes)
+        stages = [("dictionary stage", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
+    else:                  # deltas in + values out (HIP events around the DELTA kernels: the page
+        # pass, and the tiled path for pages it leaves)
         stages = [("DELTA stage", tm.values_kernel_ms, w.in_bytes + w.out_bytes, w.in_bytes)]
         if tuple(w.block) != (512, 4):
             variant = f"b{w.block[0]}x{w.block[1]}"

@@ -97,3 +97,27 @@ def test_dictionaries_of_several_chunks(oracle, ctx):
     for order in (list(range(len(zoo))), list(reversed(range(len(zoo))))):
         st, res = _decode_batch(ctx, zoo, order)
         _check_zoo(oracle, zoo, st, res, order)
+
+
+@pytest.mark.parametrize("mean_run", [3, 12, 40, 400])
+@pytest.mark.parametrize("ptype", ["INT32", "INT64"])
+def test_dictionary_index_runs(oracle, ctx, ptype, mean_run):
+    """Indices in runs of equal values (RLE runs beside bit-packed ones): tiles of few records
+    (their indices read from the stream by the gather kernel), of many (kept by the tile expand)
+    and of more than one index batch (re-walked)."""
+    rng = np.random.default_rng(34 + mean_run)
+    t = getattr(oracle, ptype)
+    nd = 5000
+    dv = _dvals(rng, t, oracle, nd)
+    d = oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode(t, dv), nd, oracle.PLAIN_DICTIONARY)
+    bw = 13
+    pages = [d]
+    for n in (60_000, 4097, 30_001):
+        lens = rng.geometric(1.0 / mean_run, n)
+        vals = rng.integers(0, nd, len(lens))
+        idx = np.repeat(vals, lens)[:n]
+        lv = np.ones(n, np.int16)
+        lv[rng.random(n) < 0.1] = 0
+        body = bytes([bw]) + oracle.rle_encode(idx[:int(lv.sum())].astype(np.uint64), bw)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(lv, 1) + body, n, oracle.RLE_DICTIONARY))
+    _same(oracle, ctx, t, pages)

@@ -108,6 +108,116 @@ __global__ __launch_bounds__(NT) void k_gather_win(const uint64_t* __restrict__ 
   }
 }
 
+// layout B: value pairs lane-contiguous (each store instruction one contiguous KiB), indices as
+// 32-bit pairs (NP pairs per thread)
+template <int NP>
+__global__ __launch_bounds__(256) void k_gather_idx2(const uint64_t* __restrict__ dict, const uint16_t* __restrict__ idx,
+                                                     uint64_t* __restrict__ out, uint64_t n) {
+  const uint64_t base = (uint64_t)blockIdx.x * 256 * 2 * NP;
+  uint32_t ix[NP];
+#pragma unroll
+  for (int s = 0; s < NP; ++s) {
+    const uint64_t o = base + ((uint64_t)s * 256 + threadIdx.x) * 2;
+    ix[s] = o + 2 <= n ? *reinterpret_cast<const uint32_t*>(idx + o) : 0u;
+  }
+  uint64_t x[NP][2];
+#pragma unroll
+  for (int s = 0; s < NP; ++s) {
+    x[s][0] = dict[ix[s] & 0xFFFFu];
+    x[s][1] = dict[ix[s] >> 16];
+  }
+#pragma unroll
+  for (int s = 0; s < NP; ++s) {
+    const uint64_t o = base + ((uint64_t)s * 256 + threadIdx.x) * 2;
+    if (o + 2 <= n)
+      *reinterpret_cast<uint4*>(out + o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32), (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
+  }
+}
+
+template <int NT, int NP, int WIN>
+__global__ __launch_bounds__(NT) void k_gather_win2(const uint64_t* __restrict__ dict, uint32_t D,
+                                                    const uint16_t* __restrict__ idx, uint64_t* __restrict__ out,
+                                                    uint64_t n) {
+  __shared__ uint4 sd4[WIN / 2];
+  const uint64_t* sd = reinterpret_cast<const uint64_t*>(sd4);
+  const uint4* dict4 = reinterpret_cast<const uint4*>(dict);
+  constexpr int F = WIN / 2 / NT;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t per = (uint64_t)NT * NP * 2;
+  for (uint64_t base = (uint64_t)blockIdx.x * per; base < n; base += (uint64_t)gridDim.x * per) {
+    uint32_t ix[NP];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const uint64_t o = base + ((uint64_t)s * NT + tid) * 2;
+      ix[s] = o + 2 <= n ? *reinterpret_cast<const uint32_t*>(idx + o) : 0u;
+    }
+    uint64_t x[NP][2];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) x[s][0] = x[s][1] = 0;
+    for (uint32_t w0 = 0; w0 < D; w0 += WIN) {
+      __syncthreads();
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const uint32_t i = f * NT + tid;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(dict4 + w0 / 2 + i),
+                                         (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)sd4 + (f * NT + (tid & ~63u)) * 16), 16, 0, 0);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < NP; ++s) {
+        const uint32_t r0 = (ix[s] & 0xFFFFu) - w0, r1 = (ix[s] >> 16) - w0;
+        if (r0 < (uint32_t)WIN) x[s][0] = sd[r0];
+        if (r1 < (uint32_t)WIN) x[s][1] = sd[r1];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const uint64_t o = base + ((uint64_t)s * NT + tid) * 2;
+      if (o + 2 <= n)
+        *reinterpret_cast<uint4*>(out + o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32), (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
+    }
+  }
+}
+
+// partial LDS slab (first S entries) + L2 for the rest, indices read from HBM, layout B
+template <int NT, int NP>
+__global__ __launch_bounds__(NT) void k_gather_slab2(const uint64_t* __restrict__ dict, uint32_t S,
+                                                     const uint16_t* __restrict__ idx, uint64_t* __restrict__ out,
+                                                     uint64_t n) {
+  __shared__ uint64_t sd[19456];
+  for (uint32_t i = threadIdx.x; i < S; i += NT) sd[i] = dict[i];
+  __syncthreads();
+  const uint32_t tid = threadIdx.x;
+  const uint64_t per = (uint64_t)NT * NP * 2;
+  for (uint64_t base = (uint64_t)blockIdx.x * per; base < n; base += (uint64_t)gridDim.x * per) {
+    uint32_t ix[NP];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const uint64_t o = base + ((uint64_t)s * NT + tid) * 2;
+      ix[s] = o + 2 <= n ? *reinterpret_cast<const uint32_t*>(idx + o) : 0u;
+    }
+    uint64_t x[NP][2];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const uint32_t a = ix[s] & 0xFFFFu, b = ix[s] >> 16;
+      x[s][0] = a < S ? sd[a] : dict[a];
+      x[s][1] = b < S ? sd[b] : dict[b];
+    }
+#pragma unroll
+    for (int s = 0; s < NP; ++s) {
+      const uint64_t o = base + ((uint64_t)s * NT + tid) * 2;
+      if (o + 2 <= n)
+        *reinterpret_cast<uint4*>(out + o) = make_uint4((uint32_t)x[s][0], (uint32_t)(x[s][0] >> 32), (uint32_t)x[s][1], (uint32_t)(x[s][1] >> 32));
+    }
+  }
+}
+
+// u16 index stream write + read alone (the two-kernel split's extra traffic)
+__global__ void k_idx_copy(const uint16_t* __restrict__ a, uint16_t* __restrict__ b, uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n / 8; i += gridDim.x * 256ull)
+    reinterpret_cast<uint4*>(b)[i] = reinterpret_cast<const uint4*>(a)[i];
+}
+
 int main() {
   const uint64_t n = 1000000000ull;
   uint64_t *out, *dict;
@@ -154,6 +264,24 @@ int main() {
     run(g("win NT=512 PT=32 WIN=8192 persistent"), [&] {
       k_gather_win<512, 32, 8192><<<512, 512>>>(dict, D, idx, out, n);
     });
+    run(g("B: L2 gather NP=8"), [&] { k_gather_idx2<8><<<(uint32_t)(n / 4096 + 1), 256>>>(dict, idx, out, n); });
+    run(g("B: L2 gather NP=16"), [&] { k_gather_idx2<16><<<(uint32_t)(n / 8192 + 1), 256>>>(dict, idx, out, n); });
+    run(g("B: win glds NT=1024 NP=16 WIN=16384 pers"), [&] {
+      k_gather_win2<1024, 16, 16384><<<256, 1024>>>(dict, D, idx, out, n);
+    });
+    run(g("B: win glds NT=1024 NP=16 WIN=16384"), [&] {
+      k_gather_win2<1024, 16, 16384><<<(uint32_t)(n / 32768 + 1), 1024>>>(dict, D, idx, out, n);
+    });
+    run(g("B: win glds NT=512 NP=16 WIN=8192 pers"), [&] {
+      k_gather_win2<512, 16, 8192><<<512, 512>>>(dict, D, idx, out, n);
+    });
+    run(g("B: slab S=19456 NT=1024 NP=8 pers"), [&] {
+      k_gather_slab2<1024, 8><<<256, 1024>>>(dict, 19456, idx, out, n);
+    });
+    run(g("B: slab S=19456 NT=1024 NP=16 pers"), [&] {
+      k_gather_slab2<1024, 16><<<256, 1024>>>(dict, 19456, idx, out, n);
+    });
   }
+  run("u16 index copy (2 GB read + 2 GB write)", [&] { k_idx_copy<<<8192, 256>>>(idx, (uint16_t*)out, n); });
   return 0;
 }
