@@ -2172,64 +2172,80 @@ struct LvLevelOut {
 // decoded): per output the entry's index, in the value-length slot (the byte-array scan and copy,
 // pqg_bytes.hip BaSrc, take the entry's address and length from there), and the page's byte total.
 // Scratch slots: the chunk's scr_base (values) and dscr_base (dictionary entries) on.
+// Run by run (wave-uniform): an RLE run's slots are one index; a bit-packed run's outputs go in
+// groups of 4 on 4-aligned slots, one 8-byte stage read and one 16-byte store per group (indices
+// of w <= 14 bits; wider ones one read per output), the groups a run boundary cuts output by
+// output.
 __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t* stage, const uint8_t* blob, uint64_t blob_len,
                                        const LvWin& x, uint32_t base, uint32_t endo, const ChunkWork& ck,
                                        PageWork* pages, ChunkWork* chunks, const uint64_t* __restrict__ dsrc0,
                                        const uint32_t* __restrict__ dlen0, uint64_t* __restrict__ vsrc0,
                                        uint32_t* __restrict__ vlen0, const uint32_t* ldlen) {
-  {
-    gptr<const uint32_t> dlen = gp(dlen0 + ck.dscr_base);
-    gptr<uint32_t> vlen = gp(vlen0 + ck.scr_base);
-    (void)dsrc0;
-    (void)vsrc0;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t ndict = pages[ck.dict_page].num_values;
-    const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
-    const uint64_t go = x.s.out;
-    uint32_t lgn = 1;
-    while (lgn * 2u <= rl.R) lgn *= 2u;
-    uint32_t b = 0, bad = 0;
-    uint64_t bytes = 0;
-    const uint32_t o0 = base + lane;
-    for (uint32_t sp = lgn; sp; sp >>= 1)
-      if (b + sp < rl.R && rl.rstart[b + sp] <= o0) b += sp;
-    constexpr uint32_t U = 4;  // outputs per lane per step: indices, then the gathers together
+  (void)dsrc0;
+  (void)vsrc0;
+  gptr<const uint32_t> dlen = gp(dlen0 + ck.dscr_base);
+  gptr<uint32_t> vlen = gp(vlen0 + ck.scr_base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t ndict = pages[ck.dict_page].num_values;
+  const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
+  const uint64_t go = x.s.out;
+  auto elen = [&](uint32_t idx) -> uint32_t { return idx < ndict ? (ldlen ? ldlen[idx] : dlen[idx]) : 0u; };
+  uint32_t bad = 0;
+  uint64_t bytes = 0;
 #pragma unroll 1
-    for (uint32_t ob = o0; ob < endo; ob += U * WAVE) {
-      uint32_t id[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t o = ob + u * WAVE;
-        id[u] = 0xFFFFFFFFu;
-        if (o >= endo) continue;
-        while (rl.rstart[b + 1] <= o) ++b;
-        const uint32_t inf = rl.rinfo[b];
-        uint32_t idx;
-        if (inf & R_RLE) {
-          idx = inf & 0x7FFFFFFFu;
-        } else {
-          const uint64_t bit = (uint64_t)inf * 8ull + (uint64_t)(o - rl.rstart[b]) * w;
-          idx = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
-        }
-        if (idx >= ndict) bad = 1;  // dict[idx] out of bounds: the reference panics
-        else id[u] = idx;
-      }
-      uint32_t lv[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u)
-        if (id[u] != 0xFFFFFFFFu) lv[u] = ldlen ? ldlen[id[u]] : dlen[id[u]];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u)
-        if (id[u] != 0xFFFFFFFFu) {
-          vlen[go + ob + u * WAVE] = id[u];  // the index (BaSrc in pqg_bytes.hip takes the entry)
-          bytes += lv[u];
-        }
+  for (uint32_t b = 0; b < rl.R; ++b) {
+    const uint32_t rs = rl.rstart[b], re = rl.rstart[b + 1], inf = rl.rinfo[b];
+    const uint32_t st = rs > base ? rs : base, en = re < endo ? re : endo;
+    if (st >= en) continue;
+    if (inf & R_RLE) {
+      const uint32_t idx = inf & 0x7FFFFFFFu;
+      bad |= idx >= ndict ? 1u : 0u;
+      for (uint32_t o = st + lane; o < en; o += WAVE) vlen[go + o] = idx;
+      if (lane == 0) bytes += (uint64_t)elen(idx) * (en - st);
+      continue;
     }
+    const uint64_t bit0 = (uint64_t)inf * 8ull;
+    auto one = [&](uint32_t o) -> uint32_t {  // the index of output o of this run
+      const uint64_t bit = bit0 + (uint64_t)(o - rs) * w;
+      return (uint32_t)(lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u)) & wm;
+    };
+    const uint64_t k0 = (go + st + 3u) / 4u, k1 = (go + en) / 4u;  // 4-aligned groups inside [st, en)
+#pragma unroll 1
+    for (uint64_t k = k0 + lane; k < k1; k += WAVE) {
+      const uint32_t o = (uint32_t)(k * 4u - go);
+      uint32_t id[4];
+      if (w <= 14u) {
+        const uint64_t bit = bit0 + (uint64_t)(o - rs) * w;
+        const uint64_t x8 = lv_bytes8(stage, blob, blob_len, x, (uint32_t)(bit >> 3)) >> (bit & 7u);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off, 64);
-    if (lane == 0 && bytes) atomicAdd((unsigned long long*)&pages[x.p].nbytes_out, (unsigned long long)bytes);
-    if (__ballot(bad) && lane == 0) report(pages, chunks, (int)x.p, ST_PANIC);
+        for (uint32_t j = 0; j < 4; ++j) id[j] = (uint32_t)(x8 >> (j * w)) & wm;
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) id[j] = one(o + j);
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        bad |= id[j] >= ndict ? 1u : 0u;
+        bytes += elen(id[j]);
+      }
+      gst16(reinterpret_cast<gptr<uint8_t>>(vlen + k * 4u), make_uint4(id[0], id[1], id[2], id[3]));
+    }
+    // the cut groups: outputs [st, 4 k0 - go) and [4 k1 - go, en) (at most 3 each), or the whole
+    // run when no group lies inside it
+    const uint32_t h1 = k0 < k1 ? (uint32_t)(k0 * 4u - go) : en, t0 = k0 < k1 ? (uint32_t)(k1 * 4u - go) : en;
+    const uint32_t nh = h1 - st, nt = en - t0;
+    for (uint32_t j = lane; j < nh + nt; j += WAVE) {
+      const uint32_t o = j < nh ? st + j : t0 + (j - nh);
+      const uint32_t idx = one(o);
+      bad |= idx >= ndict ? 1u : 0u;
+      bytes += elen(idx);
+      vlen[go + o] = idx;
+    }
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off, 64);
+  if (lane == 0 && bytes) atomicAdd((unsigned long long*)&pages[x.p].nbytes_out, (unsigned long long)bytes);
+  if (__ballot(bad) && lane == 0) report(pages, chunks, (int)x.p, ST_PANIC);
 }
 
 // Dictionary indices of every chunk on this path (ChunkWork::lvdict), by the chunk's value type:
@@ -2719,6 +2735,21 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
   if (walked) wr.page(chunks[pages[p].chunk], pages, blob, sel, xw);
   LeLoad nf;  // the next window's loads, issued while the current one is written
   nf.ok = false;
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 1024, unpipelined writers): per wave s_memtime cycles in the run
+  // bounds + records, the payload staging and the writes by value size (0: byte arrays, 4, 8),
+  // then the units and outputs written
+  const bool wst = !Writer::PIPE && (chunks[0].cp.debug & 1024) && chunks[0].cp.dbgbuf;
+  uint64_t wt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wt0 = 0;
+#define LW_STAMP(k)                                   \
+  if (wst) {                                          \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+    wt[k] += t1 - wt0;                                \
+    wt0 = t1;                                         \
+  }
+#else
+#define LW_STAMP(k)
+#endif
   uint32_t nb0 = 0, nb1 = 0, nbk = 0;  // run bounds (wfirst) of window nbk of the page, read ahead
   bool nbv = false;
   for (uint32_t g = g0; g < g1; ++g) {
@@ -2741,6 +2772,9 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     const uint2* recp = lt.rec + (uint64_t)LW_REC * (wb + 2ull * p);
     const uint32_t w = (uint32_t)x.s.w;
     if constexpr (!Writer::PIPE) {  // a unit of windows at a time: records and payload straight to LDS
+#ifdef PQG_DIAG
+      if (wst) wt0 = __builtin_amdgcn_s_memtime();
+#endif
       // the unit: windows [x.k, x.k + nu) of this page with at most LW_RPW runs in all (lane i
       // reads the run bound of window x.k + i)
       const uint32_t lim = S > 1 ? 1u : min(LE_UNIT, min(g1, pend) - g);
@@ -2764,12 +2798,22 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
         E.rinfo[i] = r.y;
       }
       x.W0 = x.k * LV_WIN;
+      LW_STAMP(0)
       lv_stage(blob, blob_len, x, E.stage, le_nch(w, nu, LE_STG_U));  // ends with a wave LDS sync (run list too)
+      LW_STAMP(1)
       uint32_t base = E.rstart[0];
       uint32_t endo = endn < x.s.n ? endn : x.s.n;
       if (endo > base) cut(base, endo);
       if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
       wave_lds_sync();
+#ifdef PQG_DIAG
+      if (wst) {
+        const uint32_t es = chunks[pages[p].chunk].es;
+        LW_STAMP(es == 8 ? 4 : es == 4 ? 3 : 2)
+        wt[5] += 1;
+        wt[es ? 6 : 7] += endo > base ? endo - base : 0u;
+      }
+#endif
       continue;
     }
     bool have = nf.ok && nf.k == x.k;
@@ -2824,6 +2868,13 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
     if (endo > base) wr(LvRuns{E.rstart, E.rinfo, R}, E.stage, blob, blob_len, x, base, endo, sel, chunks, pages, xw);
     wave_lds_sync();  // the run list and stage are refilled by the next window
   }
+#ifdef PQG_DIAG
+  if (wst && lane == 0) {
+    uint64_t* d = chunks[0].cp.dbgbuf + 8ull * gw;
+    for (int i = 0; i < 8; ++i) d[i] = wt[i];
+  }
+#endif
+#undef LW_STAMP
 }
 
 // Plan, segment starts and walks, page scan, run compaction: every page of stream `sel` ends

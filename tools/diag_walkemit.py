@@ -1,0 +1,53 @@
+"""Diagnostics: where the walked-page dictionary emit (k_lv_emit_walk<LvDictOut>) spends its
+cycles on config 5 (PQG_DIAG build, PQG_DEBUG=1024): per wave s_memtime cycles in the run bounds
+and records, the payload staging and the writes by value size, per unit and per output.
+
+    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=1024 python tools/diag_walkemit.py [--rowgroups 2]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rowgroups", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+    import pqgpu
+    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", "lib_diag", "libpqgpu.so")
+    L = pqgpu.lib()
+    L.pqg_debug_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    import bench
+    args = bench.parse(["--config", "alltypes", "--rowgroups", str(a.rowgroups)])
+    w = bench.AlltypesWorkload(pqgpu, args, 0, 1)
+    ctx = pqgpu.Context(torch.cuda.current_device())
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):
+        w.decode_step(ctx, s)
+        r = ctx.sync_detail()
+        assert r[0] == 0, r
+    n = 2048 * 16
+    buf = np.zeros(8 * n, np.uint64)
+    assert L.pqg_debug_read(ctx.h, buf.ctypes.data, buf.size) == 0
+    d = buf.reshape(n, 8).astype(np.float64)
+    d = d[d[:, 5] > 0]
+    units, of, ob = d[:, 5].sum(), d[:, 6].sum(), d[:, 7].sum()
+    print(f"waves {len(d)} units {units:.0f} outputs fixed {of:.0f} byte-array {ob:.0f}")
+    tot = d[:, :5].sum()
+    for k, name in enumerate(("bounds+records", "staging", "writes BA", "writes 4 B", "writes 8 B")):
+        print(f"  {name:15s} {d[:, k].sum() / units:9.0f} cycles per unit  ({d[:, k].sum() / tot:.2f} of the stamped)")
+    print(f"  per output: fixed {(d[:, 3].sum() + d[:, 4].sum()) / max(of, 1):.2f}, BA {d[:, 2].sum() / max(ob, 1):.2f} cycles")
+    print(f"  wave busy cycles: mean {d[:, :5].sum(1).mean():.0f} max {d[:, :5].sum(1).max():.0f}")
+
+
+if __name__ == "__main__":
+    main()
