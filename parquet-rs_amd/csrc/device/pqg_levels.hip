@@ -2335,7 +2335,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   // diagnostics (PQG_DEBUG bit 256): per wave s_memtime cycles in the window's staging wait,
   // chain / run placement, bitmap generation and output stores, and the windows written
   const bool stamps = (chunks[0].cp.debug & 256) && chunks[0].cp.dbgbuf;
-  uint64_t ts0 = 0, tacc[4] = {0, 0, 0, 0}, tn = 0, tmiss = 0;
+  uint64_t ts0 = 0, tacc[4] = {0, 0, 0, 0}, tn = 0, tmiss = 0, tw0 = 0, tspec = 0, nspec = 0;
 #define LE_STAMP(k)                                   \
   if (stamps) {                                       \
     const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
@@ -2347,7 +2347,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
 #endif
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
 #ifdef PQG_DIAG
-    if (stamps) ts0 = __builtin_amdgcn_s_memtime();
+    if (stamps) tw0 = ts0 = __builtin_amdgcn_s_memtime();
 #endif
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
     const uint2 wi = pf.ok && pf.p == x.p && pf.k == x.k ? pf.wi : lt.win[D.wb + x.k];
@@ -2581,6 +2581,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
 #ifdef PQG_DIAG
     tn += 1ull | (viaref ? 1ull << 20 : 0ull) | (bm ? 1ull << 40 : 0ull);  // windows | via the reference | bitmap
     tmiss += viaref && !placed ? 1u : 0u;  // the entry's chain missed the meeting point
+    if (stamps && !placed) {  // windows through the segment tables: their whole time
+      tspec += ts0 - tw0;
+      ++nspec;
+    }
 #endif
   }
 #ifdef PQG_DIAG
@@ -2593,6 +2597,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     d[3] = tacc[3];
     d[4] = tn;
     d[5] = tmiss;
+    d[6] = tspec;
+    d[7] = nspec;
   }
 #endif
 #undef LE_STAMP

@@ -39,10 +39,11 @@ def main():
     n = 2048 * 64
     buf = np.zeros(8 * n, np.uint64)
     assert L.pqg_debug_read(ctx.h, buf.ctypes.data, buf.size) == 0
-    raw = buf.reshape(n, 8)[:, :6]
+    raw = buf.reshape(n, 8)
     raw = raw[raw[:, 4] > 0]
     cnt = raw[:, 4]
     miss = raw[:, 5].sum()
+    tspec, nspec = raw[:, 6].astype(np.float64).sum(), raw[:, 7].sum()
     via, bmw = ((cnt >> 20) & 0xFFFFF).sum(), (cnt >> 40).sum()
     d = raw.astype(np.float64)
     d[:, 4] = (cnt & 0xFFFFF).astype(np.float64)
@@ -51,6 +52,9 @@ def main():
           f"bitmap writes {bmw / tot:.3f}")
     for k, name in enumerate(("stage wait", "placement", "bitmap gen", "stores")):
         print(f"  {name:11s} {d[:, k].sum() / tot:9.0f} cycles per window (wave mean {d[:, k].mean():10.0f})")
+    allc = d[:, :4].sum()
+    print(f"  windows through the segment tables: {nspec / tot:.3f} of them, {tspec / max(nspec, 1):.0f} cycles each, "
+          f"{tspec / allc:.2f} of all cycles")
     print("levels_kernel_ms", ctx.timings().levels_kernel_ms)
 
 
