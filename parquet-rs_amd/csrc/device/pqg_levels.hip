@@ -1760,11 +1760,11 @@ struct LvBm {
 // Generation: each lane ORs its own runs' bits (outputs from oa, page-relative) into the bitmap.
 // Returns the lane's count of 1s, or 0xFFFFFFFF for the whole wave at a run the window path does
 // not take.
-__device__ inline uint32_t lv_bm_gen(LvWave& W, const uint8_t* __restrict__ blob, uint64_t blob_len, const LvWin& x,
-                                     const LvBm& B, uint32_t mym, uint64_t oa, uint32_t n) {
+__device__ inline uint32_t lv_bm_gen(const uint32_t* stage, uint32_t* bm, const uint8_t* __restrict__ blob,
+                                     uint64_t blob_len, const LvWin& x, const LvBm& B, uint32_t mym, uint64_t oa,
+                                     uint32_t n) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t slen = x.s.slen, i0 = lane * LV_SEG;
-  uint32_t* bm = reinterpret_cast<uint32_t*>(W.JC);
   wave_lds_sync();  // (the jump table / prefix list is read)
   for (uint32_t i = lane; i < B.nw; i += WAVE) bm[i] = 0u;
   wave_lds_sync();
@@ -1776,7 +1776,7 @@ __device__ inline uint32_t lv_bm_gen(LvWave& W, const uint8_t* __restrict__ blob
     const uint32_t t = (uint32_t)__builtin_ctz(m);
     uint32_t nx, c, v;
     bool bp;
-    lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, 1u, 1u, nx, c, v, bp);  // (a true header: parses)
+    lv_parse4(stage, i0 + t + x.sb, x.W0 + i0 + t, slen, 1u, 1u, nx, c, v, bp);  // (a true header: parses)
     bad |= !lv_run_ok(bp, v, c, oa, n, slen, 1u);
     const uint32_t e = (uint64_t)rs + c < B.rb ? rs + c : B.rb;
 #pragma unroll 1
@@ -1787,7 +1787,7 @@ __device__ inline uint32_t lv_bm_gen(LvWave& W, const uint8_t* __restrict__ blob
       uint32_t bits;
       if (bp) {
         const uint32_t d = q - rs;
-        bits = (uint32_t)(lv_bytes8(W.stage, blob, blob_len, x, v + (d >> 3)) >> (d & 7u)) & mk;
+        bits = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, v + (d >> 3)) >> (d & 7u)) & mk;
       } else {
         bits = (v & 1u) ? mk : 0u;
       }
@@ -1811,11 +1811,10 @@ __device__ inline uint32_t lv_bm_gen(LvWave& W, const uint8_t* __restrict__ blob
 // Stores: the bitmap expanded, one contiguous KiB per store instruction (chunks shared with a
 // neighbouring window element by element), and the page's def count.
 template <int OUT>
-__device__ inline void lv_bm_store(LvWave& W, const LvWin& x, const LvBm& B, uint32_t cnt, int sel, PageWork* pages,
-                                   gptr<uint8_t> __restrict__ out) {
+__device__ inline void lv_bm_store(const uint32_t* bm, const LvWin& x, const LvBm& B, uint32_t cnt, int sel,
+                                   PageWork* pages, gptr<uint8_t> __restrict__ out) {
   constexpr uint32_t V = 16u / OUT;  // outputs per 16-byte chunk
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t* bm = reinterpret_cast<const uint32_t*>(W.JC);
   wave_lds_sync();
   gptr<uint8_t> ob = out + B.A0 * OUT;
   // chunks [c0, c1) lie inside [ra, rb); chunk ka (holding ra) and kb (holding rb - 1) may not
@@ -2317,6 +2316,48 @@ struct LvDictOut {
   }
 };
 
+// Bit width 1, the true entry's chain meets the window's reference chain at `me`: the window's
+// true headers are the reference chain's (k_lv_win's mask per segment, refm) from the meeting
+// point on, plus the entry's own headers before it, which one lane walks into per-segment masks
+// (pm: 65 LDS words). Sets the lane's header mask (mym), its segment's outputs (so), their place
+// (myacc) and the window's total (T); false (wave-uniform) when the walk does not land on the
+// meeting point (a table k_lv_win made wrong: the caller takes the chain walk instead).
+__device__ inline bool lv_ref_headers(const uint32_t* stage, uint32_t* pm, const LvWin& x, uint32_t e0, uint32_t me,
+                                      uint32_t refm, uint32_t& mym, uint64_t& so, uint64_t& myacc, uint64_t& T) {
+  constexpr uint32_t SEG = LV_SEG;
+  const uint32_t lane = threadIdx.x & 63u, i0 = lane * SEG, slen = x.s.slen;
+  pm[lane] = 0u;
+  wave_lds_sync();
+  if (lane == 0) {
+    uint32_t qq = e0;
+    while (qq < me) {  // (every hop advances: at most LV_WIN + 64 of them)
+      uint32_t nx, c, v;
+      bool bp;
+      if (!lv_parse4(stage, qq + x.sb, x.W0 + qq, slen, 1u, 1u, nx, c, v, bp)) break;
+      pm[qq / SEG] |= 1u << (qq % SEG);
+      qq = nx - x.W0;
+    }
+    pm[64] = qq == me ? 1u : 0u;
+  }
+  wave_lds_sync();
+  if (!pm[64]) return false;
+  mym = (i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0))) | pm[lane];
+  // outputs of this segment's true headers, then their place: a lane scan
+  so = 0;
+#pragma unroll 1
+  for (uint32_t m = mym; m; m &= m - 1u) {
+    const uint32_t t = (uint32_t)__builtin_ctz(m);
+    uint32_t nx, c, v;
+    bool bp;
+    lv_parse4(stage, i0 + t + x.sb, x.W0 + i0 + t, slen, 1u, 1u, nx, c, v, bp);  // (chain headers parse)
+    so += c;
+  }
+  const uint64_t si = wave_incl_scan_cnt64(so);
+  myacc = si - so;
+  T = __shfl(si, 63, 64);
+  return true;
+}
+
 // ------------------------------------------------------------------------------ k_lv_emit
 // Window path: windows g2 of the dense pages.
 template <int OUT>
@@ -2382,41 +2423,11 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
     bool bm = false;
     bool placed = false;  // (wave-uniform) the window's true headers found
     if (viaref) {
-      constexpr uint32_t SEG = LV_SEG;
-      const uint32_t me = nh, i0 = lane * SEG;
-      // the entry's own headers before the meeting point: one lane, serially, as a mask per
-      // segment (pm[s]); pm[64]: the walk landed on the meeting point
-      uint32_t* pm = W.runs.rinfo;  // (the run list is written after these are read)
-      pm[lane] = 0u;
-      wave_lds_sync();
-      if (lane == 0) {
-        uint32_t qq = e0;
-        while (qq < me) {  // (every hop advances: at most LV_WIN + 64 of them)
-          uint32_t nx, c, v;
-          bool bp;
-          if (!lv_parse4(W.stage, qq + x.sb, x.W0 + qq, slen, w, vb, nx, c, v, bp)) break;
-          pm[qq / SEG] |= 1u << (qq % SEG);
-          qq = nx - x.W0;
-        }
-        pm[64] = qq == me ? 1u : 0u;
-      }
-      wave_lds_sync();
-      if (pm[64]) {  // (else a table k_lv_win made wrong: the window takes the chain walk below)
+      const uint32_t i0 = lane * LV_SEG;
+      uint64_t so = 0;
+      // (pm: the run list's space, written after the masks are read)
+      if (lv_ref_headers(W.stage, W.runs.rinfo, x, e0, nh, refm, mym, so, myacc, T)) {
         placed = true;
-        mym = (i0 + SEG <= me ? 0u : i0 >= me ? refm : refm & (0xFFFFu << (me - i0))) | pm[lane];
-        // outputs of this segment's true headers, then their place: a lane scan
-        uint64_t so = 0;
-#pragma unroll 1
-        for (uint32_t m = mym; m; m &= m - 1u) {
-          const uint32_t t = (uint32_t)__builtin_ctz(m);
-          uint32_t nx, c, v;
-          bool bp;
-          lv_parse4(W.stage, i0 + t + x.sb, x.W0 + i0 + t, slen, w, vb, nx, c, v, bp);  // (chain headers parse)
-          so += c;
-        }
-        const uint64_t si = wave_incl_scan_cnt64(so);
-        myacc = si - so;
-        T = __shfl(si, 63, 64);
         bm = lv_bm_fits(x, base, (uint64_t)base + T < n ? (uint64_t)base + T : (uint64_t)n, so);
         wave_lds_sync();  // (the prefix masks are read)
         if (!bm) {
@@ -2559,12 +2570,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       LE_STAMP(1)
       if (endo > base) {
         const LvBm B(x, base, (uint32_t)endo);
-        const uint32_t cnt = lv_bm_gen(W, blob, blob_len, x, B, mym, (uint64_t)base + myacc, n);
+        const uint32_t cnt = lv_bm_gen(W.stage, reinterpret_cast<uint32_t*>(W.JC), blob, blob_len, x, B, mym,
+                                       (uint64_t)base + myacc, n);
         LE_STAMP(2)
         if (cnt == 0xFFFFFFFFu) {
           if (lane == 0) LV_BAIL(rt, lt, x.p, PF_PAGE, 5);
         } else {
-          lv_bm_store<OUT>(W, x, B, cnt, sel, pages, gp(D.out));
+          lv_bm_store<OUT>(reinterpret_cast<const uint32_t*>(W.JC), x, B, cnt, sel, pages, gp(D.out));
         }
       }
     } else {
