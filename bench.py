@@ -889,7 +889,15 @@ def main(argv=None):
     dist = None
     if world > 1:  # barrier + max over ranks: two host scalars, gloo (no RCCL on this path)
         import torch.distributed as td
-        td.init_process_group("gloo")
+        # (gloo prints its connection report on stdout: kept off it, which carries only the JSON line)
+        sys.stdout.flush()
+        keep = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            td.init_process_group("gloo")
+        finally:
+            os.dup2(keep, 1)
+            os.close(keep)
         dist = td
     if args.dry_run:
         dry_run(args, world, rank, dist)
@@ -897,7 +905,8 @@ def main(argv=None):
             dist.destroy_process_group()
         return
     import torch
-    torch.cuda.set_device(local if world > 1 else 0)
+    # PQG_BENCH_DEVICE: every rank on one device (rehearsing the multi-rank path on a 1-GPU box)
+    torch.cuda.set_device(int(os.environ.get("PQG_BENCH_DEVICE", local if world > 1 else 0)))
     import pqgpu
     stream = torch.cuda.current_stream().cuda_stream
     head = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
