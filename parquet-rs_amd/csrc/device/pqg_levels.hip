@@ -1264,19 +1264,39 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
   LvPf pf;
   pf.ok = false;
   if (!D.begin(blob, pages, npages, chunks, sel, rt, lt, x)) return;
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 2048, bit width 1): per wave s_memtime cycles in the stage wait, the
+  // segment tables, the chain from 0 and the entry walks, the reference choice (and second chain),
+  // the table writes; the windows, and those that needed a second chain
+  const bool wst = (chunks[0].cp.debug & 2048) && chunks[0].cp.dbgbuf;
+  uint64_t wt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wt0 = 0;
+#define LWN_STAMP(k)                                  \
+  if (wst) {                                          \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+    wt[k] += t1 - wt0;                                \
+    wt0 = t1;                                         \
+  }
+#else
+#define LWN_STAMP(k)
+#endif
   for (uint32_t g2 = D.g0; g2 < D.g1; ++g2) {
     if (!D.at(blob, pages, chunks, sel, rt, lt, x, g2)) continue;
+#ifdef PQG_DIAG
+    if (wst) wt0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t g = D.wb + x.k;
     x.W0 = x.k * LV_WIN;
     const uint32_t w = (uint32_t)x.s.w;
     pf.stage(blob, blob_len, x, W.stage);
     if (g2 + 1 < D.g1 && g2 + 1 < D.pend) pf.issue(blob, blob_len, x, x.k + 1);
+    LWN_STAMP(0)
     // table of the entry offsets: (exit offset from W0 or terminal code | headers << 16, outputs)
     const uint32_t ent = lv_ent(w);
     uint2* tab = lt.tab + (uint64_t)g * lt.tstride;
     if (w == 1) {  // 64 entry offsets: lane e follows entry e across the segments
       uint32_t pc[LV_SEG], pv[LV_SEG], bpm;
       lv_seg_build(W, x, pc, pv, bpm);
+      LWN_STAMP(1)
       uint32_t e = lane, c = 0, me = 0xFFFFu;
       // the chain from position 0, speculatively (lv_spec_chain); each entry's chain is then
       // followed only until it meets it (me: where), the rest from the chain's per-segment suffix
@@ -1316,6 +1336,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
           c = s2 < c ? 0xFFFFFFFFu : s2;
         }
       }
+      LWN_STAMP(2)
       // the reference chain of the window's emit (k_lv_emit: the true chain's headers are its
       // headers from where the true entry's chain meets it, and the few before): the chain most
       // entries leave the window by (the chain from 0 when entry 0 is one of them), so that the
@@ -1355,9 +1376,17 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
           }
         }
       }
+#ifdef PQG_DIAG
+      if (wst) wt[6] += spec && e0x != bx ? 1u : 0u;
+#endif
+      LWN_STAMP(3)
       lt.bmp[(uint64_t)g * WAVE + lane] = ref;
       tab[lane] = make_uint2(e | (me << 16), c);
       wave_lds_sync();  // the next window's stage and table
+      LWN_STAMP(4)
+#ifdef PQG_DIAG
+      if (wst) wt[5] += 1;
+#endif
       continue;
     }
     uint32_t jv[LV_PPL], cv[LV_PPL];
@@ -1368,6 +1397,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       if (i < ent) tab[i] = make_uint2(jv[j], cv[j]);
     }
   }
+#ifdef PQG_DIAG
+  if (wst && lane == 0) {
+    uint64_t* d = chunks[0].cp.dbgbuf + 8ull * (blockIdx.x * (WG / WAVE) + wid);
+    for (int i = 0; i < 8; ++i) d[i] = wt[i];
+  }
+#endif
+#undef LWN_STAMP
 }
 
 // ------------------------------------------------------------------------------ k_lv_stitch
