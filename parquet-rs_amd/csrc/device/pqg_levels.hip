@@ -1125,7 +1125,17 @@ __device__ inline void lv_seg_build(LvWave& W, const LvWin& x, uint32_t (&pc)[LV
 #define PQG_LV_SPK 4
 #endif
 constexpr uint32_t LV_SPK = PQG_LV_SPK;  // segments walked per guess
-constexpr uint32_t LV_SPR = 4;  // repair rounds
+#ifndef PQG_LV_SPEND
+#define PQG_LV_SPEND 1
+#endif
+#ifndef PQG_LV_SPR
+#define PQG_LV_SPR 4
+#endif
+constexpr uint32_t LV_SPR = PQG_LV_SPR;  // repair rounds
+#ifndef PQG_LV_K2
+#define PQG_LV_K2 4
+#endif
+constexpr uint32_t LV_K2 = PQG_LV_K2;  // window path: segments walked before the second chain (0: none)
 
 __device__ inline bool lv_spec_chain(const LvWave& W, uint32_t e0, uint64_t lim, uint32_t& q, bool& valid, uint2& r,
                                      uint64_t& inc) {
@@ -1146,7 +1156,22 @@ __device__ inline bool lv_spec_chain(const LvWave& W, uint32_t e0, uint64_t lim,
     const bool okl = xq < LV_WIN ? nxt < 64u && gn == xq : nxt == 64u;
     const uint32_t c = valid ? r.y : 0u;
     inc = wave_incl_scan_cnt(c);
-    if (!__any(valid && inc - c < lim && inc < lim && !okl)) return true;
+    const uint64_t bad = __ballot(valid && inc - c < lim && inc < lim && !okl);
+    if (!bad) return true;
+#if PQG_LV_SPEND
+    // the lanes up to the first bad one are verified; if that one leaves the window (or ends the
+    // stream) the chain ends there and the guesses after it are off it (repairing them would take
+    // a round per lane)
+    const uint32_t b = (uint32_t)__builtin_ctzll(bad);
+    if ((uint32_t)__shfl((int)xq, (int)b, 64) >= LV_WIN) {
+      if (lane > b) {
+        valid = false;
+        r = make_uint2(LV_J_END, 0u);
+      }
+      inc = wave_incl_scan_cnt(valid ? r.y : 0u);
+      return true;
+    }
+#endif
     if (round == LV_SPR) return false;
     // repair: from the guess of the valid lane before this one (e0 for the lanes before any)
     const uint64_t before = vm & ((1ull << lane) - 1ull);
@@ -1318,6 +1343,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
         sp[128 + lane] = cs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cs;
         wave_lds_sync();
       }
+      // entries still off the chain after LV_K2 segments are mostly on one other chain (when
+      // position 0 is inside a run's values its chain soon ends: 21% of the windows at p_null
+      // 0.1): that chain too is built speculatively, from the first such entry, and they meet it
+      // instead of walking every segment of the window
+      uint32_t exit2 = LV_J_END, hops = 0, m2 = 0xFFFFu;  // m2: where the second chain meets the first
+      uint32_t ref2 = 0;  // the second chain's headers in this lane's segment
+      bool two = false;
 #pragma unroll 1
       while (__any(e < LV_WIN)) {
         if (e < LV_WIN) {
@@ -1327,6 +1359,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
             me = me == 0xFFFFu ? e : me;
             dc = sp[128 + sg];
             e = exitc;
+          } else if (two && sp[64 + sg] == e) {  // on the second chain: its rest
+            me = me == 0xFFFFu ? m2 : me;
+            dc = sp[192 + sg];
+            e = exit2;
           } else {
             const uint2 t = W.JC[(e % LV_SEG) * WAVE + sg];
             dc = t.y;
@@ -1334,6 +1370,30 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
           }
           const uint32_t s2 = c + dc;
           c = s2 < c ? 0xFFFFFFFFu : s2;
+        }
+        if (++hops == LV_K2 && spec) {
+          const uint64_t un = __ballot(e < LV_WIN);
+          if (un) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(un);  // (from that entry: the whole chain)
+            uint32_t q2;
+            bool v2;
+            uint2 r2;
+            uint64_t ci2;
+            if (lv_spec_chain(W, f, ~0ull, q2, v2, r2, ci2)) {
+              const uint32_t cc = v2 ? r2.y : 0u;
+              const uint64_t ctot = __shfl(ci2, 63, 64);
+              const uint64_t vm = __ballot(v2);
+              exit2 = (uint32_t)__shfl((int)(r2.x & 0xFFFFu), 63 - __builtin_clzll(vm), 64);
+              const uint64_t cs = ctot - ci2 + cc;
+              sp[64 + lane] = v2 ? q2 : LV_NONE;
+              ref2 = v2 ? r2.x >> 16 : 0u;
+              sp[192 + lane] = cs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cs;
+              const uint64_t mg = __ballot(v2 && sp[lane] == q2);
+              m2 = mg ? (uint32_t)__builtin_amdgcn_readlane((int)q2, (int)__builtin_ctzll(mg)) : 0xFFFFu;
+              wave_lds_sync();
+              two = true;
+            }
+          }
         }
       }
       LWN_STAMP(2)
@@ -1358,19 +1418,29 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       const uint32_t e0x = (uint32_t)__builtin_amdgcn_readlane((int)e, 0);
       if (!spec) me = 0xFFFFu;
       if (spec && e0x != bx) {  // another chain leaves by the majority exit: it is the reference
-        wave_lds_sync();  // (every read of sp is done)
+        uint32_t sb = 64;       // (the second chain's positions when it is that chain)
+        bool rk = true;
         me = 0xFFFFu;
-        ref = 0;
-        if (lv_spec_chain(W, bl, ~0ull, q, valid, r, ci)) {
-          sp[lane] = valid ? q : LV_NONE;
-          ref = (uint16_t)(valid ? (r.x >> 16) : 0u);
-          wave_lds_sync();
+        if (two && exit2 == bx) {
+          ref = (uint16_t)ref2;
+        } else {
+          wave_lds_sync();  // (every read of sp is done)
+          sb = 0;
+          ref = 0;
+          rk = lv_spec_chain(W, bl, ~0ull, q, valid, r, ci);
+          if (rk) {
+            sp[lane] = valid ? q : LV_NONE;
+            ref = (uint16_t)(valid ? (r.x >> 16) : 0u);
+            wave_lds_sync();
+          }
+        }
+        if (rk) {  // where the entries that leave by it meet it (those that do not never do)
           uint32_t f = lane;
 #pragma unroll 1
-          while (__any(f < LV_WIN && me == 0xFFFFu)) {
-            if (f < LV_WIN && me == 0xFFFFu) {
+          while (__any(f < LV_WIN && me == 0xFFFFu && e == bx)) {
+            if (f < LV_WIN && me == 0xFFFFu && e == bx) {
               const uint32_t sg = f / LV_SEG;
-              if (sp[sg] == f) me = f;
+              if (sp[sb + sg] == f) me = f;
               else f = W.JC[(f % LV_SEG) * WAVE + sg].x & 0xFFFFu;
             }
           }
@@ -1378,6 +1448,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
       }
 #ifdef PQG_DIAG
       if (wst) wt[6] += spec && e0x != bx ? 1u : 0u;
+      // entry-walk steps, windows whose chain from 0 failed, those with a second chain
+      if (wst) wt[7] += hops + (!spec ? (1ull << 24) : 0ull) + (two ? (1ull << 44) : 0ull);
 #endif
       LWN_STAMP(3)
       lt.bmp[(uint64_t)g * WAVE + lane] = ref;

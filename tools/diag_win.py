@@ -24,7 +24,8 @@ def main():
     a = ap.parse_args()
     import torch
     import pqgpu
-    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", "lib_diag", "libpqgpu.so")
+    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", os.environ.get("PQG_DIAG_LIBDIR", "lib_diag"),
+                                  "libpqgpu.so")
     L = pqgpu.lib()
     L.pqg_debug_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     import bench
@@ -39,10 +40,14 @@ def main():
     n = 2048 * 16
     buf = np.zeros(8 * n, np.uint64)
     assert L.pqg_debug_read(ctx.h, buf.ctypes.data, buf.size) == 0
-    d = buf.reshape(n, 8).astype(np.float64)
-    d = d[d[:, 5] > 0]
+    raw = buf.reshape(n, 8)
+    raw = raw[raw[:, 5] > 0]
+    d = raw.astype(np.float64)
     win, sec = d[:, 5].sum(), d[:, 6].sum()
-    print(f"waves {len(d)} windows {win:.0f}, second chain {sec / win:.3f}")
+    steps, tried, two = (raw[:, 7] & 0xFFFFFF).sum(), ((raw[:, 7] >> 24) & 0xFFFFF).sum(), (raw[:, 7] >> 44).sum()
+    print(f"waves {len(d)} windows {win:.0f}, reference not from 0 {sec / win:.3f}, "
+          f"entry-walk steps {steps / win:.1f} per window, chain from 0 failed {tried / win:.3f}, "
+          f"second entry chain {two / win:.3f}")
     for k, name in enumerate(("stage wait", "segment tables", "chain + entries", "reference", "writes")):
         print(f"  {name:15s} {d[:, k].sum() / win:9.0f} cycles per window")
 
