@@ -44,8 +44,12 @@ namespace pqg {
 
 constexpr uint32_t LV_WIN = 1024;                  // stream bytes per window (one wave)
 constexpr uint32_t LV_PPL = LV_WIN / WAVE;         // positions per lane (16)
-constexpr uint32_t LV_STG = LV_WIN + 48;           // window path: staged bytes (+ alignment, read-ahead)
-constexpr uint32_t LV_STG_CH = LV_STG / 16;        // 16-byte chunks (67)
+#ifndef PQG_LV_STG_EXTRA
+#define PQG_LV_STG_EXTRA 48
+#endif
+constexpr uint32_t LV_STG = LV_WIN + PQG_LV_STG_EXTRA;  // window path: staged bytes (+ alignment, read-ahead)
+constexpr uint32_t LV_STG_CH = LV_STG / 16;             // 16-byte chunks
+static_assert(LV_STG % 16 == 0 && LV_STG_CH <= 2 * 64, "two chunks per lane at most");
 constexpr uint32_t LV_RCAP = LV_WIN;               // runs per window
 constexpr uint32_t LV_ROUNDS = 10;                 // 2^10 = LV_WIN: chains of any length
 constexpr uint32_t LV_SERIAL = 64;                 // k_lv_emit: windows with at most this many
