@@ -1849,6 +1849,10 @@ constexpr uint32_t LV_BM_SPAN = 2048;         // outputs one lane generates at m
 #define PQG_LV_BM 1  // (0: every dense window through the run list, for A/B runs)
 #endif
 
+#ifndef PQG_LV_BMW
+#define PQG_LV_BMW 1  // lv_bm_gen: payload bits by aligned dword pairs (0: unaligned 8-byte reads)
+#endif
+
 __device__ inline bool lv_bm_fits(const LvWin& x, uint32_t base, uint64_t endo, uint64_t span) {
   if (!PQG_LV_BM) return false;
   const uint64_t lo = x.s.out + base, hi = x.s.out + endo;
@@ -1899,7 +1903,17 @@ __device__ inline uint32_t lv_bm_gen(const uint32_t* stage, uint32_t* bm, const 
       uint32_t bits;
       if (bp) {
         const uint32_t d = q - rs;
+#if PQG_LV_BMW
+        // 32 payload bits from the staged words: one aligned dword pair and a funnel shift
+        const uint32_t r = v - x.W0 + x.sb;  // (the run's payload, stage-relative)
+        const uint32_t B = r * 8u + d;
+        if (v >= x.W0 && (B >> 3) + 8u <= x.cap)
+          bits = __builtin_amdgcn_alignbit(stage[(B >> 5) + 1u], stage[B >> 5], B & 31u) & mk;
+        else
+          bits = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, v + (d >> 3)) >> (d & 7u)) & mk;
+#else
         bits = (uint32_t)(lv_bytes8(stage, blob, blob_len, x, v + (d >> 3)) >> (d & 7u)) & mk;
+#endif
       } else {
         bits = (v & 1u) ? mk : 0u;
       }
