@@ -1527,7 +1527,7 @@ static uint64_t delta_sub_u64(int t, int64_t l, int64_t r) {
 size_t or_delta_encode_shape(int t, const void *values, size_t n, size_t block_size,
                              size_t num_mini_blocks, uint8_t *out, size_t cap) {
   if (block_size == 0 || num_mini_blocks == 0 || block_size % num_mini_blocks ||
-      (block_size / num_mini_blocks) % 8 || block_size > 65536)
+      (block_size / num_mini_blocks) % 8 || block_size > (1u << 22))
     return (size_t)-1;
   const size_t mini = block_size / num_mini_blocks;
   uint8_t hdr[32];

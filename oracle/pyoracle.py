@@ -233,7 +233,7 @@ def delta_encode(ptype, values, block_size=128, mini_blocks=4):
     """DeltaBitPackEncoder (encoding.rs:534-714); the reference writes 128 / 4 x 32 blocks,
     other shapes exercise what the decoder accepts (decoding.rs:501-533)."""
     v = np.ascontiguousarray(values, dtype=np.int32 if ptype == INT32 else np.int64)
-    cap = len(v) * 10 + 256 + 16 * (len(v) // max(block_size, 1) + 2)
+    cap = len(v) * 10 + 256 + (16 + mini_blocks) * (len(v) // max(block_size, 1) + 2)
     if (block_size, mini_blocks) == (128, 4):
         return _enc(lib().or_delta_encode, ptype, _ptr(v), len(v), cap=cap)
     return _enc(lib().or_delta_encode_shape, ptype, _ptr(v), len(v), block_size, mini_blocks, cap=cap)

@@ -11,8 +11,8 @@
 //          page decoded by k_ba_dict_prep, DELTA_LENGTH_BYTE_ARRAY :682-712, DELTA_BYTE_ARRAY
 //          :768-835), and the page's output byte count;
 //   scan   k_scan_bytes: page byte offsets, capacity check, final offset;
-//   copy   k_ba_copy (gathers slices) and k_dba_copy (DELTA_BYTE_ARRAY: value i = the first
-//          prefix_i bytes of value i-1 ++ suffix_i, rebuilt in an LDS buffer per page).
+//   copy   k_ba_copy (gathers slices) and the DELTA_BYTE_ARRAY rebuild (value i = the first
+//          prefix_i bytes of value i-1 ++ suffix_i, as slices of earlier suffixes: k_dba_*).
 //
 // PLAIN BYTE_ARRAY lengths are inline ([u32 len][bytes]...), so value starts form a serial
 // chain: one lane walks it over LDS-staged 16 KiB regions of the page.
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(WG) k_badict_fallback(const uint8_t* __restric
     if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
     return;
   }
-  if (pages[ck.dict_page].status != 0) return;
+  if (!dict_usable(pages, ck)) return;
   if (threadIdx.x < 64) {
     const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
                                  rt.nruns + pw.ltile0, ism);
@@ -455,9 +455,12 @@ constexpr uint32_t BA_VPT = 16;            // values per thread
 constexpr uint32_t BA_T = BA_VPT * WG;     // values per tile: the pages' RUN_TILE tiles (ltile0, ntiles)
 static_assert(BA_T == RUN_TILE, "byte-array tiles are the page table's tiles");
 
-__device__ inline bool ba_page_ok(const PageWork& pw, const ChunkWork& ck) {
+// (a dictionary page's data pages: only with a usable dictionary, dict_usable, as their index
+// producers take them)
+__device__ inline bool ba_page_ok(const PageWork* pages, const PageWork& pw, const ChunkWork& ck) {
   return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) && ck.es == 0 && ck.val_out &&
-         pw.encoding != E_DELTA_BYTE_ARRAY && ck.res.total_bytes <= ck.val_cap;
+         pw.encoding != E_DELTA_BYTE_ARRAY && ck.res.total_bytes <= ck.val_cap &&
+         (pw.encoding != E_RLE_DICTIONARY || dict_usable(pages, ck));
 }
 
 // Value k of a byte-array page (k: its index among the chunk's values): source address and length.
@@ -470,8 +473,8 @@ struct BaSrc {
   const uint64_t* dsrc;
   const uint32_t* dlen;
   bool via_dict;
-  uint32_t nd;  // dictionary entries: an index slot the level path did not write (a failed page's:
-                // the kernels run before the status is read; the scratch is not cleared) is empty
+  uint32_t nd;  // dictionary entries: the consumers take only pages whose index slots were written
+                // (ba_page_ok / dict_usable); an index past the dictionary still reads as empty
   __device__ BaSrc(const ChunkWork& ck, const PageWork& pw, const PageWork* pages, const uint64_t* vsrc0,
                    const uint32_t* vlen0, const uint64_t* dsrc0, const uint32_t* dlen0)
       : vsrc(vsrc0 + ck.scr_base), vlen(vlen0 + ck.scr_base), dsrc(dsrc0 + ck.dscr_base),
@@ -500,7 +503,7 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pw, ck)) return;
+  if (!ba_page_ok(pages, pw, ck)) return;
   const uint32_t t = gt - pw.ltile0;
   const BaSrc bs(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
   const uint64_t n = pw.nonnull, vo = pw.value_out;
@@ -520,7 +523,7 @@ __global__ void __launch_bounds__(WG) k_ba_tscan(PageWork* pages, const ChunkWor
   __shared__ DeltaSmem sm;
   const uint32_t p = blockIdx.x;
   const PageWork pw = pages[p];
-  if (!ba_page_ok(pw, chunks[pw.chunk])) return;
+  if (!ba_page_ok(pages, pw, chunks[pw.chunk])) return;
   const uint32_t nt = (uint32_t)((pw.nonnull + BA_T - 1) / BA_T);
   uint64_t carry = pw.byte_out;
   uint64_t* ts = tsum + pw.ltile0;
@@ -594,7 +597,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pw, ck) || ba_small_dict(pw, ck, pages)) return;  // (small dictionaries: k_ba_copy_sd)
+  if (!ba_page_ok(pages, pw, ck) || ba_small_dict(pw, ck, pages)) return;  // (small dictionaries: k_ba_copy_sd)
   const uint32_t t = gt - pw.ltile0;
   const BaSrc bs(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
   const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
@@ -747,7 +750,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pw, ck) || !ba_small_dict(pw, ck, pages)) return;
+  if (!ba_page_ok(pages, pw, ck) || !ba_small_dict(pw, ck, pages)) return;
   const uint32_t t = gt - pw.ltile0;
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   const uint64_t t0 = (uint64_t)t * BA_T;
@@ -820,45 +823,327 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   }
 }
 
-// DELTA_BYTE_ARRAY values (decoding.rs:788-822), one wave per page: the previous value lives
-// in LDS; value i overwrites bytes [prefix_i, prefix_i + suffix_len) of it and is then
-// streamed to the output.
-constexpr int DBA_PREV = 32768;
+// ====================================================================== DELTA_BYTE_ARRAY rebuild
+//
+// Value i = the first pre_i bytes of value i-1 ++ suffix_i (DeltaByteArrayDecoder::get,
+// decoding.rs:794-822): a serial dependency from value to value. Unrolled, byte j of value i is
+// byte j of value k = max{k <= i : pre_k <= j}, i.e. a byte of k's suffix. With a = psv(i) =
+// max{k < i : pre_k < pre_i} (the previous strictly smaller prefix length), every value in
+// (a, i) has pre >= pre_i, so bytes [pre_a, pre_i) of value i are suffix_a's first
+// pre_i - pre_a bytes, and bytes [0, pre_a) are value a's, by the same rule from a. A value is
+// therefore a few slices of earlier suffixes (its chain i, psv(i), psv(psv(i)), ... down to a
+// prefix length of 0), each copied straight from the page into the output; nothing is rebuilt
+// value by value and there is no length limit. Four passes over the tiles of BA_T values:
+//   k_dba_tiles  per tile: byte total (sum of pre + suffix length), the prefix-length minimum of
+//                each 64-value block and of the tile;
+//   k_dba_pages  per page: the tiles' byte starts (page byte_out + scan) and each tile's
+//                previous tile of smaller minimum (tpsv, a pointer jump over the tiles);
+//   k_dba_psv    per tile: value offsets (in-tile scan), psv of every value: its own block, then
+//                the tile's blocks (minima in LDS), then earlier tiles through tpsv and their
+//                block minima (at most ~64 + 64 steps + the tile jumps + 64 + 64);
+//   k_dba_copy   per tile: each lane its values' slices (suffix first, then the chain); slices
+//                longer than DBA_LONG are queued in LDS and copied by whole waves.
+// Validity (pre_i <= length of value i-1, pre_0 = 0) is checked by k_ba_index, so every chain
+// ends at a value of prefix length 0.
+constexpr uint32_t DBA_NONE = 0xFFFFFFFFu;
+constexpr uint32_t DBA_TSTRIDE = 66;  // per tile: 64 block minima, the tile minimum, tpsv
+constexpr uint32_t DBA_LONG = 256;    // slices longer than this: copied by a whole wave
+constexpr uint32_t DBA_QCAP = 512;    // queued long slices per tile
 
-__global__ void __launch_bounds__(64) k_dba_copy(const uint8_t* __restrict__ blob, PageWork* pages,
-                                                 ChunkWork* chunks, const uint64_t* __restrict__ vsrc0,
-                                                 const uint32_t* __restrict__ vlen0,
-                                                 const uint32_t* __restrict__ vpre0) {
-  __shared__ uint8_t prev[DBA_PREV];
-  const int p = blockIdx.x;
+__device__ inline bool dba_page_ok(const PageWork& pw, const ChunkWork& ck) {
+  return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) && pw.encoding == E_DELTA_BYTE_ARRAY &&
+         ck.es == 0 && ck.val_out && ck.res.total_bytes <= ck.val_cap;
+}
+
+__global__ void __launch_bounds__(WG) k_dba_tiles(PageWork* pages, const ChunkWork* chunks,
+                                                  const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
+                                                  const uint32_t* __restrict__ vlen0, const uint32_t* __restrict__ vpre0,
+                                                  uint64_t* __restrict__ tsum, uint32_t* __restrict__ dtile) {
+  __shared__ uint64_t red[WG / 64];
+  __shared__ uint32_t mred[WG / 64];
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
-  if (pw.status != 0) return;
-  if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
-  if (pw.encoding != E_DELTA_BYTE_ARRAY) return;
   const ChunkWork& ck = chunks[pw.chunk];
-  if (ck.es != 0 || !ck.val_out || ck.res.total_bytes > ck.val_cap) return;
-  const uint64_t* vsrc = vsrc0 + ck.scr_base;
-  const uint32_t* vlen = vlen0 + ck.scr_base;
-  const uint32_t* vpre = vpre0 + ck.scr_base;
-  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
-  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
-  const uint32_t lane = threadIdx.x;
-  const uint64_t n = pw.nonnull, vo = pw.value_out;
-  uint64_t d = pw.byte_out;
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint32_t pl = vpre[vo + i], sl = vlen[vo + i];
-    const uint64_t tot = (uint64_t)pl + sl;
-    if (tot > DBA_PREV) {  // values longer than the LDS buffer: not supported yet
-      if (lane == 0) report(pages, chunks, p, ST_NYI);
-      return;
+  if (!dba_page_ok(pw, ck)) return;
+  const uint64_t n = pw.nonnull, t0 = (uint64_t)(gt - pw.ltile0) * BA_T;
+  if (t0 >= n) return;
+  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
+  const uint32_t* vlen = vlen0 + ck.scr_base + pw.value_out + t0;
+  const uint32_t* vpre = vpre0 + ck.scr_base + pw.value_out + t0;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  uint32_t* dt = dtile + (uint64_t)gt * DBA_TSTRIDE;
+  uint64_t s = 0;
+  uint32_t tm = DBA_NONE;
+#pragma unroll 4
+  for (uint32_t k = 0; k < BA_VPT; ++k) {  // block k * 4 + wave: 64 consecutive values
+    const uint32_t j = k * WG + tid;
+    const uint32_t pre = j < cnt ? vpre[j] : DBA_NONE;
+    if (j < cnt) s += (uint64_t)pre + vlen[j];
+    const uint32_t bm = wave_min_u32(pre);
+    if (lane == 0) dt[k * 4 + wv] = bm;
+    tm = bm < tm ? bm : tm;
+  }
+  if (lane == 0) mred[wv] = tm;
+  const uint64_t tot = block_sum_u64(s, red);  // (its barriers order mred too)
+  if (tid == 0) {
+    tsum[gt] = tot;
+    uint32_t m = mred[0];
+    for (uint32_t w = 1; w < WG / 64; ++w) m = mred[w] < m ? mred[w] : m;
+    dt[64] = m;
+  }
+}
+
+__global__ void __launch_bounds__(WG) k_dba_pages(PageWork* pages, const ChunkWork* chunks, uint64_t* __restrict__ tsum,
+                                                  uint32_t* __restrict__ dtile) {
+  __shared__ uint64_t wsum[WG / 64];
+  __shared__ uint64_t carry_s;
+  const uint32_t p = blockIdx.x;
+  const PageWork pw = pages[p];
+  if (!dba_page_ok(pw, chunks[pw.chunk])) return;
+  const uint32_t nt = (uint32_t)((pw.nonnull + BA_T - 1) / BA_T);
+  const uint32_t tid = threadIdx.x;
+  uint64_t* ts = tsum + pw.ltile0;
+  if (tid == 0) carry_s = pw.byte_out;
+  __syncthreads();
+  for (uint32_t b = 0; b < nt; b += WG) {  // tile byte starts
+    const uint32_t t = b + tid;
+    const uint64_t x = t < nt ? ts[t] : 0ull;
+    uint64_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, 64);
+      if ((tid & 63u) >= (uint32_t)off) incl += y;
     }
-    const uint8_t* s = blob + vsrc[vo + i];
-    for (uint32_t k = lane; k < sl; k += 64) prev[pl + k] = s[k];
+    if ((tid & 63u) == 63u) wsum[tid >> 6] = incl;
     __syncthreads();
-    for (uint32_t k = lane; k < tot; k += 64) out[d + k] = prev[k];
-    if (lane == 0) offsets[vo + i] = (int64_t)d;
-    d += tot;
+    uint64_t pre = carry_s + incl - x, tot = 0;
+    for (uint32_t w = 0; w < WG / 64; ++w) {
+      if (w < (tid >> 6)) pre += wsum[w];
+      tot += wsum[w];
+    }
+    if (t < nt) ts[t] = pre;
     __syncthreads();
+    if (tid == 0) carry_s += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {  // previous tile of strictly smaller minimum (amortized O(1) per tile)
+    uint32_t* dt = dtile + (uint64_t)pw.ltile0 * DBA_TSTRIDE;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t m = dt[(uint64_t)t * DBA_TSTRIDE + 64];
+      uint32_t j = t ? t - 1 : DBA_NONE;
+      while (j != DBA_NONE && dt[(uint64_t)j * DBA_TSTRIDE + 64] >= m) j = dt[(uint64_t)j * DBA_TSTRIDE + 65];
+      dt[(uint64_t)t * DBA_TSTRIDE + 65] = j;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(WG) k_dba_psv(PageWork* pages, const ChunkWork* chunks,
+                                                const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
+                                                const uint32_t* __restrict__ vlen0, const uint32_t* __restrict__ vpre0,
+                                                const uint64_t* __restrict__ tsum, const uint32_t* __restrict__ dtile,
+                                                uint32_t* __restrict__ vaux0) {
+  __shared__ uint32_t pre_s[BA_T + BA_T / 16 + 1];
+  __shared__ uint32_t off_s[BA_T + BA_T / 16 + 1];  // value lengths, then tile-relative offsets
+  __shared__ uint32_t bmin_s[64];
+  __shared__ uint64_t wsum[WG / 64];
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
+  const PageWork pw = pages[p];
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!dba_page_ok(pw, ck)) return;
+  const uint32_t t = gt - pw.ltile0;
+  const uint64_t n = pw.nonnull, t0 = (uint64_t)t * BA_T;
+  if (t0 >= n) return;
+  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
+  const uint64_t vb = ck.scr_base + pw.value_out;  // scratch slot of the page's value 0
+  const uint32_t* vpre = vpre0 + vb;
+  const uint32_t tid = threadIdx.x;
+#pragma unroll 4
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint32_t j = k * WG + tid;
+    const uint32_t pr = j < cnt ? vpre[t0 + j] : 0u;
+    pre_s[ba_pad(j)] = pr;
+    off_s[ba_pad(j)] = j < cnt ? pr + vlen0[vb + t0 + j] : 0u;
+  }
+  if (tid < 64) bmin_s[tid] = dtile[(uint64_t)gt * DBA_TSTRIDE + tid];
+  __syncthreads();
+  // ---- value offsets: tile start + in-tile scan (each thread 16 consecutive values)
+  uint32_t l[BA_VPT];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    l[k] = off_s[tid * 17u + k];
+    s += l[k];
+  }
+  uint64_t incl = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if ((tid & 63u) >= (uint32_t)off) incl += y;
+  }
+  if ((tid & 63u) == 63u) wsum[tid >> 6] = incl;
+  __syncthreads();
+  uint64_t pre = incl - s, total = 0;
+  for (uint32_t w = 0; w < WG / 64; ++w) {
+    if (w < (tid >> 6)) pre += wsum[w];
+    total += wsum[w];
+  }
+  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out) + pw.value_out + t0;
+  const uint64_t base = tsum[gt];
+  if (total >> 32) {  // (a tile of > 4 GiB: offsets straight from registers)
+#pragma unroll 1
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      const uint32_t j = tid * BA_VPT + k;
+      if (j < cnt) offsets[j] = (int64_t)(base + pre);
+      pre += l[k];
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      off_s[tid * 17u + k] = (uint32_t)pre;
+      pre += l[k];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      const uint32_t j = k * WG + tid;
+      if (j < cnt) offsets[j] = (int64_t)(base + off_s[ba_pad(j)]);
+    }
+  }
+  // ---- psv of every value (page-relative index; DBA_NONE for prefix length 0)
+  const uint32_t* dtp = dtile + (uint64_t)pw.ltile0 * DBA_TSTRIDE;  // the page's tiles
+  uint32_t* vaux = vaux0 + vb;
+#pragma unroll 1
+  for (uint32_t k = 0; k < BA_VPT; ++k) {
+    const uint32_t j = k * WG + tid;
+    if (j >= cnt) break;
+    const uint32_t x = pre_s[ba_pad(j)];
+    uint32_t r = DBA_NONE;
+    if (x > 0) {
+      // own block, then the tile's earlier blocks
+      for (uint32_t q = j; q > (j & ~63u);) {
+        --q;
+        if (pre_s[ba_pad(q)] < x) {
+          r = (uint32_t)t0 + q;
+          break;
+        }
+      }
+      if (r == DBA_NONE) {
+        for (uint32_t b = j >> 6; b > 0 && r == DBA_NONE;) {
+          --b;
+          if (bmin_s[b] < x)
+            for (uint32_t q = b * 64u + 64u; q > b * 64u;) {
+              --q;
+              if (pre_s[ba_pad(q)] < x) {
+                r = (uint32_t)t0 + q;
+                break;
+              }
+            }
+        }
+      }
+      if (r == DBA_NONE && t > 0) {  // earlier tiles: jump to the nearest of minimum < x
+        uint32_t u = t - 1;
+        while (u != DBA_NONE && dtp[(uint64_t)u * DBA_TSTRIDE + 64] >= x) u = dtp[(uint64_t)u * DBA_TSTRIDE + 65];
+        if (u != DBA_NONE) {
+          const uint32_t* um = dtp + (uint64_t)u * DBA_TSTRIDE;
+          for (uint32_t b = 64; b > 0 && r == DBA_NONE;) {
+            --b;
+            if (um[b] < x)
+              for (uint32_t q = b * 64u + 64u; q > b * 64u;) {
+                --q;
+                const uint32_t g = u * BA_T + q;
+                if (vpre[g] < x) {
+                  r = g;
+                  break;
+                }
+              }
+          }
+        }
+      }
+    }
+    vaux[t0 + j] = r;
+  }
+}
+
+// One slice of a value: dst <- src[0, len), 8 bytes at a time.
+__device__ inline void dba_slice(gptr<uint8_t> dst, const uint8_t* src, uint32_t len) {
+  uint32_t q = 0;
+  for (; q + 8 <= len; q += 8) {
+    uint64_t x;
+    __builtin_memcpy(&x, src + q, 8);
+    __builtin_memcpy(dst + q, &x, 8);
+  }
+  for (; q < len; ++q) dst[q] = src[q];
+}
+
+__global__ void __launch_bounds__(WG) k_dba_copy(const uint8_t* __restrict__ blob, PageWork* pages, const ChunkWork* chunks,
+                                                 const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
+                                                 const uint64_t* __restrict__ vsrc0, const uint32_t* __restrict__ vlen0,
+                                                 const uint32_t* __restrict__ vpre0, const uint32_t* __restrict__ vaux0) {
+  __shared__ uint64_t qdst[DBA_QCAP], qsrc[DBA_QCAP];
+  __shared__ uint32_t qlen[DBA_QCAP];
+  __shared__ uint32_t qn;
+  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
+  const PageWork pw = pages[p];
+  const ChunkWork& ck = chunks[pw.chunk];
+  if (!dba_page_ok(pw, ck)) return;
+  const uint64_t n = pw.nonnull, t0 = (uint64_t)(gt - pw.ltile0) * BA_T;
+  if (t0 >= n) return;
+  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
+  const uint64_t vb = ck.scr_base + pw.value_out;
+  const uint64_t* vsrc = vsrc0 + vb;
+  const uint32_t* vlen = vlen0 + vb;
+  const uint32_t* vpre = vpre0 + vb;
+  const uint32_t* vaux = vaux0 + vb;
+  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out) + pw.value_out;
+  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) qn = 0;
+  __syncthreads();
+  auto slice = [&](uint64_t d, uint64_t src, uint32_t len) {
+    if (len > DBA_LONG) {
+      const uint32_t qi = atomicAdd(&qn, 1u);
+      if (qi < DBA_QCAP) {
+        qdst[qi] = d;
+        qsrc[qi] = src;
+        qlen[qi] = len;
+        return;
+      }
+    }
+    dba_slice(out + d, blob + src, len);
+  };
+#pragma unroll 1
+  for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values
+    const uint64_t i = t0 + k * WG + tid;
+    if (i >= n) break;
+    const uint64_t o = (uint64_t)offsets[i];
+    uint32_t cp = vpre[i];
+    slice(o + cp, vsrc[i], vlen[i]);  // its own suffix
+    uint64_t cur = i;
+    while (cp > 0) {  // then the chain of previous smaller prefix lengths
+      const uint32_t a = vaux[cur];
+      if (a == DBA_NONE) break;  // (not reached: k_ba_index checked the prefix lengths)
+      const uint32_t pa = vpre[a];
+      slice(o + pa, vsrc[a], cp - pa);
+      cp = pa;
+      cur = a;
+    }
+  }
+  __syncthreads();
+  const uint32_t nq = qn < DBA_QCAP ? qn : DBA_QCAP;
+  const uint32_t lane = tid & 63u;
+#pragma unroll 1
+  for (uint32_t e = tid >> 6; e < nq; e += WG / 64) {  // long slices: one wave each
+    const gptr<uint8_t> d = out + qdst[e];
+    const uint8_t* sp = blob + qsrc[e];
+    const uint32_t len = qlen[e];
+    uint32_t q = lane * 8u;
+    for (; q + 8 <= len; q += 512u) {
+      uint64_t x;
+      __builtin_memcpy(&x, sp + q, 8);
+      __builtin_memcpy(d + q, &x, 8);
+    }
+    if (q < len)  // the lane holding the tail
+      for (; q < len; ++q) d[q] = sp[q];
   }
 }
 
@@ -903,7 +1188,7 @@ hipError_t pqg_launch_badict_general(const uint8_t* blob, uint64_t blob_len, Pag
 hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                             const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, bool has_lvdict,
                             uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen,
-                            uint64_t* tsum, hipStream_t s) {
+                            uint64_t* tsum, uint32_t* vaux, uint32_t* dtile, hipStream_t s) {
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
   if (ntl) {
@@ -916,8 +1201,14 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
       hipLaunchKernelGGL(k_ba_copy_sd, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vlen,
                          dsrc, dlen, tsum);
   }
-  if (has_dba)
-    hipLaunchKernelGGL(k_dba_copy, dim3(npages), dim3(64), 0, s, blob, pages, chunks, vsrc, vlen, vpre);
+  if (has_dba && ntl) {
+    hipLaunchKernelGGL(k_dba_tiles, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vlen, vpre, tsum, dtile);
+    hipLaunchKernelGGL(k_dba_pages, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum, dtile);
+    hipLaunchKernelGGL(k_dba_psv, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vlen, vpre, tsum, dtile,
+                       vaux);
+    hipLaunchKernelGGL(k_dba_copy, dim3(ntl), dim3(WG), 0, s, blob, pages, chunks, tile_page, tl, vsrc, vlen, vpre,
+                       vaux);
+  }
   return hipGetLastError();
 }
 

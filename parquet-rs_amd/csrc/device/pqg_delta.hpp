@@ -18,14 +18,16 @@ constexpr int DBLK = 16384;
 constexpr int DREGION = DBLK + 128;
 constexpr int DREGION_WORDS = DREGION / 4 + 4;
 constexpr int NBCAP = 48;     // blocks per batch
-constexpr int MBCAP = 64;     // mini-blocks per block supported
+constexpr int MBCAP = 64;     // mini-blocks per block-table entry
 constexpr int DPT = 16;       // deltas per thread per pass
 
 struct DeltaSmem {
   uint32_t region[DREGION_WORDS];
   uint32_t pay[NBCAP];             // stream-relative payload start of block
   uint64_t mind[NBCAP];            // min_delta
-  uint32_t first_delta[NBCAP + 1]; // batch-relative delta index of the block's first delta
+  uint32_t first_delta[NBCAP + 1]; // batch-relative delta index of the entry's first delta
+  uint32_t nmbe[NBCAP];            // mini-blocks of the entry (a block of more than MBCAP
+                                   // mini-blocks takes several entries)
   uint8_t width[NBCAP][MBCAP];
   uint32_t mboff[NBCAP][MBCAP];    // byte offset of mini-block m from pay[b]
   uint64_t wsum[WG / 64];
@@ -110,7 +112,6 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
     else {
       vpmb = (uint64_t)((int64_t)block_size / (int64_t)nmb);
       if (vpmb % 8 != 0) err = ST_PANIC;  // assert!(values_per_mini_block % 8 == 0)
-      else if (nmb > MBCAP) err = ST_NYI;
     }
   }
   if (err) return err;
@@ -134,6 +135,13 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
   uint64_t A0 = (S + pos) & ~15ull;
   uint64_t carry = (uint64_t)first;
   uint32_t end_off = q;
+  // Block walk state (lane 0 only; kept across batches, since a block of more than MBCAP
+  // mini-blocks is recorded as several table entries of at most MBCAP, possibly in several
+  // batches): the next header, and inside a block the next mini-block to record, the block's
+  // payload start, the byte offset of that mini-block in it, min_delta, width bytes, needed
+  // mini-blocks.
+  uint32_t wcur = q, bm = 0, bpay = 0, bw = 0, bmneed = 0;
+  uint64_t bboff = 0, bmind = 0;
 
   delta_load_region(sm, blob, blob_len, A0);
   __syncthreads();
@@ -144,59 +152,81 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
       uint32_t nb = 0;
       uint64_t dcount = 0;
       int32_t e = 0;
-      uint32_t cur = pos, endp = 0;
+      uint32_t endp = 0;
+      // a width byte: staged when inside the region, else global memory (blocks whose width
+      // bytes run past the region: a few thousand mini-blocks per block)
+      auto wbyte = [&](uint64_t off) -> uint32_t {
+        const uint64_t a = S + off;
+        return (a >= A0 && a - A0 < (uint64_t)DREGION) ? lbyte(sm.region, (uint32_t)(a - A0)) : (uint32_t)blob[a];
+      };
       while (nb < NBCAP && done + dcount < need) {
-        uint64_t rel = S + cur - A0;
-        if (rel >= DBLK) break;
-        uint32_t ridx = (uint32_t)rel;
-        uint64_t zz;
-        int vl = lds_vlq(sm.region, ridx, cur, slen, zz);
-        if (vl <= 0) {
-          e = vl ? ST_PANIC : ST_EOF;  // "Not enough data to decode 'min_delta'"
-          break;
+        if (bm == 0) {  // at a block header (init_block, decoding.rs:448-468)
+          uint64_t rel = S + wcur - A0;
+          if (rel >= DBLK) break;
+          uint32_t ridx = (uint32_t)rel;
+          uint64_t zz;
+          int vl = lds_vlq(sm.region, ridx, wcur, slen, zz);
+          if (vl <= 0) {
+            e = vl ? ST_PANIC : ST_EOF;  // "Not enough data to decode 'min_delta'"
+            break;
+          }
+          if ((uint64_t)wcur + vl + nmb > slen) {
+            e = ST_EOF;  // "Not enough data to decode 'width'" (every width is read)
+            break;
+          }
+          uint64_t left = need - done - dcount;
+          uint64_t inblk = left < vpb ? left : vpb;
+          bmneed = (uint32_t)((inblk + vpmb - 1) / vpmb);
+          bw = wcur + (uint32_t)vl;
+          bpay = bw + (uint32_t)nmb;
+          bboff = 0;
+          bmind = (uint64_t)unzigzag(zz);
         }
-        if ((uint64_t)cur + vl + nmb > slen) {
-          e = ST_EOF;  // "Not enough data to decode 'width'"
-          break;
-        }
-        uint64_t left = need - done - dcount;
-        uint64_t inblk = left < vpb ? left : vpb;
-        uint32_t mneed = (uint32_t)((inblk + vpmb - 1) / vpmb);
-        uint32_t payload = cur + (uint32_t)vl + (uint32_t)nmb;
-        uint64_t boff = 0, bend = 0;
-        for (uint32_t m = 0; m < (uint32_t)nmb; ++m) {
-          uint32_t wdt = lbyte(sm.region, ridx + (uint32_t)vl + m);
-          sm.width[nb][m] = (uint8_t)wdt;
-          sm.mboff[nb][m] = (uint32_t)boff;
-          if (m < mneed) {
+        // one table entry: mini-blocks [bm, m1) of the block
+        const uint32_t m1 = (uint64_t)bm + MBCAP < nmb ? bm + MBCAP : (uint32_t)nmb;
+        const uint64_t boff0 = bboff;
+        for (uint32_t m = bm; m < m1; ++m) {
+          uint32_t wdt = wbyte((uint64_t)bw + m);
+          sm.width[nb][m - bm] = (uint8_t)wdt;
+          sm.mboff[nb][m - bm] = (uint32_t)(bboff - boff0);
+          if (m < bmneed) {
             if (wdt > (ES == 4 ? 32u : 64u)) {
               e = ST_PANIC;  // get_batch / get_value assert on num_bits
               break;
             }
             // the reference loads the whole mini-block, padding included (decoding.rs:472-495)
-            if ((uint64_t)payload + boff + (vpmb * wdt) / 8 > slen) {
+            if ((uint64_t)bpay + bboff + (vpmb * wdt) / 8 > slen) {
               e = (ES == 4) ? ST_PANIC : ST_EOF;
               break;
             }
-            bend = boff + (vpmb * wdt) / 8;
+            endp = (uint32_t)((uint64_t)bpay + bboff + (vpmb * wdt) / 8);
           }
-          boff += (vpmb * wdt) / 8;
+          bboff += (vpmb * wdt) / 8;
         }
         if (e) break;
-        sm.pay[nb] = payload;
-        sm.mind[nb] = (uint64_t)unzigzag(zz);
+        const uint64_t left = need - done - dcount;
+        const uint64_t span = (uint64_t)(m1 - bm) * vpmb;
+        sm.pay[nb] = (uint32_t)(bpay + boff0);
+        sm.mind[nb] = bmind;
+        sm.nmbe[nb] = m1 - bm;
         sm.first_delta[nb] = (uint32_t)dcount;
-        dcount += inblk;
+        dcount += left < span ? left : span;
         nb++;
-        endp = (uint32_t)(payload + bend);
-        uint64_t nx = (uint64_t)payload + boff;
-        cur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+        bm = m1;
+        if (bm == (uint32_t)nmb) {  // the block is done: the next header follows its payload
+          bm = 0;
+          uint64_t nx = (uint64_t)bpay + bboff;
+          wcur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+        }
       }
       sm.first_delta[nb] = (uint32_t)dcount;
       sm.ctl[0] = nb;
       sm.ctl[1] = (uint32_t)dcount;
       sm.ctl[2] = (uint32_t)e;
-      sm.ctl[3] = cur;
+      // where the stream continues (the region follows it): the next header, or inside a block
+      // the next mini-block's payload
+      uint64_t at = bm ? (uint64_t)bpay + bboff : (uint64_t)wcur;
+      sm.ctl[3] = at > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)at;
       sm.ctl[4] = endp;
     }
     __syncthreads();
@@ -254,7 +284,7 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
             s += v[j];
             if (++k == vpmb) {
               k = 0;
-              if (++m == (uint32_t)nmb) {
+              if (++m == sm.nmbe[b]) {
                 m = 0;
                 ++b;
               }

@@ -40,6 +40,16 @@ __device__ inline void report(PageWork* pages, ChunkWork* chunks, int page, int3
   }
 }
 
+// A dictionary-encoded page's per-value scratch (kept indices, byte-array index slots and entry
+// sources) is written only when its chunk's dictionary page decoded. Every kernel that writes or
+// reads such scratch takes a page through this one predicate (with the page's own status), so a
+// consumer never reads scratch its producer skipped: the scratch is reused across decodes
+// without clearing, and a slot left by an earlier decode may hold any value. The dictionary's
+// status is final before any data page's kernel runs (k_prepare / k_ba_dict_prep come first).
+__device__ inline bool dict_usable(const PageWork* pages, const ChunkWork& ck) {
+  return ck.dict_page >= 0 && pages[ck.dict_page].status == 0;
+}
+
 // The column parameters of page pw's chunk.
 __device__ inline const ColumnParams& pcp(const ChunkWork* chunks, const PageWork& pw) { return chunks[pw.chunk].cp; }
 

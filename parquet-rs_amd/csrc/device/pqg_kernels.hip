@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(64) k_run_index(const uint8_t* __restrict__ bl
       if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
       return;
     }
-    if (pages[ck.dict_page].status != 0) return;
+    if (!dict_usable(pages, ck)) return;
   }
   const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0,
                               rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT, rt.nruns + pw.ltile0, sm,
@@ -437,7 +437,11 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
                                                          ((uint32_t)f * DW_NT + (tid & ~63u)) * 16u),
               16, 0, 0);
       }
-      __syncthreads();  // (vmcnt(0): the window has landed)
+      // every wave's LDS-DMA fill must have landed before any wave reads the window: each wave
+      // waits for its own (vmcnt(0), explicit: the barrier alone does not promise it), then the
+      // barrier orders the waves
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
       if (sh) {  // a dictionary at an odd offset: the window moved down by sh bytes, in place
         const uint32_t k0 = sh >> 2, bs = sh & 3u;
 #pragma unroll 1
@@ -511,7 +515,7 @@ __global__ void __launch_bounds__(WG) k_dict_fallback(const uint8_t* __restrict_
     if (threadIdx.x == 0) report(pages, chunks, p, ST_PANIC);
     return;
   }
-  if (pages[ck.dict_page].status != 0) return;
+  if (!dict_usable(pages, ck)) return;
   if (threadIdx.x < 64) {
     const int32_t st = run_index(blob, blob_len, s, rt.ck + pw.ltile0, rt.runs + (uint64_t)pw.ltile0 * RUN_CAPT,
                                  rt.nruns + pw.ltile0, ism);

@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(WG) k_lv_probe(const uint8_t* __restrict__ blo
 // streams start their count at 0.
 __device__ inline bool lv_nodict(const PageWork* pages, const ChunkWork& ck, int sel) {
   // dictionary indices without a usable dictionary: the general decoder reports it
-  return sel == SS_DICT && (ck.dict_page < 0 || pages[ck.dict_page].status != 0);
+  return sel == SS_DICT && !dict_usable(pages, ck);
 }
 
 __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,

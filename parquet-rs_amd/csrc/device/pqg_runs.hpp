@@ -807,7 +807,7 @@ __device__ inline QDesc quarter_desc(const uint8_t* blob, const PageWork* pages,
   if (pw.status != 0) return d;
   if (rt.pflag && pf_level_path(rt.pflag[p])) return d;  // decoded by the level path
   const ChunkWork& ck = chunks[pw.chunk];
-  if (sel == SS_DICT && (ck.dict_page < 0 || pages[ck.dict_page].status != 0)) return d;
+  if (sel == SS_DICT && !dict_usable(pages, ck)) return d;
   Stream s;
   if (!get_stream(blob, pw, sel, ck.cp, s) || s.err) return d;
   const uint32_t k = t - pw.ltile0;

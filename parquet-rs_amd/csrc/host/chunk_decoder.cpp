@@ -56,7 +56,7 @@ hipError_t pqg_launch_badict_general(const uint8_t*, uint64_t, PageWork*, int, C
                                      int, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
                             uint32_t, bool, bool, uint64_t*, uint32_t*, uint32_t*, const uint64_t*, const uint32_t*,
-                            uint64_t*, hipStream_t);
+                            uint64_t*, uint32_t*, uint32_t*, hipStream_t);
 }
 
 // Stream kinds of the hybrid-stream tables: def, rep, dictionary indices, RLE booleans.
@@ -112,6 +112,10 @@ struct Slot {
   uint32_t* dlen = nullptr;
   size_t dcap = 0;
   uint64_t* tsum = nullptr;  // byte-array copy: per tile, bytes then start
+  uint32_t* vaux = nullptr;  // DELTA_BYTE_ARRAY: per value, the previous smaller prefix length's value
+  size_t vaux_cap = 0;
+  uint32_t* dtile = nullptr;  // DELTA_BYTE_ARRAY: per tile, prefix-length minima and tile jumps
+  size_t dtile_cap = 0;
   uint16_t* didx = nullptr;  // TL_W4 / TL_W8 tiles: RUN_TILE dictionary indices each
   size_t didx_cap = 0;
   // hybrid-stream expand tiles: tile -> page map and the index-pass tables per stream kind
@@ -332,6 +336,8 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.vlen);
     hipFree(sl.vpre);
     hipFree(sl.tsum);
+    hipFree(sl.vaux);
+    hipFree(sl.dtile);
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
     hipFree(sl.didx);
@@ -779,6 +785,12 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       HIPCHK(hipMalloc(&sl.dlen, sl.dcap * 4), "hipMalloc dlen");
     }
   }
+  if (any_dba) {
+    int st;
+    if ((st = grow(ctx, (void**)&sl.vaux, &sl.vaux_cap, scr, 4, "hipMalloc vaux"))) return st;
+    if ((st = grow(ctx, (void**)&sl.dtile, &sl.dtile_cap, ((size_t)total_tiles + 1) * 66, 4, "hipMalloc dtile")))
+      return st;
+  }
   if (ntl[TL_W4] + ntl[TL_W8]) {
     const int st = grow(ctx, (void**)&sl.didx, &sl.didx_cap, (size_t)(ntl[TL_W4] + ntl[TL_W8]) * RUN_TILE, 2,
                         "hipMalloc dictionary indices");
@@ -966,7 +978,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     if (any_ba) {
       if (!ctx->values_kernel) ctx->values_kernel = any_dba ? PQG_DELTA_BYTE_ARRAY : PQG_PLAIN;
       HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba, ba_lv,
-                              sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, s),
+                              sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, sl.vaux, sl.dtile, s),
              "byte arrays");
     }
     if (any_plain || any_pbool) {

@@ -327,8 +327,11 @@ int pqg_column_reader_read_batch(pqg_column_reader* cr, size_t batch_size, int16
   if (cr->col.max_def > 0 && !def) return PQG_ERR_INVALID;
   uint64_t left = cr->total_levels - cr->L;
   uint64_t nlev = batch_size < left ? batch_size : left;
-  // (a failure after the last decoded page fails the call that finds no levels left)
-  if (cr->status != PQG_OK && cr->L + (nlev ? nlev : 1) > cr->bad_level) return cr->status;
+  // The reference's loop (column/reader.rs:181-262) keeps reading while fewer than batch_size
+  // levels are in hand, so a call whose requested range reaches the failing page (or a failure
+  // after the last decoded page: has_next -> read_new_page fails) returns its error, whatever was
+  // read before it in that call; batch_size 0 never enters the loop (Ok((0, 0))).
+  if (cr->status != PQG_OK && batch_size && cr->L + batch_size > cr->bad_level) return cr->status;
   if (nlev == 0) return PQG_OK;
   uint64_t nval = nlev;
   if (use_def) {

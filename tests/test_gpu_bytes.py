@@ -128,6 +128,46 @@ def test_delta_byte_array(oracle, ctx, p_null):
     check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
 
 
+def test_delta_byte_array_long_values(oracle, ctx):
+    """Values of any length (the reference builds a Vec per value, decoding.rs:794-822): 40 KiB
+    and 1 MiB values sharing long prefixes, between short ones."""
+    rng = np.random.default_rng(61)
+    big = bytes(rng.integers(0, 256, 1 << 20, dtype=np.uint8))
+    mid = bytes(rng.integers(0, 256, 40 << 10, dtype=np.uint8))
+    vals = [b"a", mid, mid + b"x", mid[:30000] + b"yz", big, big[:700000] + mid, big + b"!", b"b",
+            big[:5] + mid, mid + big]
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_byte_array_encode(vals), len(vals),
+                             oracle.DELTA_BYTE_ARRAY)]
+    got, _ = check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+    offs = got["offsets"]
+    assert [got["bytes"][offs[i]:offs[i + 1]] for i in range(len(vals))] == vals
+
+
+def _prefix_chain_values(n):
+    """Value i = 'a' * (i % 3000 + 1) and similar: prefix lengths rising by one, so every byte
+    of a value comes from a different earlier suffix (chains as long as the values)."""
+    return [b"a" * (i % 3000 + 1) + bytes([98 + (i % 3000 == 2999)]) for i in range(n)]
+
+
+@pytest.mark.parametrize("shape", ["rising", "common_prefix", "million"])
+def test_delta_byte_array_prefix_chains(oracle, ctx, shape):
+    """Prefix-length shapes for the slice rebuild: prefix lengths rising by one (chains of
+    thousands of slices), one 23-byte prefix shared by every value across many 4096-value tiles
+    (each value's chain jumps back to value 0), and a 1 M-value page of sorted URL-like strings."""
+    rng = np.random.default_rng(62)
+    if shape == "rising":
+        vals = _prefix_chain_values(7000)
+    elif shape == "common_prefix":
+        vals = [b"http://www.example.com/" + b"%07d" % int(x) for x in rng.integers(0, 10 ** 7, 50000)]
+    else:
+        xs = np.sort(rng.integers(0, 10 ** 12, 1 << 20))
+        vals = [b"http://www.example.com/%d/%012d" % (x % 7, x) + b"/q" * int(x % 5) for x in xs]
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_byte_array_encode(vals), len(vals),
+                             oracle.DELTA_BYTE_ARRAY)]
+    got, _ = check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+    assert got["bytes"] == b"".join(vals)
+
+
 def test_delta_byte_array_flba(oracle, ctx):
     rng = np.random.default_rng(7)
     vals = sorted(rand_strings(rng, 3000, 10, 10, b"ab"))

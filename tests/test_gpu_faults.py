@@ -111,6 +111,36 @@ def test_truncated_small_ba_dictionary_nullable(oracle, ctx):
     _same_error(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
 
 
+@pytest.mark.parametrize("nd", [300, 60000])
+def test_failing_ba_dictionary_after_stale_in_range_indices(oracle, ctx, nd):
+    """The per-value index slots are scratch reused across decodes. Two good decodes (one per
+    context slot) first fill them with in-range indices of another dictionary; then a chunk whose
+    dictionary page is cut decodes. No kernel may read those slots (dict_usable: the producers
+    skip the chunk's data pages, so the consumers do too): the status is the oracle's, and a good
+    decode afterwards is still exact."""
+    import pqgpu
+    rng = np.random.default_rng(24)
+    d = list(dict.fromkeys(_strings(rng, nd + nd // 2, 4, 16)))[:nd]
+    bw = max(1, int(np.ceil(np.log2(len(d)))))
+
+    def idx(n):
+        return bytes([bw]) + oracle.rle_encode(rng.integers(0, len(d), n).astype(np.uint64), bw)
+
+    good = [oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode_ba(d), len(d), oracle.PLAIN)]
+    good += [_opt(oracle, n, idx, oracle.RLE_DICTIONARY, rng) for n in (90_000, 40_000)]
+    ref_good = oracle.read_column(oracle.BYTE_ARRAY, good, max_def=1)
+    for _ in range(2):
+        got = pqgpu.decode_column(ctx, oracle.BYTE_ARRAY, good, max_def=1)
+        assert got["status"] == 0 and got["bytes"] == ref_good["bytes"]
+    bad = [oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode_ba(d)[:-3], len(d), oracle.PLAIN)]
+    bad += [_opt(oracle, n, idx, oracle.RLE_DICTIONARY, rng) for n in (90_000, 40_000)]
+    for _ in range(2):
+        _same_error(oracle, ctx, oracle.BYTE_ARRAY, bad, max_def=1)
+    got = pqgpu.decode_column(ctx, oracle.BYTE_ARRAY, good, max_def=1)
+    assert got["status"] == 0 and got["bytes"] == ref_good["bytes"]
+    np.testing.assert_array_equal(got["offsets"], ref_good["offsets"])
+
+
 # ---- (3) DELTA_BINARY_PACKED page pass -> tiled fallback
 
 def _delta_blocks(buf):

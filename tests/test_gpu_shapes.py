@@ -90,6 +90,30 @@ def test_delta_block_shapes(oracle, ctx, ptype, shape):
     np.testing.assert_array_equal(got["values"], expect)  # decode(encode(x)) == x as well
 
 
+# Blocks of many mini-blocks: DeltaBitPackDecoder::init_block reads num_mini_blocks width bytes
+# into a Vec, any count (decoding.rs:448-468). 128 and 1024 mini-blocks of 8 values; 32 768
+# mini-blocks put a block's width bytes (32 KiB) past the decoder's 16 KiB staged region.
+MANY_MB_SHAPES = [(1024, 128), (8192, 1024), (32768, 1024), (262144, 32768)]
+
+
+@pytest.mark.parametrize("shape", MANY_MB_SHAPES)
+@pytest.mark.parametrize("ptype", ["INT32", "INT64"])
+def test_delta_many_mini_blocks(oracle, ctx, ptype, shape):
+    bs, nmb = shape
+    t = getattr(oracle, ptype)
+    dt = np.int32 if ptype == "INT32" else np.int64
+    rng = np.random.default_rng(bs + nmb + (3 if ptype == "INT64" else 0))
+    pages, vals = [], []
+    for n, mode in ((1, "d16"), (2, "d16"), (9, "small"), (bs + 1, "d16"), (3 * bs + 77, "small"),
+                    (70001, "d16"), (5000, "ext"), (3001, "wide")):
+        v = _delta_values(rng, dt, n, mode)
+        vals.append(v)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_encode(t, v, bs, nmb), n,
+                                     oracle.DELTA_BINARY_PACKED))
+    got, _ = _same(oracle, ctx, t, pages)
+    np.testing.assert_array_equal(got["values"], np.concatenate(vals))
+
+
 @pytest.mark.parametrize("ptype", ["INT32", "INT64"])
 def test_delta_config4_page(oracle, ctx, ptype):
     """One full benchmark page: 2^20 values, 16-bit deltas, 512 / 4 x 128 (bench.py config 4),

@@ -162,6 +162,7 @@ __global__ __launch_bounds__(NT) void k_gather_win2(const uint64_t* __restrict__
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(dict4 + w0 / 2 + i),
                                          (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)sd4 + (f * NT + (tid & ~63u)) * 16), 16, 0, 0);
       }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's fills landed, then the barrier
       __syncthreads();
 #pragma unroll
       for (int s = 0; s < NP; ++s) {
