@@ -401,6 +401,11 @@ def pmc_traffic(kind, kernel, variant=None):
         except (OSError, ValueError, KeyError):
             continue
         names = {k.replace("pqg::", ""): e for k, e in ks.items() if "traffic_bytes" in e}
+        if kernel == "whole step":  # config 5: every decode kernel of the step (each launched once)
+            tot = [e["traffic_bytes"] for k, e in ks.items() if k.startswith("pqg::") and "traffic_bytes" in e]
+            if tot:
+                return sum(tot), os.path.relpath(path, ROOT)
+            continue
         if kernel in ("level path", "DELTA stage", "dictionary stage"):  # kernels timed as one: their sum
             pre = {"level path": LEVEL_PATH, "DELTA stage": DELTA_STAGE, "dictionary stage": DICT_STAGE}[kernel]
             tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(pre)]
@@ -840,6 +845,8 @@ def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
     per_step = max_over_ranks(alltypes_steps(ctx, w, stream, args.steps, args.warmup, dist, bctx), dist)
     step_bytes = w.in_bytes + w.out_bytes
     achieved = step_bytes / per_step / 1e9
+    # traffic: the PMC bytes of every decode kernel of one step (one pqg_decode_chunks per step)
+    at_traffic, at_src = pmc_traffic("alltypes", "whole step") if bctx is not None else (None, None)
     res = {
         "value": w.job_rgs * w.rows * len(w.cols) / per_step, "unit": "values/s (cells: one level + its value)",
         "ms_per_step": per_step * 1e3, "gbps": step_bytes / per_step / 1e9 * world,
@@ -855,7 +862,8 @@ def run_alltypes(pqgpu, args, world, rank, dist, stream, extras=True):
                             else "pqg_rg_decode per row group, two streams",
                    "parallelism": f"row-group partitions x{world}, no collective"},
         "roofline": {"bound": "hbm", "kernel": "whole step (every chunk decode)", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": at_traffic, "traffic_source": at_src,
                      "bytes_per_launch": step_bytes, "avg_ms": per_step * 1e3,
                      "frac_of_achievable": achieved / HBM_ACHIEVABLE_GBS},
         "value_check": checked,

@@ -186,6 +186,19 @@ int pqg_space_values(pqg_ctx *ctx, const int16_t *def_levels, uint64_t num_level
 int pqg_get_timings(pqg_ctx *ctx, pqg_timings *t);
 int pqg_reset_timings(pqg_ctx *ctx);
 const char *pqg_error_message(pqg_ctx *ctx);
+/* The value-kernel families the last decode enqueued (diagnostics and tests: which path a page
+ * shape takes), a mask of PQG_PATH_*. */
+enum {
+  PQG_PATH_PLAIN = 1,          /* fixed-width PLAIN copy */
+  PQG_PATH_DICT_LEVEL = 2,     /* dictionary indices on the level path (LDS dictionary) */
+  PQG_PATH_DICT_WINDOW = 4,    /* windowed dictionary gather, 257..65536 entries of 4 / 8 bytes */
+  PQG_PATH_DICT_TILES = 8,     /* general dictionary tiles (L2 gather) */
+  PQG_PATH_BYTES = 16,         /* byte arrays (PLAIN, dictionary, DELTA_LENGTH) */
+  PQG_PATH_DELTA_BYTES = 32,   /* DELTA_BYTE_ARRAY slice rebuild */
+  PQG_PATH_DELTA = 64,         /* DELTA_BINARY_PACKED */
+  PQG_PATH_RLE_BOOL = 128      /* RLE booleans */
+};
+int pqg_ctx_last_paths(pqg_ctx *ctx, uint32_t *mask);
 
 /* ---------------------------------------------------------------- row groups
  * The column chunks of one row group decoded together. The reference reads every column chunk

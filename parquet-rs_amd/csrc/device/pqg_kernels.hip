@@ -344,10 +344,11 @@ struct DictIdxMaker {
   PageWork* pages;
   ChunkWork* chunks;
   uint16_t* idx;  // the list's slots
+  uint32_t p;     // the tile's position in the list (its slot)
   __device__ TxDictIdx make(const QDesc& d) {
     if (!d.qhi) return TxDictIdx{gptr<uint16_t>(nullptr), 0u, 0u, 0};
     const ChunkWork& ck = chunks[pages[d.page].chunk];
-    return TxDictIdx{gp(idx) + (uint64_t)blockIdx.x * RUN_TILE, d.qlo, pages[ck.dict_page].num_values, 0};
+    return TxDictIdx{gp(idx) + (uint64_t)p * RUN_TILE, d.qlo, pages[ck.dict_page].num_values, 0};
   }
   __device__ void done(const QDesc& d, uint32_t, TxDictIdx& em) {
     const uint64_t bad = __ballot(em.err != 0);
@@ -355,13 +356,46 @@ struct DictIdxMaker {
   }
 };
 
+// Tiles k_dict_win decodes itself (its stage region takes the tile's run records and payload).
+// The others -- more run records than DF_RC, or than the index pass keeps (re-walk), or a
+// payload past DF_PAY -- have their indices kept in the tile's slot by k_texpand_didx first.
+constexpr uint32_t DF_TB = 16384;                  // LDS bytes per tile region (8 tiles: the window)
+constexpr uint32_t DF_RC = 128;                    // run records per tile
+constexpr uint32_t DF_POFF = (DF_RC + 2) * 8;      // payload offset in the region (start[], info[] first)
+constexpr uint32_t DF_BLK = DF_TB - 512;           // per 256-output block of the tile: its first two runs
+constexpr uint32_t DF_PAY = DF_BLK - DF_POFF - 16;  // staged payload bytes at most
+static_assert(DF_POFF % 16 == 0, "16-byte payload chunks");
+static_assert(DF_RC <= 128, "one record per thread of a tile");
+
+__device__ inline bool df_easy(const QDesc& d) {
+  if (!d.qhi || d.rec == RUN_REWALK || tx_wide(d) || tx_nrec(d) > DF_RC) return false;
+  if (!d.bhi) return true;  // RLE runs only
+  const uint64_t A0 = (d.S + d.blo) & ~15ull;
+  return d.S + d.bhi - A0 <= (uint64_t)DF_PAY;
+}
+
+// The list's other tiles: index expand into their slots. A workgroup takes 256 entries of the
+// list, checks them all at once and expands the few k_dict_win does not decode itself (none at
+// the benchmark's shape).
 __global__ void __launch_bounds__(WG) k_texpand_didx(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     const uint32_t* __restrict__ tl, PageWork* pages,
+                                                     const uint32_t* __restrict__ tl, uint32_t ntl, PageWork* pages,
                                                      ChunkWork* chunks, RunTables rt, uint16_t* idx) {
   __shared__ TileSmem sm;
+  __shared__ uint32_t hard[WG];
+  __shared__ uint32_t nhard;
   if (*rt.nfall == 0) return;
-  DictIdxMaker mk{pages, chunks, idx};
-  tile_one(blob, blob_len, rt.desc, tl[blockIdx.x], rt.runs, sm, mk);
+  if (threadIdx.x == 0) nhard = 0;
+  __syncthreads();
+  const uint32_t p0 = blockIdx.x * WG, pi = p0 + threadIdx.x;
+  if (pi < ntl && !df_easy(rt.desc[tl[pi]])) hard[atomicAdd(&nhard, 1u)] = pi;
+  __syncthreads();
+  const uint32_t nh = nhard;
+  for (uint32_t k = 0; k < nh; ++k) {
+    const uint32_t p = hard[k];
+    DictIdxMaker mk{pages, chunks, idx, p};
+    tile_one(blob, blob_len, rt.desc, tl[p], rt.runs, sm, mk);
+    __syncthreads();
+  }
 }
 
 constexpr int DW_NT = 1024;                         // k_dict_win threads
@@ -374,9 +408,8 @@ constexpr int DW_F = (int)((DW_CH + DW_NT - 1) / DW_NT);
 template <int ES>
 __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                     const uint32_t* __restrict__ tl, uint32_t ntl,
-                                                    const PageWork* __restrict__ pages,
-                                                    const ChunkWork* __restrict__ chunks, RunTables rt,
-                                                    const uint16_t* __restrict__ idx) {
+                                                    PageWork* __restrict__ pages, ChunkWork* __restrict__ chunks,
+                                                    RunTables rt, const uint16_t* __restrict__ idx) {
   using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
   constexpr uint32_t WIN = DW_BYTES / ES;  // entries per window
   __shared__ uint4 win[DW_CH + 1];         // (+1: the unaligned reads' third word)
@@ -384,32 +417,148 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   if (*rt.nfall == 0) return;
   const uint32_t tid = threadIdx.x, q = tid >> 7, lt = tid & 127u;
   const uint32_t p = blockIdx.x * DW_TPW + q;
-  uint32_t qlo = 0, qhi = 0;
+  const QDesc d = p < ntl ? rt.desc[tl[p]] : QDesc{};
+  const uint32_t qlo = d.qlo, qhi = d.qhi;
   uint64_t obase = 0;
   int32_t key = -1;
-  if (p < ntl) {
-    const QDesc& d = rt.desc[tl[p]];
-    qhi = d.qhi;
-    if (qhi) {
-      qlo = d.qlo;
-      const ChunkWork& ck = chunks[pages[d.page].chunk];
-      key = ck.dict_page;
-      obase = reinterpret_cast<uint64_t>(ck.val_out) + (d.out + qlo) * (uint64_t)ES;
-    }
+  uint32_t D0 = 0;
+  if (qhi) {
+    const ChunkWork& ck = chunks[pages[d.page].chunk];
+    key = ck.dict_page;
+    D0 = pages[key].num_values;
+    obase = reinterpret_cast<uint64_t>(ck.val_out) + (d.out + qlo) * (uint64_t)ES;
   }
   if (lt == 0) dkey[q] = key;
   // the thread's 32 values: 16 pairs, pair s at tile outputs qlo + 2 (128 s + lt) + {0, 1} (each
   // store instruction of a wave one contiguous run of 64 pairs); rem: the tile's outputs from the
   // thread's first pair on
   const int32_t rem = (int32_t)(qhi - qlo) - (int32_t)(2u * lt);
-  const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + (uint64_t)p * RUN_TILE) + lt;
   uint32_t ix[16];
+  const bool easy = df_easy(d);
+  // ---- an easy tile's indices are decoded here (rle.rs:437-487): its run records and payload go
+  // to the tile's region of the window, then each thread takes its 32 indices from the LDS copy
+  uint8_t* R = reinterpret_cast<uint8_t*>(win) + q * DF_TB;
+  uint32_t* rs = reinterpret_cast<uint32_t*>(R);  // run starts (page-relative outputs)
+  uint32_t* ri = rs + DF_RC + 2;                  // run info (payload offset, or R_RLE | value)
+  const uint32_t nr = tx_nrec(d);
+  uint32_t sb32 = 0;
+  if (easy) {
+    if (d.kind == LK_BIT_PACKED) {  // one header-less run from output 0
+      if (lt == 0) {
+        rs[0] = 0;
+        ri[0] = 0;
+      }
+    } else if (lt < nr) {  // (nr <= DF_RC = 128: one record per thread)
+      const uint2 r = rt.runs[d.rec + lt];
+      rs[lt] = r.x;
+      ri[lt] = r.y;
+    }
+    if (lt == 0) rs[nr] = rs[nr + 1] = qhi;
+    uint32_t nch = 0;
+    if (d.bhi) {
+      const uint64_t A0 = (d.S + d.blo) & ~15ull;
+      nch = (uint32_t)((d.S + d.bhi - A0 + 15) / 16);
+      sb32 = (uint32_t)(A0 - d.S);
+      const bool fast = A0 + (uint64_t)nch * 16 <= blob_len;
+      uint4* P = reinterpret_cast<uint4*>(R + DF_POFF);
+      constexpr uint32_t NCH = (DF_PAY / 16 + 127) / 128;  // chunks per thread at most
+      uint4 v[NCH];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) ix[s] = s * 256 < rem ? ip[s * 128] : 0u;
+      for (uint32_t k = 0; k < NCH; ++k) {  // every load in flight before the first LDS write
+        const uint32_t c = lt + k * 128;
+        const uint64_t a = A0 + (uint64_t)c * 16;
+        v[k] = c >= nch ? make_uint4(0u, 0u, 0u, 0u)
+               : fast   ? *reinterpret_cast<const uint4*>(blob + a)
+                        : gload_u128_tail(blob, blob_len, a);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < NCH; ++k)
+        if (lt + k * 128 <= nch) P[lt + k * 128] = v[k];  // (chunk nch: zeros, the last funnel word)
+    }
+  }
+  __syncthreads();  // (every wave: the tiles of one workgroup may differ in kind)
+  // per 256-output block k of an easy tile (pair s of every thread lies in block s): the run
+  // holding its first output and the run after it (start, info each, and the start after them),
+  // found once by thread k
+  uint4* blk = reinterpret_cast<uint4*>(R + DF_BLK);
+  uint32_t* blk2 = reinterpret_cast<uint32_t*>(R + DF_BLK + 16 * 16);
+  if (easy && lt < 16) {
+    const uint32_t o = qlo + 256u * lt;
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t step = DF_RC / 2; step; step >>= 1)
+      if (a + step < nr && rs[a + step] <= o) a += step;
+    const bool two = a + 1 < nr;
+    blk[lt] = make_uint4(rs[a], ri[a], rs[a + 1], two ? ri[a + 1] : 0u);
+    blk2[2 * lt] = two ? rs[a + 2] : qhi;
+    blk2[2 * lt + 1] = a;
+  }
+  __syncthreads();
+  if (easy) {
+    const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(R + DF_POFF);
+    const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
+    bool bad = false;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      uint32_t v0 = 0, v1 = 0;
+      const uint32_t o0 = qlo + 2u * (128u * (uint32_t)s + lt);
+      if (s * 256 < rem) {
+        const uint4 b = blk[s];
+        const uint32_t nx2 = blk2[2 * s];
+        // the pair inside one of the block's two runs (w <= 16: both values in one 32-bit window)
+        const bool inA = o0 + 1 < b.z, inB = o0 >= b.z && o0 + 1 < nx2;
+        if ((inA || inB) && w <= 16) {
+          const uint32_t st = inA ? b.x : b.z, inf = inA ? b.y : b.w;
+          if (inf & R_RLE) {
+            v0 = v1 = inf & 0x7FFFFFFFu;
+          } else {
+            const uint32_t bit = (inf - sb32) * 8u + (o0 - st) * w;
+            const uint32_t wi = bit >> 5;
+            const uint32_t x = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u);
+            v0 = x & wm;
+            v1 = (x >> w) & wm;
+          }
+        } else {  // any other case, value by value from the block's first run on
+          uint32_t a = blk2[2 * s + 1], st = b.x, inf = b.y, nx = b.z;
+          uint32_t v2[2] = {0u, 0u};
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t o = o0 + (uint32_t)j;
+#pragma unroll 1
+            while (nx <= o && a + 1 < nr) {
+              ++a;
+              st = nx;
+              inf = ri[a];
+              nx = rs[a + 1];
+            }
+            if (inf & R_RLE) {
+              v2[j] = inf & 0x7FFFFFFFu;
+            } else {
+              const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
+              const uint32_t wi = bit >> 5;
+              v2[j] = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u) & wm;
+            }
+          }
+          v0 = v2[0];
+          v1 = v2[1];
+        }
+        if (s * 256 + 1 >= rem) v1 = 0;  // (the tile's last output: no second value)
+        // dict[idx] out of bounds: the reference panics (rle.rs:455,470)
+        bad |= v0 >= D0 || (s * 256 + 1 < rem && v1 >= D0);
+      }
+      ix[s] = (v0 & 0xFFFFu) | (v1 << 16);
+    }
+    const uint64_t bm = __ballot(bad);
+    if (bm && (tid & 63u) == (uint32_t)__builtin_ctzll(bm)) report(pages, chunks, (int)d.page, ST_PANIC);
+  } else {
+    const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + (uint64_t)p * RUN_TILE) + lt;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) ix[s] = s * 256 < rem ? ip[s * 128] : 0u;
+  }
   T x[16][2];
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s][0] = x[s][1] = 0;
-  __syncthreads();
+  __syncthreads();  // (the stage regions are the window's)
   for (int qq = 0; qq < DW_TPW; ++qq) {  // each distinct dictionary of the 8 tiles (uniform)
     const int32_t kq = dkey[qq];
     bool seen = kq < 0;
@@ -857,7 +1006,9 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
     uint16_t* slot = didx;
     for (int k = 0; k < 2; ++k) {
       if (!wn[k]) continue;
-      hipLaunchKernelGGL(k_texpand_didx, dim3(wn[k]), dim3(WG), 0, s, blob, blob_len, wl[k], pages, chunks, rt, slot);
+      // the tiles k_dict_win does not decode itself (none at the benchmark's shape), 256 list entries per workgroup
+      hipLaunchKernelGGL(k_texpand_didx, dim3((wn[k] + WG - 1) / WG), dim3(WG), 0, s, blob, blob_len, wl[k], wn[k],
+                         pages, chunks, rt, slot);
       const dim3 g((wn[k] + DW_TPW - 1) / DW_TPW);
       if (k == 0)
         hipLaunchKernelGGL((k_dict_win<4>), g, dim3(DW_NT), 0, s, blob, blob_len, wl[k], wn[k], pages, chunks, rt, slot);

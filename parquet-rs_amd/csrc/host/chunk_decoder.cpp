@@ -172,6 +172,7 @@ struct pqg_ctx {
   uint32_t dbg_n = 0;
   uint64_t acc_n = 0;
   uint32_t values_kernel = 0;
+  uint32_t paths = 0;  // PQG_PATH_* of the last decode
   uint64_t* sp_tiles = nullptr;  // pqg_space_values: per tile of levels, max_def count then base
   size_t sp_cap = 0;
   std::string msg;
@@ -949,11 +950,19 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   if (np && !fused_scan) HIPCHK(pqg_launch_scan(d_pages, ni, d_chunks, s), "scan");
   if (ctx->timing) hipEventRecord(ev[3], s);
   ctx->values_kernel = 0;
+  ctx->paths = 0;
   if (np) {
     const RunTables& rd = sl.rt[K_DICT];
     if (any_badict)
       HIPCHK(pqg_launch_ba_dict_prep(b, blob_len, d_pages, d_chunks, (int)nc, sl.dsrc, sl.dlen, s),
              "byte-array dictionary");
+    if (nlvdict) ctx->paths |= PQG_PATH_DICT_LEVEL;
+    if (ntl[TL_W4] + ntl[TL_W8]) ctx->paths |= PQG_PATH_DICT_WINDOW;
+    if (ntl[TL_D1] + ntl[TL_D4] + ntl[TL_D8] + ntl[TL_D12]) ctx->paths |= PQG_PATH_DICT_TILES;
+    if (any_ba) ctx->paths |= PQG_PATH_BYTES | (any_dba ? PQG_PATH_DELTA_BYTES : 0u);
+    if (any_plain) ctx->paths |= PQG_PATH_PLAIN;
+    if (delta_es) ctx->paths |= PQG_PATH_DELTA;
+    if (any_rbool) ctx->paths |= PQG_PATH_RLE_BOOL;
     if (nlvdict)  // every dictionary chunk the level path takes, fixed-width and byte-array, in one pass
       HIPCHK(pqg_launch_lv(b, blob_len, d_pages, ni, d_chunks, SS_DICT, 0u, sl.dsrc, sl.dlen, sl.vsrc, sl.vlen, rd,
                            sl.lt(K_DICT, 64), s),
@@ -1124,6 +1133,12 @@ int pqg_get_timings(pqg_ctx* ctx, pqg_timings* t) {
   t->levels_kernel_ms = (float)(ctx->acc_ms[5] / n);
   t->values_kernel_ms = (float)(ctx->acc_ms[6] / n);
   t->values_kernel = ctx->values_kernel;
+  return PQG_OK;
+}
+
+int pqg_ctx_last_paths(pqg_ctx* ctx, uint32_t* mask) {
+  if (!ctx || !mask) return PQG_ERR_INVALID;
+  *mask = ctx->paths;
   return PQG_OK;
 }
 

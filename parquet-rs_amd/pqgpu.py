@@ -78,7 +78,7 @@ EXPORTS = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_set_timing", "pqg_ctx_set_overlap", "pqg_decode_chunk",
     "pqg_decode_chunks",
     "pqg_sync", "pqg_sync_detail",
-    "pqg_get_timings", "pqg_reset_timings", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
+    "pqg_get_timings", "pqg_reset_timings", "pqg_ctx_last_paths", "pqg_error_message", "pqg_file_open", "pqg_file_open_memory",
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
     "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
@@ -114,6 +114,7 @@ def lib():
         L.pqg_sync_detail.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.pqg_get_timings.argtypes = [vp, C.POINTER(Timings)]
         L.pqg_reset_timings.argtypes = [vp]
+        L.pqg_ctx_last_paths.argtypes = [vp, C.POINTER(C.c_uint32)]
         L.pqg_error_message.argtypes = [vp]
         L.pqg_error_message.restype = C.c_char_p
         L.pqg_file_open.argtypes = [C.c_char_p, C.POINTER(vp)]
@@ -259,6 +260,12 @@ class Context:
         lib().pqg_get_timings(self.h, C.byref(t))
         return t
 
+    def last_paths(self):
+        """PATH_* mask of the value-kernel families the last decode enqueued."""
+        m = C.c_uint32(0)
+        lib().pqg_ctx_last_paths(self.h, C.byref(m))
+        return m.value
+
 
 class RowGroupDecoder:
     """pqg_rg_ctx: the column chunks of a row group decoded concurrently on `nstreams` HIP
@@ -317,13 +324,19 @@ class RowGroupDecoder:
         return st, call.value, col.value, page.value
 
 
-def make_pages(specs):
+# pqg_ctx_last_paths bits (pqgpu.h PQG_PATH_*)
+PATH_PLAIN, PATH_DICT_LEVEL, PATH_DICT_WINDOW, PATH_DICT_TILES = 1, 2, 4, 8
+PATH_BYTES, PATH_DELTA_BYTES, PATH_DELTA, PATH_RLE_BOOL = 16, 32, 64, 128
+
+
+def make_pages(specs, misalign=0):
     """Pack page specs (objects with page_type, buf, num_values, encoding, def_encoding,
-    rep_encoding, def_len, rep_len) into a host blob with 64-byte aligned payloads."""
+    rep_encoding, def_len, rep_len) into a host blob with 64-byte aligned payloads (at
+    `misalign` bytes past a 64-byte boundary: the C ABI takes any payload offset)."""
     arr = (Page * max(len(specs), 1))()
     parts, off = [], 0
     for i, s in enumerate(specs):
-        pad = (-off) % 64
+        pad = (misalign - off) % 64
         if pad:
             parts.append(b"\0" * pad)
             off += pad
@@ -337,7 +350,7 @@ def make_pages(specs):
 
 
 def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_def=True,
-                  want_rep=True, device=None, stream=None, values_capacity=None):
+                  want_rep=True, device=None, stream=None, values_capacity=None, misalign=0):
     """Decode one column chunk on the GPU; returns a dict with numpy def/rep/values.
 
     Equivalent to reading every batch of ColumnReaderImpl::read_batch (column/reader.rs
@@ -345,7 +358,7 @@ def decode_column(ctx, ptype, specs, max_def=0, max_rep=0, type_length=-1, want_
     dense non-null values (BYTE_ARRAY/FLBA: list of bytes, plus "offsets" and "bytes")."""
     torch = _torch()
     dev = device if device is not None else torch.device("cuda", ctx.device)
-    blob, pages = make_pages(specs)
+    blob, pages = make_pages(specs, misalign)
     d_blob = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
     nlev = sum(s.num_values for s in specs if s.page_type in (PAGE_DATA, PAGE_DATA_V2))
     ba = ptype in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY)

@@ -85,8 +85,10 @@ def test_dictionary_pages_bench_shape(oracle, ctx):
     data pages of bit width 16, written by the bench's own generator (pqg_gen_dict_int64: reference
     DictEncoder + RleEncoder, rle.rs:152-316), four full pages and a ragged fifth, against the
     oracle's read_batch (get_batch_with_dict, rle.rs:437-487; DictDecoder, decoding.rs:282-309):
-    every value. This is the general decoder's full-page path (k_run_index's 64-run fast-forward,
-    k_tile_desc, 256 k_texpand_dict tiles per page)."""
+    every value. This is the windowed dictionary path the benchmark times (k_run_index's 64-run
+    fast-forward, k_tile_desc, then k_dict_win: each workgroup decodes its 8 tiles' indices from
+    their run records and payload in LDS and gathers them through 128 KiB dictionary windows);
+    the test asserts that this path ran (pqg_ctx_last_paths)."""
     import ctypes as C
 
     import pqgpu
@@ -106,6 +108,7 @@ def test_dictionary_pages_bench_shape(oracle, ctx):
     got = pqgpu.decode_column(ctx, pqgpu.INT64, specs)
     assert ref["status"] == 0, ref["message"]
     assert got["status"] == 0, got["message"]
+    assert ctx.last_paths() & pqgpu.PATH_DICT_WINDOW, ctx.last_paths()
     assert got["num_values"] == n == len(ref["values"])
     np.testing.assert_array_equal(got["values"], ref["values"])
     # and the generator's own truth for the ragged last page

@@ -404,3 +404,34 @@ def test_delta_bench_pages_lookback(oracle, ctx, ptype, shape):
             o += k
     got, ref = _same(oracle, ctx, t, specs)
     assert got["num_values"] == n
+
+
+@pytest.mark.parametrize("misalign", [1, 3, 8, 13])
+def test_unaligned_payloads(oracle, ctx, misalign):
+    """The C ABI takes any payload offset (pqgpu.h pqg_page.offset): every page here starts
+    `misalign` bytes past a 64-byte boundary. Windowed dictionary gathers (5 000 INT64 / 3 000
+    INT32 entries: the window realigned in LDS), PLAIN copies, DELTA and byte arrays."""
+    import pqgpu
+    rng = np.random.default_rng(500 + misalign)
+    cases = []
+    for ptype, dt, nd in (("INT64", np.int64, 5000), ("INT32", np.int32, 3000)):
+        t = getattr(oracle, ptype)
+        dvals = np.unique(rng.integers(-2**30, 2**30, 2 * nd).astype(dt))[:nd]
+        bw = int(np.ceil(np.log2(len(dvals))))
+        pages = [oracle.PageSpec(oracle.PAGE_DICTIONARY, dvals.tobytes(), len(dvals), oracle.PLAIN)]
+        for n in (50000, 4099):
+            body = bytes([bw]) + _hybrid(rng.integers(0, len(dvals), n), bw)
+            pages.append(oracle.PageSpec(oracle.PAGE_DATA, body, n, oracle.RLE_DICTIONARY))
+        cases.append((t, pages, pqgpu.PATH_DICT_WINDOW))
+    v = rng.integers(-2**31, 2**31, 30001, dtype=np.int64).astype(np.int32)
+    cases.append((oracle.INT32, [oracle.PageSpec(oracle.PAGE_DATA, v.tobytes(), len(v), oracle.PLAIN)],
+                  pqgpu.PATH_PLAIN))
+    v = _delta_values(rng, np.int64, 20001, "d16")
+    cases.append((oracle.INT64, [oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_encode(oracle.INT64, v, 512, 4),
+                                                 len(v), oracle.DELTA_BINARY_PACKED)], pqgpu.PATH_DELTA))
+    for t, pages, path in cases:
+        ref = oracle.read_column(t, pages)
+        got = pqgpu.decode_column(ctx, t, pages, misalign=misalign)
+        assert ref["status"] == 0 and got["status"] == 0, (got["message"], ref["message"])
+        assert ctx.last_paths() & path, (path, ctx.last_paths())
+        assert got["values"].tobytes() == ref["values"].tobytes()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing on the GPU box: bench.py once per argument set (no profiler), one summary line each.
-#   tools/ab.sh <tag> "<bench args 1>" "<bench args 2>" ...
+#   tools/diag/ab.sh <tag> "<bench args 1>" "<bench args 2>" ...
 # An argument "VAR=value ...|<bench args>" runs that set with the environment assignments first
 # (e.g. "PQG_LIBDIR=lib_spk2|--config levels": an experiment build).
 set -o pipefail

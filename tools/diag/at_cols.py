@@ -1,13 +1,13 @@
 """Per-column decode time of one alltypes row group (bench.py's AlltypesWorkload), HIP events
 around each column's decode_async. Not part of the product or the bench.
 
-    python tools/at_cols.py [--rg-rows 8388608] [--reps 5]
+    python tools/diag/at_cols.py [--rg-rows 8388608] [--reps 5]
 """
 import argparse
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for d in ("", "parquet-rs_amd", os.path.join("tools", "gen")):
     sys.path.insert(0, os.path.join(ROOT, d))
 

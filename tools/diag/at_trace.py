@@ -1,4 +1,4 @@
-"""Per-column kernel breakdown of tools/at_cols.py from a rocprofv3 kernel trace (decodes split
+"""Per-column kernel breakdown of tools/diag/at_cols.py from a rocprofv3 kernel trace (decodes split
 at each k_prepare launch: the row-group check's 11 decodes first, then reps + 1 per column)."""
 import collections
 import csv

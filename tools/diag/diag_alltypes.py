@@ -1,7 +1,7 @@
 """Diagnostics: decode one alltypes column chunk with the diagnostic library (PQG_DEBUG modes) and
 compare levels / value count / values with the generator. Not part of the product or the bench.
 
-    PQG_DEBUG=256 python tools/diag_alltypes.py --col 6
+    PQG_DEBUG=256 python tools/diag/diag_alltypes.py --col 6
 """
 import argparse
 import os
@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for d in ("parquet-rs_amd", os.path.join("tools", "gen"), "oracle"):
     sys.path.insert(0, os.path.join(ROOT, d))
 

@@ -1,7 +1,7 @@
 """Diagnostics: which pages of an alltypes row group the level path hands back to the general
 decoder, and where (PQG_DIAG build, PQG_DEBUG=512; sites in pqg_levels.hip LV_BAIL).
 
-    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=512 python tools/diag_bail.py [--rows 8388608]
+    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=512 python tools/diag/diag_bail.py [--rows 8388608]
 """
 import argparse
 import collections
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for d in ("parquet-rs_amd", os.path.join("tools", "gen"), "oracle"):
     sys.path.insert(0, os.path.join(ROOT, d))
 

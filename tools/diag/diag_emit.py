@@ -2,7 +2,7 @@
 per window, the staging wait, chain / run placement, bitmap generation and output stores
 (s_memtime stamps).
 
-    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=256 python tools/diag_emit.py --p-null 0.1
+    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=256 python tools/diag/diag_emit.py --p-null 0.1
 """
 import argparse
 import ctypes as C
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 sys.path.insert(0, ROOT)

@@ -2,8 +2,8 @@
 build (make -C parquet-rs_amd DIAG=1 -> lib_diag/libpqgpu.so). Not part of the product or the
 bench: PQG_DEBUG is read only by the diagnostic library.
 
-    PQG_DEBUG=64 python tools/diag_walk.py --p-null 0.5 [--n 2e8]     # page verdicts
-    PQG_DEBUG=128 python tools/diag_walk.py --p-null 0.5 --stamps      # segment walk cycles
+    PQG_DEBUG=64 python tools/diag/diag_walk.py --p-null 0.5 [--n 2e8]     # page verdicts
+    PQG_DEBUG=128 python tools/diag/diag_walk.py --p-null 0.5 --stamps      # segment walk cycles
 """
 import argparse
 import collections
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 sys.path.insert(0, ROOT)

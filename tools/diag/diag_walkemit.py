@@ -2,7 +2,7 @@
 cycles on config 5 (PQG_DIAG build, PQG_DEBUG=1024): per wave s_memtime cycles in the run bounds
 and records, the payload staging and the writes by value size, per unit and per output.
 
-    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=1024 python tools/diag_walkemit.py [--rowgroups 2]
+    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=1024 python tools/diag/diag_walkemit.py [--rowgroups 2]
 """
 import argparse
 import ctypes as C
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 sys.path.insert(0, ROOT)

@@ -2,7 +2,7 @@
 build, PQG_DEBUG=2048): stage wait, segment tables, the chain from 0 and the entry walks, the
 reference choice (with the second chain when entry 0 is not on the majority chain), table writes.
 
-    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=2048 python tools/diag_win.py --p-null 0.1
+    make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=2048 python tools/diag/diag_win.py --p-null 0.1
 """
 import argparse
 import ctypes as C
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "parquet-rs_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools", "gen"))
 sys.path.insert(0, ROOT)

@@ -4,7 +4,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for d in ("", "parquet-rs_amd", os.path.join("tools", "gen")):
     sys.path.insert(0, os.path.join(ROOT, d))
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Memory-instruction census of kernels in a device assembly file (hipcc --cuda-device-only -S):
-  python tools/isa_ops.py file.s [name-substring]"""
+  python tools/diag/isa_ops.py file.s [name-substring]"""
 import collections
 import re
 import sys

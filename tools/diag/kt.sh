@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-trace one or more bench runs on the GPU box and print per-kernel average times.
-#   tools/kt.sh <tag> "<bench args 1>" ["<bench args 2>" ...]
+#   tools/diag/kt.sh <tag> "<bench args 1>" ["<bench args 2>" ...]
 set -o pipefail
 tag=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box check used while iterating: gpu parity tests, then bench + kernel-trace stats per config.
-#   tools/quick.sh <tag> [configs...]
+#   tools/diag/quick.sh <tag> [configs...]
 set -o pipefail
 tag=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

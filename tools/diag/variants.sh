@@ -1,6 +1,6 @@
 #!/bin/bash
 # Time one bench config under several PQG_DEBUG diagnostics variants (kernel-trace stats each).
-#   tools/variants.sh <tag> <config> <debug values...>
+#   tools/diag/variants.sh <tag> <config> <debug values...>
 set -o pipefail
 tag=$1; cfg=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
