@@ -492,6 +492,8 @@ struct BaSrc {
   }
 };
 
+constexpr uint32_t TS_DL = 2048;  // k_ba_tsum: dictionaries of at most this many entries staged in LDS
+
 // Per listed tile (gt, global) of a byte-array page: the tile's byte count into tsum[gt] (the
 // offsets themselves are written once, by k_ba_copy, from the scanned tile starts).
 __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork* chunks,
@@ -500,6 +502,7 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
                                                 const uint64_t* dsrc0, const uint32_t* dlen0,
                                                 uint64_t* __restrict__ tsum) {
   __shared__ uint64_t red[WG / 64];
+  __shared__ uint32_t sdl[TS_DL];  // a small dictionary's entry lengths
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
@@ -509,10 +512,27 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
   const uint64_t n = pw.nonnull, vo = pw.value_out;
   if ((uint64_t)t * BA_T >= n) return;
   uint64_t s = 0;
+#ifdef PQG_TS_OFF
+  if (false) {
+#else
+  if (bs.via_dict && bs.nd <= TS_DL) {  // the level path's dictionary chunks: lengths from LDS
+#endif
+    for (uint32_t i = threadIdx.x; i < bs.nd; i += WG) sdl[i] = bs.dlen[i];
+    uint32_t ix[BA_VPT];
 #pragma unroll
-  for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
-    const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
-    s += i < n ? bs.len(vo + i) : 0u;
+    for (uint32_t k = 0; k < BA_VPT; ++k) {  // every index load in flight
+      const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+      ix[k] = i < n ? bs.vlen[vo + i] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < BA_VPT; ++k) s += ix[k] < bs.nd ? sdl[ix[k]] : 0u;
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
+      const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+      s += i < n ? bs.len(vo + i) : 0u;
+    }
   }
   const uint64_t tot = block_sum_u64(s, red);
   if (threadIdx.x == 0) tsum[gt] = tot;
@@ -743,7 +763,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
                                                    const uint32_t* __restrict__ tl, const uint32_t* __restrict__ vlen0,
                                                    const uint64_t* __restrict__ dsrc0, const uint32_t* __restrict__ dlen0,
                                                    const uint64_t* __restrict__ tsum) {
-  __shared__ __attribute__((aligned(16))) uint8_t ldict[BSD_BYTES + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t ldict[BSD_BYTES + 48];
   __shared__ uint32_t doff[BSD_N], dln[BSD_N];
   __shared__ __attribute__((aligned(16))) uint8_t img[BSD_IMG + 32];
   __shared__ uint32_t wsum[WG / 64];
@@ -770,9 +790,16 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   // the dictionary page and its entries into LDS
   const PageWork& dp = pages[ck.dict_page];
   const uint32_t nd = dp.num_values, nb = dp.nbytes;
-  for (uint32_t i = tid; i < nb; i += WG) ldict[i] = blob[dp.base + i];
+  // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it)
+  const uint64_t db = dp.base & ~15ull;
+  const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
+  for (uint32_t c = tid; c < nch; c += WG) {
+    const uint64_t a = db + (uint64_t)c * 16;
+    reinterpret_cast<uint4*>(ldict)[c] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a)
+                                                            : gload_u128_tail(blob, blob_len, a);
+  }
   for (uint32_t i = tid; i < nd; i += WG) {
-    doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - dp.base);
+    doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - db);
     dln[i] = dlen0[ck.dscr_base + i];
   }
   __syncthreads();
