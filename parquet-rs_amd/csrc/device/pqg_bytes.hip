@@ -575,7 +575,7 @@ __device__ inline uint32_t ba_pad(uint32_t j) { return j + (j >> 4); }
 // Small dictionaries of the level path's byte-array chunks take k_ba_copy_sd (below).
 constexpr uint32_t BSD_N = 1024;
 constexpr uint32_t BSD_BYTES = 12288;
-constexpr uint32_t BSD_IMG = WG * 16;  // round image (longer rounds: byte stores from LDS)
+constexpr uint32_t BSD_IMG = WG * 8 * 8 + 32;  // round image: BSD_RN (2048) values of up to 8 bytes (longer: byte stores from LDS)
 
 __device__ inline bool ba_small_dict(const PageWork& pw, const ChunkWork& ck, const PageWork* pages) {
   if (!(pw.encoding == E_RLE_DICTIONARY && ck.lvdict && ck.dict_page >= 0)) return false;
@@ -755,9 +755,14 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
 // BSD_N entries in at most BSD_BYTES bytes: short categorical strings): the dictionary page's bytes
 // and its entries' offsets and lengths are staged in LDS, so a value's length and bytes cost LDS
 // reads only; the only global loads are the values' indices (coalesced, all 16 in flight at once).
-// The tile goes in rounds of WG values (lane l: value k * WG + l): a workgroup scan of the round's
-// lengths gives its offsets (stored coalesced) and its bytes are assembled in an LDS image of the
-// round's output and stored with 16-byte stores. The general kernel exits for these tiles.
+// The tile goes in two rounds of BSD_RN values (lane l: values k * WG + l, k-major): eight wave
+// scans of the round's lengths and one exchange of their totals give its offsets (stored
+// coalesced); its bytes are assembled in an LDS image of the round's output (8-byte strings of a
+// whole round fit) and stored with 16-byte stores. The general kernel exits for these tiles.
+constexpr uint32_t BSD_RV = 8;                    // values per thread per round
+constexpr uint32_t BSD_RN = BSD_RV * WG;          // values per round
+static_assert(BSD_RN * 2 == BA_T, "two rounds per tile");
+
 __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
                                                    const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
                                                    const uint32_t* __restrict__ tl, const uint32_t* __restrict__ vlen0,
@@ -766,7 +771,7 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   __shared__ __attribute__((aligned(16))) uint8_t ldict[BSD_BYTES + 48];
   __shared__ uint32_t doff[BSD_N], dln[BSD_N];
   __shared__ __attribute__((aligned(16))) uint8_t img[BSD_IMG + 32];
-  __shared__ uint32_t wsum[WG / 64];
+  __shared__ uint32_t wsum[BSD_RV][WG / 64];
   const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
@@ -787,10 +792,9 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
     const uint32_t j = k * WG + tid;
     idx[k] = j < cnt ? vlen[vo + t0 + j] : 0u;
   }
-  // the dictionary page and its entries into LDS
+  // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it)
   const PageWork& dp = pages[ck.dict_page];
   const uint32_t nd = dp.num_values, nb = dp.nbytes;
-  // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it)
   const uint64_t db = dp.base & ~15ull;
   const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
   for (uint32_t c = tid; c < nch; c += WG) {
@@ -805,31 +809,47 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   __syncthreads();
   uint64_t run = tsum[gt];  // output byte offset of the round's first value
 #pragma unroll 1
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    const uint32_t j = k * WG + tid;
-    if (k * WG >= cnt) break;
-    const bool vj = j < cnt, in = vj && idx[k] < nd;  // (an index slot not written: empty, as BaSrc)
-    const uint32_t ln = in ? dln[idx[k]] : 0u;
-    uint32_t incl = ln;
+  for (uint32_t r = 0; r < 2; ++r) {
+    if (r * BSD_RN >= cnt) break;
+    uint32_t ln[BSD_RV], so[BSD_RV], pre[BSD_RV];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
-      if (lane >= (uint32_t)off) incl += y;
+    for (uint32_t k = 0; k < BSD_RV; ++k) {
+      const uint32_t kk = r * BSD_RV + k, j = kk * WG + tid;
+      // (an index slot past the dictionary: empty, as BaSrc)
+      const bool in = j < cnt && idx[kk] < nd;
+      ln[k] = in ? dln[idx[kk]] : 0u;
+      so[k] = in ? doff[idx[kk]] : 0u;
+      const uint32_t inc = wave_scan_incl_u32(ln[k]);
+      pre[k] = inc - ln[k];
+      if (lane == 63u) wsum[k][wv] = inc;
     }
-    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    uint32_t pre = incl - ln, tot = 0;
+    uint32_t tot = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < WG / 64; ++w) {
-      if (w < wv) pre += wsum[w];
-      tot += wsum[w];
+    for (uint32_t k = 0; k < BSD_RV; ++k) {  // value (k, tid): the rows before, the waves before
+      uint32_t rb = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < WG / 64; ++w) {
+        const uint32_t x = wsum[k][w];
+        if (w < wv) pre[k] += x;
+        rb += x;
+      }
+      pre[k] += tot;
+      tot += rb;
     }
-    if (vj) offsets[vo + t0 + j] = (int64_t)(run + pre);
+#pragma unroll
+    for (uint32_t k = 0; k < BSD_RV; ++k) {
+      const uint32_t j = (r * BSD_RV + k) * WG + tid;
+      if (j < cnt) offsets[vo + t0 + j] = (int64_t)(run + pre[k]);
+    }
     const uint64_t gA = run, gB = run + tot;
     const uint32_t sh = (uint32_t)(gA & 15u);
-    if (tot + 16 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is
-      const uint32_t b0 = pre + sh, so = in ? doff[idx[k]] : 0u;
-      for (uint32_t q = 0; q < ln; ++q) img[b0 + q] = ldict[so + q];
+    if (tot + 32 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is
+#pragma unroll
+      for (uint32_t k = 0; k < BSD_RV; ++k) {
+        const uint32_t b0 = pre[k] + sh;
+        for (uint32_t q = 0; q < ln[k]; ++q) img[b0 + q] = ldict[so[k] + q];
+      }
       __syncthreads();
       const uint64_t c0 = gA & ~15ull;
       for (uint64_t c = c0 + (uint64_t)tid * 16u; c < gB; c += (uint64_t)WG * 16u) {
@@ -841,9 +861,10 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
             if (c + q >= gA && c + q < gB) out[c + q] = img[ii + q];
         }
       }
-    } else if (in) {  // long values: straight from the LDS dictionary
-      const uint32_t so = doff[idx[k]];
-      for (uint32_t q = 0; q < ln; ++q) out[gA + pre + q] = ldict[so + q];
+    } else {  // long values: straight from the LDS dictionary
+#pragma unroll 1
+      for (uint32_t k = 0; k < BSD_RV; ++k)
+        for (uint32_t q = 0; q < ln[k]; ++q) out[gA + pre[k] + q] = ldict[so[k] + q];
     }
     run += tot;
     __syncthreads();  // (wsum and the image are reused by the next round)
