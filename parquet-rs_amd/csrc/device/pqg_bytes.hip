@@ -135,14 +135,25 @@ __device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen,
                                        const uint32_t* len, uint64_t* src) {
   uint64_t carry = 0;
   int32_t bad = 0;
-  for (uint64_t b = 0; b < n; b += WG) {
-    const uint64_t i = b + threadIdx.x;
-    const int32_t l = i < n ? (int32_t)len[i] : 0;
+  constexpr uint32_t PT = 16;  // lengths per thread per pass (one workgroup scan per 4096 values)
+  for (uint64_t b = 0; b < n; b += (uint64_t)WG * PT) {
+    const uint64_t i0 = b + (uint64_t)threadIdx.x * PT;
+    int32_t l[PT];
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      l[k] = i0 + k < n ? (int32_t)len[i0 + k] : 0;
+      s += l[k] > 0 ? (uint64_t)l[k] : 0;
+    }
     uint64_t tot;
-    const uint64_t pre = block_exscan(sm, l > 0 ? (uint64_t)l : 0, tot);
-    if (i < n) {
-      if (l < 0 || carry + pre + (uint64_t)l > dlen) bad = 1;
-      else src[i] = D + carry + pre;
+    uint64_t off = carry + block_exscan(sm, s, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      if (i0 + k < n) {
+        if (l[k] < 0 || off + (uint64_t)l[k] > dlen) bad = 1;
+        else src[i0 + k] = D + off;
+      }
+      off += l[k] > 0 ? (uint64_t)l[k] : 0;
     }
     carry += tot;
   }
@@ -1067,43 +1078,38 @@ __global__ void __launch_bounds__(WG) k_dba_psv(PageWork* pages, const ChunkWork
     const uint32_t x = pre_s[ba_pad(j)];
     uint32_t r = DBA_NONE;
     if (x > 0) {
-      // own block, then the tile's earlier blocks
-      for (uint32_t q = j; q > (j & ~63u);) {
-        --q;
-        if (pre_s[ba_pad(q)] < x) {
-          r = (uint32_t)t0 + q;
-          break;
-        }
+      // every scan below reads its 64 candidates at once (unrolled, no early exit): a dependent
+      // load per step took ~128 global round trips for a value whose psv lies tiles back
+      const uint32_t b0 = j & ~63u;
+      int lr = -1;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {  // own block, before j
+        const uint32_t q = b0 + (uint32_t)i;
+        lr = (q < j && pre_s[ba_pad(q)] < x) ? i : lr;
       }
-      if (r == DBA_NONE) {
-        for (uint32_t b = j >> 6; b > 0 && r == DBA_NONE;) {
-          --b;
-          if (bmin_s[b] < x)
-            for (uint32_t q = b * 64u + 64u; q > b * 64u;) {
-              --q;
-              if (pre_s[ba_pad(q)] < x) {
-                r = (uint32_t)t0 + q;
-                break;
-              }
+      if (lr >= 0) {
+        r = (uint32_t)t0 + b0 + (uint32_t)lr;
+      } else {
+        int lb = -1;  // the tile's earlier blocks
+#pragma unroll
+        for (int bb = 0; bb < 64; ++bb) lb = ((uint32_t)bb < (j >> 6) && bmin_s[bb] < x) ? bb : lb;
+        if (lb >= 0) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) lr = pre_s[ba_pad((uint32_t)lb * 64u + (uint32_t)i)] < x ? i : lr;
+          r = (uint32_t)t0 + (uint32_t)lb * 64u + (uint32_t)lr;
+        } else if (t > 0) {  // earlier tiles: jump to the nearest of minimum < x
+          uint32_t u = t - 1;
+          while (u != DBA_NONE && dtp[(uint64_t)u * DBA_TSTRIDE + 64] >= x) u = dtp[(uint64_t)u * DBA_TSTRIDE + 65];
+          if (u != DBA_NONE) {
+            const uint32_t* um = dtp + (uint64_t)u * DBA_TSTRIDE;
+#pragma unroll
+            for (int bb = 0; bb < 64; ++bb) lb = um[bb] < x ? bb : lb;
+            if (lb >= 0) {
+              const uint32_t* up = vpre + (uint64_t)u * BA_T + (uint32_t)lb * 64u;
+#pragma unroll
+              for (int i = 0; i < 64; ++i) lr = up[i] < x ? i : lr;
+              if (lr >= 0) r = u * BA_T + (uint32_t)lb * 64u + (uint32_t)lr;
             }
-        }
-      }
-      if (r == DBA_NONE && t > 0) {  // earlier tiles: jump to the nearest of minimum < x
-        uint32_t u = t - 1;
-        while (u != DBA_NONE && dtp[(uint64_t)u * DBA_TSTRIDE + 64] >= x) u = dtp[(uint64_t)u * DBA_TSTRIDE + 65];
-        if (u != DBA_NONE) {
-          const uint32_t* um = dtp + (uint64_t)u * DBA_TSTRIDE;
-          for (uint32_t b = 64; b > 0 && r == DBA_NONE;) {
-            --b;
-            if (um[b] < x)
-              for (uint32_t q = b * 64u + 64u; q > b * 64u;) {
-                --q;
-                const uint32_t g = u * BA_T + q;
-                if (vpre[g] < x) {
-                  r = g;
-                  break;
-                }
-              }
           }
         }
       }
@@ -1136,7 +1142,6 @@ __global__ void __launch_bounds__(WG) k_dba_copy(const uint8_t* __restrict__ blo
   if (!dba_page_ok(pw, ck)) return;
   const uint64_t n = pw.nonnull, t0 = (uint64_t)(gt - pw.ltile0) * BA_T;
   if (t0 >= n) return;
-  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
   const uint64_t vb = ck.scr_base + pw.value_out;
   const uint64_t* vsrc = vsrc0 + vb;
   const uint32_t* vlen = vlen0 + vb;

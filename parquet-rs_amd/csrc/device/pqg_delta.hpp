@@ -147,8 +147,85 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
   __syncthreads();
 
   while (done < need) {
-    // ---------------- walk block headers (one lane)
-    if (tid == 0) {
+    // ---------------- walk block headers
+    if (nmb <= 8 && tid < 64) {
+      // wave 0: a hop loop finds the batch's headers (varint length and the sum of the widths give
+      // the next one, ~10 operations a hop), then lane j parses block j and makes every check the
+      // serial walk below makes; the first failing block (stream order) ends the batch as there
+      const uint32_t lane = tid, nmb32 = (uint32_t)nmb, hs = (uint32_t)(vpmb >> 3);
+      uint32_t cur = wcur, k = 0, posv = 0;
+      while (k < (uint32_t)NBCAP && done + (uint64_t)k * vpb < need) {
+        const uint64_t rel = S + cur - A0;
+        if (rel >= DBLK) break;
+        posv = lane == k ? cur : posv;
+        ++k;
+        if (cur >= slen) break;  // (its lane reports the stream end)
+        const uint64_t w0 = lload_u64(sm.region, (uint32_t)rel);
+        const uint64_t t8 = ~w0 & 0x8080808080808080ull;
+        if (!t8) break;  // a varint of 8 bytes or more: its lane parses it, the batch ends there
+        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
+        const uint64_t wy = lload_u64(sm.region, (uint32_t)rel + vl);
+        const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
+        const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+        const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+        const uint64_t nx = (uint64_t)cur + vl + nmb32 + (uint64_t)hs * sumw;
+        cur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+      }
+      int32_t e = 0;
+      uint32_t nxt = 0, endp = 0;
+      if (lane < k) {
+        const uint32_t pos = posv, ridx = (uint32_t)(S + pos - A0);
+        uint64_t zz;
+        const int vl = lds_vlq(sm.region, ridx, pos, slen, zz);
+        if (vl <= 0) {
+          e = vl ? ST_PANIC : ST_EOF;  // "Not enough data to decode 'min_delta'"
+        } else if ((uint64_t)pos + vl + nmb32 > slen) {
+          e = ST_EOF;  // "Not enough data to decode 'width'" (every width is read)
+        } else {
+          const uint64_t left = need - done - (uint64_t)lane * vpb;
+          const uint64_t inblk = left < vpb ? left : vpb;
+          const uint32_t mneed = (uint32_t)((inblk + vpmb - 1) / vpmb);
+          const uint32_t pay = pos + (uint32_t)vl + nmb32;
+          uint64_t boff = 0;
+          for (uint32_t m = 0; m < nmb32; ++m) {
+            const uint32_t wdt = lbyte(sm.region, ridx + (uint32_t)vl + m);
+            sm.width[lane][m] = (uint8_t)wdt;
+            sm.mboff[lane][m] = (uint32_t)boff;
+            if (m < mneed && !e) {
+              if (wdt > (ES == 4 ? 32u : 64u)) e = ST_PANIC;  // get_batch / get_value assert on num_bits
+              else if ((uint64_t)pay + boff + (vpmb * wdt) / 8 > slen) e = (ES == 4) ? ST_PANIC : ST_EOF;
+              else endp = (uint32_t)((uint64_t)pay + boff + (vpmb * wdt) / 8);
+            }
+            boff += (vpmb * wdt) / 8;
+          }
+          sm.pay[lane] = pay;
+          sm.mind[lane] = (uint64_t)unzigzag(zz);
+          sm.nmbe[lane] = nmb32;
+          sm.first_delta[lane] = lane * (uint32_t)vpb;
+          const uint64_t nx = (uint64_t)pay + boff;
+          nxt = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+        }
+      }
+      const uint64_t em = __ballot(e != 0);
+      const uint32_t nb = em ? (uint32_t)__builtin_ctzll(em) : k;  // blocks before the first failing one
+      const int32_t e0 = em ? __shfl(e, (int)nb, 64) : 0;
+      if (lane == 0) {
+        const uint64_t left = need - done, cap = (uint64_t)nb * vpb;
+        const uint32_t dcount = (uint32_t)(left < cap ? left : cap);
+        sm.first_delta[nb] = dcount;
+        sm.ctl[0] = nb;
+        sm.ctl[1] = dcount;
+        sm.ctl[2] = (uint32_t)e0;
+      }
+      const uint32_t last = nb ? nb - 1u : 0u;
+      const uint32_t ncur = nb ? (uint32_t)__shfl((int)nxt, (int)last, 64) : cur;
+      const uint32_t ep = (uint32_t)__shfl((int)endp, (int)last, 64);
+      if (lane == 0) {
+        sm.ctl[3] = ncur;
+        sm.ctl[4] = ep;
+      }
+      wcur = ncur;
+    } else if (nmb > 8 && tid == 0) {
       uint32_t nb = 0;
       uint64_t dcount = 0;
       int32_t e = 0;
