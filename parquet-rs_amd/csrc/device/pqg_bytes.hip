@@ -132,8 +132,8 @@ __device__ inline uint64_t block_exscan(DeltaSmem& sm, uint64_t x, uint64_t& tot
 // and whose bytes start at D (dlen bytes available). data.range(offset, len) asserts
 // (PANIC) on negative lengths or running past the data.
 __device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen, uint64_t n,
-                                       const uint32_t* len, uint64_t* src) {
-  uint64_t carry = 0;
+                                       const uint32_t* len, uint64_t* src, uint64_t& carry) {
+  carry = 0;
   int32_t bad = 0;
   constexpr uint32_t PT = 16;  // lengths per thread per pass (one workgroup scan per 4096 values)
   for (uint64_t b = 0; b < n; b += (uint64_t)WG * PT) {
@@ -151,7 +151,7 @@ __device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen,
     for (uint32_t k = 0; k < PT; ++k) {
       if (i0 + k < n) {
         if (l[k] < 0 || off + (uint64_t)l[k] > dlen) bad = 1;
-        else src[i0 + k] = D + off;
+        else gp(src)[i0 + k] = D + off;
       }
       off += l[k] > 0 ? (uint64_t)l[k] : 0;
     }
@@ -162,6 +162,74 @@ __device__ int32_t slices_from_lengths(DeltaSmem& sm, uint64_t D, uint64_t dlen,
   __syncthreads();
   if (bad) sm.ctl[5] = 1;
   __syncthreads();
+  return sm.ctl[5] ? ST_PANIC : 0;
+}
+
+// DELTA_BYTE_ARRAY after its two length streams (prefix lengths pre[0, n), suffix lengths
+// len[0, ns)), in one pass of 16 values per thread per workgroup scan with every load of a pass in
+// flight at once: the suffix slices of the first ns values from D (dlen bytes; a negative length
+// or one past the data panics, as data.range asserts); values past ns repeat the last suffix
+// (decoding.rs:796-801); each prefix length at most the previous value's length
+// (previous_value[0..prefix_len], :804; 0 for the first); bytes: the page's output bytes (prefix
+// + suffix lengths).
+__device__ int32_t dba_slices(DeltaSmem& sm, uint64_t D, uint64_t dlen, uint64_t n, uint64_t ns, const uint32_t* len,
+                              const uint32_t* pre, uint64_t* src, uint64_t& bytes) {
+  uint64_t carry = 0, by = 0;
+  int32_t bad = 0;
+  constexpr uint32_t PT = 16;
+  const uint32_t lastl = ns ? len[ns - 1] : 0u;
+#pragma unroll 1
+  for (uint64_t b = 0; b < n; b += (uint64_t)WG * PT) {
+    const uint64_t i0 = b + (uint64_t)threadIdx.x * PT;
+    int32_t l[PT];
+    uint32_t pr[PT];
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      const uint64_t i = i0 + k;
+      l[k] = i < ns ? (int32_t)len[i] : i < n ? (int32_t)lastl : 0;
+      pr[k] = i < n ? pre[i] : 0u;
+    }
+    // the value before the thread's first: its full length
+    uint64_t prevlen = 0;
+    if (i0 > 0 && i0 < n) {
+      const uint64_t j = i0 - 1;
+      prevlen = (uint64_t)pre[j] + (uint64_t)(uint32_t)(j < ns ? len[j] : lastl);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      const uint64_t i = i0 + k;
+      if (i < ns) s += l[k] > 0 ? (uint64_t)l[k] : 0;
+      if (i < n) {
+        const int32_t pl = (int32_t)pr[k];
+        if (pl < 0 || (uint64_t)pl > prevlen) bad = 1;
+        prevlen = (uint64_t)pr[k] + (uint64_t)(uint32_t)l[k];
+        by += prevlen;
+      }
+    }
+    uint64_t tot;
+    uint64_t off = carry + block_exscan(sm, s, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+      const uint64_t i = i0 + k;
+      if (i < ns) {
+        if (l[k] < 0 || off + (uint64_t)l[k] > dlen) bad = 1;
+        else gp(src)[i] = D + off;
+        off += l[k] > 0 ? (uint64_t)l[k] : 0;
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();  // (the last scan's reads of sm.wsum)
+  const uint64_t tb = block_sum_u64(by, sm.wsum);
+  if (threadIdx.x == 0) {
+    sm.ctl[5] = 0;
+    sm.carry = tb;
+  }
+  __syncthreads();
+  if (bad) sm.ctl[5] = 1;
+  __syncthreads();
+  bytes = sm.carry;
   return sm.ctl[5] ? ST_PANIC : 0;
 }
 
@@ -357,7 +425,8 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
   uint64_t* src = vsrc + vo;
   uint32_t* len = vlen + vo;
   int32_t st = 0;
-  bool dba = false;
+  bool dba = false, have_bytes = false;
+  uint64_t bytes = 0;
   switch (pw.encoding) {
     case E_PLAIN:
       if (type_length > 0) {
@@ -377,7 +446,8 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
       st = delta_stream<4>(sm, blob, blob_len, S, slen, ~0ull, n, reinterpret_cast<uint8_t*>(len), li);
       if (!st && li.total < n) st = ST_EOF;  // the reference returns a short batch
       if (!st && li.end_off > slen) st = ST_PANIC;
-      if (!st) st = slices_from_lengths(sm, S + li.end_off, slen - li.end_off, n, len, src);
+      if (!st) st = slices_from_lengths(sm, S + li.end_off, slen - li.end_off, n, len, src, bytes);
+      have_bytes = true;
       break;
     }
     case E_DELTA_BYTE_ARRAY: {
@@ -398,27 +468,15 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
         const uint64_t e2 = (uint64_t)e1 + si.end_off;
         const uint64_t ns = si.total < n ? si.total : n;
         if (n > 0 && ns == 0) st = ST_PANIC;  // ByteArray::data() before set_data
-        if (!st) st = slices_from_lengths(sm, S + e2, slen - e2, ns, len, src);
-        __syncthreads();
-        if (!st) {
+        if (!st) st = dba_slices(sm, S + e2, slen - e2, n, ns, len, pre, src, bytes);
+        have_bytes = true;
+        if (!st && ns < n) {
           // suffix decoder exhausted: `v` keeps the last suffix (decoding.rs:796-801)
+          __syncthreads();
           for (uint64_t i = ns + threadIdx.x; i < n; i += WG) {
             src[i] = src[ns - 1];
             len[i] = len[ns - 1];
           }
-          __syncthreads();
-          // previous_value[0..prefix_len] (:804)
-          int32_t bad = 0;
-          for (uint64_t i = threadIdx.x; i < n; i += WG) {
-            const int32_t pl = (int32_t)pre[i];
-            const uint64_t prev = i ? (uint64_t)pre[i - 1] + len[i - 1] : 0;
-            if (pl < 0 || (uint64_t)pl > prev) bad = 1;
-          }
-          if (threadIdx.x == 0) sm.ctl[6] = 0;
-          __syncthreads();
-          if (bad) sm.ctl[6] = 1;
-          __syncthreads();
-          if (sm.ctl[6]) st = ST_PANIC;
         }
       }
       break;
@@ -431,7 +489,11 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
     return;
   }
   __syncthreads();
-  page_bytes(sm, pages, p, n, len, dba ? vpre + vo : nullptr);
+  if (have_bytes) {
+    if (threadIdx.x == 0) pages[p].nbytes_out = bytes;
+  } else {
+    page_bytes(sm, pages, p, n, len, nullptr);
+  }
 }
 
 // Page byte offsets chunk by chunk (exclusive scan of nbytes_out restarted at each chunk's first

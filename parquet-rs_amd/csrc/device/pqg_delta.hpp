@@ -123,8 +123,8 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
   if (n_decode == 0) return 0;
   const int64_t first = unzigzag(fz);
   if (tid == 0 && n_store > 0) {
-    if (ES == 4) *reinterpret_cast<int32_t*>(o) = (int32_t)first;
-    else *reinterpret_cast<int64_t*>(o) = first;
+    if (ES == 4) *gp(reinterpret_cast<int32_t*>(o)) = (int32_t)first;
+    else *gp(reinterpret_cast<int64_t*>(o)) = first;
   }
   if (n_decode == 1) return 0;
   if (vpmb == 0) return ST_HANG;  // block_size < num_mini_blocks: every mini-block is empty
@@ -141,6 +141,8 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
   // payload start, the byte offset of that mini-block in it, min_delta, width bytes, needed
   // mini-blocks.
   uint32_t wcur = q, bm = 0, bpay = 0, bw = 0, bmneed = 0;
+  uint32_t hguess = 0;    // mean block length of the last batch (the header scan's guesses)
+  bool hserial = false;   // the last batch's blocks varied in length: walk them one by one
   uint64_t bboff = 0, bmind = 0;
 
   delta_load_region(sm, blob, blob_len, A0);
@@ -149,27 +151,99 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
   while (done < need) {
     // ---------------- walk block headers
     if (nmb <= 8 && tid < 64) {
-      // wave 0: a hop loop finds the batch's headers (varint length and the sum of the widths give
-      // the next one, ~10 operations a hop), then lane j parses block j and makes every check the
-      // serial walk below makes; the first failing block (stream order) ends the batch as there
+      // wave 0: the batch's headers by a speculative scan (lane j guesses block j's offset from the
+      // mean block length so far, parses the hop there -- varint length and the sum of the widths --
+      // and the wave's scan of the hops checks the guesses; the exact prefix grows every round, one
+      // or two rounds for the writer's blocks), then lane j parses block j and makes every check the
+      // serial walk below makes; the first failing block (stream order) ends the batch as there.
+      // The batch ends before a header past the staged region and after one past the stream or
+      // with a varint of 8 bytes or more (its lane reports or parses it; the next batch goes on)
       const uint32_t lane = tid, nmb32 = (uint32_t)nmb, hs = (uint32_t)(vpmb >> 3);
-      uint32_t cur = wcur, k = 0, posv = 0;
-      while (k < (uint32_t)NBCAP && done + (uint64_t)k * vpb < need) {
-        const uint64_t rel = S + cur - A0;
-        if (rel >= DBLK) break;
-        posv = lane == k ? cur : posv;
-        ++k;
-        if (cur >= slen) break;  // (its lane reports the stream end)
-        const uint64_t w0 = lload_u64(sm.region, (uint32_t)rel);
-        const uint64_t t8 = ~w0 & 0x8080808080808080ull;
-        if (!t8) break;  // a varint of 8 bytes or more: its lane parses it, the batch ends there
-        const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
-        const uint64_t wy = lload_u64(sm.region, (uint32_t)rel + vl);
-        const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
-        const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
-        const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
-        const uint64_t nx = (uint64_t)cur + vl + nmb32 + (uint64_t)hs * sumw;
-        cur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+      const uint64_t want = (need - done + vpb - 1) / vpb;
+      const uint32_t kmax = want < (uint64_t)NBCAP ? (uint32_t)want : (uint32_t)NBCAP;
+      const uint64_t left_b = slen > wcur ? (uint64_t)(slen - wcur) : 0ull;
+      const uint32_t avg = hguess ? hguess : (uint32_t)min(left_b / (want ? want : 1ull), (uint64_t)DBLK);
+      uint32_t posv = wcur + lane * avg, k = 0;
+      if (!hserial) {
+        uint32_t rounds = 0;
+#pragma unroll 1
+        for (uint32_t round = 0; round <= kmax; ++round) {
+          rounds = round + 1u;
+          const bool act = lane < kmax;
+          const uint64_t rel = S + (uint64_t)posv - A0;
+          const bool inreg = posv >= wcur && rel < DBLK;  // (a guess below the batch start: not exact)
+          bool good = false, term = false;
+          uint32_t h = 0;
+          if (act && inreg) {
+            if (posv >= slen) {
+              term = true;  // (its lane reports the stream end)
+            } else {
+              const uint64_t w0 = lload_u64(sm.region, (uint32_t)rel);
+              const uint64_t t8 = ~w0 & 0x8080808080808080ull;
+              if (!t8) {
+                term = true;  // a varint of 8 bytes or more: its lane parses it, the batch ends there
+              } else {
+                const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u;
+                const uint64_t wy = lload_u64(sm.region, (uint32_t)rel + vl);
+                const uint64_t y = nmb32 >= 8 ? wy : (wy & ((1ull << (8 * nmb32)) - 1ull));
+                const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+                const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+                const uint64_t hh = (uint64_t)vl + nmb32 + (uint64_t)hs * sumw;
+                h = hh > 0x03FFFFFFull ? 0x03FFFFFFu : (uint32_t)hh;  // (64 hops stay below 2^32)
+                good = true;
+              }
+            }
+          }
+          const uint32_t incl = wave_scan_incl_u32(good ? h : 0u);
+          const uint64_t Q64 = (uint64_t)wcur + (incl - (good ? h : 0u));
+          const uint32_t Q = Q64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Q64;
+          const uint64_t diff = __ballot(act && Q != posv);
+          const uint32_t m = diff ? (uint32_t)__builtin_ctzll(diff) : kmax;  // lanes [0, m) exact
+          const uint64_t stop = __ballot(act && lane < m && !good);          // an exact lane that ends it
+          if (stop) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(stop);
+            const bool fterm = __shfl((int)(term ? 1 : 0), (int)f, 64) != 0;
+            k = fterm ? f + 1u : f;  // (outside the region: the next batch moves it there)
+            break;
+          }
+          if (m >= kmax) {
+            k = kmax;
+            break;
+          }
+          posv = Q;
+        }
+        // (each round fixes at least one lane; many rounds: block lengths vary, walk them in turn)
+        hserial = rounds > 4u;
+      } else {
+        // blocks of varying length: one walk (every lane alike), one LDS round trip per header
+        uint32_t cur = wcur, hmin = 0xFFFFFFFFu, hmax = 0;
+#pragma unroll 1
+        while (k < kmax) {
+          const uint64_t rel = S + (uint64_t)cur - A0;
+          if (rel >= DBLK) break;
+          posv = lane == k ? cur : posv;
+          ++k;
+          if (cur >= slen) break;
+          const uint32_t wi = (uint32_t)rel >> 2, sh = ((uint32_t)rel & 3u) * 8u;
+          const uint32_t x0 = sm.region[wi], x1 = sm.region[wi + 1], x2 = sm.region[wi + 2], x3 = sm.region[wi + 3],
+                         x4 = sm.region[wi + 4];
+          const uint64_t lo8 = ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32) | __builtin_amdgcn_alignbit(x1, x0, sh);
+          const uint64_t hi8 = ((uint64_t)__builtin_amdgcn_alignbit(x4, x3, sh) << 32) | __builtin_amdgcn_alignbit(x3, x2, sh);
+          const uint64_t t8 = ~lo8 & 0x8080808080808080ull;
+          if (!t8) break;
+          const uint32_t vl = ((uint32_t)__builtin_ctzll(t8) >> 3) + 1u, vs = vl * 8u;
+          const uint64_t wv = vs < 64 ? ((lo8 >> vs) | (hi8 << (64 - vs))) : hi8;
+          const uint64_t y = nmb32 >= 8 ? wv : (wv & ((1ull << (8 * nmb32)) - 1ull));
+          const uint64_t s16 = (y & 0x00FF00FF00FF00FFull) + ((y >> 8) & 0x00FF00FF00FF00FFull);
+          const uint32_t sumw = (uint32_t)((s16 * 0x0001000100010001ull) >> 48);
+          const uint64_t hh = (uint64_t)vl + nmb32 + (uint64_t)hs * sumw;
+          const uint32_t h = hh > 0x03FFFFFFull ? 0x03FFFFFFu : (uint32_t)hh;
+          hmin = min(hmin, h);
+          hmax = max(hmax, h);
+          const uint64_t nx = (uint64_t)cur + h;
+          cur = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+        }
+        hserial = hmax != hmin;  // blocks of one length: the guesses are exact again
       }
       int32_t e = 0;
       uint32_t nxt = 0, endp = 0;
@@ -218,11 +292,13 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
         sm.ctl[2] = (uint32_t)e0;
       }
       const uint32_t last = nb ? nb - 1u : 0u;
-      const uint32_t ncur = nb ? (uint32_t)__shfl((int)nxt, (int)last, 64) : cur;
+      const uint32_t ncur = nb ? (uint32_t)__shfl((int)nxt, (int)last, 64) : wcur;
+      if (nb && ncur > wcur) hguess = (ncur - wcur) / nb;
       const uint32_t ep = (uint32_t)__shfl((int)endp, (int)last, 64);
       if (lane == 0) {
         sm.ctl[3] = ncur;
         sm.ctl[4] = ep;
+        sm.ctl[5] = 1;  // the batch's entries are whole blocks (expand: entry = delta / vpb)
       }
       wcur = ncur;
     } else if (nmb > 8 && tid == 0) {
@@ -305,12 +381,14 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
       uint64_t at = bm ? (uint64_t)bpay + bboff : (uint64_t)wcur;
       sm.ctl[3] = at > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)at;
       sm.ctl[4] = endp;
+      sm.ctl[5] = 0;
     }
     __syncthreads();
     const uint32_t nb = sm.ctl[0];
     const uint32_t dcount = sm.ctl[1];
     const int32_t e = (int32_t)sm.ctl[2];
     const uint32_t ncur = sm.ctl[3];
+    const bool whole = sm.ctl[5] != 0 && vpmb % 16 == 0;  // a thread's 16 deltas: one mini-block
     if (nb) end_off = sm.ctl[4];
     __syncthreads();
     if (e) return e;
@@ -329,10 +407,30 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
       uint64_t s = 0;
       if (d0 < dcount) {
         int b = 0;
-        while (b + 1 < (int)nb && sm.first_delta[b + 1] <= d0) ++b;
+        if (whole) {
+          b = (int)(d0 / vpb);
+        } else {
+          while (b + 1 < (int)nb && sm.first_delta[b + 1] <= d0) ++b;
+        }
         uint64_t inb = d0 - sm.first_delta[b];
         uint32_t m = (uint32_t)(inb / vpmb);
         uint32_t k = (uint32_t)(inb - (uint64_t)m * vpmb);
+        const uint32_t wd0 = sm.width[b][m];
+        const uint64_t sbit = (S + sm.pay[b] + sm.mboff[b][m]) * 8ull + (uint64_t)k * wd0;  // absolute
+        const bool fast = whole && wd0 <= 32 && sbit >= A0 * 8ull &&
+                          sbit - A0 * 8ull + (uint64_t)DPT * wd0 + 32ull <= (uint64_t)DREGION * 8ull;
+        if (fast) {  // staged, one mini-block, at most 32 bits: one funnel shift per delta
+          const uint32_t rb = (uint32_t)(sbit - A0 * 8ull);
+          const uint32_t wm = wd0 >= 32 ? 0xFFFFFFFFu : (1u << wd0) - 1u;
+          const uint64_t mn = sm.mind[b];
+#pragma unroll
+          for (int j = 0; j < DPT; ++j) {
+            const uint32_t bit = rb + (uint32_t)j * wd0, wi = bit >> 5;
+            const uint32_t r = __builtin_amdgcn_alignbit(sm.region[wi + 1], sm.region[wi], bit & 31u) & wm;
+            v[j] = d0 + j < dcount ? mn + r : 0ull;
+            s += v[j];
+          }
+        } else {
 #pragma unroll
         for (int j = 0; j < DPT; ++j) {
           v[j] = 0;
@@ -368,6 +466,10 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
             }
           }
         }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) v[j] = 0;
       }
       // workgroup exclusive scan of s
       uint64_t incl = s;
@@ -390,8 +492,8 @@ __device__ int32_t delta_stream(DeltaSmem& sm, const uint8_t* __restrict__ blob,
           if (d0 + j < dcount) {
             acc += v[j];
             if (oi + j < n_store) {
-              if (ES == 8) reinterpret_cast<int64_t*>(o)[oi + j] = (int64_t)acc;
-              else reinterpret_cast<int32_t*>(o)[oi + j] = (int32_t)(uint32_t)acc;
+              if (ES == 8) gp(reinterpret_cast<int64_t*>(o))[oi + j] = (int64_t)acc;  // (global stores:
+              else gp(reinterpret_cast<int32_t*>(o))[oi + j] = (int32_t)(uint32_t)acc;  // no lgkmcnt)
             }
           }
         }
