@@ -417,6 +417,21 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   if (*rt.nfall == 0) return;
   const uint32_t tid = threadIdx.x, q = tid >> 7, lt = tid & 127u;
   const uint32_t p = blockIdx.x * DW_TPW + q;
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 4096, tools/diag/diag_dict.py): thread 0's s_memtime cycles per
+  // phase -- stage, block descriptors, index decode, window fills (issue to the barrier after the
+  // wait), gathers, stores
+  const bool dst = tid == 0 && (chunks[0].cp.debug & 4096) && chunks[0].cp.dbgbuf;
+  uint64_t dt_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dt0 = __builtin_amdgcn_s_memtime();
+#define DW_STAMP(k)                                   \
+  if (dst) {                                          \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+    dt_[k] += t1 - dt0;                               \
+    dt0 = t1;                                         \
+  }
+#else
+#define DW_STAMP(k)
+#endif
   const QDesc d = p < ntl ? rt.desc[tl[p]] : QDesc{};
   const uint32_t qlo = d.qlo, qhi = d.qhi;
   uint64_t obase = 0;
@@ -477,6 +492,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     }
   }
   __syncthreads();  // (every wave: the tiles of one workgroup may differ in kind)
+  DW_STAMP(0)
   // per 256-output block k of an easy tile (pair s of every thread lies in block s): the run
   // holding its first output and the run after it (start, info each, and the start after them),
   // found once by thread k
@@ -494,6 +510,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     blk2[2 * lt + 1] = a;
   }
   __syncthreads();
+  DW_STAMP(1)
   if (easy) {
     const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(R + DF_POFF);
     const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
@@ -559,6 +576,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s][0] = x[s][1] = 0;
   __syncthreads();  // (the stage regions are the window's)
+  DW_STAMP(2)
   for (int qq = 0; qq < DW_TPW; ++qq) {  // each distinct dictionary of the 8 tiles (uniform)
     const int32_t kq = dkey[qq];
     bool seen = kq < 0;
@@ -591,6 +609,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       // barrier orders the waves
       __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();
+      DW_STAMP(3)
       if (sh) {  // a dictionary at an odd offset: the window moved down by sh bytes, in place
         const uint32_t k0 = sh >> 2, bs = sh & 3u;
 #pragma unroll 1
@@ -624,6 +643,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
             if (r < WIN) x[s][j] = wt[r];
           }
       }
+      DW_STAMP(4)
     }
   }
   gptr<uint8_t> o = reinterpret_cast<gptr<uint8_t>>(obase) + (uint64_t)lt * 2u * ES;
@@ -639,6 +659,15 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       *reinterpret_cast<gptr<T>>(os) = x[s][0];
     }
   }
+#ifdef PQG_DIAG
+  DW_STAMP(5)
+  if (dst) {
+    dt_[7] = 1;
+    uint64_t* d = chunks[0].cp.dbgbuf + 8ull * blockIdx.x;
+    for (int i = 0; i < 8; ++i) d[i] = dt_[i];
+  }
+#endif
+#undef DW_STAMP
 }
 
 // Dictionary index streams the level path handed back, when they are expected to be rare (the
