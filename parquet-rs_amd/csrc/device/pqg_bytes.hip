@@ -402,7 +402,10 @@ __global__ void __launch_bounds__(WG) k_badict_fallback(const uint8_t* __restric
   const uint64_t bad = __ballot(em.err != 0);
   if (bad && (threadIdx.x & 63) == 0) report(pages, chunks, p, ST_PANIC);
   const uint64_t tb = block_sum_u64(em.bytes, red);
-  if (threadIdx.x == 0) pages[p].nbytes_out = tb;
+  if (threadIdx.x == 0) {
+    pages[p].nbytes_out = tb;
+    pages[p].tile_bytes = 0;  // (windows the level path emitted before handing the page back)
+  }
 }
 
 __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
@@ -608,7 +611,10 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
     }
   }
   const uint64_t tot = block_sum_u64(s, red);
-  if (threadIdx.x == 0) tsum[gt] = tot;
+  if (threadIdx.x == 0) {
+    tsum[gt] = tot;
+    if (pw.tile_bytes) atomicAdd((unsigned long long*)&pages[p].nbytes_out, (unsigned long long)tot);
+  }
 }
 
 // Per byte-array page: its tiles' start offsets (page byte_out + exclusive scan of the tile sums).
@@ -1305,10 +1311,13 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
                             uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen,
                             uint64_t* tsum, uint32_t* vaux, uint32_t* dtile, hipStream_t s) {
   hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
-  hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
-  if (ntl) {
+  // tile sums before the page scan: the level path's dictionary pages take their byte totals
+  // from them (PageWork::tile_bytes)
+  if (ntl)
     hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
                        tsum);
+  hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
+  if (ntl) {
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
     hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vsrc, vlen,
                        dsrc, dlen, tsum);

@@ -2324,9 +2324,9 @@ __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t
   const uint32_t ndict = pages[ck.dict_page].num_values;
   const uint32_t w = (uint32_t)x.s.w, wm = (1u << w) - 1u;
   const uint64_t go = x.s.out;
-  auto elen = [&](uint32_t idx) -> uint32_t { return idx < ndict ? (ldlen ? ldlen[idx] : dlen[idx]) : 0u; };
+  (void)dlen;
+  (void)ldlen;
   uint32_t bad = 0;
-  uint64_t bytes = 0;
 #pragma unroll 1
   for (uint32_t b = 0; b < rl.R; ++b) {
     const uint32_t rs = rl.rstart[b], re = rl.rstart[b + 1], inf = rl.rinfo[b];
@@ -2336,7 +2336,6 @@ __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t
       const uint32_t idx = inf & 0x7FFFFFFFu;
       bad |= idx >= ndict ? 1u : 0u;
       for (uint32_t o = st + lane; o < en; o += WAVE) vlen[go + o] = idx;
-      if (lane == 0) bytes += (uint64_t)elen(idx) * (en - st);
       continue;
     }
     const uint64_t bit0 = (uint64_t)inf * 8ull;
@@ -2359,10 +2358,7 @@ __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t
         for (uint32_t j = 0; j < 4; ++j) id[j] = one(o + j);
       }
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        bad |= id[j] >= ndict ? 1u : 0u;
-        bytes += elen(id[j]);
-      }
+      for (uint32_t j = 0; j < 4; ++j) bad |= id[j] >= ndict ? 1u : 0u;
       gst16(reinterpret_cast<gptr<uint8_t>>(vlen + k * 4u), make_uint4(id[0], id[1], id[2], id[3]));
     }
     // the cut groups: outputs [st, 4 k0 - go) and [4 k1 - go, en) (at most 3 each), or the whole
@@ -2373,13 +2369,11 @@ __device__ __forceinline__ void lv_write_badict(const LvRuns& rl, const uint32_t
       const uint32_t o = j < nh ? st + j : t0 + (j - nh);
       const uint32_t idx = one(o);
       bad |= idx >= ndict ? 1u : 0u;
-      bytes += elen(idx);
       vlen[go + o] = idx;
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off, 64);
-  if (lane == 0 && bytes) atomicAdd((unsigned long long*)&pages[x.p].nbytes_out, (unsigned long long)bytes);
+  // the page's bytes: the sum of its tiles' (k_ba_tsum, from the indices written here)
+  if (lane == 0) pages[x.p].tile_bytes = 1u;
   if (__ballot(bad) && lane == 0) report(pages, chunks, (int)x.p, ST_PANIC);
 }
 

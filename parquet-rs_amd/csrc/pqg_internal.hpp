@@ -68,7 +68,9 @@ struct PageWork {
   uint64_t spec_out;
   // ---- host-filled
   uint32_t chunk;       // the column chunk of the batch this page belongs to (ChunkWork index)
-  uint32_t pad1;
+  // ---- level path: 1 when nbytes_out is the sum of the page's tile byte sums (k_ba_tsum adds
+  // them): the byte-array dictionary emit writes entry indices only
+  uint32_t tile_bytes;
 };
 
 // Chunk-level result, copied to pinned host memory at the end of a decode.

@@ -23,7 +23,8 @@ def main():
     a = ap.parse_args()
     import torch
     import pqgpu
-    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", "lib_diag", "libpqgpu.so")
+    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", os.environ.get("PQG_DIAG_LIBDIR", "lib_diag"),
+                                  "libpqgpu.so")
     L = pqgpu.lib()
     L.pqg_debug_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     import bench
@@ -46,7 +47,18 @@ def main():
     for k, name in enumerate(("bounds+records", "staging", "writes BA", "writes 4 B", "writes 8 B")):
         print(f"  {name:15s} {d[:, k].sum() / units:9.0f} cycles per unit  ({d[:, k].sum() / tot:.2f} of the stamped)")
     print(f"  per output: fixed {(d[:, 3].sum() + d[:, 4].sum()) / max(of, 1):.2f}, BA {d[:, 2].sum() / max(ob, 1):.2f} cycles")
-    print(f"  wave busy cycles: mean {d[:, :5].sum(1).mean():.0f} max {d[:, :5].sum(1).max():.0f}")
+    busy = d[:, :5].sum(1)
+    outs = d[:, 6] + d[:, 7]
+    print(f"  wave busy cycles: mean {busy.mean():.0f} p50 {np.percentile(busy, 50):.0f} "
+          f"p90 {np.percentile(busy, 90):.0f} max {busy.max():.0f}")
+    print(f"  wave outputs: mean {outs.mean():.0f} p50 {np.percentile(outs, 50):.0f} "
+          f"p90 {np.percentile(outs, 90):.0f} max {outs.max():.0f}; units: mean {d[:, 5].mean():.1f} max {d[:, 5].max():.0f}")
+    top = np.argsort(busy)[-5:]
+    for i in top:
+        print(f"    busy {busy[i]:.0f}: units {d[i, 5]:.0f} outputs {outs[i]:.0f} (BA {d[i, 7]:.0f}) "
+              + " ".join(f"{d[i, k]:.0f}" for k in range(5)))
+    c = np.corrcoef(busy, outs)[0, 1]
+    print(f"  correlation busy ~ outputs {c:.2f}")
 
 
 if __name__ == "__main__":
