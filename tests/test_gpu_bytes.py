@@ -104,6 +104,44 @@ def test_dictionary_byte_array(oracle, ctx):
     check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
 
 
+def _leb_padded(x, nbytes):
+    """x as a non-minimal LEB128 varint of nbytes bytes (bit_util.rs get_vlq_int accepts it; the
+    level path's fast parse takes up to 4 bytes)."""
+    return bytes(((x >> (7 * i)) & 0x7F) | (0x80 if i < nbytes - 1 else 0) for i in range(nbytes))
+
+
+@pytest.mark.parametrize("nbytes", [5, 9])
+def test_dictionary_byte_array_pages_handed_back(oracle, ctx, nbytes):
+    """A small byte-array dictionary (the level path's dictionary emit) over pages of which every
+    other one holds a padded 5..10-byte RLE run header inside its index stream: the level path
+    hands those pages back and the general decoder's fallback writes their indices and byte
+    totals; the emitted pages' totals are their tiles' sums (PageWork::tile_bytes). Offsets and
+    bytes of every page must be the oracle's."""
+    import pqgpu
+    rng = np.random.default_rng(40 + nbytes)
+    d = list(dict.fromkeys(rand_strings(rng, 120, 1, 9)))[:80]
+    dpage = oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode_ba(d), len(d), oracle.PLAIN)
+    bw = max(1, int(np.ceil(np.log2(len(d)))))
+    pages = [dpage]
+    for k in range(6):
+        n = 6000 + 517 * k
+        lv = (rng.random(n) >= 0.2).astype(np.int16)
+        nn = int(lv.sum())
+        idx = rng.integers(0, len(d), nn).astype(np.uint64)
+        if k % 2 == 0:
+            cut = (nn // 3) & ~7
+            idx[cut - 16:cut] = idx[cut - 16]  # (the prefix's encoding ends in an RLE run)
+            run = 200
+            idx[cut:cut + run] = idx[cut]
+            body = (bytes([bw]) + oracle.rle_encode(idx[:cut], bw) + _leb_padded(run << 1, nbytes) +
+                    int(idx[cut]).to_bytes((bw + 7) // 8, "little") + oracle.rle_encode(idx[cut + run:], bw))
+        else:
+            body = bytes([bw]) + oracle.rle_encode(idx, bw)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(lv, 1) + body, n, oracle.RLE_DICTIONARY))
+    check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+    assert ctx.last_paths() & pqgpu.PATH_DICT_LEVEL, "the small dictionary takes the level path"
+
+
 def test_dictionary_flba_v2(oracle, ctx):
     rng = np.random.default_rng(4)
     pages = _dict_pages(oracle, rng, oracle.FIXED_LEN_BYTE_ARRAY, rand_strings(rng, 300, 16, 16),
