@@ -493,11 +493,12 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   }
   __syncthreads();  // (every wave: the tiles of one workgroup may differ in kind)
   DW_STAMP(0)
-  // per 256-output block k of an easy tile (pair s of every thread lies in block s): the run
-  // holding its first output and the run after it (start, info each, and the start after them),
-  // found once by thread k
-  uint4* blk = reinterpret_cast<uint4*>(R + DF_BLK);
-  uint32_t* blk2 = reinterpret_cast<uint32_t*>(R + DF_BLK + 16 * 16);
+  // per 256-output block k of an easy tile (pair s of every thread lies in block s), found once
+  // by thread k: the run holding its first output (A) and the run after it (B), as block-relative
+  // ends and, for a bit-packed run, the bit offset of the block's first output in the staged
+  // payload (the pair at block output r then starts at bit base + r w); an RLE run's value instead
+  uint4* blk = reinterpret_cast<uint4*>(R + DF_BLK);        // (end A, base A, end B, base B)
+  uint32_t* blk2 = reinterpret_cast<uint32_t*>(R + DF_BLK + 16 * 16);  // (RLE flags, run A)
   if (easy && lt < 16) {
     const uint32_t o = qlo + 256u * lt;
     uint32_t a = 0;
@@ -505,8 +506,11 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     for (uint32_t step = DF_RC / 2; step; step >>= 1)
       if (a + step < nr && rs[a + step] <= o) a += step;
     const bool two = a + 1 < nr;
-    blk[lt] = make_uint4(rs[a], ri[a], rs[a + 1], two ? ri[a + 1] : 0u);
-    blk2[2 * lt] = two ? rs[a + 2] : qhi;
+    const uint32_t ia = ri[a], ib = two ? ri[a + 1] : 0u, w = d.w;
+    const uint32_t ba = ia & R_RLE ? ia & 0x7FFFFFFFu : (ia - sb32) * 8u + (o - rs[a]) * w;
+    const uint32_t bb = ib & R_RLE ? ib & 0x7FFFFFFFu : (ib - sb32) * 8u - (rs[a + 1] - o) * w;  // (mod 2^32)
+    blk[lt] = make_uint4(rs[a + 1] - o, ba, rs[a + 2] - o, bb);  // (rs[nr] = rs[nr + 1] = qhi)
+    blk2[2 * lt] = (ia & R_RLE ? 1u : 0u) | (two && (ib & R_RLE) ? 2u : 0u);
     blk2[2 * lt + 1] = a;
   }
   __syncthreads();
@@ -514,29 +518,30 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   if (easy) {
     const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(R + DF_POFF);
     const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
+    const uint32_t r = 2u * lt, rw = r * w;  // the thread's pair in every block
     bool bad = false;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       uint32_t v0 = 0, v1 = 0;
-      const uint32_t o0 = qlo + 2u * (128u * (uint32_t)s + lt);
       if (s * 256 < rem) {
         const uint4 b = blk[s];
-        const uint32_t nx2 = blk2[2 * s];
+        const uint32_t fl = blk2[2 * s];
         // the pair inside one of the block's two runs (w <= 16: both values in one 32-bit window)
-        const bool inA = o0 + 1 < b.z, inB = o0 >= b.z && o0 + 1 < nx2;
+        const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
         if ((inA || inB) && w <= 16) {
-          const uint32_t st = inA ? b.x : b.z, inf = inA ? b.y : b.w;
-          if (inf & R_RLE) {
-            v0 = v1 = inf & 0x7FFFFFFFu;
+          const uint32_t base = inA ? b.y : b.w;
+          if (fl & (inA ? 1u : 2u)) {
+            v0 = v1 = base;
           } else {
-            const uint32_t bit = (inf - sb32) * 8u + (o0 - st) * w;
+            const uint32_t bit = base + rw;
             const uint32_t wi = bit >> 5;
             const uint32_t x = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u);
             v0 = x & wm;
             v1 = (x >> w) & wm;
           }
         } else {  // any other case, value by value from the block's first run on
-          uint32_t a = blk2[2 * s + 1], st = b.x, inf = b.y, nx = b.z;
+          const uint32_t o0 = qlo + 256u * (uint32_t)s + r;
+          uint32_t a = blk2[2 * s + 1], st = rs[a], inf = ri[a], nx = rs[a + 1];
           uint32_t v2[2] = {0u, 0u};
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
