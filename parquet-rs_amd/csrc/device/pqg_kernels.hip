@@ -520,55 +520,70 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
     const uint32_t r = 2u * lt, rw = r * w;  // the thread's pair in every block
     bool bad = false;
+    // fast pass, branch-free so that every LDS read of a phase is in flight at once: each pair
+    // inside one of its block's two runs (w <= 16: both values in one 32-bit window) -- a bit
+    // offset, or an RLE run's value; the rest marked for the slow pass
+    uint32_t q[16], slow = 0, rle = 0, dead = 0;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      uint32_t v0 = 0, v1 = 0;
-      if (s * 256 < rem) {
-        const uint4 b = blk[s];
-        const uint32_t fl = blk2[2 * s];
-        // the pair inside one of the block's two runs (w <= 16: both values in one 32-bit window)
-        const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
-        if ((inA || inB) && w <= 16) {
-          const uint32_t base = inA ? b.y : b.w;
-          if (fl & (inA ? 1u : 2u)) {
-            v0 = v1 = base;
-          } else {
-            const uint32_t bit = base + rw;
-            const uint32_t wi = bit >> 5;
-            const uint32_t x = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u);
-            v0 = x & wm;
-            v1 = (x >> w) & wm;
-          }
-        } else {  // any other case, value by value from the block's first run on
-          const uint32_t o0 = qlo + 256u * (uint32_t)s + r;
-          uint32_t a = blk2[2 * s + 1], st = rs[a], inf = ri[a], nx = rs[a + 1];
-          uint32_t v2[2] = {0u, 0u};
+      const uint4 b = blk[s];
+      const uint32_t fl = blk2[2 * s];
+      const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
+      q[s] = inA ? b.y : b.w;
+      if (s * 256 >= rem) dead |= 1u << s;
+      else if (!((inA || inB) && w <= 16)) slow |= 1u << s;
+      if (fl & (inA ? 1u : 2u)) rle |= 1u << s;
+    }
+    uint32_t lo[16], hi[16];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const uint32_t o = o0 + (uint32_t)j;
-#pragma unroll 1
-            while (nx <= o && a + 1 < nr) {
-              ++a;
-              st = nx;
-              inf = ri[a];
-              nx = rs[a + 1];
-            }
-            if (inf & R_RLE) {
-              v2[j] = inf & 0x7FFFFFFFu;
-            } else {
-              const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
-              const uint32_t wi = bit >> 5;
-              v2[j] = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u) & wm;
-            }
-          }
-          v0 = v2[0];
-          v1 = v2[1];
-        }
-        if (s * 256 + 1 >= rem) v1 = 0;  // (the tile's last output: no second value)
-        // dict[idx] out of bounds: the reference panics (rle.rs:455,470)
-        bad |= v0 >= D0 || (s * 256 + 1 < rem && v1 >= D0);
-      }
+    for (int s = 0; s < 16; ++s) {  // (RLE, slow and dead pairs read word 0: in bounds, unused)
+      const uint32_t wi = ((rle | slow | dead) >> s) & 1u ? 0u : (q[s] + rw) >> 5;
+      lo[s] = pw32[wi];
+      hi[s] = pw32[wi + 1];
+    }
+    // dict[idx] out of bounds: the reference panics (rle.rs:455,470); the tile's last output has
+    // no second value
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t x = __builtin_amdgcn_alignbit(hi[s], lo[s], (q[s] + rw) & 31u);
+      uint32_t v0 = (rle >> s) & 1u ? q[s] : x & wm;
+      uint32_t v1 = (rle >> s) & 1u ? q[s] : (x >> w) & wm;
+      if (((dead | slow) >> s) & 1u) v0 = v1 = 0;
+      if (s * 256 + 1 >= rem) v1 = 0;
+      bad |= v0 >= D0 || v1 >= D0;
       ix[s] = (v0 & 0xFFFFu) | (v1 << 16);
+    }
+    // slow pass (a pair across a run boundary, a block past its first two runs, w > 16): value by
+    // value from the block's first run on
+    if (slow) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (!((slow >> s) & 1u)) continue;
+        const uint32_t o0 = qlo + 256u * (uint32_t)s + r;
+        uint32_t a = blk2[2 * s + 1], st = rs[a], inf = ri[a], nx = rs[a + 1];
+        uint32_t v2[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t o = o0 + (uint32_t)j;
+#pragma unroll 1
+          while (nx <= o && a + 1 < nr) {
+            ++a;
+            st = nx;
+            inf = ri[a];
+            nx = rs[a + 1];
+          }
+          if (inf & R_RLE) {
+            v2[j] = inf & 0x7FFFFFFFu;
+          } else {
+            const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
+            const uint32_t wi = bit >> 5;
+            v2[j] = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u) & wm;
+          }
+        }
+        if (s * 256 + 1 >= rem) v2[1] = 0;
+        bad |= v2[0] >= D0 || v2[1] >= D0;
+        ix[s] = (v2[0] & 0xFFFFu) | (v2[1] << 16);
+      }
     }
     const uint64_t bm = __ballot(bad);
     if (bm && (tid & 63u) == (uint32_t)__builtin_ctzll(bm)) report(pages, chunks, (int)d.page, ST_PANIC);
