@@ -27,7 +27,8 @@ def main():
     a = ap.parse_args()
     import torch
     import pqgpu
-    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", "lib_diag", "libpqgpu.so")
+    pqgpu.LIB_PATH = os.path.join(ROOT, "parquet-rs_amd", os.environ.get("PQG_DIAG_LIBDIR", "lib_diag"),
+                                  "libpqgpu.so")
     L = pqgpu.lib()
     L.pqg_debug_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     import bench
