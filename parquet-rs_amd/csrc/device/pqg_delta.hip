@@ -933,6 +933,21 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
   };
   const uint32_t ntl = (need + TT - 1) / TT;
   if (ntl) issue(SB, win);
+#ifdef PQG_DIAG
+  // diagnostics (PQG_DEBUG bit 32, tools/diag/diag_delta.py): thread 0's s_memtime cycles per
+  // phase over the page's tiles -- stage install, header scan, unpack (with the next tile's load
+  // issue), scan, stores -- and the tiles
+  const bool dst = tid == 0 && dt.dbg;
+  uint64_t dd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d0 = __builtin_amdgcn_s_memtime();
+#define DP_STAMP(k)                                   \
+  if (dst) {                                          \
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+    dd[k] += t1 - d0;                                 \
+    d0 = t1;                                          \
+  }
+#else
+#define DP_STAMP(k)
+#endif
   uint32_t hdr = hd.q;        // header of the current tile's first block (stream offset)
   uint64_t carry = hd.first;  // value before the tile's first delta
   uint32_t hguess = 0;        // block length guess for the header scan (the last tile's average)
@@ -945,6 +960,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
     for (int c = 0; c < SH::CH; ++c) sm.stq[tid + c * NT] = pv[c];
     if (tid < 16) sm.stage[STG / 4 + tid] = 0;
     __syncthreads();
+    DP_STAMP(0)
     const uint32_t sb = (uint32_t)(SB - S);  // stream offset of staged byte 0 (mod 2^32)
     if (tid < 64) {
       bool fb, shortwin;
@@ -957,6 +973,7 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
       }
     }
     __syncthreads();
+    DP_STAMP(1)
     if (sm.ctl[2] && !sm.ctl[0] && win < (uint32_t)STG) {  // stage the full window and redo
       win = STG;
       issue(SB, win);
@@ -978,8 +995,10 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
     if (k + 1 < ntl) issue(SBn, winn);
     uint64_t x[DPT];
     const uint64_t s = dpg_unpack<NT>(sm, blob, blob_len, S, sb, win, D0, D1, nmb32, vpmb32, x);
+    DP_STAMP(2)
     uint64_t acc;
     carry += dpg_scan<NT>(sm, s, carry, acc);  // (the barrier also ends every read of the stage)
+    DP_STAMP(3)
     uint64_t val[DPT];
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
@@ -987,9 +1006,18 @@ __global__ void __attribute__((amdgpu_waves_per_eu(4, 8))) __launch_bounds__(NT)
       val[j] = acc;
     }
     dpg_store<ES, NT>(sm, val, ob + (uint64_t)(D0 + 1) * ES, D1 - D0);
+    DP_STAMP(4)
+#ifdef PQG_DIAG
+    if (dst) dd[7] += 1;
+#endif
     SB = SBn;
     win = winn;
   }
+#ifdef PQG_DIAG
+  if (dst)
+    for (int i = 0; i < 8; ++i) dt.dbg[8 * p + i] = dd[i];
+#endif
+#undef DP_STAMP
   if (tid == 0) {
     info.first = hd.first;
     info.vpmb = vpmb32;
