@@ -2959,7 +2959,9 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
         const uint32_t es = chunks[pages[p].chunk].es;
         LW_STAMP(es == 8 ? 4 : es == 4 ? 3 : 2)
         wt[5] += 1;
-        wt[es ? 6 : 7] += endo > base ? endo - base : 0u;
+        const uint64_t no = endo > base ? endo - base : 0u;
+        if (es) wt[6] += es == 8 ? no << 32 : no;  // (4-byte outputs low, 8-byte high)
+        else wt[7] += no;
       }
 #endif
       continue;
@@ -3058,7 +3060,16 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
   lv_front(blob, blob_len, pages, npages, chunks, sel, rt, lt, wgrid, s);
   if (front) (void)hipEventRecord(front, s);
   if (sel == SS_DICT) {  // (dense dictionary streams went to the general decoder)
-    hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut>, dim3(wgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks,
+    // short window ranges (one or two two-window units per wave on config 5): the waves' costs
+    // differ by value kind and index width (1.6x) and the hardware's workgroup dispatch evens
+    // them out, better than a cost-weighted split (k_lv_emit_walk<LvDictOut> on config 5: 2048
+    // workgroups 0.98-0.99 ms, cost-weighted 0.96, 4096 0.89-0.91, 8192 0.84, 16384 0.83, 32768
+    // 0.79-0.80, 65536 0.76-0.77, 120 K 0.87); one per 16 KiB of the batch up to 65536
+#ifndef PQG_LD_GRID
+#define PQG_LD_GRID 65536
+#endif
+    const uint32_t ldgrid = (uint32_t)std::min<uint64_t>(PQG_LD_GRID, std::max<uint64_t>(wgrid, blob_len >> 14));
+    hipLaunchKernelGGL(k_lv_emit_walk<LvDictOut>, dim3(ldgrid), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks,
                        sel, rt, lt, LvDictOut{dsrc, dlen, vsrc, vlen});
     return hipGetLastError();
   }

@@ -40,13 +40,18 @@ def main():
     buf = np.zeros(8 * n, np.uint64)
     assert L.pqg_debug_read(ctx.h, buf.ctypes.data, buf.size) == 0
     d = buf.reshape(n, 8).astype(np.float64)
-    d = d[d[:, 5] > 0]
+    d_keep = d[:, 5] > 0
+    d = d[d_keep]
+    f4 = (buf.reshape(n, 8)[:, 6] & 0xFFFFFFFF).astype(np.float64)[d_keep]
+    f8 = (buf.reshape(n, 8)[:, 6] >> 32).astype(np.float64)[d_keep]
+    d[:, 6] = f4 + f8
     units, of, ob = d[:, 5].sum(), d[:, 6].sum(), d[:, 7].sum()
     print(f"waves {len(d)} units {units:.0f} outputs fixed {of:.0f} byte-array {ob:.0f}")
     tot = d[:, :5].sum()
     for k, name in enumerate(("bounds+records", "staging", "writes BA", "writes 4 B", "writes 8 B")):
         print(f"  {name:15s} {d[:, k].sum() / units:9.0f} cycles per unit  ({d[:, k].sum() / tot:.2f} of the stamped)")
-    print(f"  per output: fixed {(d[:, 3].sum() + d[:, 4].sum()) / max(of, 1):.2f}, BA {d[:, 2].sum() / max(ob, 1):.2f} cycles")
+    print(f"  per output: fixed {(d[:, 3].sum() + d[:, 4].sum()) / max(of, 1):.2f} (4 B {d[:, 3].sum() / max(f4.sum(), 1):.2f}, "
+          f"8 B {d[:, 4].sum() / max(f8.sum(), 1):.2f}), BA {d[:, 2].sum() / max(ob, 1):.2f} cycles")
     busy = d[:, :5].sum(1)
     outs = d[:, 6] + d[:, 7]
     print(f"  wave busy cycles: mean {busy.mean():.0f} p50 {np.percentile(busy, 50):.0f} "
