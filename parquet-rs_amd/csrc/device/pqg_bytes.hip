@@ -837,116 +837,132 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
 // The tile goes in two rounds of BSD_RN values (lane l: values k * WG + l, k-major): eight wave
 // scans of the round's lengths and one exchange of their totals give its offsets (stored
 // coalesced); its bytes are assembled in an LDS image of the round's output (8-byte strings of a
-// whole round fit) and stored with 16-byte stores. The general kernel exits for these tiles.
+// whole round fit) and stored with 16-byte stores. The general kernel exits for these tiles. A
+// workgroup takes BSD_K consecutive list entries and stages a dictionary once for those of its
+// tiles that share it (one tile per workgroup: 0.56 ms per config-5 step, 2 or 4: 0.52; the same
+// for k_ba_tsum measured 0.19 -> 0.62-0.66 ms and is not done).
+#ifndef PQG_BSD_K
+#define PQG_BSD_K 4
+#endif
+constexpr uint32_t BSD_K = PQG_BSD_K;
 constexpr uint32_t BSD_RV = 8;                    // values per thread per round
 constexpr uint32_t BSD_RN = BSD_RV * WG;          // values per round
 static_assert(BSD_RN * 2 == BA_T, "two rounds per tile");
 
 __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
                                                    const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
-                                                   const uint32_t* __restrict__ tl, const uint32_t* __restrict__ vlen0,
-                                                   const uint64_t* __restrict__ dsrc0, const uint32_t* __restrict__ dlen0,
-                                                   const uint64_t* __restrict__ tsum) {
+                                                   const uint32_t* __restrict__ tl, uint32_t ntl,
+                                                   const uint32_t* __restrict__ vlen0, const uint64_t* __restrict__ dsrc0,
+                                                   const uint32_t* __restrict__ dlen0, const uint64_t* __restrict__ tsum) {
   __shared__ __attribute__((aligned(16))) uint8_t ldict[BSD_BYTES + 48];
   __shared__ uint32_t doff[BSD_N], dln[BSD_N];
   __shared__ __attribute__((aligned(16))) uint8_t img[BSD_IMG + 32];
   __shared__ uint32_t wsum[BSD_RV][WG / 64];
-  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
-  const PageWork pw = pages[p];
-  const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pages, pw, ck) || !ba_small_dict(pw, ck, pages)) return;
-  const uint32_t t = gt - pw.ltile0;
-  const uint64_t n = pw.nonnull, vo = pw.value_out;
-  const uint64_t t0 = (uint64_t)t * BA_T;
-  if (t0 >= n) return;
-  const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
-  const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
-  const uint32_t* vlen = vlen0 + ck.scr_base;
-  // the tile's indices, all loads in flight (lane l: values k * WG + l)
-  uint32_t idx[BA_VPT];
-#pragma unroll
-  for (uint32_t k = 0; k < BA_VPT; ++k) {
-    const uint32_t j = k * WG + tid;
-    idx[k] = j < cnt ? vlen[vo + t0 + j] : 0u;
-  }
-  // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it)
-  const PageWork& dp = pages[ck.dict_page];
-  const uint32_t nd = dp.num_values, nb = dp.nbytes;
-  const uint64_t db = dp.base & ~15ull;
-  const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
-  for (uint32_t c = tid; c < nch; c += WG) {
-    const uint64_t a = db + (uint64_t)c * 16;
-    reinterpret_cast<uint4*>(ldict)[c] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a)
-                                                            : gload_u128_tail(blob, blob_len, a);
-  }
-  for (uint32_t i = tid; i < nd; i += WG) {
-    doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - db);
-    dln[i] = dlen0[ck.dscr_base + i];
-  }
-  __syncthreads();
-  uint64_t run = tsum[gt];  // output byte offset of the round's first value
+  int32_t staged = -1;  // the dictionary page ldict / doff / dln hold (uniform)
+  const uint32_t e1 = min(ntl, (blockIdx.x + 1u) * BSD_K);
 #pragma unroll 1
-  for (uint32_t r = 0; r < 2; ++r) {
-    if (r * BSD_RN >= cnt) break;
-    uint32_t ln[BSD_RV], so[BSD_RV], pre[BSD_RV];
+  for (uint32_t e = blockIdx.x * BSD_K; e < e1; ++e) {
+    const uint32_t gt = tl[e], p = tile_page[gt];
+    const PageWork pw = pages[p];
+    const ChunkWork& ck = chunks[pw.chunk];
+    if (!ba_page_ok(pages, pw, ck) || !ba_small_dict(pw, ck, pages)) continue;
+    const uint32_t t = gt - pw.ltile0;
+    const uint64_t n = pw.nonnull, vo = pw.value_out;
+    const uint64_t t0 = (uint64_t)t * BA_T;
+    if (t0 >= n) continue;
+    const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
+    const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
+    const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
+    const uint32_t* vlen = vlen0 + ck.scr_base;
+    // the tile's indices, all loads in flight (lane l: values k * WG + l)
+    uint32_t idx[BA_VPT];
 #pragma unroll
-    for (uint32_t k = 0; k < BSD_RV; ++k) {
-      const uint32_t kk = r * BSD_RV + k, j = kk * WG + tid;
-      // (an index slot past the dictionary: empty, as BaSrc)
-      const bool in = j < cnt && idx[kk] < nd;
-      ln[k] = in ? dln[idx[kk]] : 0u;
-      so[k] = in ? doff[idx[kk]] : 0u;
-      const uint32_t inc = wave_scan_incl_u32(ln[k]);
-      pre[k] = inc - ln[k];
-      if (lane == 63u) wsum[k][wv] = inc;
+    for (uint32_t k = 0; k < BA_VPT; ++k) {
+      const uint32_t j = k * WG + tid;
+      idx[k] = j < cnt ? vlen[vo + t0 + j] : 0u;
     }
-    __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < BSD_RV; ++k) {  // value (k, tid): the rows before, the waves before
-      uint32_t rb = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < WG / 64; ++w) {
-        const uint32_t x = wsum[k][w];
-        if (w < wv) pre[k] += x;
-        rb += x;
+    // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it),
+    // staged once for the workgroup's tiles of one dictionary
+    const PageWork& dp = pages[ck.dict_page];
+    const uint32_t nd = dp.num_values, nb = dp.nbytes;
+    const uint64_t db = dp.base & ~15ull;
+    if (staged != ck.dict_page) {
+      const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
+      for (uint32_t c = tid; c < nch; c += WG) {
+        const uint64_t a = db + (uint64_t)c * 16;
+        reinterpret_cast<uint4*>(ldict)[c] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a)
+                                                                : gload_u128_tail(blob, blob_len, a);
       }
-      pre[k] += tot;
-      tot += rb;
+      for (uint32_t i = tid; i < nd; i += WG) {
+        doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - db);
+        dln[i] = dlen0[ck.dscr_base + i];
+      }
+      staged = ck.dict_page;
+      __syncthreads();
     }
-#pragma unroll
-    for (uint32_t k = 0; k < BSD_RV; ++k) {
-      const uint32_t j = (r * BSD_RV + k) * WG + tid;
-      if (j < cnt) offsets[vo + t0 + j] = (int64_t)(run + pre[k]);
-    }
-    const uint64_t gA = run, gB = run + tot;
-    const uint32_t sh = (uint32_t)(gA & 15u);
-    if (tot + 32 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is
+    uint64_t run = tsum[gt];  // output byte offset of the round's first value
+#pragma unroll 1
+    for (uint32_t r = 0; r < 2; ++r) {
+      if (r * BSD_RN >= cnt) break;
+      uint32_t ln[BSD_RV], so[BSD_RV], pre[BSD_RV];
 #pragma unroll
       for (uint32_t k = 0; k < BSD_RV; ++k) {
-        const uint32_t b0 = pre[k] + sh;
-        for (uint32_t q = 0; q < ln[k]; ++q) img[b0 + q] = ldict[so[k] + q];
+        const uint32_t kk = r * BSD_RV + k, j = kk * WG + tid;
+        // (an index slot past the dictionary: empty, as BaSrc)
+        const bool in = j < cnt && idx[kk] < nd;
+        ln[k] = in ? dln[idx[kk]] : 0u;
+        so[k] = in ? doff[idx[kk]] : 0u;
+        const uint32_t inc = wave_scan_incl_u32(ln[k]);
+        pre[k] = inc - ln[k];
+        if (lane == 63u) wsum[k][wv] = inc;
       }
       __syncthreads();
-      const uint64_t c0 = gA & ~15ull;
-      for (uint64_t c = c0 + (uint64_t)tid * 16u; c < gB; c += (uint64_t)WG * 16u) {
-        const uint32_t ii = (uint32_t)(c - c0);
-        if (c >= gA && c + 16 <= gB) {
-          gst16(out + c, *reinterpret_cast<const uint4*>(img + ii));
-        } else {
-          for (uint32_t q = 0; q < 16; ++q)
-            if (c + q >= gA && c + q < gB) out[c + q] = img[ii + q];
+      uint32_t tot = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < BSD_RV; ++k) {  // value (k, tid): the rows before, the waves before
+        uint32_t rb = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < WG / 64; ++w) {
+          const uint32_t x = wsum[k][w];
+          if (w < wv) pre[k] += x;
+          rb += x;
         }
+        pre[k] += tot;
+        tot += rb;
       }
-    } else {  // long values: straight from the LDS dictionary
+#pragma unroll
+      for (uint32_t k = 0; k < BSD_RV; ++k) {
+        const uint32_t j = (r * BSD_RV + k) * WG + tid;
+        if (j < cnt) offsets[vo + t0 + j] = (int64_t)(run + pre[k]);
+      }
+      const uint64_t gA = run, gB = run + tot;
+      const uint32_t sh = (uint32_t)(gA & 15u);
+      if (tot + 32 <= BSD_IMG) {  // staged: the round's bytes in an LDS image aligned as the output is
+#pragma unroll
+        for (uint32_t k = 0; k < BSD_RV; ++k) {
+          const uint32_t b0 = pre[k] + sh;
+          for (uint32_t q = 0; q < ln[k]; ++q) img[b0 + q] = ldict[so[k] + q];
+        }
+        __syncthreads();
+        const uint64_t c0 = gA & ~15ull;
+        for (uint64_t c = c0 + (uint64_t)tid * 16u; c < gB; c += (uint64_t)WG * 16u) {
+          const uint32_t ii = (uint32_t)(c - c0);
+          if (c >= gA && c + 16 <= gB) {
+            gst16(out + c, *reinterpret_cast<const uint4*>(img + ii));
+          } else {
+            for (uint32_t q = 0; q < 16; ++q)
+              if (c + q >= gA && c + q < gB) out[c + q] = img[ii + q];
+          }
+        }
+      } else {  // long values: straight from the LDS dictionary
 #pragma unroll 1
-      for (uint32_t k = 0; k < BSD_RV; ++k)
-        for (uint32_t q = 0; q < ln[k]; ++q) out[gA + pre[k] + q] = ldict[so[k] + q];
+        for (uint32_t k = 0; k < BSD_RV; ++k)
+          for (uint32_t q = 0; q < ln[k]; ++q) out[gA + pre[k] + q] = ldict[so[k] + q];
+      }
+      run += tot;
+      __syncthreads();  // (wsum and the image are reused by the next round)
     }
-    run += tot;
-    __syncthreads();  // (wsum and the image are reused by the next round)
   }
 }
 
@@ -1322,7 +1338,8 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
     hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vsrc, vlen,
                        dsrc, dlen, tsum);
     if (has_lvdict)
-      hipLaunchKernelGGL(k_ba_copy_sd, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vlen,
+      hipLaunchKernelGGL(k_ba_copy_sd, dim3((ntl + BSD_K - 1) / BSD_K), dim3(WG), 0, s, blob, blob_len, pages, chunks,
+                         tile_page, tl, ntl, vlen,
                          dsrc, dlen, tsum);
   }
   if (has_dba && ntl) {
