@@ -551,6 +551,7 @@ struct BaSrc {
   bool via_dict;
   uint32_t nd;  // dictionary entries: the consumers take only pages whose index slots were written
                 // (ba_page_ok / dict_usable); an index past the dictionary still reads as empty
+  BaSrc() = default;
   __device__ BaSrc(const ChunkWork& ck, const PageWork& pw, const PageWork* pages, const uint64_t* vsrc0,
                    const uint32_t* vlen0, const uint64_t* dsrc0, const uint32_t* dlen0)
       : vsrc(vsrc0 + ck.scr_base), vlen(vlen0 + ck.scr_base), dsrc(dsrc0 + ck.dscr_base),
@@ -571,49 +572,86 @@ struct BaSrc {
 constexpr uint32_t TS_DL = 2048;  // k_ba_tsum: dictionaries of at most this many entries staged in LDS
 
 // Per listed tile (gt, global) of a byte-array page: the tile's byte count into tsum[gt] (the
-// offsets themselves are written once, by k_ba_copy, from the scanned tile starts).
+// offsets themselves are written once, by k_ba_copy, from the scanned tile starts). A workgroup
+// takes TS_K consecutive list entries: their tiles and pages are loaded at once, and the page's
+// descriptors (and a small dictionary's entry lengths, staged in LDS) only when the page changes
+// -- with one tile per workgroup, the chain of dependent loads before a tile's first index load
+// (list entry, page, chunk, dictionary page) was most of the kernel's time.
+#ifndef PQG_TS_K
+#define PQG_TS_K 8
+#endif
+constexpr uint32_t TS_K = PQG_TS_K;
 __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork* chunks,
                                                 const uint32_t* __restrict__ tile_page, const uint32_t* __restrict__ tl,
-                                                const uint64_t* vsrc0, const uint32_t* __restrict__ vlen0,
+                                                uint32_t ntl, const uint64_t* vsrc0, const uint32_t* __restrict__ vlen0,
                                                 const uint64_t* dsrc0, const uint32_t* dlen0,
                                                 uint64_t* __restrict__ tsum) {
   __shared__ uint64_t red[WG / 64];
   __shared__ uint32_t sdl[TS_DL];  // a small dictionary's entry lengths
-  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
-  const PageWork pw = pages[p];
-  const ChunkWork& ck = chunks[pw.chunk];
-  if (!ba_page_ok(pages, pw, ck)) return;
-  const uint32_t t = gt - pw.ltile0;
-  const BaSrc bs(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
-  const uint64_t n = pw.nonnull, vo = pw.value_out;
-  if ((uint64_t)t * BA_T >= n) return;
-  uint64_t s = 0;
-#ifdef PQG_TS_OFF
-  if (false) {
-#else
-  if (bs.via_dict && bs.nd <= TS_DL) {  // the level path's dictionary chunks: lengths from LDS
-#endif
-    for (uint32_t i = threadIdx.x; i < bs.nd; i += WG) sdl[i] = bs.dlen[i];
-    uint32_t ix[BA_VPT];
-#pragma unroll
-    for (uint32_t k = 0; k < BA_VPT; ++k) {  // every index load in flight
-      const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
-      ix[k] = i < n ? bs.vlen[vo + i] : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < BA_VPT; ++k) s += ix[k] < bs.nd ? sdl[ix[k]] : 0u;
-  } else {
-#pragma unroll
-    for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
-      const uint64_t i = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
-      s += i < n ? bs.len(vo + i) : 0u;
-    }
+  __shared__ uint32_t lgt[TS_K], lpg[TS_K];
+  const uint32_t e0 = blockIdx.x * TS_K, ne = min(TS_K, ntl - e0);
+  if (threadIdx.x < ne) {
+    const uint32_t gt = tl[e0 + threadIdx.x];
+    lgt[threadIdx.x] = gt;
+    lpg[threadIdx.x] = tile_page[gt];
   }
-  const uint64_t tot = block_sum_u64(s, red);
-  if (threadIdx.x == 0) {
-    tsum[gt] = tot;
-    if (pw.tile_bytes) atomicAdd((unsigned long long*)&pages[p].nbytes_out, (unsigned long long)tot);
+  __syncthreads();
+  uint32_t cur = 0xFFFFFFFFu;  // the page whose descriptors are loaded (uniform)
+  bool ok = false, lds = false;
+  uint64_t n = 0, vo = 0;
+  uint32_t ltile0 = 0, tbytes = 0;
+  BaSrc bs;
+#pragma unroll 1
+  for (uint32_t i = 0; i < ne; ++i) {
+    const uint32_t gt = lgt[i], p = lpg[i];
+    if (p != cur) {
+      cur = p;
+      const PageWork pw = pages[p];
+      const ChunkWork& ck = chunks[pw.chunk];
+      ok = ba_page_ok(pages, pw, ck);
+      if (ok) {
+        bs = BaSrc(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
+        n = pw.nonnull;
+        vo = pw.value_out;
+        ltile0 = pw.ltile0;
+        tbytes = pw.tile_bytes;
+#ifdef PQG_TS_OFF
+        lds = false;
+#else
+        lds = bs.via_dict && bs.nd <= TS_DL;  // the level path's dictionary chunks: lengths from LDS
+#endif
+        if (lds) {
+          __syncthreads();  // (the previous page's lengths are read)
+          for (uint32_t k = threadIdx.x; k < bs.nd; k += WG) sdl[k] = bs.dlen[k];
+          __syncthreads();
+        }
+      }
+    }
+    if (!ok) continue;
+    const uint32_t t = gt - ltile0;
+    if ((uint64_t)t * BA_T >= n) continue;
+    uint64_t s = 0;
+    if (lds) {
+      uint32_t ix[BA_VPT];
+#pragma unroll
+      for (uint32_t k = 0; k < BA_VPT; ++k) {  // every index load in flight
+        const uint64_t j = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+        ix[k] = j < n ? bs.vlen[vo + j] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < BA_VPT; ++k) s += ix[k] < bs.nd ? sdl[ix[k]] : 0u;
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < BA_VPT; ++k) {  // lanes on consecutive values: coalesced
+        const uint64_t j = (uint64_t)t * BA_T + (uint64_t)k * WG + threadIdx.x;
+        s += j < n ? bs.len(vo + j) : 0u;
+      }
+    }
+    const uint64_t tot = block_sum_u64(s, red);
+    if (threadIdx.x == 0) {
+      tsum[gt] = tot;
+      if (tbytes) atomicAdd((unsigned long long*)&pages[p].nbytes_out, (unsigned long long)tot);
+    }
   }
 }
 
@@ -684,16 +722,15 @@ __device__ inline void ba_load16(const uint8_t* __restrict__ blob, uint64_t blob
   }
 }
 
-__global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
-                                                const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
-                                                const uint32_t* __restrict__ tl, const uint64_t* __restrict__ vsrc0,
-                                                const uint32_t* __restrict__ vlen0, const uint64_t* dsrc0,
-                                                const uint32_t* dlen0, const uint64_t* __restrict__ tsum) {
+// (one listed tile; every return is uniform over the workgroup)
+__device__ inline void ba_copy_tile(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
+                                    const ChunkWork* chunks, uint32_t gt, uint32_t p,
+                                    const uint64_t* __restrict__ vsrc0, const uint32_t* __restrict__ vlen0,
+                                    const uint64_t* dsrc0, const uint32_t* dlen0, const uint64_t* __restrict__ tsum) {
   __shared__ uint32_t loff[BA_T + BA_T / 16 + 1];  // lengths, then tile-relative offsets (padded)
   __shared__ __attribute__((aligned(16))) uint8_t img[BA_IMG];
   __shared__ uint64_t wsum[WG / 64];
   __shared__ uint32_t wmax[WG / 64];
-  const uint32_t gt = tl[blockIdx.x], p = tile_page[gt];
   const PageWork pw = pages[p];
   const ChunkWork& ck = chunks[pw.chunk];
   if (!ba_page_ok(pages, pw, ck) || ba_small_dict(pw, ck, pages)) return;  // (small dictionaries: k_ba_copy_sd)
@@ -830,6 +867,44 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
   }
 }
 
+// BA_CK listed tiles per workgroup: their tiles and pages loaded at once, each page's check made
+// once, so that the tiles k_ba_copy_sd takes (and those of pages past their checks) are passed
+// over without a chain of dependent loads each
+#ifndef PQG_BA_CK
+#define PQG_BA_CK 8
+#endif
+constexpr uint32_t BA_CK = PQG_BA_CK;
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_ba_copy(const uint8_t* __restrict__ blob, uint64_t blob_len, PageWork* pages,
+                                                const ChunkWork* chunks, const uint32_t* __restrict__ tile_page,
+                                                const uint32_t* __restrict__ tl, uint32_t ntl,
+                                                const uint64_t* __restrict__ vsrc0, const uint32_t* __restrict__ vlen0,
+                                                const uint64_t* dsrc0, const uint32_t* dlen0,
+                                                const uint64_t* __restrict__ tsum) {
+  __shared__ uint32_t lgt[BA_CK], lpg[BA_CK];
+  const uint32_t e0 = blockIdx.x * BA_CK, ne = min(BA_CK, ntl - e0);
+  if (threadIdx.x < ne) {
+    const uint32_t gt = tl[e0 + threadIdx.x];
+    lgt[threadIdx.x] = gt;
+    lpg[threadIdx.x] = tile_page[gt];
+  }
+  __syncthreads();
+  uint32_t cur = 0xFFFFFFFFu;
+  bool ok = false;
+#pragma unroll 1
+  for (uint32_t i = 0; i < ne; ++i) {
+    const uint32_t p = lpg[i];
+    if (p != cur) {
+      cur = p;
+      const PageWork pw = pages[p];
+      const ChunkWork& ck = chunks[pw.chunk];
+      ok = ba_page_ok(pages, pw, ck) && !ba_small_dict(pw, ck, pages);
+    }
+    if (!ok) continue;
+    ba_copy_tile(blob, blob_len, pages, chunks, lgt[i], p, vsrc0, vlen0, dsrc0, dlen0, tsum);
+    __syncthreads();  // (the next tile reuses the LDS)
+  }
+}
+
 // k_ba_copy for the dictionary pages of the level path's chunks whose dictionary is small (at most
 // BSD_N entries in at most BSD_BYTES bytes: short categorical strings): the dictionary page's bytes
 // and its entries' offsets and lengths are staged in LDS, so a value's length and bytes cost LDS
@@ -839,10 +914,10 @@ __global__ void __launch_bounds__(WG) k_ba_copy(const uint8_t* __restrict__ blob
 // coalesced); its bytes are assembled in an LDS image of the round's output (8-byte strings of a
 // whole round fit) and stored with 16-byte stores. The general kernel exits for these tiles. A
 // workgroup takes BSD_K consecutive list entries and stages a dictionary once for those of its
-// tiles that share it (one tile per workgroup: 0.56 ms per config-5 step, 2 or 4: 0.52; the same
-// for k_ba_tsum measured 0.19 -> 0.62-0.66 ms and is not done).
+// tiles that share it (one tile per workgroup: 0.56 ms per config-5 step, 2 to 8: 0.50-0.52); the
+// list entries and their pages are loaded at once and a page's descriptors once.
 #ifndef PQG_BSD_K
-#define PQG_BSD_K 4
+#define PQG_BSD_K 8
 #endif
 constexpr uint32_t BSD_K = PQG_BSD_K;
 constexpr uint32_t BSD_RV = 8;                    // values per thread per round
@@ -858,48 +933,71 @@ __global__ void __launch_bounds__(WG) k_ba_copy_sd(const uint8_t* __restrict__ b
   __shared__ uint32_t doff[BSD_N], dln[BSD_N];
   __shared__ __attribute__((aligned(16))) uint8_t img[BSD_IMG + 32];
   __shared__ uint32_t wsum[BSD_RV][WG / 64];
+  __shared__ uint32_t lgt[BSD_K], lpg[BSD_K];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t e0 = blockIdx.x * BSD_K, ne = min(BSD_K, ntl - e0);
+  if (tid < ne) {  // the workgroup's list entries and their pages, loaded at once
+    const uint32_t gt = tl[e0 + tid];
+    lgt[tid] = gt;
+    lpg[tid] = tile_page[gt];
+  }
+  __syncthreads();
+  uint32_t cur = 0xFFFFFFFFu;  // the page whose descriptors are loaded (uniform)
+  bool ok = false;
+  uint64_t n = 0, vo = 0;
+  uint32_t ltile0 = 0, nd = 0;
+  gptr<int64_t> offsets = gptr<int64_t>(nullptr);
+  gptr<uint8_t> out = gptr<uint8_t>(nullptr);
+  const uint32_t* vlen = nullptr;
   int32_t staged = -1;  // the dictionary page ldict / doff / dln hold (uniform)
-  const uint32_t e1 = min(ntl, (blockIdx.x + 1u) * BSD_K);
 #pragma unroll 1
-  for (uint32_t e = blockIdx.x * BSD_K; e < e1; ++e) {
-    const uint32_t gt = tl[e], p = tile_page[gt];
-    const PageWork pw = pages[p];
-    const ChunkWork& ck = chunks[pw.chunk];
-    if (!ba_page_ok(pages, pw, ck) || !ba_small_dict(pw, ck, pages)) continue;
-    const uint32_t t = gt - pw.ltile0;
-    const uint64_t n = pw.nonnull, vo = pw.value_out;
+  for (uint32_t i = 0; i < ne; ++i) {
+    const uint32_t gt = lgt[i], p = lpg[i];
+    if (p != cur) {  // the page's descriptors, and its dictionary staged unless it is already
+      cur = p;
+      const PageWork pw = pages[p];
+      const ChunkWork& ck = chunks[pw.chunk];
+      ok = ba_page_ok(pages, pw, ck) && ba_small_dict(pw, ck, pages);
+      if (ok) {
+        n = pw.nonnull;
+        vo = pw.value_out;
+        ltile0 = pw.ltile0;
+        offsets = gp(ck.off_out);
+        out = gp(ck.val_out);
+        vlen = vlen0 + ck.scr_base;
+        // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it)
+        const PageWork& dp = pages[ck.dict_page];
+        nd = dp.num_values;
+        if (staged != ck.dict_page) {
+          const uint32_t nb = dp.nbytes;
+          const uint64_t db = dp.base & ~15ull;
+          const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
+          __syncthreads();  // (the previous dictionary's reads are done)
+          for (uint32_t c = tid; c < nch; c += WG) {
+            const uint64_t a = db + (uint64_t)c * 16;
+            reinterpret_cast<uint4*>(ldict)[c] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a)
+                                                                    : gload_u128_tail(blob, blob_len, a);
+          }
+          for (uint32_t k = tid; k < nd; k += WG) {
+            doff[k] = (uint32_t)(dsrc0[ck.dscr_base + k] - db);
+            dln[k] = dlen0[ck.dscr_base + k];
+          }
+          staged = ck.dict_page;
+          __syncthreads();
+        }
+      }
+    }
+    if (!ok) continue;
+    const uint32_t t = gt - ltile0;
     const uint64_t t0 = (uint64_t)t * BA_T;
     if (t0 >= n) continue;
     const uint32_t cnt = (uint32_t)(n - t0 < BA_T ? n - t0 : BA_T);
-    const gptr<int64_t> __restrict__ offsets = gp(ck.off_out);
-    const gptr<uint8_t> __restrict__ out = gp(ck.val_out);
-    const uint32_t* vlen = vlen0 + ck.scr_base;
     // the tile's indices, all loads in flight (lane l: values k * WG + l)
     uint32_t idx[BA_VPT];
 #pragma unroll
     for (uint32_t k = 0; k < BA_VPT; ++k) {
       const uint32_t j = k * WG + tid;
       idx[k] = j < cnt ? vlen[vo + t0 + j] : 0u;
-    }
-    // the dictionary page in 16-byte chunks from its aligned start (entry offsets relative to it),
-    // staged once for the workgroup's tiles of one dictionary
-    const PageWork& dp = pages[ck.dict_page];
-    const uint32_t nd = dp.num_values, nb = dp.nbytes;
-    const uint64_t db = dp.base & ~15ull;
-    if (staged != ck.dict_page) {
-      const uint32_t nch = (uint32_t)((dp.base + nb - db + 15) / 16);
-      for (uint32_t c = tid; c < nch; c += WG) {
-        const uint64_t a = db + (uint64_t)c * 16;
-        reinterpret_cast<uint4*>(ldict)[c] = a + 16 <= blob_len ? *reinterpret_cast<const uint4*>(blob + a)
-                                                                : gload_u128_tail(blob, blob_len, a);
-      }
-      for (uint32_t i = tid; i < nd; i += WG) {
-        doff[i] = (uint32_t)(dsrc0[ck.dscr_base + i] - db);
-        dln[i] = dlen0[ck.dscr_base + i];
-      }
-      staged = ck.dict_page;
-      __syncthreads();
     }
     uint64_t run = tsum[gt];  // output byte offset of the round's first value
 #pragma unroll 1
@@ -1330,12 +1428,13 @@ hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pa
   // tile sums before the page scan: the level path's dictionary pages take their byte totals
   // from them (PageWork::tile_bytes)
   if (ntl)
-    hipLaunchKernelGGL(k_ba_tsum, dim3(ntl), dim3(WG), 0, s, pages, chunks, tile_page, tl, vsrc, vlen, dsrc, dlen,
-                       tsum);
+    hipLaunchKernelGGL(k_ba_tsum, dim3((ntl + TS_K - 1) / TS_K), dim3(WG), 0, s, pages, chunks, tile_page, tl, ntl, vsrc,
+                       vlen, dsrc, dlen, tsum);
   hipLaunchKernelGGL(k_scan_bytes, dim3(1), dim3(WG), 0, s, pages, chunks, npages);
   if (ntl) {
     hipLaunchKernelGGL(k_ba_tscan, dim3(npages), dim3(WG), 0, s, pages, chunks, tsum);
-    hipLaunchKernelGGL(k_ba_copy, dim3(ntl), dim3(WG), 0, s, blob, blob_len, pages, chunks, tile_page, tl, vsrc, vlen,
+    hipLaunchKernelGGL(k_ba_copy, dim3((ntl + BA_CK - 1) / BA_CK), dim3(WG), 0, s, blob, blob_len, pages, chunks,
+                       tile_page, tl, ntl, vsrc, vlen,
                        dsrc, dlen, tsum);
     if (has_lvdict)
       hipLaunchKernelGGL(k_ba_copy_sd, dim3((ntl + BSD_K - 1) / BSD_K), dim3(WG), 0, s, blob, blob_len, pages, chunks,
