@@ -283,7 +283,10 @@ __device__ inline void lv_fallback_page(const uint8_t* __restrict__ blob, uint64
 
 __device__ inline void scan_values(PageWork* pages, ChunkWork* chunks, int npages);
 
-constexpr int LF_GRID = 256;  // k_lv_fallback workgroups at most
+#ifndef PQG_LF_GRID
+#define PQG_LF_GRID 256
+#endif
+constexpr int LF_GRID = PQG_LF_GRID;  // k_lv_fallback workgroups at most
 
 // scan != 0 (a def stream, no rep stream after it): the grid's last workgroup also runs
 // k_scan_values (the non-null counts are final), one launch fewer per decode.
