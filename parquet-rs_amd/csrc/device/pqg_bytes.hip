@@ -914,10 +914,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) k_
 // coalesced); its bytes are assembled in an LDS image of the round's output (8-byte strings of a
 // whole round fit) and stored with 16-byte stores. The general kernel exits for these tiles. A
 // workgroup takes BSD_K consecutive list entries and stages a dictionary once for those of its
-// tiles that share it (one tile per workgroup: 0.56 ms per config-5 step, 2 to 8: 0.50-0.52); the
-// list entries and their pages are loaded at once and a page's descriptors once.
+// tiles that share it (one tile per workgroup: 0.56 ms per config-5 step, 4: 0.51, 8: 0.51-0.52,
+// 16: 0.54); the list entries and their pages are loaded at once and a page's descriptors once.
 #ifndef PQG_BSD_K
-#define PQG_BSD_K 8
+#define PQG_BSD_K 4
 #endif
 constexpr uint32_t BSD_K = PQG_BSD_K;
 constexpr uint32_t BSD_RV = 8;                    // values per thread per round
