@@ -3076,8 +3076,11 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
     return hipGetLastError();
   }
   // (k_lv_plan2's scan ran in k_lv_segscan's last workgroup)
+// window table and window emit kernels on 4x grids (round 5, kernel times: config 5 k_lv_win
+// 0.286 -> 0.267 ms, k_lv_emit 0.536 -> 0.515; config 2 at p_null 0.1 0.401 -> 0.386 and 0.698 ->
+// 0.679; 2x about half of that)
 #ifndef PQG_LW_GRIDX
-#define PQG_LW_GRIDX 1
+#define PQG_LW_GRIDX 4
 #endif
   hipLaunchKernelGGL(k_lv_win, dim3(wgrid * PQG_LW_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt,
                      lt);
@@ -3094,7 +3097,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
                        chunks, sel, rt, lt, LvLevelOut<1>{});
   } else {
 #ifndef PQG_LE_GRIDX
-#define PQG_LE_GRIDX 1
+#define PQG_LE_GRIDX 4
 #endif
     hipLaunchKernelGGL(k_lv_emit<2>, dim3(wgrid * PQG_LE_GRIDX), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel,
                        rt, lt);
