@@ -258,6 +258,20 @@ void pqg_column_reader_close(pqg_column_reader *cr);
 int pqg_column_reader_read_batch(pqg_column_reader *cr, size_t batch_size, int16_t *def,
                                  int16_t *rep, void *values, uint64_t values_bytes_cap,
                                  uint32_t *lengths, size_t *values_read, size_t *levels_read);
+/* read_batch with the reference's slice lengths (column/reader.rs:159-205): `def_cap` /
+ * `rep_cap` levels (when def / rep are given) and `values_cap` values (BYTE_ARRAY/FLBA: entries of
+ * `lengths`) clamp the batch and every page iteration as `def_levels.len()`, `rep_levels.len()`
+ * and `values.len()` do; pqg_column_reader_read_batch is this call with every cap = batch_size.
+ * def = NULL on a column with max_def > 0 reads iter_batch_size values per page iteration out of
+ * step with the levels (:212-226, 247-250): PLAIN fixed width then ends in EOF and
+ * PLAIN BYTE_ARRAY in PQG_ERR_PANIC once a page's non-null values are used up, the DELTA
+ * encodings return short reads and then PQG_ERR_HANG (the reference's loop makes no progress);
+ * dictionary and boolean pages read that far return PQG_ERR_NYI (the reference reads the
+ * stream's padding bits there). */
+int pqg_column_reader_read_batch_caps(pqg_column_reader *cr, size_t batch_size, int16_t *def,
+                                      size_t def_cap, int16_t *rep, size_t rep_cap, void *values,
+                                      size_t values_cap, uint64_t values_bytes_cap, uint32_t *lengths,
+                                      size_t *values_read, size_t *levels_read);
 
 /* ---------------------------------------------------------------- file -> device row groups
  * The product path of whole row groups, from the file to device (and host) memory, pipelined:

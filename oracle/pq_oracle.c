@@ -1148,25 +1148,30 @@ static void vpush(vec_u8 *v, const void *src, size_t n) {
   v->n += n;
 }
 
-/* read_batch, column/reader.rs:159-265, for a single call. def/rep/values are the
- * caller's slices (capacity batch_size each). */
-static int read_batch(or_col_reader *r, size_t batch_size, int16_t *def, int16_t *rep,
-                      uint8_t *values, size_t *values_read_out, size_t *levels_read_out) {
+/* read_batch, column/reader.rs:159-265, for a single call. def/rep/values are the caller's
+ * slices of dcap / rcap / vcap elements (def_levels.len(), rep_levels.len(), values.len()). */
+static int read_batch(or_col_reader *r, size_t batch_size, int16_t *def, size_t dcap, int16_t *rep,
+                      size_t rcap, uint8_t *values, size_t vcap, size_t *values_read_out,
+                      size_t *levels_read_out) {
   size_t values_read = 0, levels_read = 0;
   size_t es = or_type_size(r->col->physical_type);
   *values_read_out = *levels_read_out = 0;
-  /* slices all have length batch_size, so batch_size stays */
+  /* the smallest batch the slices allow (:170-177) */
+  if (vcap < batch_size) batch_size = vcap;
+  if (def && dcap < batch_size) batch_size = dcap;
+  if (rep && rcap < batch_size) batch_size = rcap;
   while ((values_read > levels_read ? values_read : levels_read) < batch_size) {
     int st;
     int hn = has_next(r, &st);
     if (hn < 0) return st;
     if (hn == 0) break;
+    /* iter_batch_size (:187-205) */
     size_t iter = batch_size;
     size_t left = (size_t)(r->num_buffered_values - r->num_decoded_values);
     if (left < iter) iter = left;
-    if (batch_size - values_read < iter) iter = batch_size - values_read;
-    if (def && batch_size - levels_read < iter) iter = batch_size - levels_read;
-    if (rep && batch_size - levels_read < iter) iter = batch_size - levels_read;
+    if (vcap - values_read < iter) iter = vcap - values_read;
+    if (def && dcap - levels_read < iter) iter = dcap - levels_read;
+    if (rep && rcap - levels_read < iter) iter = rcap - levels_read;
 
     size_t values_to_read = 0, num_def = 0, num_rep = 0;
     if (r->col->max_def > 0 && def) {
@@ -1198,8 +1203,9 @@ static int read_batch(or_col_reader *r, size_t batch_size, int16_t *def, int16_t
   return OR_OK;
 }
 
-int or_read_column(const or_column *col, const or_page *pages, size_t npages,
-                   size_t batch_size, int want_def, int want_rep, or_column_result *res) {
+int or_read_column_caps(const or_column *col, const or_page *pages, size_t npages,
+                        size_t batch_size, size_t vcap, size_t dcap, size_t rcap, int want_def,
+                        int want_rep, uint64_t *counts, size_t counts_cap, or_column_result *res) {
   memset(res, 0, sizeof(*res));
   or_col_reader r;
   memset(&r, 0, sizeof(r));
@@ -1210,18 +1216,22 @@ int or_read_column(const or_column *col, const or_page *pages, size_t npages,
   size_t es = or_type_size(col->physical_type);
   int isba = col->physical_type == OR_BYTE_ARRAY || col->physical_type == OR_FIXED_LEN_BYTE_ARRAY;
   if (batch_size == 0) batch_size = 1024;
-  int16_t *def = want_def ? (int16_t *)malloc(batch_size * 2) : NULL;
-  int16_t *rep = want_rep ? (int16_t *)malloc(batch_size * 2) : NULL;
-  uint8_t *vals = (uint8_t *)malloc(batch_size * es);
+  int16_t *def = want_def ? (int16_t *)malloc((dcap ? dcap : 1) * 2) : NULL;
+  int16_t *rep = want_rep ? (int16_t *)malloc((rcap ? rcap : 1) * 2) : NULL;
+  uint8_t *vals = (uint8_t *)malloc((vcap ? vcap : 1) * es);
   vec_u8 vdef = {0}, vrep = {0}, vval = {0}, voff = {0}, vbytes = {0};
   int64_t off0 = 0;
   if (isba) vpush(&voff, &off0, 8);
   int st = OR_OK;
   for (;;) {
     size_t vr = 0, lr = 0;
-    st = read_batch(&r, batch_size, def, rep, vals, &vr, &lr);
+    st = read_batch(&r, batch_size, def, dcap, rep, rcap, vals, vcap, &vr, &lr);
     if (st) break;
     if (vr == 0 && lr == 0) break;
+    if (counts && 2 * res->num_batches + 1 < counts_cap) {
+      counts[2 * res->num_batches] = vr;
+      counts[2 * res->num_batches + 1] = lr;
+    }
     res->num_batches++;
     if (def) vpush(&vdef, def, lr * 2);
     if (rep) vpush(&vrep, rep, lr * 2);
@@ -1254,6 +1264,13 @@ int or_read_column(const or_column *col, const or_page *pages, size_t npages,
       free(r.decoders[i]);
     }
   return st;
+}
+
+int or_read_column(const or_column *col, const or_page *pages, size_t npages,
+                   size_t batch_size, int want_def, int want_rep, or_column_result *res) {
+  if (batch_size == 0) batch_size = 1024;
+  return or_read_column_caps(col, pages, npages, batch_size, batch_size, batch_size, batch_size,
+                             want_def, want_rep, NULL, 0, res);
 }
 
 void or_column_result_free(or_column_result *res) {

@@ -191,6 +191,12 @@ typedef struct {
 
 int or_read_column(const or_column *col, const or_page *pages, size_t npages,
                    size_t batch_size, int want_def, int want_rep, or_column_result *res);
+/* The same with the reference's slice lengths: values / def / rep slices of vcap / dcap / rcap
+ * elements (column/reader.rs:170-205); counts (if given) receives (values_read, levels_read) of
+ * each read_batch call, counts_cap entries. */
+int or_read_column_caps(const or_column *col, const or_page *pages, size_t npages,
+                        size_t batch_size, size_t vcap, size_t dcap, size_t rcap, int want_def,
+                        int want_rep, uint64_t *counts, size_t counts_cap, or_column_result *res);
 void or_column_result_free(or_column_result *res);
 
 /* ---------------------------------------------------------------- encoders (generators) */

@@ -88,6 +88,8 @@ def _declare(L):
     L.or_delta_decode.argtypes = [C.c_int, vp, sz, vp, sz, szp, szp, szp]
     L.or_read_column.argtypes = [C.POINTER(Column), C.POINTER(Page), sz, sz, C.c_int, C.c_int,
                                  C.POINTER(ColumnResult)]
+    L.or_read_column_caps.argtypes = [C.POINTER(Column), C.POINTER(Page), sz, sz, sz, sz, sz, C.c_int,
+                                      C.c_int, vp, sz, C.POINTER(ColumnResult)]
     L.or_column_result_free.argtypes = [C.POINTER(ColumnResult)]
     for name, args in [
         ("or_rle_encode", [vp, sz, C.c_int, vp, sz]),
@@ -299,10 +301,12 @@ class PageSpec:
 
 
 def read_column(ptype, pages, max_def=0, max_rep=0, type_length=-1, batch_size=1024,
-                want_def=True, want_rep=True):
-    """ColumnReaderImpl::read_batch over all pages (column/reader.rs:159-265).
+                want_def=True, want_rep=True, values_cap=None, def_cap=None, rep_cap=None):
+    """ColumnReaderImpl::read_batch over all pages (column/reader.rs:159-265), every call with
+    slices of values_cap / def_cap / rep_cap elements (default batch_size).
 
-    Returns dict(status, message, def, rep, values, offsets, bytes, batches)."""
+    Returns dict(status, message, def, rep, values, offsets, bytes, batches, counts: the
+    (values_read, levels_read) of each call)."""
     col = Column(ptype, type_length, max_def, max_rep)
     keep = []
     arr = (Page * max(len(pages), 1))()
@@ -312,10 +316,18 @@ def read_column(ptype, pages, max_def=0, max_rep=0, type_length=-1, batch_size=1
         arr[i] = Page(p.page_type, b.ctypes.data, len(p.buf), p.num_values, p.encoding,
                       p.def_encoding, p.rep_encoding, p.def_len, p.rep_len)
     res = ColumnResult()
-    st = lib().or_read_column(C.byref(col), arr, len(pages), batch_size, int(want_def),
-                              int(want_rep), C.byref(res))
+    bs = batch_size or 1024
+    caps = [bs] + [c for c in (values_cap, def_cap, rep_cap) if c]
+    ccap = 2 * min(sum(p.num_values for p in pages) // max(1, min(caps)) + 2 * len(pages) + 8, 1 << 20)
+    counts = np.zeros(ccap, np.uint64)
+    st = lib().or_read_column_caps(C.byref(col), arr, len(pages), bs,
+                                   bs if values_cap is None else values_cap,
+                                   bs if def_cap is None else def_cap,
+                                   bs if rep_cap is None else rep_cap, int(want_def),
+                                   int(want_rep), counts.ctypes.data, ccap, C.byref(res))
     out = {"status": st, "message": res.message.decode(errors="replace"),
-           "batches": res.num_batches}
+           "batches": res.num_batches,
+           "counts": [(int(counts[2 * k]), int(counts[2 * k + 1])) for k in range(min(res.num_batches, ccap // 2))]}
     nl, nv = res.num_levels, res.num_values
     out["def"] = (np.ctypeslib.as_array(res.def_levels, (nl,)).copy()
                   if res.def_levels and nl else np.zeros(0, np.int16))

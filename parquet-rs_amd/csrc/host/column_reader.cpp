@@ -2,14 +2,15 @@
 // pqg_column_reader_* (ColumnReaderImpl::read_batch over a GPU-decoded chunk,
 // column/reader.rs:159-265).
 //
-// read_batch contract served here (derived from the loop at column/reader.rs:175-262):
-//  * def levels requested and max_def > 0: every call returns exactly
-//    min(batch_size, levels left in the chunk) levels and the values whose def == max_def;
-//  * otherwise values = min(batch_size, levels left) (each level slot is one value), and
-//    levels_read = values when rep levels are requested and max_rep > 0, else 0.
+// read_batch is the reference's loop (column/reader.rs:159-265) replayed page by page over the
+// decoded chunk: the batch clamped to the slices, per iteration iter_batch_size clamped to the page
+// and the slices, def levels counted for the values to read (or iter_batch_size values without def
+// levels), num_decoded_values advanced by max(levels, values). The def / rep / value
+// positions within a page move independently, as the reference's three decoders do.
 // Chunk errors surface lazily, like the reference: batches that end before the first bad
 // page succeed; the batch that reaches it returns the page's status.
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -34,9 +35,18 @@ struct pqg_column_reader {
   std::vector<int16_t> def, rep;
   std::vector<uint8_t> values;
   std::vector<int64_t> offsets;
-  uint64_t L = 0, V = 0;       // level / value cursors
+  // data pages in file order: level count (num_values), first level, first dense value, dense
+  // (non-null) value count, value encoding
+  std::vector<uint64_t> pN, pL, pV, pK;
+  std::vector<int32_t> pEnc;
+  // ColumnReaderImpl's page state (column/reader.rs:106-137): the current data page, its
+  // num_decoded_values, and the positions of its def / rep level decoders and of its value
+  // decoder, which read_batch advances independently (:212-259)
+  int64_t pg = -1;
+  uint64_t buffered = 0, nd = 0, dpos = 0, rpos = 0, vpos = 0;
+  uint64_t V = 0;              // absolute dense-value cursor (vstart of the page + vpos)
   int status = 0;              // chunk status
-  uint64_t bad_level = ~0ull;  // first level index of the failing page
+  int64_t bad_page = INT64_MAX;  // data-page index whose read_new_page fails (npages: after the last)
   std::string err;
 };
 
@@ -204,16 +214,21 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
   cr->col.max_rep = l.max_rep;
   cr->is_ba = l.physical_type == PQG_BYTE_ARRAY || l.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
   cr->es = value_size(l.physical_type, l.type_length);
-  std::vector<uint64_t> page_start;  // level start of each page (data pages)
+  std::vector<int64_t> data_index;  // per page: index among the data pages read before it
   for (const pqg_page& p : c->pages) {
-    page_start.push_back(cr->total_levels);
-    if (p.page_type == PQG_PAGE_DATA || p.page_type == PQG_PAGE_DATA_V2) cr->total_levels += p.num_values;
+    data_index.push_back((int64_t)cr->pN.size());
+    if (p.page_type == PQG_PAGE_DATA || p.page_type == PQG_PAGE_DATA_V2) {
+      cr->pN.push_back(p.num_values);
+      cr->pL.push_back(cr->total_levels);
+      cr->pEnc.push_back(p.encoding);
+      cr->total_levels += p.num_values;
+    }
   }
   const uint64_t n = cr->total_levels;
   if (host_st && c->pages.empty()) {  // nothing before the failure: the first batch fails
     cr->status = host_st;
     cr->err = c->err;
-    cr->bad_level = 0;
+    cr->bad_page = 0;
     *out = cr.release();
     return PQG_OK;
   }
@@ -302,12 +317,36 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
   cr->status = st;
   cr->err = msg;
   if (st != PQG_OK) {
-    cr->bad_level = (bad >= 0 && bad < (int)page_start.size()) ? page_start[bad] : 0;
-    // a bad dictionary page (or any failure before the first data page) fails the first batch
+    // the failing page's read_new_page (set_data) or first get fails the batch that reaches it; a
+    // bad dictionary page (any failure before the first data page) fails the first batch
+    cr->bad_page = (bad >= 0 && bad < (int)data_index.size()) ? data_index[bad] : 0;
   } else if (host_st) {  // every page before the host failure decoded: it fails the batch after them
     cr->status = host_st;
     cr->err = c->err;
-    cr->bad_level = n;
+    cr->bad_page = (int64_t)cr->pN.size();
+  }
+  // dense values per data page: the levels equal to max_def (the count read_batch makes,
+  // column/reader.rs:216-220), or every level slot of a column without def levels; pages at or
+  // after a failing page are never served
+  const size_t np = cr->pN.size();
+  cr->pV.assign(np, 0);
+  cr->pK.assign(np, 0);
+  uint64_t vs = 0;
+  for (size_t i = 0; i < np && (int64_t)i < cr->bad_page; ++i) {
+    uint64_t k = cr->pN[i];
+    if (l.max_def > 0) {
+      k = 0;
+      const int16_t* d = cr->def.data() + cr->pL[i];
+      for (uint64_t j = 0; j < cr->pN[i]; ++j) k += d[j] == l.max_def;
+    }
+    cr->pV[i] = vs;
+    cr->pK[i] = k;
+    vs += k;
+  }
+  if (cr->status == PQG_OK && vs != cr->total_values) {  // the decode's count disagrees with the levels
+    cr->status = PQG_ERR_GENERAL;
+    cr->err = "decoded value count does not match the def levels";
+    cr->bad_page = 0;
   }
   *out = cr.release();
   return PQG_OK;
@@ -315,50 +354,158 @@ int pqg_column_reader_open(pqg_file_reader* r, int rg, int col, pqg_ctx* ctx,
 
 void pqg_column_reader_close(pqg_column_reader* cr) { delete cr; }
 
+// has_next (column/reader.rs:416-430) with read_new_page (:269-380): the next data page is loaded
+// when the current one is used up or empty; loading the failing page fails.
+static int rb_has_next(pqg_column_reader* cr, bool* more) {
+  *more = true;
+  if (cr->pg >= 0 && cr->buffered != 0 && cr->nd != cr->buffered) return PQG_OK;
+  const int64_t next = cr->pg + 1;
+  if (cr->status != PQG_OK && next >= cr->bad_page) return cr->status;
+  if (next >= (int64_t)cr->pN.size()) {  // no page left
+    *more = false;
+    return PQG_OK;
+  }
+  cr->pg = next;
+  cr->buffered = cr->pN[next];
+  cr->nd = cr->dpos = cr->rpos = cr->vpos = 0;
+  *more = cr->buffered != 0;  // an empty page ends this call's loop
+  return PQG_OK;
+}
+
+// Value decoder get (read_values, column/reader.rs:451-460) asking `want` values of the current
+// page: how many the page's decoder returns, or its error. The page holds K dense values; asked past
+// them (read_batch without def levels on a column with nulls) each decoder does what
+// its get does once its stream is used up:
+//  PLAIN fixed width / INT96 / FLBA: min(want, num_values left of the N set) values, EOF when the
+//    value bytes run short ("Not enough bytes to decode", decoding.rs:138-156, 158-186, 228-247);
+//  PLAIN BYTE_ARRAY: the length prefix read past the end panics (read_num_bytes!, bit_util.rs:30-43);
+//  DELTA_BINARY_PACKED / DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY: min(want, values left of the
+//    header's count) (decoding.rs:535-572, 697-711, 794-822);
+//  dictionary indices and booleans (PLAIN, RLE): the reference goes on into the stream's padding
+//    bits; not replayed here (NYI).
+static int rb_values(pqg_column_reader* cr, uint64_t want, uint64_t* got) {
+  const uint64_t N = cr->pN[cr->pg], K = cr->pK[cr->pg], v = cr->vpos;
+  const int enc = cr->pEnc[cr->pg];
+  *got = 0;
+  switch (enc) {
+    case PQG_DELTA_BINARY_PACKED:
+    case PQG_DELTA_LENGTH_BYTE_ARRAY:
+    case PQG_DELTA_BYTE_ARRAY:
+      *got = want < K - v ? want : K - v;
+      return PQG_OK;
+    case PQG_PLAIN:
+      if (cr->col.physical_type != PQG_BOOLEAN) {
+        const uint64_t n = want < N - v ? want : N - v;
+        if (v + n > K) {
+          if (cr->col.physical_type == PQG_BYTE_ARRAY) {
+            cr->err = "assertion failed: 4 <= src.len() (PLAIN BYTE_ARRAY length read past the page)";
+            return PQG_ERR_PANIC;
+          }
+          cr->err = "Not enough bytes to decode";
+          return PQG_ERR_EOF;
+        }
+        *got = n;
+        return PQG_OK;
+      }
+      break;
+    default:
+      break;
+  }
+  if (v + want > K) {
+    cr->err = "read_batch without def levels past a page's non-null values: the reference reads "
+              "the stream's padding here (dictionary / boolean encodings), not replayed";
+    return PQG_ERR_NYI;
+  }
+  *got = want;
+  return PQG_OK;
+}
+
+// ColumnReaderImpl::read_batch (column/reader.rs:159-265) replayed over the decoded chunk, with the
+// reference's slice lengths: values_cap values, def_cap / rep_cap levels (when given).
+int pqg_column_reader_read_batch_caps(pqg_column_reader* cr, size_t batch_size, int16_t* def,
+                                      size_t def_cap, int16_t* rep, size_t rep_cap, void* values,
+                                      size_t values_cap, uint64_t values_bytes_cap, uint32_t* lengths,
+                                      size_t* values_read, size_t* levels_read) {
+  if (!cr || !values_read || !levels_read) return PQG_ERR_INVALID;
+  *values_read = *levels_read = 0;
+  // the smallest batch the slices allow (:170-177)
+  uint64_t batch = batch_size < values_cap ? batch_size : values_cap;
+  if (def && def_cap < batch) batch = def_cap;
+  if (rep && rep_cap < batch) batch = rep_cap;
+  const int16_t md = cr->col.max_def;
+  const bool read_def = md > 0 && def, read_rep = cr->col.max_rep > 0 && rep;
+  uint64_t vr = 0, lr = 0, bytes = 0;
+  while ((vr > lr ? vr : lr) < batch) {
+    bool more;
+    int st = rb_has_next(cr, &more);
+    if (st != PQG_OK) return st;
+    if (!more) break;
+    // iter_batch_size (:187-205)
+    uint64_t iter = batch < cr->buffered - cr->nd ? batch : cr->buffered - cr->nd;
+    if (values_cap - vr < iter) iter = values_cap - vr;
+    if (def && def_cap - lr < iter) iter = def_cap - lr;
+    if (rep && rep_cap - lr < iter) iter = rep_cap - lr;
+    const uint64_t N = cr->buffered, lbase = cr->pL[cr->pg];
+    uint64_t to_read = iter, ndef = 0, nrep = 0;
+    if (read_def) {  // LevelDecoder::get clamps to the page's levels left (levels.rs:249-271)
+      ndef = iter < N - cr->dpos ? iter : N - cr->dpos;
+      const int16_t* src = cr->def.data() + lbase + cr->dpos;
+      memcpy(def + lr, src, ndef * 2);
+      to_read = 0;
+      for (uint64_t i = 0; i < ndef; ++i) to_read += src[i] == md;
+    }
+    if (read_rep) {
+      nrep = iter < N - cr->rpos ? iter : N - cr->rpos;
+      memcpy(rep + lr, cr->rep.data() + lbase + cr->rpos, nrep * 2);
+      if (def && ndef != nrep) {  // assert_eq! (:233-239)
+        cr->err = "Number of decoded rep / def levels did not match";
+        return PQG_ERR_PANIC;
+      }
+    }
+    uint64_t nv = 0;
+    st = rb_values(cr, to_read, &nv);
+    if (st != PQG_OK) return st;
+    const uint64_t v0 = cr->pV[cr->pg] + cr->vpos;
+    if (cr->is_ba) {
+      const uint64_t b0 = (uint64_t)cr->offsets[v0], b1 = (uint64_t)cr->offsets[v0 + nv];
+      if (bytes + (b1 - b0) > values_bytes_cap) return PQG_ERR_CAPACITY;
+      if (values && b1 > b0) memcpy((uint8_t*)values + bytes, cr->values.data() + b0, b1 - b0);
+      if (lengths)
+        for (uint64_t i = 0; i < nv; ++i)
+          lengths[vr + i] = (uint32_t)(cr->offsets[v0 + i + 1] - cr->offsets[v0 + i]);
+      bytes += b1 - b0;
+    } else {
+      const uint64_t nb = nv * (uint64_t)cr->es;
+      if ((vr + nv) * (uint64_t)cr->es > values_bytes_cap) return PQG_ERR_CAPACITY;
+      if (values && nb) memcpy((uint8_t*)values + vr * cr->es, cr->values.data() + v0 * cr->es, nb);
+    }
+    const uint64_t nlev = ndef > nrep ? ndef : nrep;
+    const uint64_t adv = nlev > nv ? nlev : nv;
+    if (adv == 0) {  // no progress: the reference's loop never ends
+      cr->err = "read_batch makes no progress (the reference loops forever)";
+      return PQG_ERR_HANG;
+    }
+    cr->dpos += ndef;
+    cr->rpos += nrep;
+    cr->vpos += nv;
+    cr->nd += adv;  // num_decoded_values (:259)
+    cr->V = cr->pV[cr->pg] + cr->vpos;
+    lr += nlev;
+    vr += nv;
+  }
+  *values_read = vr;
+  *levels_read = lr;
+  return PQG_OK;
+}
+
+// The original entry: every slice holds batch_size elements (values: batch_size values, their
+// bytes bounded by values_bytes_cap).
 int pqg_column_reader_read_batch(pqg_column_reader* cr, size_t batch_size, int16_t* def,
                                  int16_t* rep, void* values, uint64_t values_bytes_cap,
                                  uint32_t* lengths, size_t* values_read, size_t* levels_read) {
-  if (!cr || !values_read || !levels_read) return PQG_ERR_INVALID;
-  *values_read = *levels_read = 0;
-  const bool use_def = def && cr->col.max_def > 0;
-  const bool use_rep = rep && cr->col.max_rep > 0;
-  // The chunk was decoded with its def levels; reading an optional column without them would
-  // make the reference decode one value per level slot, which this reader does not replay.
-  if (cr->col.max_def > 0 && !def) return PQG_ERR_INVALID;
-  uint64_t left = cr->total_levels - cr->L;
-  uint64_t nlev = batch_size < left ? batch_size : left;
-  // The reference's loop (column/reader.rs:181-262) keeps reading while fewer than batch_size
-  // levels are in hand, so a call whose requested range reaches the failing page (or a failure
-  // after the last decoded page: has_next -> read_new_page fails) returns its error, whatever was
-  // read before it in that call; batch_size 0 never enters the loop (Ok((0, 0))).
-  if (cr->status != PQG_OK && batch_size && cr->L + batch_size > cr->bad_level) return cr->status;
-  if (nlev == 0) return PQG_OK;
-  uint64_t nval = nlev;
-  if (use_def) {
-    nval = 0;
-    const int16_t md = cr->col.max_def;
-    for (uint64_t i = 0; i < nlev; ++i) nval += cr->def[cr->L + i] == md;
-  }
-  if (cr->V + nval > cr->total_values) return PQG_ERR_GENERAL;  // inconsistent chunk
-  if (cr->is_ba) {
-    uint64_t b0 = (uint64_t)cr->offsets[cr->V], b1 = (uint64_t)cr->offsets[cr->V + nval];
-    if (b1 - b0 > values_bytes_cap) return PQG_ERR_CAPACITY;
-    if (values && b1 > b0) memcpy(values, cr->values.data() + b0, b1 - b0);
-    if (lengths)
-      for (uint64_t i = 0; i < nval; ++i)
-        lengths[i] = (uint32_t)(cr->offsets[cr->V + i + 1] - cr->offsets[cr->V + i]);
-  } else {
-    uint64_t nb = nval * (uint64_t)cr->es;
-    if (nb > values_bytes_cap) return PQG_ERR_CAPACITY;
-    if (values && nb) memcpy(values, cr->values.data() + cr->V * cr->es, nb);
-  }
-  if (use_def) memcpy(def, cr->def.data() + cr->L, nlev * 2);
-  if (use_rep) memcpy(rep, cr->rep.data() + cr->L, nlev * 2);
-  cr->L += nlev;
-  cr->V += nval;
-  *values_read = nval;
-  *levels_read = (use_def || use_rep) ? nlev : 0;
-  return PQG_OK;
+  return pqg_column_reader_read_batch_caps(cr, batch_size, def, batch_size, rep, batch_size, values,
+                                           batch_size, values_bytes_cap, lengths, values_read,
+                                           levels_read);
 }
 
 }  // extern "C"

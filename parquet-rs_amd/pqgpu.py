@@ -82,7 +82,7 @@ EXPORTS = [
     "pqg_file_close", "pqg_file_error", "pqg_file_num_rows", "pqg_file_num_row_groups",
     "pqg_file_num_columns", "pqg_file_column", "pqg_row_group_num_rows", "pqg_chunk_pages",
     "pqg_chunk_blob", "pqg_column_reader_open", "pqg_column_reader_close",
-    "pqg_column_reader_read_batch", "pqg_triplet_iter_open", "pqg_triplet_iter_close",
+    "pqg_column_reader_read_batch", "pqg_column_reader_read_batch_caps", "pqg_triplet_iter_open", "pqg_triplet_iter_close",
     "pqg_triplet_iter_read_next", "pqg_triplet_iter_has_next", "pqg_triplet_iter_def_level",
     "pqg_triplet_iter_rep_level", "pqg_triplet_iter_is_null", "pqg_triplet_iter_value",
     "pqg_space_values", "pqg_rg_ctx_create", "pqg_rg_ctx_destroy", "pqg_rg_decode", "pqg_rg_sync",
@@ -138,6 +138,9 @@ def lib():
         L.pqg_column_reader_close.restype = None
         L.pqg_column_reader_read_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, u64, vp,
                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        L.pqg_column_reader_read_batch_caps.argtypes = [vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp,
+                                                        C.c_size_t, u64, vp, C.POINTER(C.c_size_t),
+                                                        C.POINTER(C.c_size_t)]
         L.pqg_triplet_iter_open.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
         L.pqg_triplet_iter_close.argtypes = [vp]
         L.pqg_triplet_iter_read_next.argtypes = [vp, C.POINTER(C.c_int)]
@@ -626,22 +629,28 @@ class ColumnReader:
         except Exception:
             pass
 
-    def read_batch(self, batch_size, want_def=True, want_rep=True):
+    def read_batch(self, batch_size, want_def=True, want_rep=True, def_cap=None, rep_cap=None,
+                   values_cap=None):
         """Returns (values, def, rep, values_read, levels_read). For BYTE_ARRAY/FLBA values
-        is a list of bytes objects; otherwise a numpy array in the reference layout."""
+        is a list of bytes objects; otherwise a numpy array in the reference layout. The caps are
+        the lengths of the reference's def / rep / values slices (default batch_size each,
+        column/reader.rs:170-205); want_def / want_rep False pass None for that slice."""
         t = self.col.physical_type
         es = VALUE_SIZE.get(t, 0)
         ba = t in (BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY)
-        d = np.zeros(batch_size, np.int16) if want_def and self.col.max_def > 0 else None
-        r = np.zeros(batch_size, np.int16) if want_rep and self.col.max_rep > 0 else None
-        cap = batch_size * es if not ba else 1 << 16
+        dcap = batch_size if def_cap is None else def_cap
+        rcap = batch_size if rep_cap is None else rep_cap
+        vcap = batch_size if values_cap is None else values_cap
+        d = np.zeros(max(dcap, 1), np.int16) if want_def else None
+        r = np.zeros(max(rcap, 1), np.int16) if want_rep else None
+        cap = vcap * es if not ba else 1 << 16
         while True:
             vals = np.zeros(max(cap, 1), np.uint8)
-            lens = np.zeros(max(batch_size, 1), np.uint32) if ba else None
+            lens = np.zeros(max(vcap, 1), np.uint32) if ba else None
             vr, lr = C.c_size_t(), C.c_size_t()
-            st = lib().pqg_column_reader_read_batch(
-                self.h, batch_size, d.ctypes.data if d is not None else None,
-                r.ctypes.data if r is not None else None, vals.ctypes.data, cap,
+            st = lib().pqg_column_reader_read_batch_caps(
+                self.h, batch_size, d.ctypes.data if d is not None else None, dcap,
+                r.ctypes.data if r is not None else None, rcap, vals.ctypes.data, vcap, cap,
                 lens.ctypes.data if lens is not None else None, C.byref(vr), C.byref(lr))
             if st == CAPACITY and ba:
                 cap *= 4
@@ -659,8 +668,8 @@ class ColumnReader:
         else:
             raw = vals[: nv * es]
             values = raw.reshape(-1, 12) if t == INT96 else raw.view(NP_DTYPE[t])
-        return (values, d[:nl] if d is not None else None, r[:nl] if r is not None else None,
-                nv, nl)
+        return (values, d[:nl] if d is not None and self.col.max_def > 0 else None,
+                r[:nl] if r is not None and self.col.max_rep > 0 else None, nv, nl)
 
 
 class TripletIter:
