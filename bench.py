@@ -74,8 +74,8 @@ def parse(argv=None):
                     help="alltypes: row groups per GPU (11 x 2^23 rows ~ 8 GiB decoded: 1/8 of config 5)")
     ap.add_argument("--rg-rows", type=int, default=1 << 23, help="alltypes: rows per row group")
     ap.add_argument("--at-p-null", type=float, default=0.05, help="alltypes: null fraction per column")
-    ap.add_argument("--streams", type=int, default=16,
-                    help="alltypes: HIP streams the row-group decoder spreads the column chunks over")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="alltypes: pqg_rg_ctx_create's reserved nstreams (1..16, ignored by the library)")
     ap.add_argument("--at-batch", default="step", choices=["step", "rg"],
                     help="alltypes: one pqg_decode_chunks over every chunk of the step (step) or one "
                          "pqg_rg_decode per row group on two alternating streams (rg)")

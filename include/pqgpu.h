@@ -204,8 +204,9 @@ int pqg_ctx_last_paths(pqg_ctx *ctx, uint32_t *mask);
  * The column chunks of one row group decoded together. The reference reads every column chunk
  * of a row group through its own page reader and column reader (file/reader.rs:252-260,
  * 306-330); they share nothing, so pqg_rg_decode is one pqg_decode_chunks of them on `stream`
- * (two row groups may be in flight: the ctx has two staging slots; `nstreams` is accepted for
- * compatibility, 1..16). pages[j] / npages[j] / outs[j] are column j's arguments of
+ * (two row groups may be in flight: the ctx has two staging slots). `nstreams` is reserved: it
+ * must be 1..16 (PQG_ERR_INVALID otherwise) and is otherwise ignored -- every decode runs on the
+ * caller's stream, one batched launch sequence for all columns. pages[j] / npages[j] / outs[j] are column j's arguments of
  * pqg_decode_chunk, all pages in the one device blob. Asynchronous: pqg_rg_sync waits and fills
  * every outs[j]; it returns the first failing column's status (lowest index) and names that
  * column and its page. pages and outs (the arrays and the structs) must stay valid until that

@@ -334,6 +334,14 @@ __device__ inline bool lv_nodict(const PageWork* pages, const ChunkWork& ck, int
   return sel == SS_DICT && !dict_usable(pages, ck);
 }
 
+// Dense def / rep streams of bit width 1 (int16 outputs) take the chunk walks of pqg_lvd1.hpp.
+#ifndef PQG_D1
+#define PQG_D1 1
+#endif
+__device__ inline bool lv_d1_page(const LevelTables& lt, int p, const Stream& s, int sel) {
+  return PQG_D1 && lt.dense[p] && s.w == 1 && (sel == SS_DEF || sel == SS_REP) && s.n && s.slen;
+}
+
 __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
                                                 const ChunkWork* chunks, int sel, RunTables rt, LevelTables lt) {
   // one thread per page: flag, window and segment counts (into wbase / sbase, scanned in place
@@ -350,7 +358,10 @@ __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob
         flag = PF_PAGE;
         nw = s.n ? (s.slen + LV_WIN - 1) / LV_WIN : 0u;
         if (sel == SS_DEF) pages[p].nonnull = 0;
-        if (!lt.dense[p] && s.n && s.slen) {
+        if (lv_d1_page(lt, p, s, sel)) {  // dense one-bit levels: the chunk walks (pqg_lvd1.hpp)
+          flag = PF_D1;
+          ns = (s.slen + LW_SEGW * LV_WIN - 1) / (LW_SEGW * LV_WIN);
+        } else if (!lt.dense[p] && s.n && s.slen) {
           const uint32_t sw = lw_segw((uint32_t)s.w);
           ns = ((s.slen + LV_WIN - 1) / LV_WIN + sw - 1) / sw;
         }
@@ -3029,6 +3040,8 @@ __global__ void __launch_bounds__(WG) k_lv_emit_walk(const uint8_t* __restrict__
 #undef LW_STAMP
 }
 
+#include "pqg_lvd1.hpp"
+
 // Plan, segment starts and walks, page scan, run compaction: every page of stream `sel` ends
 // walked (PF_WALK, its run list built), dense (PF_PAGE) or handed back (PF_BAIL).
 static void lv_front(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, const ChunkWork* chunks,
@@ -3076,6 +3089,7 @@ hipError_t pqg_launch_lv(const uint8_t* blob, uint64_t blob_len, PageWork* pages
     return hipGetLastError();
   }
   // (k_lv_plan2's scan ran in k_lv_segscan's last workgroup)
+  if (PQG_D1 && (sel == SS_DEF || sel == SS_REP) && (widths & 2u)) lv_launch_d1(blob, blob_len, pages, npages, chunks, sel, rt, lt, s);
 // window table and window emit kernels on 4x grids (round 5, kernel times: config 5 k_lv_win
 // 0.286 -> 0.267 ms, k_lv_emit 0.536 -> 0.515; config 2 at p_null 0.1 0.401 -> 0.386 and 0.698 ->
 // 0.679; 2x about half of that)

@@ -703,7 +703,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     p0 += n;
   }
 #ifdef PQG_DIAG
-  if (dbg_env & (16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096)) {
+  if (dbg_env & (16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | 8192)) {
     size_t need = (size_t)(total_tiles * 4 > (uint64_t)np * 2 ? total_tiles * 4 : (uint64_t)np * 2) * 16;
     if (need < (size_t)np * 64) need = (size_t)np * 64;
     if (dbg_env & 128) need = (size_t)(nwin / LW_SEGW + np + 1) * 32;  // per level-stream segment
@@ -711,6 +711,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     if (dbg_env & 1024) need = (size_t)2048 * 64 * 4 * 32;                // per wave of k_lv_emit_walk
     if (dbg_env & 2048) need = (size_t)2048 * 64 * 4 * 32;                // per wave of k_lv_win
     if (dbg_env & 4096) need = (size_t)(total_tiles / 8 + 64) * 64;       // per workgroup of k_dict_win
+    if (dbg_env & 8192) need = (size_t)2 * 2048 * 64;                    // per workgroup of k_d1_tab / k_d1_emit
     if (dbg_env & 512) need = (size_t)np * 20 + 64;  // per page: its hand-back site, then the failing window
     if (need > ctx->dbg_cap) {
       hipFree(ctx->dbgbuf);
@@ -725,7 +726,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       HIPCHK(hipMemsetAsync(sl.bail, 0, (size_t)np * 20, s), "memset bail sites");
     }
     if (dbg_env & (1024 | 2048)) HIPCHK(hipMemsetAsync(ctx->dbgbuf, 0, (size_t)2048 * 64 * 64, s), "memset stamps");
-    if (dbg_env & 4096) HIPCHK(hipMemsetAsync(ctx->dbgbuf, 0, need, s), "memset stamps");
+    if (dbg_env & (4096 | 8192)) HIPCHK(hipMemsetAsync(ctx->dbgbuf, 0, need, s), "memset stamps");
     for (ChunkWork& c : cw) c.cp.dbgbuf = ctx->dbgbuf;
   }
 #endif

@@ -22,6 +22,7 @@ struct pqg_rg_ctx {
 
 extern "C" {
 
+// nstreams is reserved (pqgpu.h): validated, then unused -- the batched decode runs on the caller's stream.
 int pqg_rg_ctx_create(int device, int nstreams, pqg_rg_ctx** out) {
   if (!out || nstreams < 1 || nstreams > 16) return PQG_ERR_INVALID;
   *out = nullptr;

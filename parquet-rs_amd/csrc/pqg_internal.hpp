@@ -215,10 +215,10 @@ struct LevelTables {
 };
 
 // RunTables::pflag values: stream decoded by the level path (pqg_levels.hip) — by its window
-// kernels (PF_PAGE) or after its page walker (PF_WALK) — or handed back by it to the general
-// hybrid decoder (pqg_runs.hpp, PF_BAIL)
-constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u, PF_WALK = 3u;
-__host__ __device__ inline bool pf_level_path(uint32_t f) { return f == PF_PAGE || f == PF_WALK; }
+// kernels (PF_PAGE), after its page walker (PF_WALK) or, dense one-bit levels, by its chunk walks
+// (pqg_lvd1.hpp, PF_D1) — or handed back by it to the general hybrid decoder (pqg_runs.hpp, PF_BAIL)
+constexpr uint32_t PF_PAGE = 1u, PF_BAIL = 2u, PF_WALK = 3u, PF_D1 = 4u;
+__host__ __device__ inline bool pf_level_path(uint32_t f) { return f == PF_PAGE || f == PF_WALK || f == PF_D1; }
 
 struct ColumnParams {
   int32_t physical_type;

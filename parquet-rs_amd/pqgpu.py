@@ -271,10 +271,10 @@ class Context:
 
 
 class RowGroupDecoder:
-    """pqg_rg_ctx: the column chunks of a row group decoded concurrently on `nstreams` HIP
-    streams, one decode context per column (pqgpu.h, file/reader.rs:252-260)."""
+    """pqg_rg_ctx: the column chunks of a row group decoded together by one batched decode on the
+    caller's stream (pqgpu.h, file/reader.rs:252-260). `nstreams` is reserved (1..16, ignored)."""
 
-    def __init__(self, device=0, nstreams=4):
+    def __init__(self, device=0, nstreams=1):
         self.device = device
         h = C.c_void_p()
         st = lib().pqg_rg_ctx_create(device, nstreams, C.byref(h))

@@ -250,8 +250,8 @@ def test_segment_without_exit(oracle, ctx):
 
 def test_alltypes_row_group_full_size():
     """One config-5 row group at the bench's size (2^23 rows, p_null 0.05, the reference writer's
-    defaults: each dictionary column a single 8 M-value page) through pqg_rg_decode over 16 streams,
-    every column (levels, values, BYTE_ARRAY offsets) against the generator's cells."""
+    defaults: each dictionary column a single 8 M-value page) through pqg_rg_decode (one batched
+    decode of the 11 chunks on the caller's stream), every column (levels, values, BYTE_ARRAY offsets) against the generator's cells."""
     import torch
 
     import pqgpu
