@@ -377,7 +377,7 @@ def pcie_inclusive(ctx, w, stream, iters=3):
             "note": "pinned H2D of page bytes + decode + D2H of decoded levels/values, best of %d" % iters}
 
 
-LEVEL_PATH = ("k_lv_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
+LEVEL_PATH = ("k_lv_", "k_d1_", "k_run_index", "k_tile_desc", "k_texpand_levels", "k_page_counts")
 DELTA_STAGE = ("k_delta_",)  # k_delta_page, the tiled path's kernels
 # the dictionary values: tile descriptors, the tile expand (16-bit indices kept, or gathered from
 # L2) and the windowed gather (k_dict_win)
@@ -389,7 +389,7 @@ def pmc_traffic(kind, kernel, variant=None):
     (profiles/<round>/<config>[_<variant>]/kernels.json, written by tools/pmc_traffic.py:
     FETCH_SIZE x2 + WRITE_SIZE, the MI355X_MICROARCH.md gfx950 corrections). The def-level path
     is a chain of kernels timed as one (HIP events around pqg_launch_levels): its traffic is their
-    sum (every kernel of the chain runs once per decode). None when not profiled."""
+    sum per step (each kernel's per-launch bytes x its launches per step). None when not profiled."""
     base = kernel.split("<")[0]
     sub = kind if variant is None else f"{kind}_{variant}"
     for rnd in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True):
@@ -401,14 +401,21 @@ def pmc_traffic(kind, kernel, variant=None):
         except (OSError, ValueError, KeyError):
             continue
         names = {k.replace("pqg::", ""): e for k, e in ks.items() if "traffic_bytes" in e}
-        if kernel == "whole step":  # config 5: every decode kernel of the step (each launched once)
-            tot = [e["traffic_bytes"] for k, e in ks.items() if k.startswith("pqg::") and "traffic_bytes" in e]
+        # per step: a kernel launched more than once per step (config 5 runs the level-path chain
+        # for its def streams twice) weighs calls / steps, steps = the fewest calls of a decode kernel
+        steps = min([e.get("calls", 1) for k, e in ks.items() if k.startswith("pqg::")] or [1])
+
+        def per_step(e):
+            return e["traffic_bytes"] * max(e.get("calls", steps), 1) / max(steps, 1)
+
+        if kernel == "whole step":  # config 5: every decode kernel of the step
+            tot = [per_step(e) for k, e in ks.items() if k.startswith("pqg::") and "traffic_bytes" in e]
             if tot:
                 return sum(tot), os.path.relpath(path, ROOT)
             continue
         if kernel in ("level path", "DELTA stage", "dictionary stage"):  # kernels timed as one: their sum
             pre = {"level path": LEVEL_PATH, "DELTA stage": DELTA_STAGE, "dictionary stage": DICT_STAGE}[kernel]
-            tot = [e["traffic_bytes"] for k, e in names.items() if k.startswith(pre)]
+            tot = [per_step(e) for k, e in names.items() if k.startswith(pre)]
             if tot:
                 return sum(tot), os.path.relpath(path, ROOT)
             continue
@@ -436,8 +443,9 @@ def roofline(name, ms, nbytes, traffic, traffic_src, note=None):
 
 
 LEVEL_NOTE = ("HIP events around pqg_launch_levels: the def-level kernel chain (k_lv_plan, k_lv_bound, "
-              "k_lv_segwalk, k_lv_segscan, k_lv_compact, k_lv_win, k_lv_stitch, k_lv_emit, k_lv_emit_walk, "
-              "k_lv_fallback + the fused value-offset scan), one launch each per step; traffic = their PMC sum")
+              "k_lv_segwalk, k_lv_segscan, k_lv_compact, the dense one-bit pages' k_d1_tab, k_d1_stitch, k_d1_emit, "
+              "the window path's k_lv_win, k_lv_stitch, k_lv_emit, k_lv_emit_walk, k_lv_fallback + the fused "
+              "value-offset scan), one launch each per step; traffic = their PMC sum")
 
 
 def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, steps=None, warmup=None,

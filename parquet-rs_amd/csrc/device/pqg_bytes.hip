@@ -533,10 +533,14 @@ static_assert(BA_T == RUN_TILE, "byte-array tiles are the page table's tiles");
 
 // (a dictionary page's data pages: only with a usable dictionary, dict_usable, as their index
 // producers take them)
-__device__ inline bool ba_page_ok(const PageWork* pages, const PageWork& pw, const ChunkWork& ck) {
+// ba_page_pre: the checks that do not need the chunk's byte total (k_ba_tsum runs before
+// k_scan_bytes sets it); ba_page_ok adds the capacity check for the kernels after the scan.
+__device__ inline bool ba_page_pre(const PageWork* pages, const PageWork& pw, const ChunkWork& ck) {
   return pw.status == 0 && (pw.page_type == P_DATA || pw.page_type == P_DATA_V2) && ck.es == 0 && ck.val_out &&
-         pw.encoding != E_DELTA_BYTE_ARRAY && ck.res.total_bytes <= ck.val_cap &&
-         (pw.encoding != E_RLE_DICTIONARY || dict_usable(pages, ck));
+         pw.encoding != E_DELTA_BYTE_ARRAY && (pw.encoding != E_RLE_DICTIONARY || dict_usable(pages, ck));
+}
+__device__ inline bool ba_page_ok(const PageWork* pages, const PageWork& pw, const ChunkWork& ck) {
+  return ba_page_pre(pages, pw, ck) && ck.res.total_bytes <= ck.val_cap;
 }
 
 // Value k of a byte-array page (k: its index among the chunk's values): source address and length.
@@ -608,7 +612,7 @@ __global__ void __launch_bounds__(WG) k_ba_tsum(PageWork* pages, const ChunkWork
       cur = p;
       const PageWork pw = pages[p];
       const ChunkWork& ck = chunks[pw.chunk];
-      ok = ba_page_ok(pages, pw, ck);
+      ok = ba_page_pre(pages, pw, ck);  // (before the scan: no byte total yet)
       if (ok) {
         bs = BaSrc(ck, pw, pages, vsrc0, vlen0, dsrc0, dlen0);
         n = pw.nonnull;

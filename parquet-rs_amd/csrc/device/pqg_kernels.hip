@@ -377,24 +377,35 @@ __device__ inline bool df_easy(const QDesc& d) {
   return d.S + d.bhi - A0 <= (uint64_t)DF_PAY;
 }
 
-// The list's other tiles: index expand into their slots. A workgroup takes 256 entries of the
-// list, checks them all at once and expands the few k_dict_win does not decode itself (none at
-// the benchmark's shape).
-__global__ void __launch_bounds__(WG) k_texpand_didx(const uint8_t* __restrict__ blob, uint64_t blob_len,
-                                                     const uint32_t* __restrict__ tl, uint32_t ntl, PageWork* pages,
-                                                     ChunkWork* chunks, RunTables rt, uint16_t* idx) {
-  __shared__ TileSmem sm;
-  __shared__ uint32_t hard[WG];
-  __shared__ uint32_t nhard;
+// The list's tiles k_dict_win does not decode itself (none at the benchmark's shape), appended
+// to a compact list: *cnt entries of the list from hl (one thread per list entry, one atomic per
+// wave).
+__global__ void __launch_bounds__(WG) k_didx_mark(const uint32_t* __restrict__ tl, uint32_t ntl, RunTables rt,
+                                                  uint32_t* cnt, uint32_t* hl) {
   if (*rt.nfall == 0) return;
-  if (threadIdx.x == 0) nhard = 0;
-  __syncthreads();
-  const uint32_t p0 = blockIdx.x * WG, pi = p0 + threadIdx.x;
-  if (pi < ntl && !df_easy(rt.desc[tl[pi]])) hard[atomicAdd(&nhard, 1u)] = pi;
-  __syncthreads();
-  const uint32_t nh = nhard;
-  for (uint32_t k = 0; k < nh; ++k) {
-    const uint32_t p = hard[k];
+  const uint32_t pi = blockIdx.x * WG + threadIdx.x, lane = threadIdx.x & (WAVE - 1);
+  const bool h = pi < ntl && !df_easy(rt.desc[tl[pi]]);
+  const uint64_t m = __ballot(h);
+  if (!m) return;
+  const int first = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if ((int)lane == first) base = atomicAdd(cnt, (uint32_t)__builtin_popcountll(m));
+  base = __shfl(base, first);
+  if (h) hl[base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = pi;
+}
+
+// Index expand of the marked tiles into their slots: the grid strides over the compact list, one
+// tile per workgroup at a time, so a list of many hard tiles (short runs: sorted or low-cardinality
+// data) is spread over the whole grid.
+__global__ void __launch_bounds__(WG) k_texpand_didx(const uint8_t* __restrict__ blob, uint64_t blob_len,
+                                                     const uint32_t* __restrict__ tl, PageWork* pages,
+                                                     ChunkWork* chunks, RunTables rt, const uint32_t* cnt,
+                                                     const uint32_t* hl, uint16_t* idx) {
+  __shared__ TileSmem sm;
+  if (*rt.nfall == 0) return;
+  const uint32_t nh = *cnt;
+  for (uint32_t k = blockIdx.x; k < nh; k += gridDim.x) {
+    const uint32_t p = hl[k];
     DictIdxMaker mk{pages, chunks, idx, p};
     tile_one(blob, blob_len, rt.desc, tl[p], rt.runs, sm, mk);
     __syncthreads();
@@ -629,7 +640,11 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       }
       // every wave's LDS-DMA fill must have landed before any wave reads the window: each wave
       // waits for its own (vmcnt(0), explicit: the barrier alone does not promise it), then the
-      // barrier orders the waves
+      // barrier orders the waves. 0x0F70 is vmcnt(0) in the gfx9 (gfx950) encoding; the guard
+      // below fails the build for a target whose encoding differs
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "k_dict_win: the s_waitcnt immediate 0x0F70 (vmcnt(0)) is the gfx9 encoding"
+#endif
       __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();
       DW_STAMP(3)
@@ -1056,11 +1071,16 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
     if (ntl[3]) hipLaunchKernelGGL((k_texpand_dict<12>), dim3(ntl[3]), dim3(WG), 0, s, blob, blob_len, tl[3], pages, chunks, rt);
     // windowed gathers (wl[0] / wl[1]: tiles of 4- / 8-byte values, slots of didx in that order)
     uint16_t* slot = didx;
+    if (wn[0] + wn[1]) (void)hipMemsetAsync(rt.hard, 0, 2 * sizeof(uint32_t), s);
+    uint32_t* hl = rt.hard + 2;
     for (int k = 0; k < 2; ++k) {
       if (!wn[k]) continue;
-      // the tiles k_dict_win does not decode itself (none at the benchmark's shape), 256 list entries per workgroup
-      hipLaunchKernelGGL(k_texpand_didx, dim3((wn[k] + WG - 1) / WG), dim3(WG), 0, s, blob, blob_len, wl[k], wn[k],
-                         pages, chunks, rt, slot);
+      // the tiles k_dict_win does not decode itself (none at the benchmark's shape): marked, then
+      // expanded by a grid striding over them
+      hipLaunchKernelGGL(k_didx_mark, dim3((wn[k] + WG - 1) / WG), dim3(WG), 0, s, wl[k], wn[k], rt, rt.hard + k, hl);
+      hipLaunchKernelGGL(k_texpand_didx, dim3(wn[k] < 1024u ? wn[k] : 1024u), dim3(WG), 0, s, blob, blob_len, wl[k],
+                         pages, chunks, rt, rt.hard + k, hl, slot);
+      hl += wn[k];
       const dim3 g((wn[k] + DW_TPW - 1) / DW_TPW);
       if (k == 0)
         hipLaunchKernelGGL((k_dict_win<4>), g, dim3(DW_NT), 0, s, blob, blob_len, wl[k], wn[k], pages, chunks, rt, slot);

@@ -294,6 +294,7 @@ static void free_run_tables(RunTables& r) {
   hipFree(r.qcount);
   hipFree(r.pflag);
   hipFree(r.nfall);
+  hipFree(r.hard);
   r = RunTables{};
 }
 
@@ -823,6 +824,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     if (e == hipSuccess) e = hipMalloc(&r.desc, sl.tcap * 4 * sizeof(QDesc));
     if (e == hipSuccess) e = hipMalloc(&r.qcount, sl.tcap * 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&r.nfall, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&r.hard, (sl.tcap + 2) * sizeof(uint32_t));
     return e;
   };
   if ((size_t)np > sl.pfcap) {  // page-pass flags, sized by pages

@@ -136,6 +136,7 @@ struct RunTables {
   uint32_t* qcount; // [tiles * 4] per quarter-tile counts (def levels == max_def; byte totals)
   uint32_t* pflag;  // [pages] PF_PAGE: stream decoded by the level path (pqg_levels.hip)
   uint32_t* nfall;  // streams the level path left to the tiled path (0: its kernels exit at once)
+  uint32_t* hard;   // [2 + tiles]: windowed-gather tiles k_dict_win leaves to k_texpand_didx (counts, lists)
 };
 
 // DELTA_BINARY_PACKED index-pass outputs (device/pqg_delta.hip). Tiles of DELTA_TILE values

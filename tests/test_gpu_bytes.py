@@ -181,6 +181,22 @@ def test_delta_byte_array_long_values(oracle, ctx):
     assert [got["bytes"][offs[i]:offs[i + 1]] for i in range(len(vals))] == vals
 
 
+def test_delta_byte_array_many_long_slices(oracle, ctx):
+    """More long slices in one 4096-value tile than k_dba_copy queues (DBA_QCAP = 512 slices over
+    DBA_LONG = 256 bytes; past that its per-lane copy): 600 values of ~1.1 KiB, each the previous
+    value's first 400 bytes (one 400-byte slice back to value 0) and a fresh 700-byte suffix, so
+    1200 long slices."""
+    rng = np.random.default_rng(63)
+    vals = [bytes(rng.integers(0, 256, 1100, dtype=np.uint8))]
+    for _ in range(599):
+        vals.append(vals[-1][:400] + bytes(rng.integers(0, 256, 700, dtype=np.uint8)))
+    pages = [oracle.PageSpec(oracle.PAGE_DATA, oracle.delta_byte_array_encode(vals), len(vals),
+                             oracle.DELTA_BYTE_ARRAY)]
+    got, _ = check(oracle, ctx, oracle.BYTE_ARRAY, pages)
+    offs = got["offsets"]
+    assert [got["bytes"][offs[i]:offs[i + 1]] for i in range(len(vals))] == vals
+
+
 def _prefix_chain_values(n):
     """Value i = 'a' * (i % 3000 + 1) and similar: prefix lengths rising by one, so every byte
     of a value comes from a different earlier suffix (chains as long as the values)."""

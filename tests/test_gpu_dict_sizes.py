@@ -1,10 +1,9 @@
 """RLE_DICTIONARY chunks of 4- and 8-byte values whose dictionary is larger than the level path's
-(2^8 entries): the general path (the index pass, then k_texpand_dict's gather served from L2).
-Values must be the oracle's (get_batch_with_dict, rle.rs:437-487; DictDecoder,
-decoding.rs:282-315) for dictionaries of 300 to 65536 entries at any byte alignment inside the
-blob, for chunks of several dictionaries in one batch, and an index past the dictionary is the
-reference's panic. (A design that streamed the dictionary through LDS windows was measured and
-not kept: DESIGN.md, config 3.)"""
+(2^8 entries): the windowed gather (indices to a buffer or decoded in the gather kernel, then the
+dictionary streamed through 128 KiB LDS windows: k_dict_win). Values must be the oracle's
+(get_batch_with_dict, rle.rs:437-487; DictDecoder, decoding.rs:282-315) for dictionaries of 257 to
+65536 entries at any byte alignment inside the blob, for chunks of several dictionaries in one
+batch, for tiles of many short runs, and an index past the dictionary is the reference's panic."""
 import numpy as np
 import pytest
 
@@ -120,4 +119,35 @@ def test_dictionary_index_runs(oracle, ctx, ptype, mean_run):
         lv[rng.random(n) < 0.1] = 0
         body = bytes([bw]) + oracle.rle_encode(idx[:int(lv.sum())].astype(np.uint64), bw)
         pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(lv, 1) + body, n, oracle.RLE_DICTIONARY))
+    _same(oracle, ctx, t, pages)
+
+
+@pytest.mark.parametrize("nd", [257, 4097, 65536])
+@pytest.mark.parametrize("ptype", ["INT32", "INT64"])
+def test_dictionary_hard_tiles_mixed(oracle, ctx, ptype, nd):
+    """Windowed-gather tiles that k_dict_win does not decode itself -- 4096-index tiles of short
+    RLE runs (each index repeated 9..12 times: ~380 run records, more than DF_RC = 128) -- beside
+    easy tiles of random indices, alternating along one long page and a ragged second: 320 hard
+    tiles, more than one k_didx_mark workgroup's 256 list entries, expanded by k_texpand_didx's
+    grid-strided list, then gathered with their easy neighbours by one k_dict_win
+    workgroup. Values against the oracle (get_batch_with_dict, rle.rs:437-487)."""
+    rng = np.random.default_rng(nd + 7 * len(ptype))
+    t = getattr(oracle, ptype)
+    dv = _dvals(rng, t, oracle, nd)
+    d = oracle.PageSpec(oracle.PAGE_DICTIONARY, oracle.plain_encode(t, dv), nd, oracle.PLAIN_DICTIONARY)
+    bw = max(1, int(np.ceil(np.log2(nd))))
+    pages = [d]
+    for ntiles in (640, 37):
+        parts = []
+        for k in range(ntiles):
+            if k % 2 == 0:
+                lens = rng.integers(9, 13, 500)
+                parts.append(np.repeat(rng.integers(0, nd, 500), lens)[:4096])
+            else:
+                parts.append(rng.integers(0, nd, 4096))
+        idx = np.concatenate(parts)[:ntiles * 4096 - 1000]
+        n = len(idx)
+        body = bytes([bw]) + oracle.rle_encode(idx.astype(np.uint64), bw)
+        pages.append(oracle.PageSpec(oracle.PAGE_DATA, oracle.level_encode(np.ones(n, np.int16), 1) + body, n,
+                                     oracle.RLE_DICTIONARY))
     _same(oracle, ctx, t, pages)
