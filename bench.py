@@ -484,7 +484,11 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
         r["read_bytes_per_launch"] = nin
         r["read_gbs"] = nin / (ms * 1e-3) / 1e9 if ms else None  # In / time
         rl.append(r)
+    # the dominant kernel by time; for the nullable level variants (p_null > 0) the level path, the
+    # decode those variants exist to measure (the PLAIN copy beside it is the same memcpy at every p_null)
     dom = max(rl, key=lambda r: r["avg_ms"] or 0)
+    if kind == "levels" and p_null:
+        dom = rl[0]
     # the stream each rank decodes: its own (weak) or its page range of the shared one (strong)
     job_units = (w.n if strong else units * world)
     res = {
@@ -510,6 +514,10 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
                                    if strong else f"row-group partitions x{world}, no collective")},
         "roofline": dom,
         "roofline_stages": rl if len(rl) > 1 else None,
+        # the whole step beside the dominant kernel: every algorithmic byte of the step / ms_per_step
+        "roofline_whole_step": {"bound": "hbm", "achieved": step_bytes / per_step / 1e9, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": step_bytes / per_step / 1e9 / HBM_PEAK_GBS,
+                                "bytes_per_step": step_bytes},
         "stages_note": ("stage and kernel times from HIP events with the stages one after the other "
                         "(pqg_ctx_set_overlap 0); ms_per_step is the production path, PLAIN copy beside "
                         "the level decode" if kind == "levels" and args.overlap else None),
@@ -940,7 +948,8 @@ def main(argv=None):
                 "encoded_mb_per_s": r["encoded_mb_per_s"], "values_per_gpu": r["config"]["values_per_gpu"],
                 "config": {k: r["config"][k] for k in ("block_size", "mini_blocks", "values_per_mini_block",
                                                        "pages_per_gpu", "parallelism") if k in r["config"]},
-                "roofline": r["roofline"], "roofline_stages": r["roofline_stages"], "stages_ms": r["stages_ms"],
+                "roofline": r["roofline"], "roofline_stages": r["roofline_stages"],
+                "roofline_whole_step": r["roofline_whole_step"], "stages_ms": r["stages_ms"],
                 "value_check": r["value_check"]}
 
     for kind in kinds:

@@ -359,22 +359,25 @@ struct DictIdxMaker {
   }
 };
 
-// Tiles k_dict_win decodes itself (its stage region takes the tile's run records and payload).
-// The others -- more run records than DF_RC, or than the index pass keeps (re-walk), or a
-// payload past DF_PAY -- have their indices kept in the tile's slot by k_texpand_didx first.
-constexpr uint32_t DF_TB = 16384;                  // LDS bytes per tile region (8 tiles: the window)
-constexpr uint32_t DF_RC = 128;                    // run records per tile
-constexpr uint32_t DF_POFF = (DF_RC + 2) * 8;      // payload offset in the region (start[], info[] first)
-constexpr uint32_t DF_BLK = DF_TB - 512;           // per 256-output block of the tile: its first two runs
-constexpr uint32_t DF_PAY = DF_BLK - DF_POFF - 16;  // staged payload bytes at most
-static_assert(DF_POFF % 16 == 0, "16-byte payload chunks");
+// Tiles k_dict_win decodes itself (their run records fit its record region). The others -- more
+// run records than DF_RC, or than the index pass keeps (re-walk), or stream offsets past 2^28
+// bytes -- have their indices kept in the tile's slot by k_texpand_didx first.
+constexpr uint32_t DF_RC = 128;                      // run records per tile
+constexpr uint32_t DF_TR = 2 * (DF_RC + 2) + 64 + 32;  // record region words: starts, info, blk, blk2
 static_assert(DF_RC <= 128, "one record per thread of a tile");
+static_assert(DF_TR % 4 == 0 && (2 * (DF_RC + 2)) % 4 == 0, "16-byte block descriptors");
 
 __device__ inline bool df_easy(const QDesc& d) {
-  if (!d.qhi || d.rec == RUN_REWALK || tx_wide(d) || tx_nrec(d) > DF_RC) return false;
-  if (!d.bhi) return true;  // RLE runs only
-  const uint64_t A0 = (d.S + d.blo) & ~15ull;
-  return d.S + d.bhi - A0 <= (uint64_t)DF_PAY;
+  return d.qhi && d.rec != RUN_REWALK && !tx_wide(d) && tx_nrec(d) <= DF_RC;
+}
+
+// A payload word (4-aligned offset a of n readable bytes; bytes past them read as zero).
+__device__ __forceinline__ uint32_t dw_word(const uint8_t* p, uint64_t n, uint64_t a) {
+  if (a + 4 <= n) return *reinterpret_cast<const uint32_t*>(p + a);
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < 4; ++k)
+    if (a + k < n) v |= (uint32_t)p[a + k] << (8 * k);
+  return v;
 }
 
 // The list's tiles k_dict_win does not decode itself (none at the benchmark's shape), appended
@@ -427,6 +430,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   using T = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
   constexpr uint32_t WIN = DW_BYTES / ES;  // entries per window
   __shared__ uint4 win[DW_CH + 1];         // (+1: the unaligned reads' third word)
+  __shared__ uint4 trec[DW_TPW][DF_TR / 4];  // per tile: run records and block descriptors
   __shared__ int32_t dkey[DW_TPW];
   if (*rt.nfall == 0) return;
   const uint32_t tid = threadIdx.x, q = tid >> 7, lt = tid & 127u;
@@ -464,13 +468,16 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   const int32_t rem = (int32_t)(qhi - qlo) - (int32_t)(2u * lt);
   uint32_t ix[16];
   const bool easy = df_easy(d);
-  // ---- an easy tile's indices are decoded here (rle.rs:437-487): its run records and payload go
-  // to the tile's region of the window, then each thread takes its 32 indices from the LDS copy
-  uint8_t* R = reinterpret_cast<uint8_t*>(win) + q * DF_TB;
-  uint32_t* rs = reinterpret_cast<uint32_t*>(R);  // run starts (page-relative outputs)
-  uint32_t* ri = rs + DF_RC + 2;                  // run info (payload offset, or R_RLE | value)
+  // ---- an easy tile's indices are decoded here (rle.rs:437-487): its run records go to the
+  // tile's record region in LDS; each thread then loads its pairs' payload words straight from
+  // the stream (a pair is 2w <= 32 bits: a wave's lanes read consecutive words), issued while the
+  // first window's LDS-DMA fill is in flight. Bit offsets count from A0 (the payload's first byte,
+  // aligned down to 16).
+  uint32_t* rs = reinterpret_cast<uint32_t*>(trec[q]);  // run starts (page-relative outputs)
+  uint32_t* ri = rs + DF_RC + 2;                        // run info (payload offset, or R_RLE | value)
   const uint32_t nr = tx_nrec(d);
-  uint32_t sb32 = 0;
+  const uint64_t A0 = ((d.bhi ? d.S + d.blo : d.S) & ~15ull);
+  const uint32_t sb32 = (uint32_t)(A0 - d.S);
   if (easy) {
     if (d.kind == LK_BIT_PACKED) {  // one header-less run from output 0
       if (lt == 0) {
@@ -483,36 +490,15 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       ri[lt] = r.y;
     }
     if (lt == 0) rs[nr] = rs[nr + 1] = qhi;
-    uint32_t nch = 0;
-    if (d.bhi) {
-      const uint64_t A0 = (d.S + d.blo) & ~15ull;
-      nch = (uint32_t)((d.S + d.bhi - A0 + 15) / 16);
-      sb32 = (uint32_t)(A0 - d.S);
-      const bool fast = A0 + (uint64_t)nch * 16 <= blob_len;
-      uint4* P = reinterpret_cast<uint4*>(R + DF_POFF);
-      constexpr uint32_t NCH = (DF_PAY / 16 + 127) / 128;  // chunks per thread at most
-      uint4 v[NCH];
-#pragma unroll
-      for (uint32_t k = 0; k < NCH; ++k) {  // every load in flight before the first LDS write
-        const uint32_t c = lt + k * 128;
-        const uint64_t a = A0 + (uint64_t)c * 16;
-        v[k] = c >= nch ? make_uint4(0u, 0u, 0u, 0u)
-               : fast   ? *reinterpret_cast<const uint4*>(blob + a)
-                        : gload_u128_tail(blob, blob_len, a);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < NCH; ++k)
-        if (lt + k * 128 <= nch) P[lt + k * 128] = v[k];  // (chunk nch: zeros, the last funnel word)
-    }
   }
   __syncthreads();  // (every wave: the tiles of one workgroup may differ in kind)
   DW_STAMP(0)
   // per 256-output block k of an easy tile (pair s of every thread lies in block s), found once
   // by thread k: the run holding its first output (A) and the run after it (B), as block-relative
-  // ends and, for a bit-packed run, the bit offset of the block's first output in the staged
-  // payload (the pair at block output r then starts at bit base + r w); an RLE run's value instead
-  uint4* blk = reinterpret_cast<uint4*>(R + DF_BLK);        // (end A, base A, end B, base B)
-  uint32_t* blk2 = reinterpret_cast<uint32_t*>(R + DF_BLK + 16 * 16);  // (RLE flags, run A)
+  // ends and, for a bit-packed run, the bit offset of the block's first output from A0 (the pair
+  // at block output r then starts at bit base + r w); an RLE run's value instead
+  uint4* blk = reinterpret_cast<uint4*>(ri + DF_RC + 2);  // (end A, base A, end B, base B)
+  uint32_t* blk2 = reinterpret_cast<uint32_t*>(blk + 16);  // (RLE flags, run A)
   if (easy && lt < 16) {
     const uint32_t o = qlo + 256u * lt;
     uint32_t a = 0;
@@ -529,87 +515,136 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   }
   __syncthreads();
   DW_STAMP(1)
-  if (easy) {
-    const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(R + DF_POFF);
-    const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
-    const uint32_t r = 2u * lt, rw = r * w;  // the thread's pair in every block
-    bool bad = false;
-    // fast pass, branch-free so that every LDS read of a phase is in flight at once: each pair
-    // inside one of its block's two runs (w <= 16: both values in one 32-bit window) -- a bit
-    // offset, or an RLE run's value; the rest marked for the slow pass
-    uint32_t q[16], slow = 0, rle = 0, dead = 0;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const uint4 b = blk[s];
-      const uint32_t fl = blk2[2 * s];
-      const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
-      q[s] = inA ? b.y : b.w;
-      if (s * 256 >= rem) dead |= 1u << s;
-      else if (!((inA || inB) && w <= 16)) slow |= 1u << s;
-      if (fl & (inA ? 1u : 2u)) rle |= 1u << s;
-    }
-    uint32_t lo[16], hi[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {  // (RLE, slow and dead pairs read word 0: in bounds, unused)
-      const uint32_t wi = ((rle | slow | dead) >> s) & 1u ? 0u : (q[s] + rw) >> 5;
-      lo[s] = pw32[wi];
-      hi[s] = pw32[wi + 1];
-    }
-    // dict[idx] out of bounds: the reference panics (rle.rs:455,470); the tile's last output has
-    // no second value
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const uint32_t x = __builtin_amdgcn_alignbit(hi[s], lo[s], (q[s] + rw) & 31u);
-      uint32_t v0 = (rle >> s) & 1u ? q[s] : x & wm;
-      uint32_t v1 = (rle >> s) & 1u ? q[s] : (x >> w) & wm;
-      if (((dead | slow) >> s) & 1u) v0 = v1 = 0;
-      if (s * 256 + 1 >= rem) v1 = 0;
-      bad |= v0 >= D0 || v1 >= D0;
-      ix[s] = (v0 & 0xFFFFu) | (v1 << 16);
-    }
-    // slow pass (a pair across a run boundary, a block past its first two runs, w > 16): value by
-    // value from the block's first run on
-    if (slow) {
+  // the index decode, run once, right after the first window's fill is issued
+  auto decode = [&]() {
+    if (easy) {
+      const uint8_t* pay = blob + A0;
+      const uint64_t plen = blob_len - A0;  // (A0 < blob_len: inside the stream)
+      const uint32_t w = d.w, wm = w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
+      const uint32_t r = 2u * lt, rw = r * w;  // the thread's pair in every block
+      bool bad = false;
+      // fast pass: each pair inside one of its block's two runs (w <= 16: both values in one
+      // 32-bit window) -- a bit offset, or an RLE run's value; the rest marked for the slow pass
+      uint32_t q[16], slow = 0, rle = 0, dead = 0;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        if (!((slow >> s) & 1u)) continue;
-        const uint32_t o0 = qlo + 256u * (uint32_t)s + r;
-        uint32_t a = blk2[2 * s + 1], st = rs[a], inf = ri[a], nx = rs[a + 1];
-        uint32_t v2[2] = {0u, 0u};
+        const uint4 b = blk[s];
+        const uint32_t fl = blk2[2 * s];
+        const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
+        q[s] = inA ? b.y : b.w;
+        if (s * 256 >= rem) dead |= 1u << s;
+        else if (!((inA || inB) && w <= 16)) slow |= 1u << s;
+        if (fl & (inA ? 1u : 2u)) rle |= 1u << s;
+      }
+      uint32_t lo[16], hi[16];
+      if (d.S + d.bhi + 8u <= blob_len) {  // (the tile's wave-uniform common case: no load near the blob's end)
+        const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(pay);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const uint32_t o = o0 + (uint32_t)j;
-#pragma unroll 1
-          while (nx <= o && a + 1 < nr) {
-            ++a;
-            st = nx;
-            inf = ri[a];
-            nx = rs[a + 1];
-          }
-          if (inf & R_RLE) {
-            v2[j] = inf & 0x7FFFFFFFu;
-          } else {
-            const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
-            const uint32_t wi = bit >> 5;
-            v2[j] = __builtin_amdgcn_alignbit(pw32[wi + 1], pw32[wi], bit & 31u) & wm;
+        for (int s = 0; s < 16; ++s) {  // (every load in flight at once; RLE, slow and dead pairs load nothing)
+          lo[s] = hi[s] = 0u;
+          if (!(((rle | slow | dead) >> s) & 1u)) {
+            const uint32_t wi = (q[s] + rw) >> 5;
+            lo[s] = pw32[wi];
+            hi[s] = pw32[wi + 1];
           }
         }
-        if (s * 256 + 1 >= rem) v2[1] = 0;
-        bad |= v2[0] >= D0 || v2[1] >= D0;
-        ix[s] = (v2[0] & 0xFFFFu) | (v2[1] << 16);
-      }
-    }
-    const uint64_t bm = __ballot(bad);
-    if (bm && (tid & 63u) == (uint32_t)__builtin_ctzll(bm)) report(pages, chunks, (int)d.page, ST_PANIC);
-  } else {
-    const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + (uint64_t)p * RUN_TILE) + lt;
+      } else {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) ix[s] = s * 256 < rem ? ip[s * 128] : 0u;
-  }
+        for (int s = 0; s < 16; ++s) {
+          lo[s] = hi[s] = 0u;
+          if (!(((rle | slow | dead) >> s) & 1u)) {
+            const uint32_t wi = (q[s] + rw) >> 5;
+            lo[s] = dw_word(pay, plen, 4ull * wi);
+            hi[s] = dw_word(pay, plen, 4ull * wi + 4u);
+          }
+        }
+      }
+      // dict[idx] out of bounds: the reference panics (rle.rs:455,470); the tile's last output
+      // has no second value
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t x = __builtin_amdgcn_alignbit(hi[s], lo[s], (q[s] + rw) & 31u);
+        uint32_t v0 = (rle >> s) & 1u ? q[s] : x & wm;
+        uint32_t v1 = (rle >> s) & 1u ? q[s] : (x >> w) & wm;
+        if (((dead | slow) >> s) & 1u) v0 = v1 = 0;
+        if (s * 256 + 1 >= rem) v1 = 0;
+        bad |= v0 >= D0 || v1 >= D0;
+        ix[s] = (v0 & 0xFFFFu) | (v1 << 16);
+      }
+      // slow pass (a pair across a run boundary, a block past its first two runs, w > 16): value
+      // by value from the block's first run on
+      if (slow) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          if (!((slow >> s) & 1u)) continue;
+          const uint32_t o0 = qlo + 256u * (uint32_t)s + r;
+          uint32_t a = blk2[2 * s + 1], st = rs[a], inf = ri[a], nx = rs[a + 1];
+          uint32_t v2[2] = {0u, 0u};
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t o = o0 + (uint32_t)j;
+#pragma unroll 1
+            while (nx <= o && a + 1 < nr) {
+              ++a;
+              st = nx;
+              inf = ri[a];
+              nx = rs[a + 1];
+            }
+            if (inf & R_RLE) {
+              v2[j] = inf & 0x7FFFFFFFu;
+            } else {
+              const uint32_t bit = (inf - sb32) * 8u + (o - st) * w;
+              const uint32_t wi = bit >> 5;
+              v2[j] = __builtin_amdgcn_alignbit(dw_word(pay, plen, 4ull * wi + 4u), dw_word(pay, plen, 4ull * wi),
+                                                bit & 31u) & wm;
+            }
+          }
+          if (s * 256 + 1 >= rem) v2[1] = 0;
+          bad |= v2[0] >= D0 || v2[1] >= D0;
+          ix[s] = (v2[0] & 0xFFFFu) | (v2[1] << 16);
+        }
+      }
+      const uint64_t bm = __ballot(bad);
+      if (bm && (tid & 63u) == (uint32_t)__builtin_ctzll(bm)) report(pages, chunks, (int)d.page, ST_PANIC);
+    } else {
+      const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + (uint64_t)p * RUN_TILE) + lt;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) ix[s] = s * 256 < rem ? ip[s * 128] : 0u;
+    }
+  };
+  // a window fill by LDS-DMA (no registers held): chunks c < lim, inside the window's bytes and
+  // the blob
+  auto fill_lim = [&](uint64_t dbase, uint32_t D, uint32_t w0) -> uint32_t {
+    const uint64_t a = dbase + (uint64_t)w0 * ES, a0 = a & ~15ull;
+    const uint32_t nb = (uint32_t)(a - a0) + (D - w0 < WIN ? D - w0 : WIN) * (uint32_t)ES;
+    const uint64_t bl = blob_len > a0 ? (blob_len - a0) / 16u : 0u;
+    return (uint32_t)min(min((uint64_t)DW_CH, (uint64_t)(nb + 15u) / 16u), bl);
+  };
+  auto fill = [&](uint64_t dbase, uint32_t D, uint32_t w0) {
+    const uint64_t a0 = (dbase + (uint64_t)w0 * ES) & ~15ull;
+    const uint32_t lim = fill_lim(dbase, D, w0);
+    const uint8_t* src = blob + a0 + (uint64_t)tid * 16u;
+#pragma unroll 1  // (unrolled, the fill's addresses and M0 values took registers the values need)
+    for (int f = 0; f < DW_F; ++f) {
+      const uint32_t c = (uint32_t)f * DW_NT + tid;
+      if (c < lim)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + (uint64_t)f * DW_NT * 16u),
+            (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)win +
+                                                       ((uint32_t)f * DW_NT + (tid & ~63u)) * 16u),
+            16, 0, 0);
+    }
+  };
+  // the first window (the first distinct dictionary's, in the loop's order) is filled while the
+  // indices are decoded
+  int32_t k1 = -1;
+  for (int qq = 0; qq < DW_TPW && k1 < 0; ++qq) k1 = dkey[qq];
+  if (k1 >= 0) fill(pages[k1].base, pages[k1].num_values, 0u);
+  decode();
+  bool first = k1 >= 0;
   T x[16][2];
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s][0] = x[s][1] = 0;
-  __syncthreads();  // (the stage regions are the window's)
   DW_STAMP(2)
   for (int qq = 0; qq < DW_TPW; ++qq) {  // each distinct dictionary of the 8 tiles (uniform)
     const int32_t kq = dkey[qq];
@@ -622,22 +657,11 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     for (uint32_t w0 = 0; w0 < D; w0 += WIN) {
       const uint64_t a = dbase + (uint64_t)w0 * ES, a0 = a & ~15ull;
       const uint32_t sh = (uint32_t)(a - a0);  // the window's first entry lands at LDS byte sh
-      const uint32_t nb = sh + (D - w0 < WIN ? D - w0 : WIN) * (uint32_t)ES;
-      __syncthreads();  // (the previous window's gathers are done)
-      // chunks c < lim: inside the window's bytes and the blob
-      const uint64_t bl = blob_len > a0 ? (blob_len - a0) / 16u : 0u;
-      const uint32_t lim = (uint32_t)min(min((uint64_t)DW_CH, (uint64_t)(nb + 15u) / 16u), bl);
-      const uint8_t* src = blob + a0 + (uint64_t)tid * 16u;
-#pragma unroll 1  // (unrolled, the fill's addresses and M0 values took registers the values need)
-      for (int f = 0; f < DW_F; ++f) {
-        const uint32_t c = (uint32_t)f * DW_NT + tid;
-        if (c < lim)
-          __builtin_amdgcn_global_load_lds(
-              (const __attribute__((address_space(1))) void*)(src + (uint64_t)f * DW_NT * 16u),
-              (__attribute__((address_space(3))) void*)((__attribute__((address_space(3))) uint8_t*)win +
-                                                         ((uint32_t)f * DW_NT + (tid & ~63u)) * 16u),
-              16, 0, 0);
+      if (!first) {
+        __syncthreads();  // (the previous window's gathers are done)
+        fill(dbase, D, w0);
       }
+      first = false;
       // every wave's LDS-DMA fill must have landed before any wave reads the window: each wave
       // waits for its own (vmcnt(0), explicit: the barrier alone does not promise it), then the
       // barrier orders the waves. 0x0F70 is vmcnt(0) in the gfx9 (gfx950) encoding; the guard
@@ -649,7 +673,7 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       __syncthreads();
       DW_STAMP(3)
       if (sh) {  // a dictionary at an odd offset: the window moved down by sh bytes, in place
-        const uint32_t k0 = sh >> 2, bs = sh & 3u;
+        const uint32_t k0 = sh >> 2, bs = sh & 3u, lim = fill_lim(dbase, D, w0);
 #pragma unroll 1
         for (int f = 0; f < DW_F; ++f) {
           const uint32_t c = (uint32_t)f * DW_NT + tid;

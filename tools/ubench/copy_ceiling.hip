@@ -1,7 +1,9 @@
 // copy_ceiling.hip — the achievable HBM copy rate on this device, for bench.py's roofline
 // context (measurement tooling; not part of the decode library). A 16-byte-per-lane
 // grid-stride copy (the MI355X_MICROARCH.md "float4 copy" shape), plain and non-temporal
-// variants at three grid sizes; the fastest is reported.
+// variants at three grid sizes, and a one-pass copy of 2 chunks per lane with one short
+// workgroup per 8 KiB (k_plain_copy's shape: many short workgroups copied fastest there); the
+// fastest is reported.
 #pragma clang diagnostic ignored "-Wunused-result"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,6 +32,27 @@ __global__ void __launch_bounds__(256) k_copy16(const v4u* __restrict__ src, v4u
   }
 }
 
+// one pass: workgroup b copies 16-byte chunks [b * 512, b * 512 + 512), two per lane
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy16_once(const v4u* __restrict__ src, v4u* __restrict__ dst,
+                                                     uint64_t n16) {
+  const uint64_t i = (uint64_t)blockIdx.x * 512u + threadIdx.x;
+  v4u v[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t j = i + (uint64_t)k * 256u;
+    if (j < n16) v[k] = NT ? __builtin_nontemporal_load(src + j) : src[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t j = i + (uint64_t)k * 256u;
+    if (j < n16) {
+      if (NT) __builtin_nontemporal_store(v[k], dst + j);
+      else dst[j] = v[k];
+    }
+  }
+}
+
 extern "C" {
 
 // Best of the plain / non-temporal copy over `iters` launches of a `bytes`-byte buffer, as
@@ -50,18 +73,22 @@ double pqg_copy_ceiling_gbs(uint64_t bytes, int iters) {
   // grids of 16, 64 and 256 workgroups per CU (tools/ubench/copy_sweep.hip: the largest grids
   // copy fastest on MI355X, 5.8-6.0 TB/s with non-temporal loads and stores)
   const unsigned grids[3] = {256 * 16, 256 * 64, 256 * 256};
-  for (int v = 0; v < 6 && best >= 0; ++v) {
+  const unsigned once = (unsigned)((n16 + 511) / 512);
+  auto launch = [&](int v) {
     const int nt = v & 1;
+    if (v >= 6) {
+      if (nt) hipLaunchKernelGGL(k_copy16_once<true>, dim3(once), dim3(256), 0, 0, a, b, n16);
+      else hipLaunchKernelGGL(k_copy16_once<false>, dim3(once), dim3(256), 0, 0, a, b, n16);
+      return;
+    }
     const unsigned grid = grids[v >> 1];
-    for (int w = 0; w < 2; ++w) {
-      if (nt) hipLaunchKernelGGL(k_copy16<true>, dim3(grid), dim3(256), 0, 0, a, b, n16);
-      else hipLaunchKernelGGL(k_copy16<false>, dim3(grid), dim3(256), 0, 0, a, b, n16);
-    }
+    if (nt) hipLaunchKernelGGL(k_copy16<true>, dim3(grid), dim3(256), 0, 0, a, b, n16);
+    else hipLaunchKernelGGL(k_copy16<false>, dim3(grid), dim3(256), 0, 0, a, b, n16);
+  };
+  for (int v = 0; v < 8 && best >= 0; ++v) {
+    for (int w = 0; w < 2; ++w) launch(v);
     hipEventRecord(e0, 0);
-    for (int i = 0; i < iters; ++i) {
-      if (nt) hipLaunchKernelGGL(k_copy16<true>, dim3(grid), dim3(256), 0, 0, a, b, n16);
-      else hipLaunchKernelGGL(k_copy16<false>, dim3(grid), dim3(256), 0, 0, a, b, n16);
-    }
+    for (int i = 0; i < iters; ++i) launch(v);
     hipEventRecord(e1, 0);
     if (hipEventSynchronize(e1) != hipSuccess) {
       best = -1;
