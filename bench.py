@@ -547,6 +547,68 @@ def run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind, p_null=None, st
     return res
 
 
+def run_bytes_page(pqgpu, ctx, stream, enc, steps, warmup):
+    """One REQUIRED BYTE_ARRAY page of 2^20 values, DELTA_BYTE_ARRAY (sorted URL-like strings:
+    prefix lengths, suffix lengths, suffixes; decoding.rs:768-835) or DELTA_LENGTH_BYTE_ARRAY
+    (random lengths 0..48; decoding.rs:682-712), written by tools/gen's restated encoders, decoded
+    whole by the production path (k_ba_index's length streams, the value-offset scan, the slice
+    copy / prefix rebuild) and checked byte for byte against the values written. Roofline: the
+    page's bytes in + the values' bytes and int64 offsets out, over the decode time."""
+    import torch
+    import pqgtools
+    n = 1 << 20
+    if enc == "dba":
+        vals = pqgtools.url_values(n, 0x5EED0006)
+        body, code = pqgtools.delta_byte_array_body(vals), pqgpu.DELTA_BYTE_ARRAY
+    else:
+        rng = np.random.default_rng(0x5EED0007)
+        lens = rng.integers(0, 49, n)
+        raw = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8).tobytes()
+        offs0 = np.concatenate([[0], np.cumsum(lens)])
+        vals = [raw[offs0[i]:offs0[i + 1]] for i in range(n)]
+        body, code = pqgtools.delta_length_body(vals), pqgpu.DELTA_LENGTH_BYTE_ARRAY
+    flat = b"".join(vals)
+    pages = (pqgpu.Page * 1)()
+    pages[0] = pqgpu.Page(0, len(body), n, pqgpu.PAGE_DATA, code, pqgpu.RLE, pqgpu.RLE, 0, 0)
+    d_blob = torch.frombuffer(bytearray(body + b"\0" * 64), dtype=torch.uint8).cuda()
+    d_val = torch.empty(len(flat) + 64, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(n + 2, dtype=torch.int64, device="cuda")
+    col = pqgpu.Column(pqgpu.BYTE_ARRAY, -1, 0, 0)
+    out = pqgpu.Output(None, None, d_val.data_ptr(), len(flat), d_off.data_ptr(), n + 1, 0, 0, 0)
+
+    def once():
+        ctx.decode_async(col, d_blob.data_ptr(), len(body) + 64, pages, out, stream, npages=1)
+
+    once()
+    st, bad = ctx.sync()
+    assert st == 0, (st, bad, ctx.error_message())
+    offs = d_off[:n + 1].cpu().numpy()
+    ok = (out.num_values == n and offs[-1] == len(flat) and
+          np.array_equal(offs, np.concatenate([[0], np.cumsum([len(v) for v in vals])])) and
+          d_val[:len(flat)].cpu().numpy().tobytes() == flat)
+    assert ok, "byte-array page decode differs from the values written"
+    for _ in range(warmup):
+        once()
+    ctx.sync()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        once()
+    st, bad = ctx.sync()
+    e1.record()
+    torch.cuda.synchronize()
+    assert st == 0, (st, bad)
+    ms = e0.elapsed_time(e1) / steps
+    nb = len(body) + len(flat) + 8 * (n + 1)
+    return {"values_per_s": n / (ms * 1e-3), "ms_per_step": ms, "values_per_gpu": n,
+            "page_bytes": len(body), "value_bytes": len(flat), "value_check": "every byte and offset",
+            "roofline": roofline("byte-array page decode (whole step)", ms, nb, None, None,
+                                 "HIP events on the decode stream around whole decodes (the host "
+                                 "enqueue of each decode included); bytes = page in + values and "
+                                 "int64 offsets out")}
+
+
 def dry_run(args, world, rank, dist):
     """Launcher / partition / reduction plumbing without a GPU: every rank derives its own
     partition (seed, config-5 row groups), the max-over-ranks step time is reduced over gloo,
@@ -975,6 +1037,9 @@ def main(argv=None):
                 r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, "delta", steps=short_steps, warmup=2,
                               extras=False, block=(128, 4), strong=strong)
                 sub[kind]["variants"] = {"block128_4x32": brief(r, unit_key)}
+                # DELTA_BYTE_ARRAY / DELTA_LENGTH_BYTE_ARRAY: one 2^20-value page each
+                for enc in ("dba", "dlba"):
+                    sub[kind]["variants"][f"{enc}_page_1M"] = run_bytes_page(pqgpu, ctx, stream, enc, short_steps, 2)
         if args.split == "auto" and world > 1:
             # strong scaling alongside: the ranks split one 1e9-value stream into page ranges
             r = run_fixed(pqgpu, ctx, args, world, rank, dist, stream, kind,

@@ -408,11 +408,14 @@ __global__ void __launch_bounds__(WG) k_badict_fallback(const uint8_t* __restric
   }
 }
 
+#include "pqg_balen.hpp"
+
 __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blob, uint64_t blob_len,
                                                  PageWork* pages, ChunkWork* chunks, uint64_t* vsrc0,
-                                                 uint32_t* vlen0, uint32_t* vpre0) {
+                                                 uint32_t* vlen0, uint32_t* vpre0, const BlPage* blp) {
   __shared__ DeltaSmem sm;
   const int p = blockIdx.x;
+  if (blp && blp[p].fast) return;  // (decoded by k_bl_*)
   const PageWork pw = pages[p];
   if (pw.status != 0) return;
   if (pw.page_type != P_DATA && pw.page_type != P_DATA_V2) return;
@@ -447,7 +450,11 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
       // set_data decodes every length, then data.start_from(get_offset()) (:682-695)
       DeltaInfo li;
       st = delta_stream<4>(sm, blob, blob_len, S, slen, ~0ull, n, reinterpret_cast<uint8_t*>(len), li);
-      if (!st && li.total < n) st = ST_EOF;  // the reference returns a short batch
+      // fewer lengths than values: the decoder's get returns short batches, then none (:697-711):
+      // without levels read_batch makes no progress and loops forever (column/reader.rs:159-265);
+      // with levels the values run short of the non-null levels (EOF here)
+      const int32_t short_st = ck.cp.max_def == 0 && ck.cp.max_rep == 0 ? ST_HANG : ST_EOF;
+      if (!st && li.total < n) st = short_st;
       if (!st && li.end_off > slen) st = ST_PANIC;
       if (!st) st = slices_from_lengths(sm, S + li.end_off, slen - li.end_off, n, len, src, bytes);
       have_bytes = true;
@@ -458,7 +465,7 @@ __global__ void __launch_bounds__(WG) k_ba_index(const uint8_t* __restrict__ blo
       uint32_t* pre = vpre + vo;
       DeltaInfo pi, si;
       st = delta_stream<4>(sm, blob, blob_len, S, slen, ~0ull, n, reinterpret_cast<uint8_t*>(pre), pi);
-      if (!st && pi.total < n) st = ST_EOF;
+      if (!st && pi.total < n) st = ck.cp.max_def == 0 && ck.cp.max_rep == 0 ? ST_HANG : ST_EOF;  // (as above)
       if (!st && pi.end_off > slen) st = ST_PANIC;
       const uint32_t e1 = pi.end_off;
       if (!st) {
@@ -1427,8 +1434,28 @@ hipError_t pqg_launch_badict_general(const uint8_t* blob, uint64_t blob_len, Pag
 hipError_t pqg_launch_bytes(const uint8_t* blob, uint64_t blob_len, PageWork* pages, int npages, ChunkWork* chunks,
                             const uint32_t* tile_page, const uint32_t* tl, uint32_t ntl, bool has_dba, bool has_lvdict,
                             uint64_t* vsrc, uint32_t* vlen, uint32_t* vpre, const uint64_t* dsrc, const uint32_t* dlen,
-                            uint64_t* tsum, uint32_t* vaux, uint32_t* dtile, hipStream_t s) {
-  hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre);
+                            uint64_t* tsum, uint32_t* vaux, uint32_t* dtile, const uint32_t* bl, uint32_t nbl,
+                            uint32_t bl_tiles, uint8_t* blbuf, uint32_t ntiles_all, hipStream_t s) {
+  BlPage* blp = nullptr;
+  if (nbl) {  // the large DELTA_LENGTH / DELTA_BYTE_ARRAY pages' length streams (pqg_balen.hpp)
+    BlArgs a;
+    a.list = bl;
+    a.nlist = nbl;
+    a.maxtiles = bl_tiles;
+    a.pg = blp = reinterpret_cast<BlPage*>(blbuf);
+    a.tile = reinterpret_cast<BlTile*>(blbuf + (size_t)npages * 64);
+    a.blk = reinterpret_cast<uint32_t*>(blbuf + (size_t)npages * 64 + ((size_t)ntiles_all + 1) * sizeof(BlTile));
+    a.blk_stride = ((uint64_t)ntiles_all + 1) * BL_BPT;
+    (void)hipMemsetAsync(blp, 0, (size_t)npages * sizeof(BlPage), s);
+    const dim3 tg(bl_tiles, nbl);
+    hipLaunchKernelGGL(k_bl_walk, dim3(nbl), dim3(BLW), 0, s, blob, blob_len, pages, chunks, a);
+    hipLaunchKernelGGL(k_bl_tile<0>, tg, dim3(WG), 0, s, blob, blob_len, pages, chunks, a, vlen, vpre);
+    hipLaunchKernelGGL(k_bl_scan<0>, dim3(nbl), dim3(WG), 0, s, pages, a);
+    hipLaunchKernelGGL(k_bl_tile<1>, tg, dim3(WG), 0, s, blob, blob_len, pages, chunks, a, vlen, vpre);
+    hipLaunchKernelGGL(k_bl_scan<1>, dim3(nbl), dim3(WG), 0, s, pages, a);
+    hipLaunchKernelGGL(k_bl_src, tg, dim3(WG), 0, s, pages, chunks, a, vsrc, vlen, vpre);
+  }
+  hipLaunchKernelGGL(k_ba_index, dim3(npages), dim3(WG), 0, s, blob, blob_len, pages, chunks, vsrc, vlen, vpre, blp);
   // tile sums before the page scan: the level path's dictionary pages take their byte totals
   // from them (PageWork::tile_bytes)
   if (ntl)

@@ -56,7 +56,8 @@ hipError_t pqg_launch_badict_general(const uint8_t*, uint64_t, PageWork*, int, C
                                      int, hipStream_t);
 hipError_t pqg_launch_bytes(const uint8_t*, uint64_t, PageWork*, int, ChunkWork*, const uint32_t*, const uint32_t*,
                             uint32_t, bool, bool, uint64_t*, uint32_t*, uint32_t*, const uint64_t*, const uint32_t*,
-                            uint64_t*, uint32_t*, uint32_t*, hipStream_t);
+                            uint64_t*, uint32_t*, uint32_t*, const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t,
+                            hipStream_t);
 }
 
 // Stream kinds of the hybrid-stream tables: def, rep, dictionary indices, RLE booleans.
@@ -70,8 +71,11 @@ constexpr int SS_DICT = 2;  // device/pqg_runs.hpp StreamSel: dictionary indices
 // TL_PSPEC: PLAIN pages of the chunks whose values are copied speculatively (ChunkWork::spec).
 // TL_W4 / TL_W8: general-path dictionary tiles of 4- / 8-byte values whose dictionary has at most
 // DW_MAXD entries (indices to a buffer, then the gather through LDS windows: k_dict_win).
+// TL_BLEN: the large DELTA_LENGTH / DELTA_BYTE_ARRAY pages (a page list) whose length streams the
+// multi-workgroup kernels decode (pqg_balen.hpp).
 enum { TL_D1 = 0, TL_D4, TL_D8, TL_D12, TL_DALL, TL_BADICT, TL_BA, TL_BOOL, TL_PLAIN, TL_PBOOL, TL_PSPEC, TL_W4, TL_W8,
-       TL_N };
+       TL_BLEN, TL_N };
+constexpr uint32_t BL_MIN_VALUES = 65536;  // pqg_balen.hpp BL_MIN
 #ifndef PQG_DWIN
 #define PQG_DWIN 1  // (0: every general-path dictionary gather served from L2, for A/B runs)
 #endif
@@ -118,6 +122,8 @@ struct Slot {
   size_t dtile_cap = 0;
   uint16_t* didx = nullptr;  // TL_W4 / TL_W8 tiles: RUN_TILE dictionary indices each
   size_t didx_cap = 0;
+  uint8_t* blbuf = nullptr;  // TL_BLEN pages: per page, per tile and per block state (pqg_balen.hpp)
+  size_t blcap = 0;
   // hybrid-stream expand tiles: tile -> page map and the index-pass tables per stream kind
   uint32_t* tile_page = nullptr;
   RunTables rt[K_N] = {};
@@ -343,6 +349,7 @@ int pqg_ctx_destroy(pqg_ctx* ctx) {
     hipFree(sl.dsrc);
     hipFree(sl.dlen);
     hipFree(sl.didx);
+    hipFree(sl.blbuf);
     hipFree(sl.tile_page);
     for (RunTables& t : sl.rt) free_run_tables(t);
     hipFree(sl.dt.page);
@@ -531,6 +538,7 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
   std::vector<uint32_t> tl[TL_N];
   std::vector<PageWork> pw(np);
   uint32_t total_tiles = 0;
+  uint32_t bl_maxtiles = 0;
   uint64_t nwin = 0, plain_max = 0, spec_max = 0, scr = 0, dscr = 0;
   uint32_t def_w = 0, rep_w = 0;  // bit masks of the level streams' widths
   bool any_def = false, any_rep = false, any_plain = false, any_pbool = false, any_ba = false, any_dba = false;
@@ -647,6 +655,15 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
         scr += lev ? lev : 1;
         list_tiles(TL_BA, -1);
         if (enc[PQG_DELTA_BYTE_ARRAY]) any_dba = true;
+        if (t == PQG_BYTE_ARRAY && (enc[PQG_DELTA_BYTE_ARRAY] || enc[PQG_DELTA_LENGTH_BYTE_ARRAY]))
+          for (uint32_t i = 0; i < n; ++i) {
+            const PageWork& w = pw[p0 + i];
+            if ((w.encoding == PQG_DELTA_BYTE_ARRAY || w.encoding == PQG_DELTA_LENGTH_BYTE_ARRAY) &&
+                w.num_values >= BL_MIN_VALUES && w.ntiles) {
+              tl[TL_BLEN].push_back(p0 + i);
+              if (w.ntiles > bl_maxtiles) bl_maxtiles = w.ntiles;
+            }
+          }
         if (enc[PQG_RLE_DICTIONARY]) {
           any_badict = true;
           c.dscr_base = dscr;
@@ -789,6 +806,11 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
       sl.dlen = nullptr;
       HIPCHK(hipMalloc(&sl.dlen, sl.dcap * 4), "hipMalloc dlen");
     }
+  }
+  if (!tl[TL_BLEN].empty()) {  // BlPage per page, BlTile per tile, two streams' block offsets per tile
+    int st;
+    const size_t need = (size_t)np * 64 + ((size_t)total_tiles + 1) * (48 + 2 * 32 * 4);
+    if ((st = grow(ctx, (void**)&sl.blbuf, &sl.blcap, need, 1, "hipMalloc byte-array length state"))) return st;
   }
   if (any_dba) {
     int st;
@@ -992,7 +1014,8 @@ static int decode_batch(pqg_ctx* ctx, uint32_t nc, const pqg_column* cols, const
     if (any_ba) {
       if (!ctx->values_kernel) ctx->values_kernel = any_dba ? PQG_DELTA_BYTE_ARRAY : PQG_PLAIN;
       HIPCHK(pqg_launch_bytes(b, blob_len, d_pages, ni, d_chunks, sl.tile_page, tlp[TL_BA], ntl[TL_BA], any_dba, ba_lv,
-                              sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, sl.vaux, sl.dtile, s),
+                              sl.vsrc, sl.vlen, sl.vpre, sl.dsrc, sl.dlen, sl.tsum, sl.vaux, sl.dtile, tlp[TL_BLEN],
+                              ntl[TL_BLEN], bl_maxtiles, sl.blbuf, total_tiles, s),
              "byte arrays");
     }
     if (any_plain || any_pbool) {

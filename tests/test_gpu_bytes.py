@@ -321,3 +321,95 @@ def test_plain_ba_one_length_truncated(oracle, ctx, cut):
     the reference's error (panic on a cut length, EOF on cut bytes)."""
     body = oracle.plain_encode_ba([b"abcdefgh"] * 50)[:-cut]
     _err(oracle, ctx, oracle.BYTE_ARRAY, [oracle.PageSpec(oracle.PAGE_DATA, body, 50, oracle.PLAIN)])
+
+
+# ------------------------------------------------------------------ large pages: pqg_balen.hpp
+def _prefixes(vals):
+    import os.path
+    pre, prev = [], b""
+    for v in vals:
+        pre.append(len(os.path.commonprefix([prev, v])))
+        prev = v
+    return pre
+
+
+def _dba_body(oracle, vals, shape=(128, 4), pre=None, suf=None):
+    """DELTA_BYTE_ARRAY with the length streams in a chosen block shape (prefix / suffix lengths
+    may be given to write malformed pages)."""
+    pre = _prefixes(vals) if pre is None else pre
+    sufs = [v[k:] for v, k in zip(vals, pre)] if suf is None else suf
+    return (oracle.delta_encode(oracle.INT32, np.array(pre, np.int32), *shape) +
+            oracle.delta_encode(oracle.INT32, np.array([len(s) for s in sufs], np.int32), *shape) + b"".join(sufs))
+
+
+def _dlba_body(oracle, vals, shape=(128, 4), lens=None):
+    lens = [len(v) for v in vals] if lens is None else lens
+    return oracle.delta_encode(oracle.INT32, np.array(lens, np.int32), *shape) + b"".join(vals)
+
+
+@pytest.mark.parametrize("shape", [(128, 4), (256, 8), (512, 4), (4096, 8), (1024, 1), (64, 2)])
+def test_large_length_streams(oracle, ctx, shape):
+    """Pages of at least 65536 values (BL_MIN): their length streams decoded by the multi-workgroup
+    kernels (k_bl_walk's block chain, per-tile sums, scans and expands, pqg_balen.hpp) for block
+    shapes the decoder accepts (decoding.rs:501-533); blocks of 64 values are not that path's
+    shape and stay with k_ba_index. DELTA_LENGTH_BYTE_ARRAY (random lengths 0..40) and
+    DELTA_BYTE_ARRAY (sorted strings with shared prefixes), every byte and offset against the
+    oracle."""
+    rng = np.random.default_rng(70 + shape[0] + shape[1])
+    vals = rand_strings(rng, 150_000, 0, 40)
+    p = oracle.PageSpec(oracle.PAGE_DATA, _dlba_body(oracle, vals, shape), len(vals), oracle.DELTA_LENGTH_BYTE_ARRAY)
+    check(oracle, ctx, oracle.BYTE_ARRAY, [p])
+    svals = sorted_strings(rng, 100_000)
+    p = oracle.PageSpec(oracle.PAGE_DATA, _dba_body(oracle, svals, shape), len(svals), oracle.DELTA_BYTE_ARRAY)
+    got, _ = check(oracle, ctx, oracle.BYTE_ARRAY, [p])
+    assert got["values"][:3] == svals[:3] and got["values"][-1] == svals[-1]
+
+
+def test_large_length_streams_optional(oracle, ctx):
+    """Nullable pages: 100 000 levels of which ~80 000 values, so the page's value count (its
+    non-null levels) decides the path, beside a small page (k_ba_index) in the same chunk."""
+    rng = np.random.default_rng(80)
+    for enc, encode in ((oracle.DELTA_LENGTH_BYTE_ARRAY, lambda v: _dlba_body(oracle, v)),
+                        (oracle.DELTA_BYTE_ARRAY, lambda v: _dba_body(oracle, v))):
+        pages = optional_pages(oracle, rng, (100_000, 3000, 90_000), 0.2,
+                               lambda k: sorted_strings(rng, k), encode, enc)
+        check(oracle, ctx, oracle.BYTE_ARRAY, pages, max_def=1)
+
+
+@pytest.mark.parametrize("case", ["negative_length", "past_data", "prefix_too_long", "negative_prefix",
+                                  "short_suffix_stream", "count_mismatch"])
+def test_large_length_streams_errors(oracle, ctx, case):
+    """Malformed large pages: the multi-workgroup path hands the page back and k_ba_index reports
+    what the reference reports (data.range's assert on a negative length or one past the data;
+    previous_value[0..prefix_len] past the previous value, decoding.rs:804; a suffix stream with
+    fewer values than the prefix stream, :796-801; a length stream whose count is not the page's)."""
+    rng = np.random.default_rng(90)
+    n = 80_000
+    if case in ("negative_length", "past_data", "count_mismatch"):
+        vals = rand_strings(rng, n, 1, 30)
+        lens = [len(v) for v in vals]
+        if case == "negative_length":
+            lens[70_001] = -3
+        body = _dlba_body(oracle, vals, lens=lens)
+        if case == "past_data":
+            body = body[:-7]
+        npage = n if case != "count_mismatch" else n + 5
+        p = oracle.PageSpec(oracle.PAGE_DATA, body, npage, oracle.DELTA_LENGTH_BYTE_ARRAY)
+    else:
+        vals = sorted_strings(rng, n)
+        pre = _prefixes(vals)
+        sufs = [v[k:] for v, k in zip(vals, pre)]
+        if case == "prefix_too_long":
+            pre[66_000] = len(vals[65_999]) + 4
+        if case == "negative_prefix":
+            pre[75_000] = -1
+        if case == "short_suffix_stream":
+            sufs = sufs[:-3]
+        p = oracle.PageSpec(oracle.PAGE_DATA, _dba_body(oracle, vals, pre=pre, suf=sufs), n, oracle.DELTA_BYTE_ARRAY)
+    import pqgpu
+    ref = oracle.read_column(oracle.BYTE_ARRAY, [p])
+    got = pqgpu.decode_column(ctx, pqgpu.BYTE_ARRAY, [p])
+    assert got["status"] == ref["status"], (case, got["message"], ref["message"])
+    if ref["status"] == 0:
+        assert got["bytes"] == ref["bytes"]
+        np.testing.assert_array_equal(got["offsets"], ref["offsets"])

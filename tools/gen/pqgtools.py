@@ -127,3 +127,44 @@ def write_alltypes_file(path, rows_per_group, row_groups, row0=0, p_null=0.0, se
                                        codec, threads)
     if st:
         raise RuntimeError("pqg_write_alltypes_file failed: %d" % st)
+
+
+def _delta_i32(vals):
+    """DeltaBitPackEncoder<Int32Type> of vals (encoding.rs:534-714, the writer's 128 / 4 blocks)."""
+    import numpy as np
+    v = np.ascontiguousarray(vals, dtype=np.int32)
+    cap = 64 + 8 * len(v) + 1024
+    out = (C.c_uint8 * cap)()
+    n = lib().pqg_encode_delta(1, v.ctypes.data, len(v), 128, 4, out, cap)
+    assert n > 0
+    return bytes(out[:n])
+
+
+def url_values(n, seed):
+    """n sorted URL-like byte strings ('http://www.example.com/' + a path of digits and letters of
+    2..24 bytes), the DELTA_BYTE_ARRAY bench shape: long shared prefixes, short suffixes."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    keys = np.sort(rng.integers(0, 10 ** 12, n))
+    tails = rng.integers(0, 10 ** 6, n)
+    return [b"http://www.example.com/%012d/%x" % (int(k), int(t)) for k, t in zip(keys, tails)]
+
+
+def delta_byte_array_body(vals):
+    """DeltaByteArrayEncoder (encoding.rs:813-889): prefix lengths against the previous value,
+    suffix lengths (both DELTA_BINARY_PACKED INT32), then the suffixes."""
+    import os.path
+    pre = [0] * len(vals)
+    prev = b""
+    for i, v in enumerate(vals):
+        k = len(os.path.commonprefix([prev, v]))
+        pre[i] = k
+        prev = v
+    sufs = [v[k:] for v, k in zip(vals, pre)]
+    return _delta_i32(pre) + _delta_i32([len(s) for s in sufs]) + b"".join(sufs)
+
+
+def delta_length_body(vals):
+    """DeltaLengthByteArrayEncoder (encoding.rs:735-800): lengths (DELTA_BINARY_PACKED INT32)
+    then the values' bytes."""
+    return _delta_i32([len(v) for v in vals]) + b"".join(vals)
