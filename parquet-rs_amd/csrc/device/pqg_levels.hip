@@ -338,8 +338,16 @@ __device__ inline bool lv_nodict(const PageWork* pages, const ChunkWork& ck, int
 #ifndef PQG_D1
 #define PQG_D1 1
 #endif
+// Dense one-bit pages with at most PQG_D1_LPB16 / 16 levels per stream byte (mostly bit-packed:
+// 6.7 at p_null 0.1) take the chunk walks; denser-in-levels streams (8.5 at p_null 0.05, config 5)
+// carry long RLE runs whose fills one thread of k_d1_emit writes alone, and stay on the window
+// path (config 5: 1.22 ms of D1 kernels per step against 0.94 on the window path).
+#ifndef PQG_D1_LPB16
+#define PQG_D1_LPB16 120
+#endif
 __device__ inline bool lv_d1_page(const LevelTables& lt, int p, const Stream& s, int sel) {
-  return PQG_D1 && lt.dense[p] && s.w == 1 && (sel == SS_DEF || sel == SS_REP) && s.n && s.slen;
+  return PQG_D1 && lt.dense[p] && s.w == 1 && (sel == SS_DEF || sel == SS_REP) && s.n && s.slen &&
+         (uint64_t)s.n * 16u <= (uint64_t)s.slen * PQG_D1_LPB16;
 }
 
 __global__ void __launch_bounds__(WG) k_lv_plan(const uint8_t* __restrict__ blob, PageWork* pages, int npages,
