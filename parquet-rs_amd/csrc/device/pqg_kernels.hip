@@ -416,6 +416,9 @@ __global__ void __launch_bounds__(WG) k_texpand_didx(const uint8_t* __restrict__
 }
 
 constexpr int DW_NT = 1024;                         // k_dict_win threads
+#ifndef PQG_DW_GRID
+#define PQG_DW_GRID 256u                            // k_dict_win workgroups (the CUs)
+#endif
 constexpr int DW_TPW = DW_NT / 128;                 // tiles per workgroup (128 threads x 32 values)
 constexpr uint32_t DW_BYTES = 128u << 10;           // window bytes
 constexpr uint32_t DW_LDS = DW_BYTES + 1024u;       // + the shift of an unaligned dictionary
@@ -434,7 +437,6 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
   __shared__ int32_t dkey[DW_TPW];
   if (*rt.nfall == 0) return;
   const uint32_t tid = threadIdx.x, q = tid >> 7, lt = tid & 127u;
-  const uint32_t p = blockIdx.x * DW_TPW + q;
 #ifdef PQG_DIAG
   // diagnostics (PQG_DEBUG bit 4096, tools/diag/diag_dict.py): thread 0's s_memtime cycles per
   // phase -- stage, block descriptors, index decode, window fills (issue to the barrier after the
@@ -450,6 +452,16 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
 #else
 #define DW_STAMP(k)
 #endif
+  // persistent: the workgroup takes batches of DW_TPW tiles in turn; the window left in LDS by one
+  // batch (res_key / res_w) is the next batch's first, its windows visited in reverse order every
+  // other batch (snake), so one fill in nw is saved per batch
+  const uint32_t nbt = (ntl + DW_TPW - 1) / DW_TPW;
+  int32_t res_key = -1;
+  uint32_t res_w = 0xFFFFFFFFu, it = 0;
+#pragma unroll 1
+  for (uint32_t bt = blockIdx.x; bt < nbt; bt += gridDim.x, ++it) {
+  const uint32_t p = bt * DW_TPW + q;
+  __syncthreads();  // (the previous batch's reads of dkey and the record regions are done)
   const QDesc d = p < ntl ? rt.desc[tl[p]] : QDesc{};
   const uint32_t qlo = d.qlo, qhi = d.qhi;
   uint64_t obase = 0;
@@ -532,9 +544,10 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
         const uint32_t fl = blk2[2 * s];
         const bool inA = r + 1 < b.x, inB = r >= b.x && r + 1 < b.z;
         q[s] = inA ? b.y : b.w;
-        if (s * 256 >= rem) dead |= 1u << s;
-        else if (!((inA || inB) && w <= 16)) slow |= 1u << s;
-        if (fl & (inA ? 1u : 2u)) rle |= 1u << s;
+        const bool dd = s * 256 >= rem, sl = !dd && !((inA || inB) && w <= 16);  // (selects, no branches)
+        dead |= (uint32_t)dd << s;
+        slow |= (uint32_t)sl << s;
+        rle |= (uint32_t)((fl & (inA ? 1u : 2u)) != 0u) << s;
       }
       uint32_t lo[16], hi[16];
       if (d.S + d.bhi + 8u <= blob_len) {  // (the tile's wave-uniform common case: no load near the blob's end)
@@ -636,12 +649,20 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     }
   };
   // the first window (the first distinct dictionary's, in the loop's order) is filled while the
-  // indices are decoded
+  // indices are decoded, unless it is the one left in LDS
+  const bool rev = (it & 1u) != 0;
   int32_t k1 = -1;
   for (int qq = 0; qq < DW_TPW && k1 < 0; ++qq) k1 = dkey[qq];
-  if (k1 >= 0) fill(pages[k1].base, pages[k1].num_values, 0u);
+  bool prefilled = false;
+  if (k1 >= 0) {
+    const uint32_t D1 = pages[k1].num_values, nw1 = (D1 + WIN - 1) / WIN;
+    const uint32_t wf = rev ? nw1 - 1u : 0u;
+    if (!(k1 == res_key && wf == res_w)) {
+      fill(pages[k1].base, D1, wf * WIN);
+      prefilled = true;
+    }
+  }
   decode();
-  bool first = k1 >= 0;
   T x[16][2];
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s][0] = x[s][1] = 0;
@@ -652,16 +673,19 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
     for (int r = 0; r < qq; ++r) seen |= dkey[r] == kq;
     if (seen) continue;
     const uint64_t dbase = pages[kq].base;
-    const uint32_t D = pages[kq].num_values;
+    const uint32_t D = pages[kq].num_values, nw = (D + WIN - 1) / WIN;
     const bool mine = key == kq;
-    for (uint32_t w0 = 0; w0 < D; w0 += WIN) {
+    for (uint32_t wk = 0; wk < nw; ++wk) {
+      const uint32_t wi = rev ? nw - 1u - wk : wk, w0 = wi * WIN;
       const uint64_t a = dbase + (uint64_t)w0 * ES, a0 = a & ~15ull;
       const uint32_t sh = (uint32_t)(a - a0);  // the window's first entry lands at LDS byte sh
-      if (!first) {
+      if (!(kq == res_key && wi == res_w)) {  // (uniform) not the window already in LDS
+      if (prefilled) {
+        prefilled = false;  // (the fill issued before the decode)
+      } else {
         __syncthreads();  // (the previous window's gathers are done)
         fill(dbase, D, w0);
       }
-      first = false;
       // every wave's LDS-DMA fill must have landed before any wave reads the window: each wave
       // waits for its own (vmcnt(0), explicit: the barrier alone does not promise it), then the
       // barrier orders the waves. 0x0F70 is vmcnt(0) in the gfx9 (gfx950) encoding; the guard
@@ -695,6 +719,9 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
           __syncthreads();
         }
       }
+      res_key = kq;
+      res_w = wi;
+      }  // (not resident)
       if (mine) {
         const T* wt = reinterpret_cast<const T*>(win);
 #pragma unroll
@@ -721,10 +748,11 @@ __global__ void __launch_bounds__(DW_NT) k_dict_win(const uint8_t* __restrict__ 
       *reinterpret_cast<gptr<T>>(os) = x[s][0];
     }
   }
-#ifdef PQG_DIAG
   DW_STAMP(5)
+  }  // batches
+#ifdef PQG_DIAG
   if (dst) {
-    dt_[7] = 1;
+    dt_[7] = it;  // batches of this workgroup
     uint64_t* d = chunks[0].cp.dbgbuf + 8ull * blockIdx.x;
     for (int i = 0; i < 8; ++i) d[i] = dt_[i];
   }
@@ -1105,7 +1133,9 @@ hipError_t pqg_launch_dict(const uint8_t* blob, uint64_t blob_len, PageWork* pag
       hipLaunchKernelGGL(k_texpand_didx, dim3(wn[k] < 1024u ? wn[k] : 1024u), dim3(WG), 0, s, blob, blob_len, wl[k],
                          pages, chunks, rt, rt.hard + k, hl, slot);
       hl += wn[k];
-      const dim3 g((wn[k] + DW_TPW - 1) / DW_TPW);
+      // persistent workgroups (one per CU: the window takes the LDS), batches of DW_TPW tiles in turn
+      const uint32_t nbt = (wn[k] + DW_TPW - 1) / DW_TPW;
+      const dim3 g(nbt < PQG_DW_GRID ? nbt : PQG_DW_GRID);
       if (k == 0)
         hipLaunchKernelGGL((k_dict_win<4>), g, dim3(DW_NT), 0, s, blob, blob_len, wl[k], wn[k], pages, chunks, rt, slot);
       else
