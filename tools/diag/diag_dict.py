@@ -1,5 +1,6 @@
 """Diagnostics: where k_dict_win's workgroups spend their cycles on config 3 (PQG_DIAG build,
-PQG_DEBUG=4096): thread 0's s_memtime per phase -- stage, block descriptors, index decode,
+PQG_DEBUG=4096): thread 0's s_memtime per phase -- run records, block descriptors, the first
+fill issued + index decode (its loads wait for that fill too),
 window fills (issue to the barrier after the wait), gathers, stores.
 
     make -C parquet-rs_amd DIAG=1 && PQG_DEBUG=4096 python tools/diag/diag_dict.py
@@ -40,7 +41,7 @@ def main():
     nb = raw[:, 7].sum()
     print(f"workgroups {len(raw)}, workgroups of 8 tiles {nb:.0f}")
     tot = raw[:, :6].sum(axis=1)
-    for k, name in enumerate(("stage", "block descriptors", "index decode", "window fills", "gathers", "stores")):
+    for k, name in enumerate(("run records", "block descriptors", "fill 1 + decode", "window fills", "gathers", "stores")):
         print(f"  {name:18s} {raw[:, k].sum() / nb:9.0f} cycles per workgroup ({raw[:, k].sum() / tot.sum():.2f})")
     print(f"  {'total':18s} {tot.sum() / nb:9.0f} cycles per workgroup")
 
