@@ -54,7 +54,10 @@ constexpr uint32_t D1_PREK = 8;                // chunks whose R header prefixes
 constexpr uint32_t D1_RES = 96, D1_RW = 128, D1_RS = D1_RW + 2 * D1_NCH;
 static_assert(D1_RS + D1_NCH / 2 <= LW_SCAP, "segment record");
 static_assert(D1_NCH == WG, "one thread per chunk");
-constexpr uint32_t D1_RB = 131072;  // bitmap bits per emit round (16 KiB)
+#ifndef PQG_D1_RB
+#define PQG_D1_RB 131072
+#endif
+constexpr uint32_t D1_RB = PQG_D1_RB;  // bitmap bits per emit round (16 KiB)
 constexpr uint32_t D1_RBW = D1_RB / 32;
 
 // Diagnostics (PQG_DIAG builds, PQG_DEBUG 8192): thread 0's s_memtime cycles per phase of each
@@ -644,7 +647,10 @@ static void lv_launch_d1(const uint8_t* blob, uint64_t blob_len, PageWork* pages
 #ifndef PQG_D1_GRID
 #define PQG_D1_GRID 2048
 #endif
-  hipLaunchKernelGGL(k_d1_tab, dim3(PQG_D1_GRID), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
+#ifndef PQG_D1_TGRID
+#define PQG_D1_TGRID 16384  // (k_d1_tab at p_null 0.1: 2048 workgroups 0.33 ms, 4096 0.28, 8192 0.25, 16384 0.24)
+#endif
+  hipLaunchKernelGGL(k_d1_tab, dim3(PQG_D1_TGRID), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
   hipLaunchKernelGGL(k_d1_stitch, dim3(npages < 1024 ? npages : 1024), dim3(WG), 0, s, blob, pages, npages, chunks, sel,
                      rt, lt);
   hipLaunchKernelGGL(k_d1_emit<2>, dim3(PQG_D1_GRID), dim3(WG), 0, s, blob, blob_len, pages, npages, chunks, sel, rt, lt);
